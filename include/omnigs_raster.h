@@ -1,0 +1,126 @@
+/*
+ * omnigs_raster.h — C ABI of the MI355X (gfx950) omnidirectional Gaussian-splat rasterizer.
+ *
+ * These entry points replace, one for one, the raw-pointer rasterizer interface of OmniGS
+ * (raikuma/OmniGS-fork @ 2025-03-04, cuda_rasterizer/rasterizer.h:28-156):
+ *
+ *   omr_rasterizer_mark_visible  <- CudaRasterizer::Rasterizer::markVisible        (rasterizer.h:32-37)
+ *   omr_rasterizer_forward       <- CudaRasterizer::Rasterizer::forward            (rasterizer.h:39-62)
+ *   omr_rasterizer_backward      <- CudaRasterizer::Rasterizer::backward           (rasterizer.h:64-93)
+ *   omr_lonlat_mark_visible      <- CudaRasterizer::LonlatRasterizer::markVisible  (rasterizer.h:98-100)
+ *   omr_lonlat_forward           <- CudaRasterizer::LonlatRasterizer::forward      (rasterizer.h:102-121)
+ *   omr_lonlat_backward          <- CudaRasterizer::LonlatRasterizer::backward     (rasterizer.h:124-154)
+ *
+ * and sit under the LibTorch boundary of include/rasterize_points.h (RasterizeGaussiansCUDA /
+ * RasterizeGaussiansBackwardCUDA / markVisible, reference include/rasterize_points.h:29-80), which
+ * omnigs-fork_amd/csrc/rasterize_points.cpp implements on top of them.
+ *
+ * Conventions (same as the reference unless stated):
+ *   - all pointers are device pointers on the current HIP device, fp32 unless typed otherwise;
+ *     means3D [P,3], shs [P,M,3], colors_precomp [P,3], opacities [P], scales [P,3], rotations [P,4]
+ *     (r,x,y,z; not renormalised), cov3D_precomp [P,6], viewmatrix / projmatrix 16 floats column-major
+ *     (Tcw^T, (P Tcw)^T as tensors), cam_pos [3], background [3];
+ *   - NULL for shs / colors_precomp / scales / rotations / cov3D_precomp means "absent" (the reference tests
+ *     data_ptr() != nullptr of empty tensors);
+ *   - out_color is [3,H,W]; radii [P] int32 (NULL: internal buffer, as the reference);
+ *   - scratch memory comes from three allocation callbacks (geometry, binning, image) replacing the
+ *     reference's std::function<char*(size_t)>; the returned memory must stay valid and be passed back
+ *     unchanged to the backward call together with R = *num_rendered; its layout is private;
+ *   - `stream` is a hipStream_t (NULL = legacy default stream). The forward synchronises the stream once,
+ *     after the scan, to size the binning buffer (as the reference's cudaMemcpy, rasterizer_impl.cu:628);
+ *   - ADDED vs the reference: the backward writes EVERY element of its gradient outputs (zeros where the
+ *     reference leaves its zero-initialised tensors untouched), so they need not be zeroed by the caller.
+ *     dL_dconic ([P,4], slots 0,1,3) and, for lonlat, dpx_dt / dpy_dt ([P,3]) are optional (NULL = skip);
+ *   - errors: calls return OMR_OK (0) or an OMR_ERR_* code; omr_last_error() gives the message of the last
+ *     failing call on this thread. The reference throws std::runtime_error / traps instead.
+ */
+#ifndef OMNIGS_RASTER_H
+#define OMNIGS_RASTER_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OMR_ABI_VERSION 1
+
+enum omr_status {
+    OMR_OK = 0,
+    OMR_ERR_INVALID_ARGUMENT = 1, /* bad sizes / missing required pointer */
+    OMR_ERR_CAMERA_TYPE = 2,      /* "[CudaRasterizer]Invalid camera_type" (rasterize_points.cu:160) */
+    OMR_ERR_ALLOCATION = 3,       /* an allocation callback returned NULL */
+    OMR_ERR_HIP = 4,              /* a HIP runtime / launch error */
+    OMR_ERR_PREFILTERED = 5,      /* prefiltered set but a point was culled (auxiliary.h:183-187 traps) */
+};
+
+enum omr_camera_type { OMR_CAMERA_PINHOLE = 1, OMR_CAMERA_LONLAT = 3 };
+
+/* replaces std::function<char*(size_t)> (rasterizer.h:43-45); must return device memory of >= bytes */
+typedef void* (*omr_alloc_fn)(void* ctx, size_t bytes);
+
+int omr_abi_version(void);
+const char* omr_last_error(void);
+
+/* --- pinhole (camera_type = 1) ------------------------------------------------------------------- */
+int omr_rasterizer_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                                bool* present, void* stream);
+
+int omr_rasterizer_forward(omr_alloc_fn geometry_alloc, void* geometry_ctx, omr_alloc_fn binning_alloc,
+                           void* binning_ctx, omr_alloc_fn image_alloc, void* image_ctx, int P, int D, int M,
+                           const float* background, int width, int height, const float* means3D, const float* shs,
+                           const float* colors_precomp, const float* opacities, const float* scales,
+                           float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                           const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
+                           float tan_fovy, bool prefiltered, float* out_color, int* radii, bool render_depth,
+                           void* stream, int* num_rendered);
+
+int omr_rasterizer_backward(int P, int D, int M, int R, const float* background, int width, int height,
+                            const float* means3D, const float* shs, const float* colors_precomp, const float* scales,
+                            float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                            const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                            float tan_fovy, const int* radii, char* geom_buffer, char* binning_buffer,
+                            char* image_buffer, const float* dL_dpix, float* dL_dmean2D, float* dL_dconic,
+                            float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh,
+                            float* dL_dscale, float* dL_drot, void* stream);
+
+/* --- equirectangular / lonlat (camera_type = 3) -------------------------------------------------- */
+int omr_lonlat_mark_visible(int P, bool* present, void* stream);
+
+int omr_lonlat_forward(omr_alloc_fn geometry_alloc, void* geometry_ctx, omr_alloc_fn binning_alloc, void* binning_ctx,
+                       omr_alloc_fn image_alloc, void* image_ctx, int P, int D, int M, const float* background,
+                       int width, int height, const float* means3D, const float* shs, const float* colors_precomp,
+                       const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                       const float* cov3D_precomp, const float* viewmatrix, const float* cam_pos, bool prefiltered,
+                       float* out_color, int* radii, void* stream, int* num_rendered);
+
+int omr_lonlat_backward(int P, int D, int M, int R, const float* background, int width, int height,
+                        const float* means3D, const float* shs, const float* colors_precomp, const float* scales,
+                        float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                        const float* viewmatrix, const float* campos, const int* radii, char* geom_buffer,
+                        char* binning_buffer, char* image_buffer, const float* dL_dpix, float* dL_dmean2D,
+                        float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D,
+                        float* dL_dsh, float* dL_dscale, float* dL_drot, float* dpx_dt, float* dpy_dt, void* stream);
+
+/* --- scratch sizes (bytes the allocation callbacks are asked for) -------------------------------- */
+size_t omr_geometry_bytes(int P);
+size_t omr_image_bytes(int width, int height);
+size_t omr_binning_bytes(int num_rendered, int width, int height);
+
+/* --- introspection for tests / tools (read from the private scratch layout) ---------------------- */
+/* copies the sorted per-instance Gaussian indices (R entries) and tile ranges ([T] uint2) to device dst */
+int omr_debug_point_list(char* binning_buffer, int R, int width, int height, uint32_t* dst, void* stream);
+int omr_debug_ranges(char* image_buffer, int width, int height, uint32_t* dst, void* stream);
+/* per-pixel final transmittance [N] f32 and contributor count [N] u32 */
+int omr_debug_image_state(char* image_buffer, int width, int height, float* final_T, uint32_t* n_contrib, void* stream);
+/* per-Gaussian pixel centre [P,2], conic+opacity [P,4], rgb [P,3], depth [P], tiles_touched [P] */
+int omr_debug_geometry(char* geom_buffer, int P, float* means2D, float* conic_opacity, float* rgb, float* depths,
+                       uint32_t* tiles_touched, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OMNIGS_RASTER_H */

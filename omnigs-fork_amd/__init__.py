@@ -1,0 +1,26 @@
+"""omnigs-fork_amd — MI355X-native (gfx950) omnidirectional Gaussian-splat rasterizer.
+
+The directory name is not a Python identifier; load it as `omnigs_fork_amd` with `_omnigs.load()` at the repo root.
+
+Layout:
+  csrc/            HIP kernels for gfx950 + the C ABI (include/omnigs_raster.h) -> lib/libomnigs_raster.so
+  csrc/rasterize_points.cpp  LibTorch drop-in of include/rasterize_points.h (reference symbols)
+  rasterizer.py    Python mirror of the reference boundary + autograd wrapper, on the C ABI
+  renderer.py      GaussianRenderer::renderLonlat / render glue (activations, settings)
+  parallel.py      view-parallel data parallelism (one view per GPU, RCCL all-reduce of Gaussian gradients)
+  scene.py         deterministic synthetic scenes and camera poses
+"""
+from . import scene  # noqa: F401
+
+__all__ = ["scene", "rasterizer"]
+
+
+def __getattr__(name):
+    # the HIP-backed modules import torch and the shared library lazily
+    if name in ("rasterizer", "renderer", "parallel"):
+        import importlib
+
+        mod = importlib.import_module(f"{__name__}.{name}")
+        globals()[name] = mod
+        return mod
+    raise AttributeError(name)

@@ -1,0 +1,454 @@
+// capi.hip — orchestration of the gfx950 rasterizer behind the C ABI of include/omnigs_raster.h.
+//
+// Forward  (reference: LonlatRasterizer::forward / Rasterizer::forward, rasterizer_impl.cu:540-697 / :250-433):
+//   preprocess -> depth sort of Gaussians -> scan of tiles_touched in depth order -> [one host sync for
+//   num_rendered] -> emit instances -> tile sort -> tile ranges -> render.
+// Backward (reference: LonlatRasterizer::backward / Rasterizer::backward, rasterizer_impl.cu:701-795 / :437-535):
+//   render backward (per-instance gradient rows) -> fused per-Gaussian backward.
+// Everything is enqueued on the caller's stream; no allocation happens outside the three callbacks.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/omnigs_raster.h"
+#include "kernels.h"
+
+namespace omr {
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg)
+{
+    g_last_error = msg;
+    return code;
+}
+
+int hip_check(const char* where)
+{
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(OMR_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+    return OMR_OK;
+}
+
+#define OMR_HIP(call)                                                                            \
+    do {                                                                                         \
+        const hipError_t e_ = (call);                                                            \
+        if (e_ != hipSuccess) return fail(OMR_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// pinned host words for the one device->host read of the forward (num_rendered, prefiltered flag)
+uint32_t* pinned_words()
+{
+    thread_local uint32_t* p = nullptr;
+    if (!p) {
+        if (hipHostMalloc(reinterpret_cast<void**>(&p), 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) p = nullptr;
+    }
+    return p;
+}
+
+}  // namespace
+
+size_t GeomState::carve(char* base, size_t P, GeomState* s)
+{
+    Carver c(base);
+    GeomState g;
+    g.means2D = c.take<float2>(P);
+    g.conic_opacity = c.take<float4>(P);
+    g.rgb = c.take<float4>(P);
+    g.depths = c.take<float>(P);
+    g.clamped = c.take<uint8_t>(P);
+    g.tiles_touched = c.take<uint32_t>(P);
+    g.key_a = c.take<uint32_t>(P);
+    g.key_b = c.take<uint32_t>(P);
+    g.val_a = c.take<uint32_t>(P);
+    g.val_b = c.take<uint32_t>(P);
+    const size_t nh = radix_hist_size(P);
+    g.hist = c.take<uint32_t>(nh);
+    g.scan_partials = c.take<uint32_t>(std::max(scan_partials_size(P), scan_partials_size(nh)));
+    g.offsets = c.take<uint32_t>(P);
+    g.emit_off = c.take<uint32_t>(P);
+    g.counters = c.take<uint32_t>(4);
+    g.internal_radii = c.take<int>(P);
+    g.order = nullptr;
+    if (s) *s = g;
+    return c.size();
+}
+
+static int* geom_internal_radii(char* base, size_t P)
+{
+    GeomState g;
+    GeomState::carve(base, P, &g);
+    return g.internal_radii;
+}
+
+size_t ImageState::carve(char* base, size_t N, size_t T, ImageState* s)
+{
+    Carver c(base);
+    ImageState im;
+    im.final_T = c.take<float>(N);
+    im.n_contrib = c.take<uint32_t>(N);
+    im.ranges = c.take<uint2>(T);
+    if (s) *s = im;
+    return c.size();
+}
+
+size_t BinningState::carve(char* base, size_t L, GeomState*, BinningState* s, int tile_passes)
+{
+    Carver c(base);
+    BinningState b;
+    b.key_a = c.take<uint32_t>(L);
+    b.key_b = c.take<uint32_t>(L);
+    b.val_a = c.take<uint32_t>(L);
+    b.val_b = c.take<uint32_t>(L);
+    const size_t nh = radix_hist_size(L);
+    b.hist = c.take<uint32_t>(nh);
+    b.scan_partials = c.take<uint32_t>(scan_partials_size(nh));
+    b.inst_grad = c.take<float>(L * GRAD_ROW);
+    const bool in_b = (tile_passes & 1) != 0;  // result buffer of the ping-pong
+    b.point_list = in_b ? b.val_b : b.val_a;
+    b.point_keys = in_b ? b.key_b : b.key_a;
+    if (s) *s = b;
+    return c.size();
+}
+
+namespace {
+
+struct Dims {
+    int W, H;
+    uint32_t gx, gy, T;
+    size_t N;
+};
+Dims dims(int width, int height)
+{
+    Dims d;
+    d.W = width;
+    d.H = height;
+    d.gx = (uint32_t)((width + BLOCK_X - 1) / BLOCK_X);
+    d.gy = (uint32_t)((height + BLOCK_Y - 1) / BLOCK_Y);
+    d.T = d.gx * d.gy;
+    d.N = (size_t)width * height;
+    return d;
+}
+
+struct ForwardIn {
+    int camera_type;
+    omr_alloc_fn geometry_alloc, binning_alloc, image_alloc;
+    void *geometry_ctx, *binning_ctx, *image_ctx;
+    int P, D, M;
+    const float* background;
+    int width, height;
+    const float *means3D, *shs, *colors_precomp, *opacities, *scales;
+    float scale_modifier;
+    const float *rotations, *cov3D_precomp, *viewmatrix, *projmatrix, *cam_pos;
+    float tan_fovx, tan_fovy;
+    bool prefiltered;
+    float* out_color;
+    int* radii;
+    bool render_depth;
+    hipStream_t stream;
+    int* num_rendered;
+};
+
+int forward_impl(const ForwardIn& in)
+{
+    g_last_error.clear();
+    if (in.num_rendered) *in.num_rendered = 0;
+    if (in.camera_type != CAM_PINHOLE && in.camera_type != CAM_LONLAT)
+        return fail(OMR_ERR_CAMERA_TYPE, "[CudaRasterizer]Invalid camera_type");
+    if (in.P < 0 || in.width <= 0 || in.height <= 0) return fail(OMR_ERR_INVALID_ARGUMENT, "bad P / width / height");
+    if (in.P == 0) return OMR_OK;  // rasterize_points.cu:97: nothing runs, image stays zero
+    if (!in.means3D || !in.opacities || !in.viewmatrix || !in.background || !in.out_color)
+        return fail(OMR_ERR_INVALID_ARGUMENT, "missing required input pointer");
+    if (!in.colors_precomp && (!in.shs || in.M <= 0))
+        return fail(OMR_ERR_INVALID_ARGUMENT, "either shs (M > 0) or colors_precomp is required");
+    if (!in.cov3D_precomp && (!in.scales || !in.rotations))
+        return fail(OMR_ERR_INVALID_ARGUMENT, "either scales+rotations or cov3D_precomp is required");
+    if (in.camera_type == CAM_PINHOLE && !in.projmatrix) return fail(OMR_ERR_INVALID_ARGUMENT, "pinhole needs projmatrix");
+    if (in.colors_precomp == nullptr && (in.shs == nullptr || in.cam_pos == nullptr))
+        return fail(OMR_ERR_INVALID_ARGUMENT, "SH colours need cam_pos");
+    const Dims d = dims(in.width, in.height);
+    const hipStream_t s = in.stream;
+    const size_t P = (size_t)in.P;
+
+    char* geom_base = static_cast<char*>(in.geometry_alloc(in.geometry_ctx, GeomState::carve(nullptr, P, nullptr)));
+    if (!geom_base) return fail(OMR_ERR_ALLOCATION, "geometry allocation failed");
+    GeomState g;
+    GeomState::carve(geom_base, P, &g);
+    char* img_base = static_cast<char*>(in.image_alloc(in.image_ctx, ImageState::carve(nullptr, d.N, d.T, nullptr)));
+    if (!img_base) return fail(OMR_ERR_ALLOCATION, "image allocation failed");
+    ImageState im;
+    ImageState::carve(img_base, d.N, d.T, &im);
+    int* radii = in.radii ? in.radii : geom_internal_radii(geom_base, P);
+
+    OMR_HIP(hipMemsetAsync(g.counters, 0, 4 * sizeof(uint32_t), s));
+    PreprocessArgs pa;
+    pa.P = in.P; pa.D = in.D; pa.M = in.M; pa.W = in.width; pa.H = in.height; pa.gx = d.gx; pa.gy = d.gy;
+    pa.means3D = in.means3D; pa.scales = in.scales; pa.scale_modifier = in.scale_modifier; pa.rotations = in.rotations;
+    pa.opacities = in.opacities; pa.shs = in.shs; pa.cov3D_precomp = in.cov3D_precomp; pa.colors_precomp = in.colors_precomp;
+    pa.viewmatrix = in.viewmatrix; pa.projmatrix = in.projmatrix; pa.campos = in.cam_pos;
+    pa.tan_fovx = in.tan_fovx; pa.tan_fovy = in.tan_fovy;
+    pa.focal_y = (float)in.height / (2.0f * in.tan_fovy);  // rasterizer_impl.cu:275-276
+    pa.focal_x = (float)in.width / (2.0f * in.tan_fovx);
+    pa.prefiltered = in.prefiltered ? 1 : 0;
+    pa.radii = radii;
+    pa.g = g;
+    pa.error_flag = reinterpret_cast<int*>(g.counters + 1);
+    launch_preprocess(in.camera_type, pa, s);
+
+    // depth order of the Gaussians (stable: ties keep index order)
+    const int which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, 0, 4, s);
+    g.order = which ? g.val_b : g.val_a;
+    launch_inclusive_scan(g.tiles_touched, g.order, g.offsets, g.scan_partials, P, s);
+
+    uint32_t* host = pinned_words();
+    if (!host) return fail(OMR_ERR_HIP, "hipHostMalloc failed");
+    OMR_HIP(hipMemcpyAsync(host, g.offsets + (P - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    OMR_HIP(hipMemcpyAsync(host + 1, g.counters + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    OMR_HIP(hipStreamSynchronize(s));
+    if (int e = hip_check("preprocess/sort/scan")) return e;
+    if (host[1] != 0)
+        return fail(OMR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    const size_t L = host[0];
+
+    const int tile_passes = tile_sort_passes(d.T);
+    char* bin_base = static_cast<char*>(
+        in.binning_alloc(in.binning_ctx, BinningState::carve(nullptr, L, nullptr, nullptr, tile_passes)));
+    if (!bin_base) return fail(OMR_ERR_ALLOCATION, "binning allocation failed");
+    BinningState b;
+    BinningState::carve(bin_base, L, nullptr, &b, tile_passes);
+
+    launch_emit_instances(in.P, g, radii, d.gx, d.gy, b.key_a, b.val_a, s);
+    radix_sort_pairs(b.key_a, b.key_b, b.val_a, b.val_b, b.hist, b.scan_partials, L, 0, tile_passes, s);
+    OMR_HIP(hipMemsetAsync(im.ranges, 0, d.T * sizeof(uint2), s));
+    launch_tile_ranges(L, b.point_keys, im.ranges, s);
+
+    RenderFwdArgs ra;
+    ra.W = in.width; ra.H = in.height; ra.gx = d.gx; ra.gy = d.gy;
+    ra.ranges = im.ranges; ra.point_list = b.point_list;
+    ra.means2D = g.means2D; ra.conic_opacity = g.conic_opacity; ra.rgb = g.rgb; ra.depths = g.depths;
+    ra.bg = in.background; ra.final_T = im.final_T; ra.n_contrib = im.n_contrib; ra.out_color = in.out_color;
+    // lonlat never renders depth (rasterize_points.cu:133-156 passes render_depth to the pinhole path only)
+    launch_render_forward(ra, in.render_depth && in.camera_type == CAM_PINHOLE, s);
+    if (int e = hip_check("emit/sort/render")) return e;
+    if (in.num_rendered) *in.num_rendered = (int)L;
+    return OMR_OK;
+}
+
+struct BackwardIn {
+    int camera_type;
+    int P, D, M, R;
+    const float* background;
+    int width, height;
+    const float *means3D, *shs, *colors_precomp, *scales;
+    float scale_modifier;
+    const float *rotations, *cov3D_precomp, *viewmatrix, *projmatrix, *campos;
+    float tan_fovx, tan_fovy;
+    const int* radii;
+    char *geom_buffer, *binning_buffer, *image_buffer;
+    const float* dL_dpix;
+    float *dL_dmean2D, *dL_dconic, *dL_dopacity, *dL_dcolor, *dL_dmean3D, *dL_dcov3D, *dL_dsh, *dL_dscale, *dL_drot;
+    float *dpx_dt, *dpy_dt;
+    hipStream_t stream;
+};
+
+int backward_impl(const BackwardIn& in)
+{
+    g_last_error.clear();
+    if (in.camera_type != CAM_PINHOLE && in.camera_type != CAM_LONLAT)
+        return fail(OMR_ERR_CAMERA_TYPE, "[CudaRasterizer]Invalid camera_type");
+    if (in.P < 0 || in.R < 0 || in.width <= 0 || in.height <= 0) return fail(OMR_ERR_INVALID_ARGUMENT, "bad sizes");
+    if (in.P == 0) return OMR_OK;
+    if (!in.geom_buffer || !in.binning_buffer || !in.image_buffer || !in.dL_dpix)
+        return fail(OMR_ERR_INVALID_ARGUMENT, "missing scratch buffer or dL_dpix");
+    if (!in.dL_dmean2D || !in.dL_dopacity || !in.dL_dcolor || !in.dL_dmean3D || !in.dL_dcov3D || !in.dL_dscale || !in.dL_drot)
+        return fail(OMR_ERR_INVALID_ARGUMENT, "missing gradient output pointer");
+    if (in.M > 0 && !in.dL_dsh) return fail(OMR_ERR_INVALID_ARGUMENT, "missing dL_dsh");
+    if ((in.dpx_dt == nullptr) != (in.dpy_dt == nullptr)) return fail(OMR_ERR_INVALID_ARGUMENT, "dpx_dt / dpy_dt: both or neither");
+    const Dims d = dims(in.width, in.height);
+    const hipStream_t s = in.stream;
+    const size_t P = (size_t)in.P;
+    GeomState g;
+    GeomState::carve(in.geom_buffer, P, &g);
+    BinningState b;
+    BinningState::carve(in.binning_buffer, (size_t)in.R, nullptr, &b, tile_sort_passes(d.T));
+    ImageState im;
+    ImageState::carve(in.image_buffer, d.N, d.T, &im);
+    const int* radii = in.radii ? in.radii : geom_internal_radii(in.geom_buffer, P);
+
+    RenderBwdArgs rb;
+    rb.W = in.width; rb.H = in.height; rb.gx = d.gx; rb.gy = d.gy;
+    rb.ranges = im.ranges; rb.point_list = b.point_list; rb.means2D = g.means2D; rb.conic_opacity = g.conic_opacity;
+    rb.rgb = g.rgb; rb.radii = radii; rb.emit_off = g.emit_off; rb.bg = in.background;
+    rb.final_T = im.final_T; rb.n_contrib = im.n_contrib; rb.dL_dpix = in.dL_dpix; rb.inst_grad = b.inst_grad;
+    launch_render_backward(rb, s);
+
+    GaussBwdArgs ga;
+    ga.P = in.P; ga.D = in.D; ga.M = in.M; ga.W = in.width; ga.H = in.height;
+    ga.means3D = in.means3D; ga.radii = radii; ga.shs = in.shs; ga.scales = in.scales; ga.rotations = in.rotations;
+    ga.scale_modifier = in.scale_modifier; ga.cov3D_precomp = in.cov3D_precomp; ga.viewmatrix = in.viewmatrix;
+    ga.projmatrix = in.projmatrix; ga.campos = in.campos; ga.tan_fovx = in.tan_fovx; ga.tan_fovy = in.tan_fovy;
+    ga.focal_y = (float)in.height / (2.0f * in.tan_fovy);
+    ga.focal_x = (float)in.width / (2.0f * in.tan_fovx);
+    ga.clamped = g.clamped; ga.emit_off = g.emit_off; ga.tiles_touched = g.tiles_touched; ga.inst_grad = b.inst_grad;
+    ga.dL_dmean2D = in.dL_dmean2D; ga.dL_dconic = in.dL_dconic; ga.dL_dopacity = in.dL_dopacity; ga.dL_dcolor = in.dL_dcolor;
+    ga.dL_dmean3D = in.dL_dmean3D; ga.dL_dcov3D = in.dL_dcov3D; ga.dL_dsh = in.M > 0 ? in.dL_dsh : nullptr;
+    ga.dL_dscale = in.dL_dscale; ga.dL_drot = in.dL_drot; ga.dpx_dt = in.dpx_dt; ga.dpy_dt = in.dpy_dt;
+    if (!in.shs) ga.shs = nullptr;
+    launch_gaussian_backward(in.camera_type, ga, s);
+    return hip_check("backward");
+}
+
+}  // namespace
+}  // namespace omr
+
+using namespace omr;
+
+extern "C" {
+
+int omr_abi_version(void) { return OMR_ABI_VERSION; }
+const char* omr_last_error(void) { return g_last_error.c_str(); }
+
+int omr_rasterizer_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                                bool* present, void* stream)
+{
+    g_last_error.clear();
+    if (P < 0) return fail(OMR_ERR_INVALID_ARGUMENT, "P < 0");
+    launch_mark_visible(CAM_PINHOLE, P, means3D, viewmatrix, projmatrix, present, (hipStream_t)stream);
+    return hip_check("mark_visible");
+}
+
+int omr_lonlat_mark_visible(int P, bool* present, void* stream)
+{
+    g_last_error.clear();
+    if (P < 0) return fail(OMR_ERR_INVALID_ARGUMENT, "P < 0");
+    launch_mark_visible(CAM_LONLAT, P, nullptr, nullptr, nullptr, present, (hipStream_t)stream);
+    return hip_check("mark_visible");
+}
+
+int omr_rasterizer_forward(omr_alloc_fn geometry_alloc, void* geometry_ctx, omr_alloc_fn binning_alloc,
+                           void* binning_ctx, omr_alloc_fn image_alloc, void* image_ctx, int P, int D, int M,
+                           const float* background, int width, int height, const float* means3D, const float* shs,
+                           const float* colors_precomp, const float* opacities, const float* scales,
+                           float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                           const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
+                           float tan_fovy, bool prefiltered, float* out_color, int* radii, bool render_depth,
+                           void* stream, int* num_rendered)
+{
+    ForwardIn in{CAM_PINHOLE, geometry_alloc, binning_alloc, image_alloc, geometry_ctx, binning_ctx, image_ctx,
+                 P, D, M, background, width, height, means3D, shs, colors_precomp, opacities, scales, scale_modifier,
+                 rotations, cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered,
+                 out_color, radii, render_depth, (hipStream_t)stream, num_rendered};
+    return forward_impl(in);
+}
+
+int omr_lonlat_forward(omr_alloc_fn geometry_alloc, void* geometry_ctx, omr_alloc_fn binning_alloc, void* binning_ctx,
+                       omr_alloc_fn image_alloc, void* image_ctx, int P, int D, int M, const float* background,
+                       int width, int height, const float* means3D, const float* shs, const float* colors_precomp,
+                       const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                       const float* cov3D_precomp, const float* viewmatrix, const float* cam_pos, bool prefiltered,
+                       float* out_color, int* radii, void* stream, int* num_rendered)
+{
+    ForwardIn in{CAM_LONLAT, geometry_alloc, binning_alloc, image_alloc, geometry_ctx, binning_ctx, image_ctx,
+                 P, D, M, background, width, height, means3D, shs, colors_precomp, opacities, scales, scale_modifier,
+                 rotations, cov3D_precomp, viewmatrix, nullptr, cam_pos, 0.f, 0.f, prefiltered,
+                 out_color, radii, false, (hipStream_t)stream, num_rendered};
+    return forward_impl(in);
+}
+
+int omr_rasterizer_backward(int P, int D, int M, int R, const float* background, int width, int height,
+                            const float* means3D, const float* shs, const float* colors_precomp, const float* scales,
+                            float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                            const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                            float tan_fovy, const int* radii, char* geom_buffer, char* binning_buffer,
+                            char* image_buffer, const float* dL_dpix, float* dL_dmean2D, float* dL_dconic,
+                            float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh,
+                            float* dL_dscale, float* dL_drot, void* stream)
+{
+    BackwardIn in{CAM_PINHOLE, P, D, M, R, background, width, height, means3D, shs, colors_precomp, scales,
+                  scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, radii,
+                  geom_buffer, binning_buffer, image_buffer, dL_dpix, dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor,
+                  dL_dmean3D, dL_dcov3D, dL_dsh, dL_dscale, dL_drot, nullptr, nullptr, (hipStream_t)stream};
+    return backward_impl(in);
+}
+
+int omr_lonlat_backward(int P, int D, int M, int R, const float* background, int width, int height,
+                        const float* means3D, const float* shs, const float* colors_precomp, const float* scales,
+                        float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                        const float* viewmatrix, const float* campos, const int* radii, char* geom_buffer,
+                        char* binning_buffer, char* image_buffer, const float* dL_dpix, float* dL_dmean2D,
+                        float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D,
+                        float* dL_dsh, float* dL_dscale, float* dL_drot, float* dpx_dt, float* dpy_dt, void* stream)
+{
+    BackwardIn in{CAM_LONLAT, P, D, M, R, background, width, height, means3D, shs, colors_precomp, scales,
+                  scale_modifier, rotations, cov3D_precomp, viewmatrix, nullptr, campos, 0.f, 0.f, radii,
+                  geom_buffer, binning_buffer, image_buffer, dL_dpix, dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor,
+                  dL_dmean3D, dL_dcov3D, dL_dsh, dL_dscale, dL_drot, dpx_dt, dpy_dt, (hipStream_t)stream};
+    return backward_impl(in);
+}
+
+size_t omr_geometry_bytes(int P) { return GeomState::carve(nullptr, (size_t)std::max(P, 0), nullptr); }
+
+size_t omr_image_bytes(int width, int height)
+{
+    const Dims d = dims(width, height);
+    return ImageState::carve(nullptr, d.N, d.T, nullptr);
+}
+
+size_t omr_binning_bytes(int num_rendered, int width, int height)
+{
+    const Dims d = dims(width, height);
+    return BinningState::carve(nullptr, (size_t)std::max(num_rendered, 0), nullptr, nullptr, tile_sort_passes(d.T));
+}
+
+int omr_debug_point_list(char* binning_buffer, int R, int width, int height, uint32_t* dst, void* stream)
+{
+    g_last_error.clear();
+    if (R <= 0) return OMR_OK;
+    const Dims d = dims(width, height);
+    BinningState b;
+    BinningState::carve(binning_buffer, (size_t)R, nullptr, &b, tile_sort_passes(d.T));
+    OMR_HIP(hipMemcpyAsync(dst, b.point_list, (size_t)R * sizeof(uint32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return OMR_OK;
+}
+
+int omr_debug_ranges(char* image_buffer, int width, int height, uint32_t* dst, void* stream)
+{
+    g_last_error.clear();
+    const Dims d = dims(width, height);
+    ImageState im;
+    ImageState::carve(image_buffer, d.N, d.T, &im);
+    OMR_HIP(hipMemcpyAsync(dst, im.ranges, d.T * sizeof(uint2), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return OMR_OK;
+}
+
+int omr_debug_image_state(char* image_buffer, int width, int height, float* final_T, uint32_t* n_contrib, void* stream)
+{
+    g_last_error.clear();
+    const Dims d = dims(width, height);
+    ImageState im;
+    ImageState::carve(image_buffer, d.N, d.T, &im);
+    OMR_HIP(hipMemcpyAsync(final_T, im.final_T, d.N * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    OMR_HIP(hipMemcpyAsync(n_contrib, im.n_contrib, d.N * sizeof(uint32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return OMR_OK;
+}
+
+int omr_debug_geometry(char* geom_buffer, int P, float* means2D, float* conic_opacity, float* rgb, float* depths,
+                       uint32_t* tiles_touched, void* stream)
+{
+    g_last_error.clear();
+    if (P <= 0) return OMR_OK;
+    GeomState g;
+    GeomState::carve(geom_buffer, (size_t)P, &g);
+    const hipStream_t s = (hipStream_t)stream;
+    if (means2D) OMR_HIP(hipMemcpyAsync(means2D, g.means2D, P * sizeof(float2), hipMemcpyDeviceToDevice, s));
+    if (conic_opacity) OMR_HIP(hipMemcpyAsync(conic_opacity, g.conic_opacity, P * sizeof(float4), hipMemcpyDeviceToDevice, s));
+    if (rgb) OMR_HIP(hipMemcpy2DAsync(rgb, 3 * sizeof(float), g.rgb, sizeof(float4), 3 * sizeof(float), P, hipMemcpyDeviceToDevice, s));
+    if (depths) OMR_HIP(hipMemcpyAsync(depths, g.depths, P * sizeof(float), hipMemcpyDeviceToDevice, s));
+    if (tiles_touched) OMR_HIP(hipMemcpyAsync(tiles_touched, g.tiles_touched, P * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    return OMR_OK;
+}
+
+}  // extern "C"

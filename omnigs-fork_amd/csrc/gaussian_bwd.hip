@@ -1,0 +1,441 @@
+// gaussian_bwd.hip — fused per-Gaussian backward, gfx950.
+//
+// One thread per Gaussian does, in registers, what the reference spreads over three kernels and two
+// zero-filled scratch tensors:
+//   * sums the Gaussian's per-instance gradient rows written by render_bwd.hip (fixed order -> deterministic),
+//     giving dL/dmean2D, dL/dconic, dL/dopacity, dL/dcolor (the reference's atomicAdd targets,
+//     backward.cu:805-840);
+//   * computeCov2DLonLatCUDA / computeCov2DCUDA (backward.cu:297-485 / :156-292): dL/dcov3D and the
+//     covariance part of dL/dmean3D; dpx_dt / dpy_dt stay in registers (the reference round-trips them
+//     through two [P,3] HBM tensors);
+//   * preprocessLonLatCUDA / preprocessCUDA backward (backward.cu:613-669 / :557-608): projection part of
+//     dL/dmean3D, SH backward (:30-151), cov3D -> scale/rotation backward (:489-552).
+// Every output element is written exactly once (zeros for culled Gaussians and unused SH slots), so the
+// caller needs no zero-initialised gradient tensors (the reference zero-fills ~324 B/Gaussian first,
+// rasterize_points.cu:200-208).
+#include "kernels.h"
+
+namespace omr {
+
+namespace {
+
+constexpr float SH_C0 = 0.28209479177387814f;  // auxiliary.h:32-49
+constexpr float SH_C1 = 0.4886025119029199f;
+constexpr float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f, -1.0925484305920792f,
+                            0.5462742152960396f};
+constexpr float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f, 0.3731763325901154f,
+                            -0.4570457994644658f, 1.445305721320277f, -0.5900435899266435f};
+constexpr float INV_PI = 0.318309886183790671537767526745028724f;
+
+struct F3 {
+    float x, y, z;
+};
+
+// dL/dconic -> dL/dcov2D -> dL/dcov3D and dL/dT (backward.cu:387-443). T0 = T[0][*], T1 = T[1][*] (glm).
+__device__ __forceinline__ void cov2d_backward(const float T0[3], const float T1[3], const float c3[6], F3 dL_dconic,
+                                               float dcov[6], float dT0[3], float dT1[3])
+{
+    const float V[3][3] = {{c3[0], c3[1], c3[2]}, {c3[1], c3[3], c3[4]}, {c3[2], c3[4], c3[5]}};
+    // cov2D = T^T Vrk T (same evaluation as the forward)
+    float B0[3], B1[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        B0[j] = T0[0] * V[j][0] + T0[1] * V[j][1] + T0[2] * V[j][2];
+        B1[j] = T1[0] * V[j][0] + T1[1] * V[j][1] + T1[2] * V[j][2];
+    }
+    const float a = B0[0] * T0[0] + B0[1] * T0[1] + B0[2] * T0[2] + 0.3f;
+    const float b = B1[0] * T0[0] + B1[1] * T0[1] + B1[2] * T0[2];
+    const float c = B1[0] * T1[0] + B1[1] * T1[1] + B1[2] * T1[2] + 0.3f;
+    const float denom = a * c - b * b;
+    float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    if (denom2inv != 0.f) {
+        dL_da = denom2inv * (-c * c * dL_dconic.x + 2 * b * c * dL_dconic.y + (denom - a * c) * dL_dconic.z);
+        dL_dc = denom2inv * (-a * a * dL_dconic.z + 2 * a * b * dL_dconic.y + (denom - a * c) * dL_dconic.x);
+        dL_db = denom2inv * 2 * (b * c * dL_dconic.x - (denom + 2 * b * b) * dL_dconic.y + a * b * dL_dconic.z);
+        dcov[0] = (T0[0] * T0[0] * dL_da + T0[0] * T1[0] * dL_db + T1[0] * T1[0] * dL_dc);
+        dcov[3] = (T0[1] * T0[1] * dL_da + T0[1] * T1[1] * dL_db + T1[1] * T1[1] * dL_dc);
+        dcov[5] = (T0[2] * T0[2] * dL_da + T0[2] * T1[2] * dL_db + T1[2] * T1[2] * dL_dc);
+        dcov[1] = 2 * T0[0] * T0[1] * dL_da + (T0[0] * T1[1] + T0[1] * T1[0]) * dL_db + 2 * T1[0] * T1[1] * dL_dc;
+        dcov[2] = 2 * T0[0] * T0[2] * dL_da + (T0[0] * T1[2] + T0[2] * T1[0]) * dL_db + 2 * T1[0] * T1[2] * dL_dc;
+        dcov[4] = 2 * T0[2] * T0[1] * dL_da + (T0[1] * T1[2] + T0[2] * T1[1]) * dL_db + 2 * T1[1] * T1[2] * dL_dc;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) dcov[i] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float v0 = T0[0] * V[k][0] + T0[1] * V[k][1] + T0[2] * V[k][2];
+        const float v1 = T1[0] * V[k][0] + T1[1] * V[k][1] + T1[2] * V[k][2];
+        dT0[k] = 2 * v0 * dL_da + v1 * dL_db;
+        dT1[k] = 2 * v1 * dL_dc + v0 * dL_db;
+    }
+}
+
+// backward.cu:489-552
+__device__ __forceinline__ void cov3d_backward(float sx, float sy, float sz, float mod, float4 q, const float d[6],
+                                               float dscale[3], float drot[4])
+{
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    const float R[3][3] = {{1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y)},
+                           {2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x)},
+                           {2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y)}};
+    const float s[3] = {mod * sx, mod * sy, mod * sz};
+    float M[3][3];  // M = S * R: M[j][i] = s_i * R[j][i]
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) M[j][i] = s[i] * R[j][i];
+    const float dS[3][3] = {{d[0], 0.5f * d[1], 0.5f * d[2]}, {0.5f * d[1], d[3], 0.5f * d[4]}, {0.5f * d[2], 0.5f * d[4], d[5]}};
+    float dM[3][3];  // dL_dM = (2 M) * dL_dSigma
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) dM[j][i] = 2.f * M[0][i] * dS[j][0] + 2.f * M[1][i] * dS[j][1] + 2.f * M[2][i] * dS[j][2];
+    // dL_dMt[j][i] = dM[i][j]; dscale_c = dot(Rt[c], dL_dMt[c]) = sum_k R[k][c] * dM[k][c]
+#pragma unroll
+    for (int cidx = 0; cidx < 3; ++cidx) dscale[cidx] = R[0][cidx] * dM[0][cidx] + R[1][cidx] * dM[1][cidx] + R[2][cidx] * dM[2][cidx];
+    float Mt[3][3];  // dL_dMt scaled: Mt[j][i] = dM[i][j] * s_j
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) Mt[j][i] = dM[i][j] * s[j];
+    drot[0] = 2 * z * (Mt[0][1] - Mt[1][0]) + 2 * y * (Mt[2][0] - Mt[0][2]) + 2 * x * (Mt[1][2] - Mt[2][1]);
+    drot[1] = 2 * y * (Mt[1][0] + Mt[0][1]) + 2 * z * (Mt[2][0] + Mt[0][2]) + 2 * r * (Mt[1][2] - Mt[2][1]) - 4 * x * (Mt[2][2] + Mt[1][1]);
+    drot[2] = 2 * x * (Mt[1][0] + Mt[0][1]) + 2 * r * (Mt[2][0] - Mt[0][2]) + 2 * z * (Mt[1][2] + Mt[2][1]) - 4 * y * (Mt[2][2] + Mt[0][0]);
+    drot[3] = 2 * r * (Mt[0][1] - Mt[1][0]) + 2 * x * (Mt[2][0] + Mt[0][2]) + 2 * y * (Mt[1][2] + Mt[2][1]) - 4 * z * (Mt[1][1] + Mt[0][0]);
+}
+
+// forward.cu:194-228 (recomputed instead of stored: saves 48 B/Gaussian of HBM round trip)
+__device__ __forceinline__ void cov3d_forward(float sx, float sy, float sz, float mod, float4 q, float c[6])
+{
+    const float s[3] = {mod * sx, mod * sy, mod * sz};
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    const float R[3][3] = {{1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y)},
+                           {2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x)},
+                           {2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y)}};
+    float M[3][3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) M[j][i] = s[i] * R[j][i];
+    auto sig = [&](int j, int i) { return M[i][0] * M[j][0] + M[i][1] * M[j][1] + M[i][2] * M[j][2]; };
+    c[0] = sig(0, 0);
+    c[1] = sig(0, 1);
+    c[2] = sig(0, 2);
+    c[3] = sig(1, 1);
+    c[4] = sig(1, 2);
+    c[5] = sig(2, 2);
+}
+
+// backward.cu:30-151; writes dL_dsh for all M coefficients (zeros beyond (deg+1)^2), returns dL/dmean part
+template <int MC>
+__device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const float* campos, const float* shs,
+                                          uint8_t clamp_bits, F3 dRGB, float* dL_dsh)
+{
+    const int Mr = MC > 0 ? MC : M;
+    const float dox = pos.x - campos[0], doy = pos.y - campos[1], doz = pos.z - campos[2];
+    const float len = sqrtf(dox * dox + doy * doy + doz * doz);
+    const float x = dox / len, y = doy / len, z = doz / len;
+    if (clamp_bits & 1) dRGB.x = 0.f;
+    if (clamp_bits & 2) dRGB.y = 0.f;
+    if (clamp_bits & 4) dRGB.z = 0.f;
+    const float* sh = shs + (size_t)idx * Mr * 3;
+    float* out = dL_dsh + (size_t)idx * Mr * 3;
+    float coef[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) coef[k] = 0.f;
+    float gx[3] = {0.f, 0.f, 0.f}, gy[3] = {0.f, 0.f, 0.f}, gz[3] = {0.f, 0.f, 0.f};  // dRGB/dx etc per channel
+    coef[0] = SH_C0;
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    if (deg > 0) {
+        coef[1] = -SH_C1 * y;
+        coef[2] = SH_C1 * z;
+        coef[3] = -SH_C1 * x;
+        if (deg > 1) {
+            coef[4] = SH_C2[0] * xy;
+            coef[5] = SH_C2[1] * yz;
+            coef[6] = SH_C2[2] * (2.f * zz - xx - yy);
+            coef[7] = SH_C2[3] * xz;
+            coef[8] = SH_C2[4] * (xx - yy);
+            if (deg > 2) {
+                coef[9] = SH_C3[0] * y * (3.f * xx - yy);
+                coef[10] = SH_C3[1] * xy * z;
+                coef[11] = SH_C3[2] * y * (4.f * zz - xx - yy);
+                coef[12] = SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                coef[13] = SH_C3[4] * x * (4.f * zz - xx - yy);
+                coef[14] = SH_C3[5] * z * (xx - yy);
+                coef[15] = SH_C3[6] * x * (xx - 3.f * yy);
+            }
+        }
+    }
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        auto s = [&](int k) { return sh[3 * k + ch]; };
+        if (deg > 0) {
+            gx[ch] = -SH_C1 * s(3);
+            gy[ch] = -SH_C1 * s(1);
+            gz[ch] = SH_C1 * s(2);
+            if (deg > 1) {
+                gx[ch] += SH_C2[0] * y * s(4) + SH_C2[2] * 2.f * -x * s(6) + SH_C2[3] * z * s(7) + SH_C2[4] * 2.f * x * s(8);
+                gy[ch] += SH_C2[0] * x * s(4) + SH_C2[1] * z * s(5) + SH_C2[2] * 2.f * -y * s(6) + SH_C2[4] * 2.f * -y * s(8);
+                gz[ch] += SH_C2[1] * y * s(5) + SH_C2[2] * 2.f * 2.f * z * s(6) + SH_C2[3] * x * s(7);
+                if (deg > 2) {
+                    gx[ch] += (SH_C3[0] * s(9) * 3.f * 2.f * xy + SH_C3[1] * s(10) * yz + SH_C3[2] * s(11) * -2.f * xy +
+                               SH_C3[3] * s(12) * -3.f * 2.f * xz + SH_C3[4] * s(13) * (-3.f * xx + 4.f * zz - yy) +
+                               SH_C3[5] * s(14) * 2.f * xz + SH_C3[6] * s(15) * 3.f * (xx - yy));
+                    gy[ch] += (SH_C3[0] * s(9) * 3.f * (xx - yy) + SH_C3[1] * s(10) * xz +
+                               SH_C3[2] * s(11) * (-3.f * yy + 4.f * zz - xx) + SH_C3[3] * s(12) * -3.f * 2.f * yz +
+                               SH_C3[4] * s(13) * -2.f * xy + SH_C3[5] * s(14) * -2.f * yz + SH_C3[6] * s(15) * -3.f * 2.f * xy);
+                    gz[ch] += (SH_C3[1] * s(10) * xy + SH_C3[2] * s(11) * 4.f * 2.f * yz +
+                               SH_C3[3] * s(12) * 3.f * (2.f * zz - xx - yy) + SH_C3[4] * s(13) * 4.f * 2.f * xz +
+                               SH_C3[5] * s(14) * (xx - yy));
+                }
+            }
+        }
+    }
+    const float d[3] = {dRGB.x, dRGB.y, dRGB.z};
+    if constexpr (MC == 16) {
+        // 16 coefficients x 3 channels = 48 floats = 12 float4 stores (row is 16-B aligned for M = 16)
+        float4* o4 = reinterpret_cast<float4*>(out);
+#pragma unroll
+        for (int q = 0; q < 12; ++q) {
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int f = 4 * q + e;
+                v[e] = (f / 3) < (deg + 1) * (deg + 1) ? coef[f / 3] * d[f % 3] : 0.f;
+            }
+            o4[q] = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    } else {
+        const int nk = (deg + 1) * (deg + 1);
+        for (int k = 0; k < Mr; ++k)
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) out[3 * k + ch] = (k < nk && k < 16) ? coef[k] * d[ch] : 0.f;
+    }
+    const F3 dL_ddir = {gx[0] * d[0] + gx[1] * d[1] + gx[2] * d[2], gy[0] * d[0] + gy[1] * d[1] + gy[2] * d[2],
+                        gz[0] * d[0] + gz[1] * d[1] + gz[2] * d[2]};
+    // dnormvdv (auxiliary.h:134-144)
+    const float sum2 = dox * dox + doy * doy + doz * doz;
+    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+    F3 r;
+    r.x = ((+sum2 - dox * dox) * dL_ddir.x - doy * dox * dL_ddir.y - doz * dox * dL_ddir.z) * invsum32;
+    r.y = (-dox * doy * dL_ddir.x + (sum2 - doy * doy) * dL_ddir.y - doz * doy * dL_ddir.z) * invsum32;
+    r.z = (-dox * doz * dL_ddir.x - doy * doz * dL_ddir.y + (sum2 - doz * doz) * dL_ddir.z) * invsum32;
+    return r;
+}
+
+template <int CAM, int MC>
+__global__ __launch_bounds__(256) void gaussian_bwd_kernel(GaussBwdArgs a)
+{
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    const int Mr = MC > 0 ? MC : a.M;
+    if (!(a.radii[idx] > 0)) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            a.dL_dmean2D[3 * idx + c] = 0.f;
+            a.dL_dcolor[3 * idx + c] = 0.f;
+            a.dL_dmean3D[3 * idx + c] = 0.f;
+            a.dL_dscale[3 * idx + c] = 0.f;
+        }
+        a.dL_dopacity[idx] = 0.f;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) a.dL_dcov3D[6 * idx + c] = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a.dL_drot[4 * idx + c] = 0.f;
+        if (a.dL_dconic)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) a.dL_dconic[4 * idx + c] = 0.f;
+        if (a.dL_dsh)
+            for (int c = 0; c < Mr * 3; ++c) a.dL_dsh[(size_t)idx * Mr * 3 + c] = 0.f;
+        if (a.dpx_dt)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) a.dpx_dt[3 * idx + c] = a.dpy_dt[3 * idx + c] = 0.f;
+        return;
+    }
+
+    // 1. sum this Gaussian's instance rows (emission order)
+    float g[GRAD_ROW];
+#pragma unroll
+    for (int c = 0; c < GRAD_ROW; ++c) g[c] = 0.f;
+    {
+        const uint32_t e0 = a.emit_off[idx], ne = a.tiles_touched[idx];
+        const float* row = a.inst_grad + (size_t)e0 * GRAD_ROW;
+        for (uint32_t e = 0; e < ne; ++e, row += GRAD_ROW)
+#pragma unroll
+            for (int c = 0; c < GRAD_ROW; ++c) g[c] += row[c];
+    }
+    a.dL_dmean2D[3 * idx + 0] = g[0];
+    a.dL_dmean2D[3 * idx + 1] = g[1];
+    a.dL_dmean2D[3 * idx + 2] = 0.f;
+    a.dL_dopacity[idx] = g[5];
+    a.dL_dcolor[3 * idx + 0] = g[6];
+    a.dL_dcolor[3 * idx + 1] = g[7];
+    a.dL_dcolor[3 * idx + 2] = g[8];
+    if (a.dL_dconic) {
+        a.dL_dconic[4 * idx + 0] = g[2];
+        a.dL_dconic[4 * idx + 1] = g[3];
+        a.dL_dconic[4 * idx + 2] = 0.f;
+        a.dL_dconic[4 * idx + 3] = g[4];
+    }
+
+    // 2. covariance backward
+    const F3 mean = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
+    const float* v = a.viewmatrix;
+    float c3[6];
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.scales) q = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
+    if (a.cov3D_precomp) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) c3[k] = a.cov3D_precomp[6 * idx + k];
+    } else {
+        cov3d_forward(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2], a.scale_modifier, q, c3);
+    }
+    const float tx = v[0] * mean.x + v[4] * mean.y + v[8] * mean.z + v[12];
+    const float ty = v[1] * mean.x + v[5] * mean.y + v[9] * mean.z + v[13];
+    const float tz = v[2] * mean.x + v[6] * mean.y + v[10] * mean.z + v[14];
+    const float W[3][3] = {{v[0], v[4], v[8]}, {v[1], v[5], v[9]}, {v[2], v[6], v[10]}};
+    const F3 dL_dconic = {g[2], g[3], g[4]};
+    float dcov[6], dT0[3], dT1[3];
+    F3 dmean;           // dL/dmean3D accumulator
+    F3 dpx = {0, 0, 0}, dpy = {0, 0, 0};
+    if constexpr (CAM == CAM_LONLAT) {
+        const float txtx = tx * tx, tyty = ty * ty, tztz = tz * tz, txtytz = tx * ty * tz;
+        const float trxztrxz = txtx + tztz;
+        const float trxztrxz_inv = 1.0f / (trxztrxz + 0.0000001f);
+        const float trxztrxztrxztrxz_inv = trxztrxz_inv * trxztrxz_inv;
+        const float trxz = sqrtf(trxztrxz);
+        const float trxz_inv = 1.0f / (trxz + 0.0000001f);
+        const float trtr = trxztrxz + tyty;
+        const float trtr_inv = 1.0f / (trtr + 0.0000001f);
+        const float trtrtrtr_inv = trtr_inv * trtr_inv;
+        const float trxz_trtrtrtr_inv = trxz_inv * trtrtrtr_inv;
+        const float trxztrxztrxz_trtrtrtr_inv = trxztrxz_inv * trxz_trtrtrtr_inv;
+        const float tyty_minus_trxztrxz = tyty - trxztrxz;
+        const float W_div_2pi = (float)a.W * 0.5f * INV_PI;
+        const float H_div_pi = (float)a.H * INV_PI;
+        const float dpx_dtx = W_div_2pi * tz * trxztrxz_inv;
+        const float dpx_dtz = -W_div_2pi * tx * trxztrxz_inv;
+        const float dpy_dtx = -H_div_pi * tx * ty * trxz_inv * trtr_inv;
+        const float dpy_dty = H_div_pi * trxz * trtr_inv;
+        const float dpy_dtz = -H_div_pi * tz * ty * trxz_inv * trtr_inv;
+        dpx = {dpx_dtx, 0.f, dpx_dtz};
+        dpy = {dpy_dtx, dpy_dty, dpy_dtz};
+        const float J0[3] = {dpx_dtx, 0.f, dpx_dtz}, J1[3] = {dpy_dtx, dpy_dty, dpy_dtz};
+        float T0[3], T1[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            T0[i] = W[0][i] * J0[0] + W[1][i] * J0[1] + W[2][i] * J0[2];
+            T1[i] = W[0][i] * J1[0] + W[1][i] * J1[1] + W[2][i] * J1[2];
+        }
+        cov2d_backward(T0, T1, c3, dL_dconic, dcov, dT0, dT1);
+        const float dL_dJ00 = W[0][0] * dT0[0] + W[0][1] * dT0[1] + W[0][2] * dT0[2];
+        const float dL_dJ02 = W[2][0] * dT0[0] + W[2][1] * dT0[1] + W[2][2] * dT0[2];
+        const float dL_dJ10 = W[0][0] * dT1[0] + W[0][1] * dT1[1] + W[0][2] * dT1[2];
+        const float dL_dJ11 = W[1][0] * dT1[0] + W[1][1] * dT1[1] + W[1][2] * dT1[2];
+        const float dL_dJ12 = W[2][0] * dT1[0] + W[2][1] * dT1[1] + W[2][2] * dT1[2];
+        // second derivatives of the lonlat projection (backward.cu:455-475; supp.pdf App. A)
+        const float temp1 = H_div_pi * tyty_minus_trxztrxz * trxz_trtrtrtr_inv;
+        const float temp2 = H_div_pi * txtytz * (trtr + 2.0f * trxztrxz) * trxztrxztrxz_trtrtrtr_inv;
+        const float temp3 = W_div_2pi * (txtx - tztz) * trxztrxztrxztrxz_inv;
+        const float temp4 = W_div_2pi * 2.0f * tx * tz * trxztrxztrxztrxz_inv;
+        const float temp5 = H_div_pi * ty * trxztrxztrxz_trtrtrtr_inv;
+        const float dL_dtx = -dL_dJ00 * temp4 + dL_dJ02 * temp3 + dL_dJ10 * temp5 * (2.0f * txtx * trxztrxz - tztz * trtr) +
+                             dL_dJ11 * tx * temp1 + dL_dJ12 * temp2;
+        const float dL_dty = dL_dJ10 * tx * temp1 - dL_dJ11 * H_div_pi * 2.0f * trxz * ty * trtrtrtr_inv + dL_dJ12 * tz * temp1;
+        const float dL_dtz = dL_dJ00 * temp3 + dL_dJ02 * temp4 + dL_dJ10 * temp2 + dL_dJ11 * tz * temp1 +
+                             dL_dJ12 * temp5 * (2.0f * tztz * trxztrxz - txtx * trtr);
+        const float3 m = transformVec4x3Transpose({dL_dtx, dL_dty, dL_dtz}, v);
+        dmean = {m.x, m.y, m.z};
+        // projection part (backward.cu:643-660)
+        const float dL_dpx = g[0] * (2.0f / (float)a.W);
+        const float dL_dpy = g[1] * (2.0f / (float)a.H);
+        const float3 mp = transformVec4x3Transpose({dL_dpx * dpx.x + dL_dpy * dpy.x, dL_dpx * dpx.y + dL_dpy * dpy.y,
+                                                    dL_dpx * dpx.z + dL_dpy * dpy.z}, v);
+        dmean.x += mp.x;
+        dmean.y += mp.y;
+        dmean.z += mp.z;
+    } else {
+        const float h_x = a.focal_x, h_y = a.focal_y;
+        const float limx = 1.3f * a.tan_fovx, limy = 1.3f * a.tan_fovy;
+        const float txtz = tx / tz, tytz = ty / tz;
+        const float txc = fminf(limx, fmaxf(-limx, txtz)) * tz;
+        const float tyc = fminf(limy, fmaxf(-limy, tytz)) * tz;
+        const float x_grad_mul = txtz < -limx || txtz > limx ? 0.f : 1.f;
+        const float y_grad_mul = tytz < -limy || tytz > limy ? 0.f : 1.f;
+        const float J0[3] = {h_x / tz, 0.f, -(h_x * txc) / (tz * tz)}, J1[3] = {0.f, h_y / tz, -(h_y * tyc) / (tz * tz)};
+        float T0[3], T1[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            T0[i] = W[0][i] * J0[0] + W[1][i] * J0[1] + W[2][i] * J0[2];
+            T1[i] = W[0][i] * J1[0] + W[1][i] * J1[1] + W[2][i] * J1[2];
+        }
+        cov2d_backward(T0, T1, c3, dL_dconic, dcov, dT0, dT1);
+        const float dL_dJ00 = W[0][0] * dT0[0] + W[0][1] * dT0[1] + W[0][2] * dT0[2];
+        const float dL_dJ02 = W[2][0] * dT0[0] + W[2][1] * dT0[1] + W[2][2] * dT0[2];
+        const float dL_dJ11 = W[1][0] * dT1[0] + W[1][1] * dT1[1] + W[1][2] * dT1[2];
+        const float dL_dJ12 = W[2][0] * dT1[0] + W[2][1] * dT1[1] + W[2][2] * dT1[2];
+        const float itz = 1.f / tz, tz2 = itz * itz, tz3 = tz2 * itz;
+        const float dL_dtx = x_grad_mul * -h_x * tz2 * dL_dJ02;
+        const float dL_dty = y_grad_mul * -h_y * tz2 * dL_dJ12;
+        const float dL_dtz = -h_x * tz2 * dL_dJ00 - h_y * tz2 * dL_dJ11 + (2 * h_x * txc) * tz3 * dL_dJ02 + (2 * h_y * tyc) * tz3 * dL_dJ12;
+        const float3 m = transformVec4x3Transpose({dL_dtx, dL_dty, dL_dtz}, v);
+        dmean = {m.x, m.y, m.z};
+        // projection part (backward.cu:583-599)
+        const float* proj = a.projmatrix;
+        const float4 m_hom = transformPoint4x4({mean.x, mean.y, mean.z}, proj);
+        const float m_w = 1.0f / (m_hom.w + 0.0000001f);
+        const float mul1 = (proj[0] * mean.x + proj[4] * mean.y + proj[8] * mean.z + proj[12]) * m_w * m_w;
+        const float mul2 = (proj[1] * mean.x + proj[5] * mean.y + proj[9] * mean.z + proj[13]) * m_w * m_w;
+        dmean.x += (proj[0] * m_w - proj[3] * mul1) * g[0] + (proj[1] * m_w - proj[3] * mul2) * g[1];
+        dmean.y += (proj[4] * m_w - proj[7] * mul1) * g[0] + (proj[5] * m_w - proj[7] * mul2) * g[1];
+        dmean.z += (proj[8] * m_w - proj[11] * mul1) * g[0] + (proj[9] * m_w - proj[11] * mul2) * g[1];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * idx + k] = dcov[k];
+    if (a.dpx_dt) {
+        a.dpx_dt[3 * idx + 0] = dpx.x; a.dpx_dt[3 * idx + 1] = dpx.y; a.dpx_dt[3 * idx + 2] = dpx.z;
+        a.dpy_dt[3 * idx + 0] = dpy.x; a.dpy_dt[3 * idx + 1] = dpy.y; a.dpy_dt[3 * idx + 2] = dpy.z;
+    }
+
+    // 3. SH backward
+    if (a.shs) {
+        const F3 dm = sh_backward<MC>(idx, a.D, a.M, mean, a.campos, a.shs, a.clamped[idx], F3{g[6], g[7], g[8]}, a.dL_dsh);
+        dmean.x += dm.x;
+        dmean.y += dm.y;
+        dmean.z += dm.z;
+    } else if (a.dL_dsh) {
+        for (int c = 0; c < Mr * 3; ++c) a.dL_dsh[(size_t)idx * Mr * 3 + c] = 0.f;
+    }
+    a.dL_dmean3D[3 * idx + 0] = dmean.x;
+    a.dL_dmean3D[3 * idx + 1] = dmean.y;
+    a.dL_dmean3D[3 * idx + 2] = dmean.z;
+
+    // 4. scale / rotation backward
+    float ds[3] = {0.f, 0.f, 0.f}, dr[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.scales) cov3d_backward(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2], a.scale_modifier, q, dcov, ds, dr);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) a.dL_dscale[3 * idx + k] = ds[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a.dL_drot[4 * idx + k] = dr[k];
+}
+
+}  // namespace
+
+void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s)
+{
+    if (a.P <= 0) return;
+    const dim3 grid(div_up(a.P, 256));
+    const bool m16 = a.M == 16 && (reinterpret_cast<uintptr_t>(a.dL_dsh) % 16) == 0;
+    if (camera_type == CAM_LONLAT) {
+        if (m16) gaussian_bwd_kernel<CAM_LONLAT, 16><<<grid, 256, 0, s>>>(a);
+        else gaussian_bwd_kernel<CAM_LONLAT, 0><<<grid, 256, 0, s>>>(a);
+    } else {
+        if (m16) gaussian_bwd_kernel<CAM_PINHOLE, 16><<<grid, 256, 0, s>>>(a);
+        else gaussian_bwd_kernel<CAM_PINHOLE, 0><<<grid, 256, 0, s>>>(a);
+    }
+}
+
+}  // namespace omr

@@ -1,0 +1,114 @@
+// kernels.h — launch-side declarations shared by the orchestration (capi.hip) and the kernel files.
+#pragma once
+
+#include "raster_common.h"
+
+namespace omr {
+
+struct PreprocessArgs {
+    int P, D, M;
+    int W, H;
+    uint32_t gx, gy;
+    const float* means3D;
+    const float* scales;
+    float scale_modifier;
+    const float* rotations;
+    const float* opacities;
+    const float* shs;
+    const float* cov3D_precomp;
+    const float* colors_precomp;
+    const float* viewmatrix;
+    const float* projmatrix;
+    const float* campos;
+    float tan_fovx, tan_fovy, focal_x, focal_y;
+    int prefiltered;
+    int* radii;
+    GeomState g;
+    int* error_flag;  // set to 1 if prefiltered and a point is culled (auxiliary.h:183-187 traps instead)
+};
+
+void launch_preprocess(int camera_type, const PreprocessArgs& a, hipStream_t s);
+void launch_mark_visible(int camera_type, int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                         bool* present, hipStream_t s);
+
+// sort.hip
+// inclusive scan of in[gather ? gather[i] : i] into out (u32, n items); partials needs scan_partials_size(n)
+size_t scan_partials_size(size_t n);
+void launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, uint32_t* partials, size_t n, hipStream_t s);
+size_t radix_hist_size(size_t n);
+// stable LSD radix sort of (key, value) over bits [0, 8*passes); returns which buffer holds the result (0: a, 1: b)
+int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* hist,
+                     uint32_t* scan_partials, size_t n, int first_pass, int passes, hipStream_t s);
+void launch_emit_instances(int P, const GeomState& g, const int* radii, uint32_t gx, uint32_t gy, uint32_t* tile_keys,
+                           uint32_t* gauss_vals, hipStream_t s);
+void launch_tile_ranges(size_t L, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s);
+
+// render_fwd.hip
+struct RenderFwdArgs {
+    int W, H;
+    uint32_t gx, gy;
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const float2* means2D;
+    const float4* conic_opacity;
+    const float4* rgb;
+    const float* depths;
+    const float* bg;
+    float* final_T;
+    uint32_t* n_contrib;
+    float* out_color;
+};
+void launch_render_forward(const RenderFwdArgs& a, bool depth_mode, hipStream_t s);
+
+// render_bwd.hip
+struct RenderBwdArgs {
+    int W, H;
+    uint32_t gx, gy;
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const float2* means2D;
+    const float4* conic_opacity;
+    const float4* rgb;
+    const int* radii;
+    const uint32_t* emit_off;
+    const float* bg;
+    const float* final_T;
+    const uint32_t* n_contrib;
+    const float* dL_dpix;
+    float* inst_grad;
+};
+void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
+
+// gaussian_bwd.hip
+struct GaussBwdArgs {
+    int P, D, M, W, H;
+    const float* means3D;
+    const int* radii;
+    const float* shs;
+    const float* scales;
+    const float* rotations;
+    float scale_modifier;
+    const float* cov3D_precomp;
+    const float* viewmatrix;
+    const float* projmatrix;
+    const float* campos;
+    float tan_fovx, tan_fovy, focal_x, focal_y;
+    const uint8_t* clamped;
+    const uint32_t* emit_off;
+    const uint32_t* tiles_touched;
+    const float* inst_grad;
+    float* dL_dmean2D;   // [P,3]
+    float* dL_dconic;    // [P,4] optional (may be null)
+    float* dL_dopacity;  // [P]
+    float* dL_dcolor;    // [P,3]
+    float* dL_dmean3D;   // [P,3]
+    float* dL_dcov3D;    // [P,6]
+    float* dL_dsh;       // [P,M,3]
+    float* dL_dscale;    // [P,3]
+    float* dL_drot;      // [P,4]
+    float* dpx_dt;       // [P,3] optional (lonlat only; may be null)
+    float* dpy_dt;       // [P,3] optional
+};
+void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s);
+
+}  // namespace omr

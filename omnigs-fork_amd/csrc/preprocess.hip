@@ -1,0 +1,271 @@
+// preprocess.hip — per-Gaussian forward preprocess for the lonlat (camera_type 3) and pinhole (camera_type 1)
+// projections, gfx950.
+//
+// Follows cuda_rasterizer/forward.cu:593-703 (preprocessLonlatCUDA) and :231-340 (preprocessCUDA):
+// cull, project, 3D covariance from scale+rotation, 2D covariance through the projection Jacobian, conic,
+// radius, tile rect, SH -> RGB. Compiled with -ffp-contract=off and evaluated in the reference's expression
+// order (glm column-major products, left-to-right sums), so radii, pixel centres, conics, tile rects and the
+// depth sort keys are bit-identical to the CPU oracle.
+//
+// MI355X notes: one wave64 per 64 Gaussians; the stores are SoA so every output array is written with
+// contiguous lanes; the depth sort's first-pass keys/values are written here directly (no extra pass).
+// HBM per Gaussian (D=3): reads 12 (xyz) + 12 (scale) + 16 (rot) + 4 (opacity) + 192 (SH) = 236 B,
+// writes 8 + 16 + 16 + 4 + 1 + 4 + 4 (radius) + 8 (sort key/value) = 61 B.
+#include "kernels.h"
+
+namespace omr {
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr float SH_C0 = 0.28209479177387814f;  // auxiliary.h:32-49
+constexpr float SH_C1 = 0.4886025119029199f;
+constexpr float SH_C2_0 = 1.0925484305920792f, SH_C2_1 = -1.0925484305920792f, SH_C2_2 = 0.31539156525252005f,
+                SH_C2_3 = -1.0925484305920792f, SH_C2_4 = 0.5462742152960396f;
+constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH_C3_2 = -0.4570457994644658f,
+                SH_C3_3 = 0.3731763325901154f, SH_C3_4 = -0.4570457994644658f, SH_C3_5 = 1.445305721320277f,
+                SH_C3_6 = -0.5900435899266435f;
+constexpr float INV_PI = 0.318309886183790671537767526745028724f;  // M_1_PIf32
+constexpr float TWO_INV_PI = 0.636619772367581343075535053490057448f;  // M_2_PIf32
+
+// forward.cu:194-228. Sigma = (S R)^T (S R) written out entry by entry in glm's evaluation order.
+__device__ __forceinline__ void cov3d_from_scale_rot(float sx, float sy, float sz, float mod, float4 q, float* c)
+{
+    const float s0 = mod * sx, s1 = mod * sy, s2 = mod * sz;
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    // R columns (glm::mat3 constructor fills column by column)
+    const float R00 = 1.f - 2.f * (y * y + z * z), R01 = 2.f * (x * y - r * z), R02 = 2.f * (x * z + r * y);
+    const float R10 = 2.f * (x * y + r * z), R11 = 1.f - 2.f * (x * x + z * z), R12 = 2.f * (y * z - r * x);
+    const float R20 = 2.f * (x * z - r * y), R21 = 2.f * (y * z + r * x), R22 = 1.f - 2.f * (x * x + y * y);
+    // M = S * R: M[j][i] = S[0][i]*R[j][0] + S[1][i]*R[j][1] + S[2][i]*R[j][2], S diagonal (zeros kept)
+    float M[3][3];
+    const float Rc[3][3] = {{R00, R01, R02}, {R10, R11, R12}, {R20, R21, R22}};
+    const float S[3][3] = {{s0, 0.f, 0.f}, {0.f, s1, 0.f}, {0.f, 0.f, s2}};
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) M[j][i] = S[0][i] * Rc[j][0] + S[1][i] * Rc[j][1] + S[2][i] * Rc[j][2];
+    // Sigma = M^T M: Sigma[j][i] = M[i][0]*M[j][0] + M[i][1]*M[j][1] + M[i][2]*M[j][2]
+    auto sig = [&](int j, int i) { return M[i][0] * M[j][0] + M[i][1] * M[j][1] + M[i][2] * M[j][2]; };
+    c[0] = sig(0, 0);
+    c[1] = sig(0, 1);
+    c[2] = sig(0, 2);
+    c[3] = sig(1, 1);
+    c[4] = sig(1, 2);
+    c[5] = sig(2, 2);
+}
+
+// cov = T^T Vrk T with T = W J (forward.cu:113-126 / :174-188); J has a zero third column.
+// T[j][i] = W[0][i]*J[j][0] + W[1][i]*J[j][1] + W[2][i]*J[j][2]; W[c] = (v[c], v[c+4], v[c+8]).
+__device__ __forceinline__ float3 cov2d_from_J(const float* v, const float J0[3], const float J1[3], const float* c3)
+{
+    const float W[3][3] = {{v[0], v[4], v[8]}, {v[1], v[5], v[9]}, {v[2], v[6], v[10]}};
+    float T0[3], T1[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        T0[i] = W[0][i] * J0[0] + W[1][i] * J0[1] + W[2][i] * J0[2];
+        T1[i] = W[0][i] * J1[0] + W[1][i] * J1[1] + W[2][i] * J1[2];
+    }
+    const float V[3][3] = {{c3[0], c3[1], c3[2]}, {c3[1], c3[3], c3[4]}, {c3[2], c3[4], c3[5]}};
+    // B = T^T * Vrk: B[j][i] = T[i][0]*V[j][0] + T[i][1]*V[j][1] + T[i][2]*V[j][2], rows i = 0, 1
+    float B0[3], B1[3];  // B[j][0], B[j][1]
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        B0[j] = T0[0] * V[j][0] + T0[1] * V[j][1] + T0[2] * V[j][2];
+        B1[j] = T1[0] * V[j][0] + T1[1] * V[j][1] + T1[2] * V[j][2];
+    }
+    // cov = B * T: cov[j][i] = B[0][i]*T[j][0] + B[1][i]*T[j][1] + B[2][i]*T[j][2]
+    float c00 = B0[0] * T0[0] + B0[1] * T0[1] + B0[2] * T0[2];
+    const float c01 = B1[0] * T0[0] + B1[1] * T0[1] + B1[2] * T0[2];
+    float c11 = B1[0] * T1[0] + B1[1] * T1[1] + B1[2] * T1[2];
+    c00 += 0.3f;
+    c11 += 0.3f;
+    return {c00, c01, c11};
+}
+
+// forward.cu:30-83, one channel at a time (glm vec3 ops are componentwise, same order)
+__device__ __forceinline__ void sh_to_rgb(int deg, float x, float y, float z, const float* sh, float out[3],
+                                          uint8_t& clamp_bits)
+{
+    clamp_bits = 0;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        auto s = [&](int k) { return sh[3 * k + ch]; };
+        float res = SH_C0 * s(0);
+        if (deg > 0) {
+            res = res - SH_C1 * y * s(1) + SH_C1 * z * s(2) - SH_C1 * x * s(3);
+            if (deg > 1) {
+                const float xx = x * x, yy = y * y, zz = z * z;
+                const float xy = x * y, yz = y * z, xz = x * z;
+                res = res + SH_C2_0 * xy * s(4) + SH_C2_1 * yz * s(5) + SH_C2_2 * (2.0f * zz - xx - yy) * s(6) +
+                      SH_C2_3 * xz * s(7) + SH_C2_4 * (xx - yy) * s(8);
+                if (deg > 2) {
+                    res = res + SH_C3_0 * y * (3.0f * xx - yy) * s(9) + SH_C3_1 * xy * z * s(10) +
+                          SH_C3_2 * y * (4.0f * zz - xx - yy) * s(11) +
+                          SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * s(12) +
+                          SH_C3_4 * x * (4.0f * zz - xx - yy) * s(13) + SH_C3_5 * z * (xx - yy) * s(14) +
+                          SH_C3_6 * x * (xx - 3.0f * yy) * s(15);
+                }
+            }
+        }
+        res += 0.5f;
+        if (res < 0) clamp_bits |= (uint8_t)(1u << ch);
+        out[ch] = fmaxf(res, 0.0f);
+    }
+}
+
+template <int CAM>
+__global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
+{
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    GeomState& g = a.g;
+    a.radii[idx] = 0;
+    g.tiles_touched[idx] = 0;
+    g.key_a[idx] = 0xFFFFFFFFu;  // culled Gaussians sort last and emit nothing
+    g.val_a[idx] = (uint32_t)idx;
+
+    const float3 p_orig = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
+    const float* v = a.viewmatrix;
+    const float3 t = transformPoint4x3(p_orig, v);
+    float2 point_image;
+    float depth;
+    float J0[3], J1[3];  // columns 0 and 1 of the glm J (column 2 is zero)
+
+    if constexpr (CAM == CAM_LONLAT) {
+        // too_close (auxiliary.h:198-220)
+        const float rr = t.x * t.x + t.y * t.y + t.z * t.z;
+        if (rr <= 0.04f) return;
+        const float r = sqrtf(rr);
+        // point3ToLonlatScreen (auxiliary.h:236-248)
+        const float inv_r = 1.0f / (r + 0.0000001f);
+        const float lon = omni::atan2f_(t.x, t.z);
+        const float lat = omni::asinf_(t.y * inv_r);
+        point_image = {ndc2Pix(lon * INV_PI, a.W), ndc2Pix(lat * TWO_INV_PI, a.H)};
+        depth = r;
+        // computeCov2DLonlat Jacobian (forward.cu:147-167)
+        const float trxztrxz = t.x * t.x + t.z * t.z;
+        const float trxztrxz_inv = 1.0f / (trxztrxz + 0.0000001f);
+        const float trxz = sqrtf(trxztrxz);
+        const float trxz_inv = 1.0f / (trxz + 0.0000001f);
+        const float trtr = trxztrxz + t.y * t.y;
+        const float trtr_inv = 1.0f / (trtr + 0.0000001f);
+        const float W_div_2pi = (float)a.W * 0.5f * INV_PI;
+        const float H_div_pi = (float)a.H * INV_PI;
+        J0[0] = W_div_2pi * t.z * trxztrxz_inv;
+        J0[1] = 0.0f;
+        J0[2] = -W_div_2pi * t.x * trxztrxz_inv;
+        J1[0] = -H_div_pi * t.x * t.y * trxz_inv * trtr_inv;
+        J1[1] = H_div_pi * trxz * trtr_inv;
+        J1[2] = -H_div_pi * t.z * t.y * trxz_inv * trtr_inv;
+    } else {
+        // in_frustum (auxiliary.h:166-196)
+        if (t.z <= 0.2f) {
+            if (a.prefiltered) atomicOr(a.error_flag, 1);
+            return;
+        }
+        const float4 p_hom = transformPoint4x4(p_orig, a.projmatrix);
+        const float p_w = 1.0f / (p_hom.w + 0.0000001f);
+        point_image = {ndc2Pix(p_hom.x * p_w, a.W), ndc2Pix(p_hom.y * p_w, a.H)};
+        depth = t.z;
+        // computeCov2D (forward.cu:92-106)
+        const float limx = 1.3f * a.tan_fovx;
+        const float limy = 1.3f * a.tan_fovy;
+        const float txtz = t.x / t.z;
+        const float tytz = t.y / t.z;
+        const float tx = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+        const float ty = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+        J0[0] = a.focal_x / t.z;
+        J0[1] = 0.0f;
+        J0[2] = -(a.focal_x * tx) / (t.z * t.z);
+        J1[0] = 0.0f;
+        J1[1] = a.focal_y / t.z;
+        J1[2] = -(a.focal_y * ty) / (t.z * t.z);
+    }
+
+    float c3[6];
+    if (a.cov3D_precomp != nullptr) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) c3[k] = a.cov3D_precomp[6 * idx + k];
+    } else {
+        const float4 q = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
+        cov3d_from_scale_rot(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2], a.scale_modifier, q, c3);
+    }
+    const float3 cov = cov2d_from_J(v, J0, J1, c3);
+
+    // conic and radius (forward.cu:660-674)
+    const float det = (cov.x * cov.z - cov.y * cov.y);
+    if (det == 0.0f) return;
+    const float det_inv = 1.f / det;
+    const float3 conic = {cov.z * det_inv, -cov.y * det_inv, cov.x * det_inv};
+    const float mid = 0.5f * (cov.x + cov.z);
+    const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
+    const int rad = (int)my_radius;
+    uint32_t x0, y0, x1, y1;
+    getRect(point_image, rad, a.gx, a.gy, x0, y0, x1, y1);
+    const uint32_t area = (y1 - y0) * (x1 - x0);
+    if (area == 0) return;
+
+    float rgb[3];
+    uint8_t clamp_bits = 0;
+    if (a.colors_precomp == nullptr) {
+        const float3 cp = {a.campos[0], a.campos[1], a.campos[2]};
+        float dx = p_orig.x - cp.x, dy = p_orig.y - cp.y, dz = p_orig.z - cp.z;
+        const float len = sqrtf(dx * dx + dy * dy + dz * dz);
+        dx = dx / len;
+        dy = dy / len;
+        dz = dz / len;
+        sh_to_rgb(a.D, dx, dy, dz, a.shs + (size_t)idx * a.M * 3, rgb, clamp_bits);
+    } else {
+        rgb[0] = a.colors_precomp[3 * idx];
+        rgb[1] = a.colors_precomp[3 * idx + 1];
+        rgb[2] = a.colors_precomp[3 * idx + 2];
+    }
+    g.rgb[idx] = {rgb[0], rgb[1], rgb[2], 0.0f};
+    g.clamped[idx] = clamp_bits;
+    g.depths[idx] = depth;
+    a.radii[idx] = rad;
+    g.means2D[idx] = point_image;
+    g.conic_opacity[idx] = {conic.x, conic.y, conic.z, a.opacities[idx]};
+    g.tiles_touched[idx] = area;
+    g.key_a[idx] = __float_as_uint(depth);
+}
+
+__global__ void mark_frustum_kernel(int P, const float* means3D, const float* viewmatrix, bool* present)
+{
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= P) return;
+    const float3 p = {means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]};
+    present[idx] = transformPoint4x3(p, viewmatrix).z > 0.2f;  // checkFrustum, rasterizer_impl.cu:66-78
+}
+
+__global__ void mark_all_kernel(int P, bool* present)  // markAllVisible, rasterizer_impl.cu:82-90
+{
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx < P) present[idx] = true;
+}
+
+}  // namespace
+
+void launch_preprocess(int camera_type, const PreprocessArgs& a, hipStream_t s)
+{
+    if (a.P <= 0) return;
+    const dim3 grid(div_up(a.P, 256));
+    if (camera_type == CAM_LONLAT) preprocess_kernel<CAM_LONLAT><<<grid, 256, 0, s>>>(a);
+    else preprocess_kernel<CAM_PINHOLE><<<grid, 256, 0, s>>>(a);
+}
+
+void launch_mark_visible(int camera_type, int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                         bool* present, hipStream_t s)
+{
+    (void)projmatrix;
+    if (P <= 0) return;
+    const dim3 grid(div_up(P, 256));
+    if (camera_type == CAM_LONLAT) mark_all_kernel<<<grid, 256, 0, s>>>(P, present);
+    else mark_frustum_kernel<<<grid, 256, 0, s>>>(P, means3D, viewmatrix, present);
+}
+
+}  // namespace omr

@@ -1,0 +1,159 @@
+// raster_common.h — constants, device helpers and the private scratch layouts of the gfx950 rasterizer.
+//
+// The three scratch buffers (geometry / binning / image) play the role of the reference's GeometryState,
+// BinningState and ImageState (cuda_rasterizer/rasterizer_impl.h:37-102). Their layout is private to this
+// library: forward writes them, backward re-carves them from the same byte buffers (the host only stores the
+// buffers and hands them back, gaussian_rasterizer.cpp:85-98). Every array starts on a 256-B boundary.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "omni_math.h"
+
+namespace omr {
+
+constexpr int BLOCK_X = 16;  // cuda_rasterizer/config.h:26 — part of the key semantics, kept
+constexpr int BLOCK_Y = 16;  // config.h:27
+constexpr int BLOCK_SIZE = BLOCK_X * BLOCK_Y;
+constexpr int NUM_CHANNELS = 3;  // config.h:25
+constexpr int CAM_PINHOLE = 1;
+constexpr int CAM_LONLAT = 3;
+
+// radix sort geometry (sort.hip)
+constexpr int SORT_THREADS = 256;
+constexpr int SORT_ITEMS = 16;  // items per thread per block tile
+constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;
+constexpr int RADIX_BITS = 8;
+constexpr int RADIX = 1 << RADIX_BITS;
+// scan geometry
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_ITEMS = 16;
+constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
+
+// per-instance gradient row written by the render backward (render_bwd.hip) and reduced per Gaussian
+// (gaussian_bwd.hip): dmean2D.x, dmean2D.y, dconic.x, dconic.y, dconic.w, dopacity, dcolor.rgb
+constexpr int GRAD_ROW = 9;
+
+constexpr size_t ALIGN = 256;
+inline size_t align_up(size_t x) { return (x + ALIGN - 1) & ~(ALIGN - 1); }
+inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+struct Carver {
+    char* base;
+    size_t off = 0;
+    explicit Carver(char* b) : base(b) {}
+    template <typename T> T* take(size_t count)
+    {
+        off = align_up(off);
+        T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+        off += count * sizeof(T);
+        return p;
+    }
+    size_t size() const { return align_up(off) + ALIGN; }
+};
+
+// ---- geometry state: P Gaussians --------------------------------------------------------------------------
+struct GeomState {
+    float2* means2D;          // pixel-space centre (forward.cu:699)
+    float4* conic_opacity;    // conic.xyz + opacity (forward.cu:701)
+    float4* rgb;              // SH colour (or colors_precomp), .w unused — 16-B gathers in render
+    float* depths;            // lonlat: |t| (forward.cu:697), pinhole: t.z (:334)
+    uint8_t* clamped;         // bit c set if channel c was clamped (forward.cu:79-81)
+    uint32_t* tiles_touched;  // rect area (forward.cu:702)
+    uint32_t* key_a;          // depth sort ping-pong keys (float bits of depth; culled -> 0xFFFFFFFF)
+    uint32_t* key_b;
+    uint32_t* val_a;          // depth sort ping-pong values (Gaussian index)
+    uint32_t* val_b;
+    uint32_t* hist;           // radix histograms [RADIX][blocks]
+    uint32_t* scan_partials;  // scan block sums
+    uint32_t* offsets;        // inclusive scan of tiles_touched in depth order
+    uint32_t* emit_off;       // per Gaussian (by index): first instance slot in emission order
+    uint32_t* counters;       // [0] = num_rendered
+    uint32_t* order;          // depth order (points at val_a or val_b after the sort)
+    int* internal_radii;      // used when the caller passes radii == NULL (rasterizer_impl.cu:284-287)
+
+    static size_t carve(char* base, size_t P, GeomState* s);
+};
+
+// ---- image state: N pixels, T tiles ------------------------------------------------------------------------
+struct ImageState {
+    float* final_T;     // accum_alpha in the reference (rasterizer_impl.cu:222)
+    uint32_t* n_contrib;
+    uint2* ranges;      // [T] (the reference allocates N, uses T)
+    static size_t carve(char* base, size_t N, size_t T, ImageState* s);
+};
+
+// ---- binning state: L instances ----------------------------------------------------------------------------
+struct BinningState {
+    uint32_t* key_a;       // tile id ping-pong
+    uint32_t* key_b;
+    uint32_t* val_a;       // Gaussian index ping-pong
+    uint32_t* val_b;
+    uint32_t* hist;        // radix histograms
+    uint32_t* scan_partials;
+    float* inst_grad;      // [L][GRAD_ROW] backward scratch, indexed by emission slot
+    uint32_t* point_list;  // sorted Gaussian indices (points at val_a or val_b)
+    uint32_t* point_keys;  // sorted tile ids
+    static size_t carve(char* base, size_t L, GeomState* unused, BinningState* s, int tile_passes);
+};
+
+// number of 8-bit passes needed for tile ids < T (rasterizer_impl.cu:651: sort end bit = 32 + getHigherMsb(T))
+inline uint32_t getHigherMsb(uint32_t n)  // rasterizer_impl.cu:47-62
+{
+    uint32_t msb = sizeof(n) * 4;
+    uint32_t step = msb;
+    while (step > 1) {
+        step /= 2;
+        if (n >> msb) msb += step;
+        else msb -= step;
+    }
+    if (n >> msb) msb++;
+    return msb;
+}
+inline int tile_sort_passes(uint32_t T) { return (int)div_up(getHigherMsb(T), RADIX_BITS); }
+
+// ---- device helpers ----------------------------------------------------------------------------------------
+#if defined(__HIPCC__)
+
+__device__ __forceinline__ float3 transformPoint4x3(const float3& p, const float* m)  // auxiliary.h:85-93
+{
+    return {m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+            m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]};
+}
+__device__ __forceinline__ float4 transformPoint4x4(const float3& p, const float* m)  // auxiliary.h:95-104
+{
+    return {m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+            m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14], m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15]};
+}
+__device__ __forceinline__ float3 transformVec4x3Transpose(const float3& p, const float* m)  // auxiliary.h:116-124
+{
+    return {m[0] * p.x + m[1] * p.y + m[2] * p.z, m[4] * p.x + m[5] * p.y + m[6] * p.z,
+            m[8] * p.x + m[9] * p.y + m[10] * p.z};
+}
+__device__ __forceinline__ float ndc2Pix(float v, int S)  // auxiliary.h:51-54 (double arithmetic)
+{
+    return (float)((((double)v + 1.0) * S - 1.0) * 0.5);
+}
+// auxiliary.h:56-66; returns rect in tiles, clamped to the grid
+__device__ __forceinline__ void getRect(float2 p, int max_radius, uint32_t gx, uint32_t gy, uint32_t& x0, uint32_t& y0,
+                                        uint32_t& x1, uint32_t& y1)
+{
+    const float r = (float)max_radius;
+    x0 = min(gx, (uint32_t)max(0, (int)((p.x - r) / (float)BLOCK_X)));
+    y0 = min(gy, (uint32_t)max(0, (int)((p.y - r) / (float)BLOCK_Y)));
+    // ((p.x + r) + 16) - 1: the reference's macro arithmetic, evaluated left to right in float
+    x1 = min(gx, (uint32_t)max(0, (int)((p.x + r + (float)BLOCK_X - 1.0f) / (float)BLOCK_X)));
+    y1 = min(gy, (uint32_t)max(0, (int)((p.y + r + (float)BLOCK_Y - 1.0f) / (float)BLOCK_Y)));
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+// number of set bits of `mask` below this lane
+__device__ __forceinline__ uint32_t mask_rank(uint64_t mask)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+#endif  // __HIPCC__
+
+}  // namespace omr

@@ -1,0 +1,224 @@
+// render_bwd.hip — per-tile back-to-front gradient replay, gfx950.
+//
+// Follows cuda_rasterizer/backward.cu:671-843 (renderCUDA backward) for the per-pixel arithmetic: T is
+// recovered by division, accum_rec / last_alpha / last_color carry the colour behind each instance, and the
+// background term uses T_final.
+//
+// What is different, and why (MI355X):
+//  * The reference issues 9 float atomicAdds per contributing (pixel, Gaussian) pair into per-Gaussian
+//    arrays. On MI355X float atomics run at ~1.3 TB/s chip-wide and ~17x slower still when the 64 lanes of
+//    an instruction hit 64 different rows (MI355X_MICROARCH.md, Global float atomics) — that would bound the
+//    kernel. Here each wave64 sums its 64 pixels' contributions with a 6-step DPP reduction (only when at
+//    least one lane contributes), the 4 waves' partials are combined in LDS, and ONE 36-B row per
+//    (tile, Gaussian) instance is stored with plain stores, indexed by the instance's emission slot. The
+//    per-Gaussian kernel (gaussian_bwd.hip) then sums each Gaussian's rows in a fixed order. No atomics:
+//    gradients are bitwise reproducible run to run.
+//  * Instances behind the last contributor of every pixel in the tile are skipped outright (the reference
+//    walks them and skips per pixel: contributor >= last_contributor); their rows are zero-filled.
+//  * XCD-aware tile order, as in the forward.
+#include "kernels.h"
+
+namespace omr {
+
+namespace {
+
+constexpr int BATCH = 128;
+constexpr int WAVES = BLOCK_SIZE / 64;
+
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t orig, uint32_t nwg)
+{
+    const uint32_t q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dpp(float v)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf, false));
+}
+
+// sum over the 64 lanes; the total lands in lane 63 (other lanes hold partial sums)
+__device__ __forceinline__ float wave_sum_lane63(float v)
+{
+    v += dpp<0xb1>(v);        // quad_perm [1,0,3,2]
+    v += dpp<0x4e>(v);        // quad_perm [2,3,0,1]
+    v += dpp<0x114>(v);       // row_shr:4
+    v += dpp<0x118>(v);       // row_shr:8
+    v += dpp<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+    v += dpp<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
+__device__ __forceinline__ uint32_t block_max(uint32_t v, uint32_t* s_tmp)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    if ((threadIdx.x & 63) == 0) s_tmp[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint32_t m = s_tmp[0];
+#pragma unroll
+    for (int k = 1; k < WAVES; ++k) m = max(m, s_tmp[k]);
+    __syncthreads();
+    return m;
+}
+
+// emission slot of Gaussian gid's instance on tile (tx, ty): slots are emitted row-major over its rect
+__device__ __forceinline__ uint32_t instance_slot(const RenderBwdArgs& a, uint32_t gid, uint32_t tx, uint32_t ty)
+{
+    uint32_t x0, y0, x1, y1;
+    getRect(a.means2D[gid], a.radii[gid], a.gx, a.gy, x0, y0, x1, y1);
+    return a.emit_off[gid] + (ty - y0) * (x1 - x0) + (tx - x0);
+}
+
+__global__ __launch_bounds__(BLOCK_SIZE) void render_bwd_kernel(RenderBwdArgs a)
+{
+    __shared__ float2 s_xy[BATCH];
+    __shared__ float4 s_co[BATCH];
+    __shared__ float4 s_rgb[BATCH];
+    __shared__ uint32_t s_slot[BATCH];
+    __shared__ float s_part[WAVES][BATCH][GRAD_ROW];
+    __shared__ uint32_t s_tmp[WAVES];
+
+    const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
+    const uint32_t tx = tile % a.gx, ty = tile / a.gx;
+    const uint32_t t = threadIdx.x;
+    const uint32_t lane = t & 63, w = t >> 6;
+    const uint32_t px = tx * BLOCK_X + (t & (BLOCK_X - 1));
+    const uint32_t py = ty * BLOCK_Y + (t / BLOCK_X);
+    const bool inside = px < (uint32_t)a.W && py < (uint32_t)a.H;
+    const uint32_t pix_id = a.W * py + px;
+    const float pxf = (float)px, pyf = (float)py;
+    const size_t plane = (size_t)a.H * a.W;
+
+    const uint2 range = a.ranges[tile];
+    const uint32_t n = range.y - range.x;
+    const float T_final = inside ? a.final_T[pix_id] : 0.f;
+    const uint32_t last_contributor = inside ? a.n_contrib[pix_id] : 0u;
+    float dpix0 = 0.f, dpix1 = 0.f, dpix2 = 0.f;
+    if (inside) {
+        dpix0 = a.dL_dpix[pix_id];
+        dpix1 = a.dL_dpix[plane + pix_id];
+        dpix2 = a.dL_dpix[2 * plane + pix_id];
+    }
+    const float bg_dot = a.bg[0] * dpix0 + a.bg[1] * dpix1 + a.bg[2] * dpix2;
+    const float ddelx_dx = (float)(0.5 * a.W);
+    const float ddely_dy = (float)(0.5 * a.H);
+
+    // instances at positions >= max_c are behind every pixel's last contributor
+    const uint32_t max_c = min(n, block_max(last_contributor, s_tmp));
+    for (uint32_t k = max_c + t; k < n; k += BLOCK_SIZE) {
+        const uint32_t gid = a.point_list[range.x + k];
+        float* row = a.inst_grad + (size_t)instance_slot(a, gid, tx, ty) * GRAD_ROW;
+#pragma unroll
+        for (int c = 0; c < GRAD_ROW; ++c) row[c] = 0.f;
+    }
+
+    float T = T_final;
+    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;  // accum_rec
+    float last_alpha = 0.f;
+    float lc0 = 0.f, lc1 = 0.f, lc2 = 0.f;  // last_color
+
+    // walk positions max_c-1 .. 0 in batches of BATCH, back to front
+    for (int hi = (int)max_c; hi > 0; hi -= BATCH) {
+        const int lo = max(0, hi - BATCH);
+        const int cnt = hi - lo;
+        // batch entry j <-> position hi-1-j
+        if ((int)t < cnt) {
+            const uint32_t pos = (uint32_t)(hi - 1 - (int)t);
+            const uint32_t gid = a.point_list[range.x + pos];
+            s_xy[t] = a.means2D[gid];
+            s_co[t] = a.conic_opacity[gid];
+            s_rgb[t] = a.rgb[gid];
+            s_slot[t] = instance_slot(a, gid, tx, ty);
+        }
+        __syncthreads();
+        for (int j = 0; j < cnt; ++j) {
+            const uint32_t pos = (uint32_t)(hi - 1 - j);
+            float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f;
+            bool contrib = false;
+            if (pos < last_contributor) {  // reference: skip if contributor >= last_contributor
+                const float2 xy = s_xy[j];
+                const float4 co = s_co[j];
+                const float dx = xy.x - pxf, dy = xy.y - pyf;
+                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                if (power <= 0.0f) {
+                    const float G = __expf(power);
+                    const float alpha = fminf(0.99f, co.w * G);
+                    if (alpha >= 1.0f / 255.0f) {
+                        contrib = true;
+                        const float one_m_a = 1.f - alpha;
+                        T = __fdividef(T, one_m_a);
+                        const float dchannel_dcolor = alpha * T;
+                        const float4 c = s_rgb[j];
+                        acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
+                        acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
+                        acc2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
+                        lc0 = c.x;
+                        lc1 = c.y;
+                        lc2 = c.z;
+                        float dL_dalpha = (c.x - acc0) * dpix0 + (c.y - acc1) * dpix1 + (c.z - acc2) * dpix2;
+                        g6 = dchannel_dcolor * dpix0;
+                        g7 = dchannel_dcolor * dpix1;
+                        g8 = dchannel_dcolor * dpix2;
+                        dL_dalpha *= T;
+                        last_alpha = alpha;
+                        dL_dalpha += __fdividef(-T_final, one_m_a) * bg_dot;
+                        const float dL_dG = co.w * dL_dalpha;
+                        const float gdx = G * dx;
+                        const float gdy = G * dy;
+                        const float dG_ddelx = -gdx * co.x - gdy * co.y;
+                        const float dG_ddely = -gdy * co.z - gdx * co.y;
+                        g0 = dL_dG * dG_ddelx * ddelx_dx;
+                        g1 = dL_dG * dG_ddely * ddely_dy;
+                        g2 = -0.5f * gdx * dx * dL_dG;
+                        g3 = -0.5f * gdx * dy * dL_dG;
+                        g4 = -0.5f * gdy * dy * dL_dG;
+                        g5 = G * dL_dalpha;
+                    }
+                }
+            }
+            float* part = s_part[w][j];
+            if (__ballot(contrib) != 0ull) {
+                g0 = wave_sum_lane63(g0);
+                g1 = wave_sum_lane63(g1);
+                g2 = wave_sum_lane63(g2);
+                g3 = wave_sum_lane63(g3);
+                g4 = wave_sum_lane63(g4);
+                g5 = wave_sum_lane63(g5);
+                g6 = wave_sum_lane63(g6);
+                g7 = wave_sum_lane63(g7);
+                g8 = wave_sum_lane63(g8);
+                if (lane == 63) {
+                    part[0] = g0; part[1] = g1; part[2] = g2; part[3] = g3; part[4] = g4;
+                    part[5] = g5; part[6] = g6; part[7] = g7; part[8] = g8;
+                }
+            } else if (lane == 63) {
+#pragma unroll
+                for (int c = 0; c < GRAD_ROW; ++c) part[c] = 0.f;
+            }
+        }
+        __syncthreads();
+        if ((int)t < cnt) {
+            float* row = a.inst_grad + (size_t)s_slot[t] * GRAD_ROW;
+#pragma unroll
+            for (int c = 0; c < GRAD_ROW; ++c) {
+                float v = s_part[0][t][c];
+#pragma unroll
+                for (int q = 1; q < WAVES; ++q) v += s_part[q][t][c];
+                row[c] = v;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+void launch_render_backward(const RenderBwdArgs& a, hipStream_t s)
+{
+    const uint32_t T = a.gx * a.gy;
+    if (T == 0) return;
+    render_bwd_kernel<<<T, BLOCK_SIZE, 0, s>>>(a);
+}
+
+}  // namespace omr

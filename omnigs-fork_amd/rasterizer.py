@@ -1,0 +1,348 @@
+"""Python host mirror of the OmniGS rasterizer boundary, on the gfx950 C ABI (include/omnigs_raster.h).
+
+Mirrors, name for name and argument for argument:
+  * include/rasterize_points.h:29-80      -> RasterizeGaussiansCUDA / RasterizeGaussiansBackwardCUDA / markVisible
+  * include/gaussian_rasterizer.h:32-141  -> GaussianRasterizationSettings / GaussianRasterizerFunction /
+    src/gaussian_rasterizer.cpp:24-223       rasterize_gaussians / GaussianRasterizer
+
+PyTorch here is plumbing only: it owns device memory (the three scratch byte tensors, outputs) and the current
+HIP stream. All compute runs in libomnigs_raster.so. There is no CPU fallback: if the HIP library is missing
+or a tensor is not on a HIP device, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+
+CAMERA_PINHOLE = 1
+CAMERA_LONLAT = 3
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libomnigs_raster.so")
+_ALLOC_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_size_t)
+_lib = None
+
+
+class RasterizerError(RuntimeError):
+    pass
+
+
+def lib() -> C.CDLL:
+    """Load libomnigs_raster.so (built by __graft_entry__.build() / `make -C omnigs-fork_amd/csrc`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RasterizerError(f"HIP rasterizer library not built: {LIB_PATH} (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        vp, i, f, b, sz = C.c_void_p, C.c_int, C.c_float, C.c_bool, C.c_size_t
+        L.omr_last_error.restype = C.c_char_p
+        L.omr_abi_version.restype = i
+        L.omr_rasterizer_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
+        L.omr_lonlat_mark_visible.argtypes = [i, vp, vp]
+        allocs = [_ALLOC_FN, vp, _ALLOC_FN, vp, _ALLOC_FN, vp]
+        L.omr_rasterizer_forward.argtypes = allocs + [i, i, i, vp, i, i, vp, vp, vp, vp, vp, f, vp, vp, vp, vp, vp, f, f,
+                                                      b, vp, vp, b, vp, C.POINTER(i)]
+        L.omr_lonlat_forward.argtypes = allocs + [i, i, i, vp, i, i, vp, vp, vp, vp, vp, f, vp, vp, vp, vp, b, vp, vp, vp,
+                                                  C.POINTER(i)]
+        L.omr_rasterizer_backward.argtypes = [i, i, i, i, vp, i, i, vp, vp, vp, vp, f, vp, vp, vp, vp, vp, f, f, vp, vp,
+                                              vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.omr_lonlat_backward.argtypes = [i, i, i, i, vp, i, i, vp, vp, vp, vp, f, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                          vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        for n in ("omr_geometry_bytes",):
+            getattr(L, n).restype = sz
+            getattr(L, n).argtypes = [i]
+        L.omr_image_bytes.restype = sz
+        L.omr_image_bytes.argtypes = [i, i]
+        L.omr_binning_bytes.restype = sz
+        L.omr_binning_bytes.argtypes = [i, i, i]
+        L.omr_debug_point_list.argtypes = [vp, i, i, i, vp, vp]
+        L.omr_debug_ranges.argtypes = [vp, i, i, vp, vp]
+        L.omr_debug_image_state.argtypes = [vp, i, i, vp, vp, vp]
+        L.omr_debug_geometry.argtypes = [vp, i, vp, vp, vp, vp, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().omr_last_error().decode(errors="replace")
+        raise RasterizerError(f"{what} failed (status {rc}): {msg}")
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    """Device pointer of a tensor; None / empty -> NULL ("absent", as data_ptr() of an empty tensor)."""
+    if t is None or t.numel() == 0:
+        return None
+    return t.data_ptr()
+
+
+def _dev_f32(t: Optional[torch.Tensor], name: str) -> Optional[torch.Tensor]:
+    if t is None or t.numel() == 0:
+        return None
+    if t.device.type != "cuda":
+        raise RasterizerError(f"{name} must be on a HIP device (got {t.device}); the rasterizer has no CPU path")
+    if t.dtype != torch.float32:
+        raise RasterizerError(f"{name} must be float32 (got {t.dtype})")
+    return t.contiguous()
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class _ByteBuffer:
+    """Allocation callback backed by a torch uint8 tensor (plays the role of resizeFunctional,
+    src/rasterize_points.cu:41-47)."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.tensor = torch.empty(0, dtype=torch.uint8, device=device)
+
+        def _cb(ctx, nbytes):
+            try:
+                self.tensor = torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
+                return self.tensor.data_ptr()
+            except Exception:  # out of memory -> NULL -> OMR_ERR_ALLOCATION
+                return None
+
+        self.fn = _ALLOC_FN(_cb)
+
+
+def RasterizeGaussiansCUDA(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                           viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                           prefiltered, camera_type=CAMERA_PINHOLE, render_depth=False):
+    """rasterize_points.cu:49-164. Returns (num_rendered, out_color[3,H,W], radii[P] i32, geomBuffer,
+    binningBuffer, imgBuffer)."""
+    if means3D.ndim != 2 or means3D.shape[1] != 3:
+        raise RasterizerError("means3D must have dimensions (num_points, 3)")
+    if camera_type not in (CAMERA_PINHOLE, CAMERA_LONLAT):
+        raise RasterizerError("[CudaRasterizer]Invalid camera_type")
+    dev = means3D.device
+    P, H, W = int(means3D.shape[0]), int(image_height), int(image_width)
+    geom, binning, img = _ByteBuffer(dev), _ByteBuffer(dev), _ByteBuffer(dev)
+    if P == 0:
+        out_color = torch.zeros((3, H, W), dtype=torch.float32, device=dev)
+        radii = torch.zeros((0,), dtype=torch.int32, device=dev)
+        return 0, out_color, radii, geom.tensor, binning.tensor, img.tensor
+    m = _dev_f32(means3D, "means3D")
+    out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)  # every pixel is written
+    radii = torch.empty((P,), dtype=torch.int32, device=dev)  # every Gaussian is written
+    M = int(sh.shape[1]) if sh is not None and sh.numel() != 0 and sh.shape[0] != 0 else 0
+    bg, shc, col, op = (_dev_f32(background, "background"), _dev_f32(sh, "sh"), _dev_f32(colors, "colors"),
+                        _dev_f32(opacity, "opacity"))
+    sc, rot, cov = _dev_f32(scales, "scales"), _dev_f32(rotations, "rotations"), _dev_f32(cov3D_precomp, "cov3D_precomp")
+    vm, pm, cp = _dev_f32(viewmatrix, "viewmatrix"), _dev_f32(projmatrix, "projmatrix"), _dev_f32(campos, "campos")
+    nr = C.c_int(0)
+    L = lib()
+    if camera_type == CAMERA_PINHOLE:
+        rc = L.omr_rasterizer_forward(geom.fn, None, binning.fn, None, img.fn, None, P, int(degree), M, _ptr(bg), W, H,
+                                      _ptr(m), _ptr(shc), _ptr(col), _ptr(op), _ptr(sc), float(scale_modifier),
+                                      _ptr(rot), _ptr(cov), _ptr(vm), _ptr(pm), _ptr(cp), float(tan_fovx),
+                                      float(tan_fovy), bool(prefiltered), out_color.data_ptr(), radii.data_ptr(),
+                                      bool(render_depth), _stream(dev), C.byref(nr))
+    else:
+        rc = L.omr_lonlat_forward(geom.fn, None, binning.fn, None, img.fn, None, P, int(degree), M, _ptr(bg), W, H,
+                                  _ptr(m), _ptr(shc), _ptr(col), _ptr(op), _ptr(sc), float(scale_modifier), _ptr(rot),
+                                  _ptr(cov), _ptr(vm), _ptr(cp), bool(prefiltered), out_color.data_ptr(),
+                                  radii.data_ptr(), _stream(dev), C.byref(nr))
+    _check(rc, "RasterizeGaussiansCUDA")
+    return int(nr.value), out_color, radii, geom.tensor, binning.tensor, img.tensor
+
+
+def RasterizeGaussiansBackwardCUDA(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp,
+                                   viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos,
+                                   geomBuffer, R, binningBuffer, imageBuffer, camera_type=CAMERA_PINHOLE, out=None):
+    """rasterize_points.cu:166-285. Returns (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh,
+    dL_dscales, dL_drotations).
+
+    `out` (extension): optional dict of preallocated, contiguous float32 tensors keyed by those names, written in
+    place (every element is written) — lets a data-parallel host place the gradients inside one flat all-reduce
+    buffer."""
+    if camera_type not in (CAMERA_PINHOLE, CAMERA_LONLAT):
+        raise RasterizerError("[CudaRasterizer]Invalid camera_type")
+    dev = means3D.device
+    P = int(means3D.shape[0])
+    H, W = int(dL_dout_color.shape[1]), int(dL_dout_color.shape[2])
+    M = int(sh.shape[1]) if sh is not None and sh.numel() != 0 and sh.shape[0] != 0 else 0
+    shapes = dict(dL_dmeans2D=(P, 3), dL_dcolors=(P, 3), dL_dopacity=(P, 1), dL_dmeans3D=(P, 3), dL_dcov3D=(P, 6),
+                  dL_dsh=(P, M, 3), dL_dscales=(P, 3), dL_drotations=(P, 4))
+    o = {}
+    for k, shp in shapes.items():
+        t = None if out is None else out.get(k)
+        if t is None:
+            t = (torch.zeros if P == 0 else torch.empty)(shp, dtype=torch.float32, device=dev)
+        elif tuple(t.shape) != shp or not t.is_contiguous() or t.dtype != torch.float32:
+            raise RasterizerError(f"out[{k}] must be a contiguous float32 tensor of shape {shp}")
+        o[k] = t
+    if P != 0:
+        L = lib()
+        args_common = dict(bg=_dev_f32(background, "background"), m=_dev_f32(means3D, "means3D"),
+                           shc=_dev_f32(sh, "sh"), col=_dev_f32(colors, "colors"), sc=_dev_f32(scales, "scales"),
+                           rot=_dev_f32(rotations, "rotations"), cov=_dev_f32(cov3D_precomp, "cov3D_precomp"),
+                           vm=_dev_f32(viewmatrix, "viewmatrix"), cp=_dev_f32(campos, "campos"),
+                           dl=_dev_f32(dL_dout_color, "dL_dout_color"))
+        a = args_common
+        rad = radii.contiguous()
+        gb, bb, ib = geomBuffer.data_ptr(), binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr()
+        if camera_type == CAMERA_PINHOLE:
+            pm = _dev_f32(projmatrix, "projmatrix")
+            rc = L.omr_rasterizer_backward(P, int(degree), M, int(R), _ptr(a["bg"]), W, H, _ptr(a["m"]), _ptr(a["shc"]),
+                                           _ptr(a["col"]), _ptr(a["sc"]), float(scale_modifier), _ptr(a["rot"]),
+                                           _ptr(a["cov"]), _ptr(a["vm"]), _ptr(pm), _ptr(a["cp"]), float(tan_fovx),
+                                           float(tan_fovy), rad.data_ptr(), gb, bb, ib, _ptr(a["dl"]),
+                                           o["dL_dmeans2D"].data_ptr(), None, o["dL_dopacity"].data_ptr(),
+                                           o["dL_dcolors"].data_ptr(), o["dL_dmeans3D"].data_ptr(),
+                                           o["dL_dcov3D"].data_ptr(), _ptr(o["dL_dsh"]), o["dL_dscales"].data_ptr(),
+                                           o["dL_drotations"].data_ptr(), _stream(dev))
+        else:
+            rc = L.omr_lonlat_backward(P, int(degree), M, int(R), _ptr(a["bg"]), W, H, _ptr(a["m"]), _ptr(a["shc"]),
+                                       _ptr(a["col"]), _ptr(a["sc"]), float(scale_modifier), _ptr(a["rot"]),
+                                       _ptr(a["cov"]), _ptr(a["vm"]), _ptr(a["cp"]), rad.data_ptr(), gb, bb, ib,
+                                       _ptr(a["dl"]), o["dL_dmeans2D"].data_ptr(), None, o["dL_dopacity"].data_ptr(),
+                                       o["dL_dcolors"].data_ptr(), o["dL_dmeans3D"].data_ptr(),
+                                       o["dL_dcov3D"].data_ptr(), _ptr(o["dL_dsh"]), o["dL_dscales"].data_ptr(),
+                                       o["dL_drotations"].data_ptr(), None, None, _stream(dev))
+        _check(rc, "RasterizeGaussiansBackwardCUDA")
+    return (o["dL_dmeans2D"], o["dL_dcolors"], o["dL_dopacity"], o["dL_dmeans3D"], o["dL_dcov3D"], o["dL_dsh"],
+            o["dL_dscales"], o["dL_drotations"])
+
+
+def markVisible(means3D, viewmatrix, projmatrix, camera_type=CAMERA_PINHOLE):
+    """rasterize_points.cu:287-319: bool [P]; pinhole = view-space z > 0.2, lonlat = all True."""
+    dev = means3D.device
+    P = int(means3D.shape[0])
+    present = torch.zeros((P,), dtype=torch.bool, device=dev)
+    if P == 0:
+        return present
+    if camera_type == CAMERA_PINHOLE:
+        m, vm, pm = _dev_f32(means3D, "means3D"), _dev_f32(viewmatrix, "viewmatrix"), _dev_f32(projmatrix, "projmatrix")
+        rc = lib().omr_rasterizer_mark_visible(P, _ptr(m), _ptr(vm), _ptr(pm), present.data_ptr(), _stream(dev))
+    elif camera_type == CAMERA_LONLAT:
+        rc = lib().omr_lonlat_mark_visible(P, present.data_ptr(), _stream(dev))
+    else:
+        raise RasterizerError("[CudaRasterizer]Invalid camera_type")
+    _check(rc, "markVisible")
+    return present
+
+
+# --------------------------------------------------------------------------------------------------------------
+# Autograd glue: include/gaussian_rasterizer.h:32-141, src/gaussian_rasterizer.cpp:24-223
+# --------------------------------------------------------------------------------------------------------------
+@dataclass
+class GaussianRasterizationSettings:
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    bg: torch.Tensor
+    scale_modifier: float
+    viewmatrix: torch.Tensor
+    projmatrix: torch.Tensor
+    RwcT: Optional[torch.Tensor]
+    sh_degree: int
+    campos: torch.Tensor
+    prefiltered: bool
+    camera_type: int = CAMERA_PINHOLE
+    render_depth: bool = False
+
+
+class GaussianRasterizerFunction(torch.autograd.Function):
+    """gaussian_rasterizer.cpp:35-171."""
+
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, settings):
+        s = settings
+        num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer = RasterizeGaussiansCUDA(
+            s.bg, means3D, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
+            s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
+            s.campos, s.prefiltered, int(s.camera_type), s.render_depth)
+        ctx.settings = s
+        ctx.num_rendered = num_rendered
+        ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,
+                              binningBuffer, imgBuffer)
+        ctx.mark_non_differentiable(radii)
+        return color, radii
+
+    @staticmethod
+    def backward(ctx, grad_out_color, grad_radii):
+        s = ctx.settings
+        colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer, binningBuffer, imgBuffer = \
+            ctx.saved_tensors
+        g = RasterizeGaussiansBackwardCUDA(s.bg, means3D, radii, colors_precomp, scales, rotations, s.scale_modifier,
+                                           cov3Ds_precomp, s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy,
+                                           grad_out_color.contiguous(), sh, s.sh_degree, s.campos, geomBuffer,
+                                           ctx.num_rendered, binningBuffer, imgBuffer, int(s.camera_type))
+        dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot = g
+        # gaussian_rasterizer.cpp:159-169: (means3D, means2D, sh, colors, opacity, scales, rotations, cov3D, settings)
+        return (dmeans3D, dmeans2D, dsh, dcolors, dopacity, dscales, drot, dcov3D, None)
+
+
+def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, settings):
+    """gaussian_rasterizer.h:87-106."""
+    return GaussianRasterizerFunction.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
+                                            cov3Ds_precomp, settings)
+
+
+class GaussianRasterizer(torch.nn.Module):
+    """gaussian_rasterizer.h:108-141 / gaussian_rasterizer.cpp:24-32, :173-223."""
+
+    def __init__(self, raster_settings: GaussianRasterizationSettings):
+        super().__init__()
+        self.raster_settings = raster_settings
+
+    def markVisibleGaussians(self, positions):
+        with torch.no_grad():
+            s = self.raster_settings
+            return markVisible(positions, s.viewmatrix, s.projmatrix)  # pinhole test, as the reference
+
+    def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
+                cov3D_precomp=None):
+        has_shs, has_col = shs is not None, colors_precomp is not None
+        has_s, has_r, has_cov = scales is not None, rotations is not None, cov3D_precomp is not None
+        if (not has_shs and not has_col) or (has_shs and has_col):
+            raise RasterizerError("Please provide excatly one of either SHs or precomputed colors!")
+        if ((not has_s or not has_r) and not has_cov) or ((has_s or has_r) and has_cov):
+            raise RasterizerError("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!")
+        dev = means3D.device
+        empty = lambda: torch.empty(0, dtype=torch.float32, device=dev)
+        color, radii = rasterize_gaussians(means3D, means2D, shs if has_shs else empty(),
+                                           colors_precomp if has_col else empty(), opacities,
+                                           scales if has_s else empty(), rotations if has_r else empty(),
+                                           cov3D_precomp if has_cov else empty(), self.raster_settings)
+        return color, radii
+
+
+# --------------------------------------------------------------------------------------------------------------
+# Introspection (tests): intermediate state of a forward, read back from the private scratch layout
+# --------------------------------------------------------------------------------------------------------------
+def debug_state(P, R, width, height, geomBuffer, binningBuffer, imgBuffer):
+    dev = geomBuffer.device
+    gx, gy = (width + 15) // 16, (height + 15) // 16
+    N = width * height
+    out = dict(
+        means2D=torch.empty((P, 2), dtype=torch.float32, device=dev),
+        conic_opacity=torch.empty((P, 4), dtype=torch.float32, device=dev),
+        rgb=torch.empty((P, 3), dtype=torch.float32, device=dev),
+        depths=torch.empty((P,), dtype=torch.float32, device=dev),
+        tiles_touched=torch.empty((P,), dtype=torch.int32, device=dev),
+        point_list=torch.empty((max(R, 0),), dtype=torch.int32, device=dev),
+        ranges=torch.empty((gx * gy, 2), dtype=torch.int32, device=dev),
+        final_T=torch.empty((N,), dtype=torch.float32, device=dev),
+        n_contrib=torch.empty((N,), dtype=torch.int32, device=dev),
+    )
+    L, st = lib(), _stream(dev)
+    if P > 0:
+        _check(L.omr_debug_geometry(geomBuffer.data_ptr(), P, out["means2D"].data_ptr(),
+                                    out["conic_opacity"].data_ptr(), out["rgb"].data_ptr(), out["depths"].data_ptr(),
+                                    out["tiles_touched"].data_ptr(), st), "debug_geometry")
+        if R > 0:
+            _check(L.omr_debug_point_list(binningBuffer.data_ptr(), R, width, height, out["point_list"].data_ptr(), st),
+                   "debug_point_list")
+        _check(L.omr_debug_ranges(imgBuffer.data_ptr(), width, height, out["ranges"].data_ptr(), st), "debug_ranges")
+        _check(L.omr_debug_image_state(imgBuffer.data_ptr(), width, height, out["final_T"].data_ptr(),
+                                       out["n_contrib"].data_ptr(), st), "debug_image_state")
+    return out

@@ -1,0 +1,145 @@
+"""ctypes wrapper of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Used by tests/ as the parity checker and fixture generator, and by bench.py's cpu_baseline leg. The product
+(omnigs-fork_amd/) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+_F32 = {"out_color", "depths", "cov3D", "rgb", "final_T", "means2D", "conic_opacity", "dmean2D", "dconic",
+        "dopacity", "dcolor", "dmean3D", "dcov3D", "dsh", "dscale", "drot"}
+_DT = {"clamped": np.uint8, "radii": np.int32, "tiles_touched": np.uint32, "point_offsets": np.uint32,
+       "point_list": np.uint32, "keys": np.uint64, "n_contrib": np.uint32, "ranges": np.uint32}
+
+
+def build() -> str:
+    """Compile oracle/_build/liboracle.so (make) if missing or stale."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        vp, i, f, d = C.c_void_p, C.c_int, C.c_float, C.c_double
+        L.oracle_new.restype = vp
+        L.oracle_new.argtypes = [i]
+        L.oracle_free.argtypes = [vp]
+        common = [i, i, i, vp, i, i, vp, vp, vp, vp, vp]
+        L.oracle_forward_f32.argtypes = [vp] + common + [f, vp, vp, vp, vp, vp, f, f, i, i, i, C.c_char_p, i]
+        L.oracle_forward_f64.argtypes = [vp] + common + [d, vp, vp, vp, vp, vp, d, d, i, i, i, C.c_char_p, i]
+        L.oracle_backward.argtypes = [vp, vp, i]
+        L.oracle_size.restype = C.c_int64
+        L.oracle_size.argtypes = [vp, C.c_char_p, C.POINTER(C.c_int)]
+        L.oracle_get.argtypes = [vp, C.c_char_p, vp]
+        L.oracle_num_rendered.argtypes = [vp]
+        L.oracle_set_threads.argtypes = [i]
+        L.oracle_higher_msb.restype = C.c_uint32
+        L.oracle_higher_msb.argtypes = [C.c_uint32]
+        L.oracle_atan2f.restype = f
+        L.oracle_atan2f.argtypes = [f, f]
+        L.oracle_asinf.restype = f
+        L.oracle_asinf.argtypes = [f]
+        L.oracle_mark_visible.argtypes = [i, vp, vp, vp, i, vp]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class Oracle:
+    """One rasterizer instance (geometry/binning/image state kept between forward and backward)."""
+
+    def __init__(self, double: bool = False):
+        self.double = double
+        self.dtype = np.float64 if double else np.float32
+        self.h = lib().oracle_new(1 if double else 0)
+        self._keep = []
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().oracle_free(self.h)
+        except Exception:
+            pass
+
+    def _arr(self, a):
+        if a is None:
+            return None
+        a = np.ascontiguousarray(a, dtype=self.dtype)
+        self._keep.append(a)
+        return a
+
+    def forward(self, *, background, means3D, opacity, scales=None, rotations=None, shs=None, colors_precomp=None,
+                cov3D_precomp=None, viewmatrix, projmatrix, campos, width, height, sh_degree=3,
+                scale_modifier=1.0, tanfovx=0.0, tanfovy=0.0, prefiltered=False, camera_type=3, render_depth=False):
+        self._keep = []
+        P = int(means3D.shape[0])
+        M = 0 if shs is None or shs.shape[0] == 0 else int(shs.shape[1])
+        args = [self._arr(x) for x in (background, means3D, shs, colors_precomp, opacity, scales)]
+        rest = [self._arr(x) for x in (rotations, cov3D_precomp, viewmatrix, projmatrix, campos)]
+        err = C.create_string_buffer(512)
+        fn = lib().oracle_forward_f64 if self.double else lib().oracle_forward_f32
+        L = fn(self.h, P, int(sh_degree), M, _ptr(args[0]), int(width), int(height), _ptr(args[1]), _ptr(args[2]),
+               _ptr(args[3]), _ptr(args[4]), _ptr(args[5]), scale_modifier, _ptr(rest[0]), _ptr(rest[1]),
+               _ptr(rest[2]), _ptr(rest[3]), _ptr(rest[4]), tanfovx, tanfovy, int(prefiltered), int(camera_type),
+               int(render_depth), err, 512)
+        if L < 0:
+            raise RuntimeError(err.value.decode())
+        self.P, self.M, self.W, self.H = P, M, int(width), int(height)
+        return L
+
+    def get(self, name: str) -> np.ndarray:
+        es = C.c_int(0)
+        n = lib().oracle_size(self.h, name.encode(), C.byref(es))
+        if n < 0:
+            raise KeyError(name)
+        dt = _DT.get(name, self.dtype)
+        out = np.empty(n, dtype=dt)
+        if n:
+            lib().oracle_get(self.h, name.encode(), _ptr(out))
+        return out
+
+    def backward(self, dL_dout: np.ndarray, nthreads: int = 1):
+        d = np.ascontiguousarray(dL_dout, dtype=self.dtype)
+        lib().oracle_backward(self.h, _ptr(d), int(nthreads))
+        P, M = self.P, self.M
+        return dict(dmean2D=self.get("dmean2D").reshape(P, 3), dconic=self.get("dconic").reshape(P, 4),
+                    dopacity=self.get("dopacity").reshape(P, 1), dcolor=self.get("dcolor").reshape(P, 3),
+                    dmean3D=self.get("dmean3D").reshape(P, 3), dcov3D=self.get("dcov3D").reshape(P, 6),
+                    dsh=self.get("dsh").reshape(P, M, 3), dscale=self.get("dscale").reshape(P, 3),
+                    drot=self.get("drot").reshape(P, 4))
+
+    @property
+    def num_rendered(self) -> int:
+        return lib().oracle_num_rendered(self.h)
+
+
+def set_threads(n: int):
+    lib().oracle_set_threads(int(n))
+
+
+def run_scene(g, cam, dL=None, bg=(0.0, 0.0, 0.0), double=False, nthreads=1, **kw):
+    """Convenience: forward (+ backward if dL given) on a scene.Gaussians / scene.Camera pair."""
+    o = Oracle(double)
+    L = o.forward(background=np.asarray(bg, dtype=np.float64), means3D=g.means3D, opacity=g.opacity,
+                  scales=kw.pop("scales", g.scales), rotations=kw.pop("rotations", g.rotations),
+                  shs=kw.pop("shs", g.shs), viewmatrix=cam.viewmatrix, projmatrix=cam.projmatrix, campos=cam.campos,
+                  width=cam.width, height=cam.height, sh_degree=kw.pop("sh_degree", g.sh_degree),
+                  tanfovx=cam.tanfovx, tanfovy=cam.tanfovy, camera_type=cam.camera_type, **kw)
+    grads = o.backward(dL, nthreads) if dL is not None else None
+    return o, L, grads

@@ -1,0 +1,86 @@
+"""Shared test helpers: run the same scene through the oracle (CPU, test infrastructure) and the HIP path."""
+from __future__ import annotations
+
+import numpy as np
+
+import _omnigs
+
+omr = _omnigs.load()
+scene = omr.scene
+
+
+def make_case(P, width, height, camera_type, seed, view_index=0, sh_degree=3, spread=None):
+    """Seeded synthetic scene. `spread` rescales the distance range (small images want fewer, bigger Gaussians)."""
+    g = scene.make_gaussians(P, seed)
+    if spread is not None:
+        g.scales = (g.scales * spread).astype(np.float32)
+    g.sh_degree = sh_degree
+    cam = scene.make_camera(camera_type, width, height, view_index)
+    dL = scene.upstream_grad(height, width, seed + 1000)
+    return g, cam, dL
+
+
+def oracle_run(g, cam, dL=None, bg=(0.0, 0.0, 0.0), double=False, colors_precomp=None, cov3D_precomp=None,
+               render_depth=False, prefiltered=False):
+    import oracle as O
+
+    o = O.Oracle(double)
+    use_cov = cov3D_precomp is not None
+    use_col = colors_precomp is not None
+    L = o.forward(background=np.asarray(bg, dtype=np.float64), means3D=g.means3D, opacity=g.opacity,
+                  scales=None if use_cov else g.scales, rotations=None if use_cov else g.rotations,
+                  shs=None if use_col else g.shs, colors_precomp=colors_precomp, cov3D_precomp=cov3D_precomp,
+                  viewmatrix=cam.viewmatrix, projmatrix=cam.projmatrix, campos=cam.campos, width=cam.width,
+                  height=cam.height, sh_degree=g.sh_degree, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
+                  camera_type=cam.camera_type, render_depth=render_depth, prefiltered=prefiltered)
+    grads = o.backward(dL) if dL is not None else None
+    return o, L, grads
+
+
+def hip_run(g, cam, dL=None, bg=(0.0, 0.0, 0.0), colors_precomp=None, cov3D_precomp=None, render_depth=False,
+            prefiltered=False, device="cuda"):
+    import torch
+
+    R = omr.rasterizer
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(device)
+    use_cov = cov3D_precomp is not None
+    use_col = colors_precomp is not None
+    empty = torch.empty(0, device=device)
+    bg_t = t(np.asarray(bg))
+    args = dict(background=bg_t, means3D=t(g.means3D), colors=t(colors_precomp) if use_col else empty,
+                opacity=t(g.opacity), scales=empty if use_cov else t(g.scales),
+                rotations=empty if use_cov else t(g.rotations), scale_modifier=1.0,
+                cov3D_precomp=t(cov3D_precomp) if use_cov else empty, viewmatrix=t(cam.viewmatrix),
+                projmatrix=t(cam.projmatrix), tan_fovx=cam.tanfovx, tan_fovy=cam.tanfovy, image_height=cam.height,
+                image_width=cam.width, sh=empty if use_col else t(g.shs), degree=g.sh_degree, campos=t(cam.campos),
+                prefiltered=prefiltered, camera_type=cam.camera_type, render_depth=render_depth)
+    num_rendered, color, radii, geomB, binB, imgB = R.RasterizeGaussiansCUDA(**args)
+    out = dict(L=num_rendered, color=color, radii=radii, geom=geomB, binning=binB, img=imgB)
+    out["state"] = R.debug_state(g.P, num_rendered, cam.width, cam.height, geomB, binB, imgB)
+    if dL is not None:
+        grads = R.RasterizeGaussiansBackwardCUDA(
+            bg_t, args["means3D"], radii, args["colors"], args["scales"], args["rotations"], 1.0, args["cov3D_precomp"],
+            args["viewmatrix"], args["projmatrix"], cam.tanfovx, cam.tanfovy, t(dL), args["sh"], g.sh_degree,
+            args["campos"], geomB, num_rendered, binB, imgB, cam.camera_type)
+        names = ["dmean2D", "dcolor", "dopacity", "dmean3D", "dcov3D", "dsh", "dscale", "drot"]
+        out["grads"] = dict(zip(names, grads))
+    import torch as _t
+
+    _t.cuda.synchronize()
+    return out
+
+
+def to_np(x):
+    return x.detach().cpu().numpy()
+
+
+def grad_close(a, b, rtol=1e-3, atol_frac=1e-4):
+    """Per-element |a-b| <= rtol*|b| + atol_frac*max|b| (documented gradient tolerance: north_star 1e-3 rel, with an
+    absolute floor at 1e-4 of the tensor's largest entry for entries that cancel to ~0)."""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    scale = np.abs(b).max() if b.size else 0.0
+    err = np.abs(a - b)
+    lim = rtol * np.abs(b) + atol_frac * scale
+    bad = err > lim
+    return (not bad.any()), (float(err.max()) if err.size else 0.0), int(bad.sum())
