@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json metric: Mpixels/s of one rasterizer forward + backward, 1M Gaussians @ 2048x1024
+equirect (config C), on 1/2/4/8 MI355X (config D: one view per GPU + RCCL all-reduce of the Gaussian gradients).
+
+A "step" = RasterizeGaussiansCUDA + RasterizeGaussiansBackwardCUDA on one view with a fixed upstream gradient
+(BASELINE.md §2), plus, for N > 1, the sum all-reduce of the flat per-Gaussian gradient buffer (236 B/Gaussian).
+Inputs are synthetic (SplitMix64) and resident in HBM before timing starts.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus N --steps K --warmup W
+
+Rank 0 prints ONE JSON line (the driver's contract), with `roofline` for the dominant kernel (HIP events on the
+launch stream over the timed region) and, at N = 1, `cpu_baseline` (the CPU oracle on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, Chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", default="C", help="scene config of omnigs-fork_amd/scene.py (default C)")
+    p.add_argument("--gaussians", type=int, default=None, help="override P (testing only)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-oracle sample budget")
+    p.add_argument("--cpu-threads", type=int, default=None)
+    p.add_argument("--bucket-mb", type=float, default=0.0, help="all-reduce bucket size (0 = one collective)")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    return p.parse_args()
+
+
+def stage_bytes(stage, P, V, L, N, T, M=16, D=3):
+    """Algorithmic HBM bytes of one launch of each stage (SURVEY.md §8(d) accounting)."""
+    sh = 12 * (D + 1) ** 2
+    return {
+        "preprocess": 28 * P + (40 + sh + 45) * V,
+        "depth_sort": 4 * 2 * 8 * P,               # 4 passes x (key+value read + write)
+        "scan": 8 * P,
+        "emit": 8 * P + 12 * V + 8 * L,
+        "tile_sort": 2 * 2 * 8 * L,                # 2 passes x (tile id + index, read + write)
+        "tile_ranges": 4 * L + 16 * T,
+        "render_forward": 40 * L + 20 * N + 8 * T,
+        "render_backward": 40 * L + 20 * N + 8 * T + 88 * V,
+        "gaussian_backward": (12 + 4 + 24 + sh + 28 + 36) * V + (12 + sh + 12 + 16 + 4 + 12 + 12 + 24) * P,
+    }.get(stage, 0)
+
+
+def cpu_baseline(g, cam, dL, seconds, threads):
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # test infrastructure: the CPU restatement, timed as the baseline only
+
+    O.build()
+    O.set_threads(threads)
+    it, t_total = 0, 0.0
+    while t_total < seconds or it == 0:
+        t0 = time.perf_counter()
+        o = O.Oracle(False)
+        o.forward(background=np.zeros(3), means3D=g.means3D, opacity=g.opacity, scales=g.scales,
+                  rotations=g.rotations, shs=g.shs, viewmatrix=cam.viewmatrix, projmatrix=cam.projmatrix,
+                  campos=cam.campos, width=cam.width, height=cam.height, sh_degree=g.sh_degree,
+                  camera_type=cam.camera_type)
+        o.backward(dL, nthreads=threads)
+        t_total += time.perf_counter() - t0
+        it += 1
+        del o
+        if it >= 3:
+            break
+    mpix = cam.width * cam.height * it / t_total / 1e6
+    return {"value": round(mpix, 4), "unit": "Mpixels/s", "cores": threads, "kind": "port",
+            "sample": f"{it} x fwd+bwd of one {cam.width}x{cam.height} view, P={g.P} (same scene as the GPU run), "
+                      f"{t_total:.1f} s, OpenMP over Gaussians/tiles, oracle/ restatement (no CPU reference exists)"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import _omnigs
+
+    omr = _omnigs.load()
+    R, scene, par = omr.rasterizer, omr.scene, omr.parallel
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    info = par.DistInfo(rank, world, local)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    if world != args.gpus and rank == 0:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+
+    # config D is config C's scene rendered one view per GPU: the same Gaussians for every N (weak scaling)
+    cfg_name = "D" if (world > 1 and args.config == "C") else args.config
+    g, cam, dL = scene.config_scene(args.config, view_index=rank % 8, P=args.gaussians)
+    P, W, H = g.P, cam.width, cam.height
+    M = g.shs.shape[1]
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)
+    means3D, opacity, scales, rots, shs = t(g.means3D), t(g.opacity), t(g.scales), t(g.rotations), t(g.shs)
+    view, proj, campos, bg = t(cam.viewmatrix), t(cam.projmatrix), t(cam.campos), torch.zeros(3, device=dev)
+    dL_dout = t(dL)
+    empty = torch.empty(0, device=dev)
+    grads = par.GradBuffer(P, M, dev)
+    out = grads.out_dict(dev)
+    bucket = int(args.bucket_mb * 1024 * 1024)
+    stats = {}
+
+    def step():
+        nr, color, radii, gb, bb, ib = R.RasterizeGaussiansCUDA(
+            bg, means3D, empty, opacity, scales, rots, 1.0, empty, view, proj, cam.tanfovx, cam.tanfovy, H, W, shs,
+            g.sh_degree, campos, False, cam.camera_type, False)
+        R.RasterizeGaussiansBackwardCUDA(bg, means3D, radii, empty, scales, rots, 1.0, empty, view, proj, cam.tanfovx,
+                                         cam.tanfovy, dL_dout, shs, g.sh_degree, campos, gb, nr, bb, ib,
+                                         cam.camera_type, out=out)
+        par.allreduce_(grads, info, average=False, bucket_bytes=bucket)
+        stats["L"] = nr
+        stats["radii"] = radii
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    V = int((stats["radii"] > 0).sum().item()) if args.warmup else None
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    R.profile_reset()
+    R.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    R.profile_enable(False)
+    prof = R.profile_read()
+    if V is None:
+        V = int((stats["radii"] > 0).sum().item())
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * W * H / (elapsed / args.steps) / 1e6
+    L, N = int(stats["L"]), W * H
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+
+    # dominant kernel from the live stage timings (HIP events on the launch stream)
+    stage_avg = {k: (ms / c if c else 0.0) for k, (ms, c) in prof.items()}
+    kernel_stages = ["render_forward", "render_backward", "gaussian_backward", "preprocess"]
+    dom = max(kernel_stages, key=lambda k: stage_avg.get(k, 0.0))
+    dom_bytes = stage_bytes(dom, P, V, L, N, T, M, g.sh_degree)
+    dom_ms = stage_avg[dom]
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            pmc = json.load(f)
+        if pmc.get("config") == cfg_name and pmc.get("P") == P and dom in pmc.get("kernels", {}):
+            traffic = pmc["kernels"][dom].get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    algo_total = sum(stage_bytes(s, P, V, L, N, T, M, g.sh_degree) for s in stage_avg)
+    result = {
+        "metric": "Mpixels/s fwd+bwd, 1M Gaussians @ 2048x1024 equirect; 1/2/4/8 GPU",
+        "value": round(value, 3),
+        "unit": "Mpixels/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (SplitMix64 scene, SURVEY.md §8(d)); random-init Gaussians, fixed dL/dout",
+        "config": {"workload": f"{cfg_name}: {P} Gaussians, {W}x{H} equirect (camera_type=3), SH degree "
+                               f"{g.sh_degree}, one view per GPU" + (", RCCL sum all-reduce of 236 B/Gaussian "
+                                                                    "gradients" if world > 1 else ""),
+                   "P": P, "V": V, "L": L, "N": N, "T": T, "width": W, "height": H,
+                   "parallelism": f"view-parallel dp{world}"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 4),
+                     "step_algorithmic_GBps": round(algo_total / (ms_per_step * 1e-3) / 1e9, 2)},
+        "stages_ms": {k: round(v, 4) for k, v in stage_avg.items()},
+    }
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        try:
+            result["cpu_baseline"] = cpu_baseline(g, cam, dL, args.cpu_seconds, threads)
+        except Exception as ex:  # the GPU number stands on its own; report why the baseline is missing
+            result["cpu_baseline"] = {"value": None, "error": repr(ex)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -109,6 +109,17 @@ size_t omr_geometry_bytes(int P);
 size_t omr_image_bytes(int width, int height);
 size_t omr_binning_bytes(int num_rendered, int width, int height);
 
+/* --- stage timing (HIP events recorded on the launch stream; for bench.py / tools) --------------- */
+/* stages: 0 preprocess, 1 depth_sort, 2 scan, 3 emit, 4 tile_sort, 5 tile_ranges, 6 render_forward,
+ *         7 render_backward, 8 gaussian_backward                                                   */
+#define OMR_NUM_STAGES 9
+void omr_profile_enable(int on);
+void omr_profile_reset(void);
+/* waits for the recorded events; fills total milliseconds and launch counts per stage since the last reset;
+ * returns the number of stages written (<= n) */
+int omr_profile_read(double* total_ms, uint64_t* counts, int n);
+const char* omr_profile_stage_name(int stage);
+
 /* --- introspection for tests / tools (read from the private scratch layout) ---------------------- */
 /* copies the sorted per-instance Gaussian indices (R entries) and tile ranges ([T] uint2) to device dst */
 int omr_debug_point_list(char* binning_buffer, int R, int width, int height, uint32_t* dst, void* stream);

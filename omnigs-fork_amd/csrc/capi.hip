@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/omnigs_raster.h"
 #include "kernels.h"
@@ -38,6 +39,59 @@ int hip_check(const char* where)
         const hipError_t e_ = (call);                                                            \
         if (e_ != hipSuccess) return fail(OMR_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
     } while (0)
+
+// ---- stage profiler: hipEvent pairs on the launch stream, resolved lazily by omr_profile_read -------------
+enum Stage { ST_PREPROCESS, ST_DEPTH_SORT, ST_SCAN, ST_EMIT, ST_TILE_SORT, ST_RANGES, ST_RENDER_FWD, ST_RENDER_BWD,
+             ST_GAUSS_BWD, ST_COUNT };
+const char* kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "scan", "emit", "tile_sort", "tile_ranges",
+                                     "render_forward", "render_backward", "gaussian_backward"};
+
+struct Profiler {
+    bool on = false;
+    struct Rec {
+        int stage;
+        hipEvent_t a, b;
+    };
+    std::vector<Rec> pending;
+    std::vector<hipEvent_t> pool;
+    double total_ms[ST_COUNT] = {};
+    uint64_t count[ST_COUNT] = {};
+    hipEvent_t get()
+    {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        return e;
+    }
+};
+Profiler g_prof;
+
+struct StageScope {
+    int stage;
+    hipStream_t s;
+    hipEvent_t a = nullptr;
+    StageScope(int st, hipStream_t stream) : stage(st), s(stream)
+    {
+        if (g_prof.on) {
+            a = g_prof.get();
+            if (a) (void)hipEventRecord(a, s);
+        }
+    }
+    ~StageScope()
+    {
+        if (a) {
+            hipEvent_t b = g_prof.get();
+            if (b) {
+                (void)hipEventRecord(b, s);
+                g_prof.pending.push_back({stage, a, b});
+            }
+        }
+    }
+};
 
 // pinned host words for the one device->host read of the forward (num_rendered, prefiltered flag)
 uint32_t* pinned_words()
@@ -196,12 +250,12 @@ int forward_impl(const ForwardIn& in)
     pa.radii = radii;
     pa.g = g;
     pa.error_flag = reinterpret_cast<int*>(g.counters + 1);
-    launch_preprocess(in.camera_type, pa, s);
+    { StageScope st_(ST_PREPROCESS, s); launch_preprocess(in.camera_type, pa, s); }
 
     // depth order of the Gaussians (stable: ties keep index order)
-    const int which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, 0, 4, s);
+    int which; { StageScope st_(ST_DEPTH_SORT, s); which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, 0, 4, s); }
     g.order = which ? g.val_b : g.val_a;
-    launch_inclusive_scan(g.tiles_touched, g.order, g.offsets, g.scan_partials, P, s);
+    { StageScope st_(ST_SCAN, s); launch_inclusive_scan(g.tiles_touched, g.order, g.offsets, g.scan_partials, P, s); }
 
     uint32_t* host = pinned_words();
     if (!host) return fail(OMR_ERR_HIP, "hipHostMalloc failed");
@@ -220,10 +274,10 @@ int forward_impl(const ForwardIn& in)
     BinningState b;
     BinningState::carve(bin_base, L, nullptr, &b, tile_passes);
 
-    launch_emit_instances(in.P, g, radii, d.gx, d.gy, b.key_a, b.val_a, s);
-    radix_sort_pairs(b.key_a, b.key_b, b.val_a, b.val_b, b.hist, b.scan_partials, L, 0, tile_passes, s);
+    { StageScope st_(ST_EMIT, s); launch_emit_instances(in.P, g, radii, d.gx, d.gy, b.key_a, b.val_a, s); }
+    { StageScope st_(ST_TILE_SORT, s); radix_sort_pairs(b.key_a, b.key_b, b.val_a, b.val_b, b.hist, b.scan_partials, L, 0, tile_passes, s); }
     OMR_HIP(hipMemsetAsync(im.ranges, 0, d.T * sizeof(uint2), s));
-    launch_tile_ranges(L, b.point_keys, im.ranges, s);
+    { StageScope st_(ST_RANGES, s); launch_tile_ranges(L, b.point_keys, im.ranges, s); }
 
     RenderFwdArgs ra;
     ra.W = in.width; ra.H = in.height; ra.gx = d.gx; ra.gy = d.gy;
@@ -231,7 +285,7 @@ int forward_impl(const ForwardIn& in)
     ra.means2D = g.means2D; ra.conic_opacity = g.conic_opacity; ra.rgb = g.rgb; ra.depths = g.depths;
     ra.bg = in.background; ra.final_T = im.final_T; ra.n_contrib = im.n_contrib; ra.out_color = in.out_color;
     // lonlat never renders depth (rasterize_points.cu:133-156 passes render_depth to the pinhole path only)
-    launch_render_forward(ra, in.render_depth && in.camera_type == CAM_PINHOLE, s);
+    { StageScope st_(ST_RENDER_FWD, s); launch_render_forward(ra, in.render_depth && in.camera_type == CAM_PINHOLE, s); }
     if (int e = hip_check("emit/sort/render")) return e;
     if (in.num_rendered) *in.num_rendered = (int)L;
     return OMR_OK;
@@ -283,7 +337,7 @@ int backward_impl(const BackwardIn& in)
     rb.ranges = im.ranges; rb.point_list = b.point_list; rb.means2D = g.means2D; rb.conic_opacity = g.conic_opacity;
     rb.rgb = g.rgb; rb.radii = radii; rb.emit_off = g.emit_off; rb.bg = in.background;
     rb.final_T = im.final_T; rb.n_contrib = im.n_contrib; rb.dL_dpix = in.dL_dpix; rb.inst_grad = b.inst_grad;
-    launch_render_backward(rb, s);
+    { StageScope st_(ST_RENDER_BWD, s); launch_render_backward(rb, s); }
 
     GaussBwdArgs ga;
     ga.P = in.P; ga.D = in.D; ga.M = in.M; ga.W = in.width; ga.H = in.height;
@@ -297,7 +351,7 @@ int backward_impl(const BackwardIn& in)
     ga.dL_dmean3D = in.dL_dmean3D; ga.dL_dcov3D = in.dL_dcov3D; ga.dL_dsh = in.M > 0 ? in.dL_dsh : nullptr;
     ga.dL_dscale = in.dL_dscale; ga.dL_drot = in.dL_drot; ga.dpx_dt = in.dpx_dt; ga.dpy_dt = in.dpy_dt;
     if (!in.shs) ga.shs = nullptr;
-    launch_gaussian_backward(in.camera_type, ga, s);
+    { StageScope st_(ST_GAUSS_BWD, s); launch_gaussian_backward(in.camera_type, ga, s); }
     return hip_check("backward");
 }
 
@@ -402,6 +456,45 @@ size_t omr_binning_bytes(int num_rendered, int width, int height)
     const Dims d = dims(width, height);
     return BinningState::carve(nullptr, (size_t)std::max(num_rendered, 0), nullptr, nullptr, tile_sort_passes(d.T));
 }
+
+void omr_profile_enable(int on) { g_prof.on = on != 0; }
+
+void omr_profile_reset(void)
+{
+    for (auto& r : g_prof.pending) {
+        (void)hipEventSynchronize(r.b);
+        g_prof.pool.push_back(r.a);
+        g_prof.pool.push_back(r.b);
+    }
+    g_prof.pending.clear();
+    for (int i = 0; i < ST_COUNT; ++i) {
+        g_prof.total_ms[i] = 0.0;
+        g_prof.count[i] = 0;
+    }
+}
+
+int omr_profile_read(double* total_ms, uint64_t* counts, int n)
+{
+    for (auto& r : g_prof.pending) {
+        (void)hipEventSynchronize(r.b);
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+            g_prof.total_ms[r.stage] += ms;
+            g_prof.count[r.stage] += 1;
+        }
+        g_prof.pool.push_back(r.a);
+        g_prof.pool.push_back(r.b);
+    }
+    g_prof.pending.clear();
+    const int m = std::min(n, (int)ST_COUNT);
+    for (int i = 0; i < m; ++i) {
+        if (total_ms) total_ms[i] = g_prof.total_ms[i];
+        if (counts) counts[i] = g_prof.count[i];
+    }
+    return m;
+}
+
+const char* omr_profile_stage_name(int stage) { return (stage >= 0 && stage < ST_COUNT) ? kStageNames[stage] : ""; }
 
 int omr_debug_point_list(char* binning_buffer, int R, int width, int height, uint32_t* dst, void* stream)
 {

@@ -63,6 +63,11 @@ def lib() -> C.CDLL:
         L.omr_debug_ranges.argtypes = [vp, i, i, vp, vp]
         L.omr_debug_image_state.argtypes = [vp, i, i, vp, vp, vp]
         L.omr_debug_geometry.argtypes = [vp, i, vp, vp, vp, vp, vp, vp]
+        L.omr_profile_enable.argtypes = [i]
+        L.omr_profile_read.restype = i
+        L.omr_profile_read.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_uint64), i]
+        L.omr_profile_stage_name.restype = C.c_char_p
+        L.omr_profile_stage_name.argtypes = [i]
         _lib = L
     return _lib
 
@@ -346,3 +351,25 @@ def debug_state(P, R, width, height, geomBuffer, binningBuffer, imgBuffer):
         _check(L.omr_debug_image_state(imgBuffer.data_ptr(), width, height, out["final_T"].data_ptr(),
                                        out["n_contrib"].data_ptr(), st), "debug_image_state")
     return out
+
+
+# --------------------------------------------------------------------------------------------------------------
+# Stage timing: HIP events recorded by the library on the launch stream (omr_profile_*)
+# --------------------------------------------------------------------------------------------------------------
+NUM_STAGES = 9
+
+
+def profile_enable(on: bool = True):
+    lib().omr_profile_enable(1 if on else 0)
+
+
+def profile_reset():
+    lib().omr_profile_reset()
+
+
+def profile_read() -> dict:
+    """{stage_name: (total_ms, launches)} accumulated since the last reset (waits for the recorded events)."""
+    tot = (C.c_double * NUM_STAGES)()
+    cnt = (C.c_uint64 * NUM_STAGES)()
+    n = lib().omr_profile_read(tot, cnt, NUM_STAGES)
+    return {lib().omr_profile_stage_name(i).decode(): (float(tot[i]), int(cnt[i])) for i in range(n)}
