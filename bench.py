@@ -55,7 +55,10 @@ def stage_bytes(stage, P, V, L, N, T, M=16, D=3):
         "tile_ranges": 4 * L + 16 * T,
         "render_forward": 40 * L + 20 * N + 8 * T,
         "render_backward": 40 * L + 20 * N + 8 * T + 88 * V,
-        "gaussian_backward": (12 + 4 + 24 + sh + 28 + 36) * V + (12 + sh + 12 + 16 + 4 + 12 + 12 + 24) * P,
+        "instance_reduce": 8 * P + 36 * L + 36 * V,
+        # reads radii 4P + (grad sums 36, xyz 12, scale 12, rot 16, SH, clamped 1) per visible Gaussian;
+        # writes every gradient output: 3+3+1+3+6+3*M(coeffs)+3+4 floats per Gaussian
+        "gaussian_backward": 4 * P + (36 + 12 + 12 + 16 + sh + 1) * V + (92 + 12 * M) * P,
     }.get(stage, 0)
 
 
@@ -168,7 +171,7 @@ def main():
 
     # dominant kernel from the live stage timings (HIP events on the launch stream)
     stage_avg = {k: (ms / c if c else 0.0) for k, (ms, c) in prof.items()}
-    kernel_stages = ["render_forward", "render_backward", "gaussian_backward", "preprocess"]
+    kernel_stages = ["render_forward", "render_backward", "gaussian_backward", "preprocess", "instance_reduce", "emit"]
     dom = max(kernel_stages, key=lambda k: stage_avg.get(k, 0.0))
     dom_bytes = stage_bytes(dom, P, V, L, N, T, M, g.sh_degree)
     dom_ms = stage_avg[dom]

@@ -111,8 +111,8 @@ size_t omr_binning_bytes(int num_rendered, int width, int height);
 
 /* --- stage timing (HIP events recorded on the launch stream; for bench.py / tools) --------------- */
 /* stages: 0 preprocess, 1 depth_sort, 2 scan, 3 emit, 4 tile_sort, 5 tile_ranges, 6 render_forward,
- *         7 render_backward, 8 gaussian_backward                                                   */
-#define OMR_NUM_STAGES 9
+ *         7 render_backward, 8 gaussian_backward, 9 instance_reduce                                */
+#define OMR_NUM_STAGES 10
 void omr_profile_enable(int on);
 void omr_profile_reset(void);
 /* waits for the recorded events; fills total milliseconds and launch counts per stage since the last reset;

@@ -42,9 +42,9 @@ int hip_check(const char* where)
 
 // ---- stage profiler: hipEvent pairs on the launch stream, resolved lazily by omr_profile_read -------------
 enum Stage { ST_PREPROCESS, ST_DEPTH_SORT, ST_SCAN, ST_EMIT, ST_TILE_SORT, ST_RANGES, ST_RENDER_FWD, ST_RENDER_BWD,
-             ST_GAUSS_BWD, ST_COUNT };
+             ST_GAUSS_BWD, ST_INSTANCE_REDUCE, ST_COUNT };
 const char* kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "scan", "emit", "tile_sort", "tile_ranges",
-                                     "render_forward", "render_backward", "gaussian_backward"};
+                                     "render_forward", "render_backward", "gaussian_backward", "instance_reduce"};
 
 struct Profiler {
     bool on = false;
@@ -126,7 +126,8 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s)
     g.emit_off = c.take<uint32_t>(P);
     g.counters = c.take<uint32_t>(4);
     g.internal_radii = c.take<int>(P);
-    g.order = nullptr;
+    g.grad_sum = c.take<float>(P * GRAD_ROW);
+    g.order = g.val_a;  // the depth sort runs DEPTH_SORT_PASSES (even) passes, so its result lands in val_a
     if (s) *s = g;
     return c.size();
 }
@@ -274,7 +275,7 @@ int forward_impl(const ForwardIn& in)
     BinningState b;
     BinningState::carve(bin_base, L, nullptr, &b, tile_passes);
 
-    { StageScope st_(ST_EMIT, s); launch_emit_instances(in.P, g, radii, d.gx, d.gy, b.key_a, b.val_a, s); }
+    { StageScope st_(ST_EMIT, s); launch_emit_instances(in.P, L, g, radii, d.gx, d.gy, b.key_a, b.val_a, s); }
     { StageScope st_(ST_TILE_SORT, s); radix_sort_pairs(b.key_a, b.key_b, b.val_a, b.val_b, b.hist, b.scan_partials, L, 0, tile_passes, s); }
     OMR_HIP(hipMemsetAsync(im.ranges, 0, d.T * sizeof(uint2), s));
     { StageScope st_(ST_RANGES, s); launch_tile_ranges(L, b.point_keys, im.ranges, s); }
@@ -346,7 +347,11 @@ int backward_impl(const BackwardIn& in)
     ga.projmatrix = in.projmatrix; ga.campos = in.campos; ga.tan_fovx = in.tan_fovx; ga.tan_fovy = in.tan_fovy;
     ga.focal_y = (float)in.height / (2.0f * in.tan_fovy);
     ga.focal_x = (float)in.width / (2.0f * in.tan_fovx);
-    ga.clamped = g.clamped; ga.emit_off = g.emit_off; ga.tiles_touched = g.tiles_touched; ga.inst_grad = b.inst_grad;
+    ga.clamped = g.clamped; ga.grad_sum = g.grad_sum;
+    {
+        StageScope st_(ST_INSTANCE_REDUCE, s);
+        launch_instance_reduce(in.P, g.order, g.offsets, b.inst_grad, g.grad_sum, s);
+    }
     ga.dL_dmean2D = in.dL_dmean2D; ga.dL_dconic = in.dL_dconic; ga.dL_dopacity = in.dL_dopacity; ga.dL_dcolor = in.dL_dcolor;
     ga.dL_dmean3D = in.dL_dmean3D; ga.dL_dcov3D = in.dL_dcov3D; ga.dL_dsh = in.M > 0 ? in.dL_dsh : nullptr;
     ga.dL_dscale = in.dL_dscale; ga.dL_drot = in.dL_drot; ga.dpx_dt = in.dpx_dt; ga.dpy_dt = in.dpy_dt;

@@ -256,17 +256,10 @@ __global__ __launch_bounds__(256) void gaussian_bwd_kernel(GaussBwdArgs a)
         return;
     }
 
-    // 1. sum this Gaussian's instance rows (emission order)
+    // 1. this Gaussian's summed instance rows (instance_reduce_kernel)
     float g[GRAD_ROW];
 #pragma unroll
-    for (int c = 0; c < GRAD_ROW; ++c) g[c] = 0.f;
-    {
-        const uint32_t e0 = a.emit_off[idx], ne = a.tiles_touched[idx];
-        const float* row = a.inst_grad + (size_t)e0 * GRAD_ROW;
-        for (uint32_t e = 0; e < ne; ++e, row += GRAD_ROW)
-#pragma unroll
-            for (int c = 0; c < GRAD_ROW; ++c) g[c] += row[c];
-    }
+    for (int c = 0; c < GRAD_ROW; ++c) g[c] = a.grad_sum[(size_t)idx * GRAD_ROW + c];
     a.dL_dmean2D[3 * idx + 0] = g[0];
     a.dL_dmean2D[3 * idx + 1] = g[1];
     a.dL_dmean2D[3 * idx + 2] = 0.f;
@@ -422,7 +415,88 @@ __global__ __launch_bounds__(256) void gaussian_bwd_kernel(GaussBwdArgs a)
     for (int k = 0; k < 4; ++k) a.dL_drot[4 * idx + k] = dr[k];
 }
 
+// Segmented sum of the per-instance rows. Gaussian order[r] (depth rank r) owns the contiguous emission slots
+// [offsets[r-1], offsets[r]). A 256-thread block owns 256 consecutive ranks and streams their rows in chunks of
+// 256 rows: one row per thread (coalesced 36-B rows), owner found by binary search of the block's offsets in
+// LDS, a wave64 segmented inclusive scan keyed by owner, and each Gaussian adds the scan value at the last row
+// of its segment in every wave it touches — in row order, so the sum is deterministic. Balanced however many
+// tiles a (polar) Gaussian covers. Culled Gaussians are not written (never read downstream).
+constexpr int RED_THREADS = 256;
+
+__global__ __launch_bounds__(RED_THREADS) void instance_reduce_kernel(int P, const uint32_t* order,
+                                                                      const uint32_t* offsets, const float* inst_grad,
+                                                                      float* grad_sum)
+{
+    __shared__ uint32_t s_end[RED_THREADS];  // inclusive scan value (segment end) of each rank in the block
+    __shared__ float s_scan[RED_THREADS][GRAD_ROW + 1];
+    const int t = threadIdx.x;
+    const int r0 = blockIdx.x * RED_THREADS;
+    const int nr = min(RED_THREADS, P - r0);
+    const uint32_t base = r0 == 0 ? 0u : offsets[r0 - 1];
+    if (t < nr) s_end[t] = offsets[r0 + t];
+    __syncthreads();
+    const uint32_t E1 = s_end[nr - 1];
+    const uint32_t my_lo = t == 0 ? base : (t < nr ? s_end[t - 1] : E1);
+    const uint32_t my_hi = t < nr ? s_end[t] : E1;
+    float acc[GRAD_ROW];
+#pragma unroll
+    for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
+    const uint32_t lane = t & 63;
+    for (uint32_t C0 = base; C0 < E1; C0 += RED_THREADS) {
+        const uint32_t e = C0 + t;
+        const bool valid = e < E1;
+        // owner: first local rank with s_end > e
+        int lo = 0, hi = nr;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_end[mid] > e) hi = mid;
+            else lo = mid + 1;
+        }
+        const int key = valid ? lo : -1 - (int)lane;  // invalid lanes never join a segment
+        float x[GRAD_ROW];
+        const float* row = inst_grad + (size_t)e * GRAD_ROW;
+#pragma unroll
+        for (int c = 0; c < GRAD_ROW; ++c) x[c] = valid ? row[c] : 0.f;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int kk = __shfl_up(key, off, 64);
+            const bool same = lane >= (uint32_t)off && kk == key;
+#pragma unroll
+            for (int c = 0; c < GRAD_ROW; ++c) {
+                const float y = __shfl_up(x[c], off, 64);
+                if (same) x[c] += y;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < GRAD_ROW; ++c) s_scan[t][c] = x[c];
+        __syncthreads();
+        // this thread's Gaussian: rows [max(my_lo, C0), min(my_hi, C0 + 256)) -> add the segment tail of each wave
+        uint32_t a = max(my_lo, C0);
+        const uint32_t b = min(my_hi, C0 + RED_THREADS);
+        while (a < b) {
+            const uint32_t wave_end = C0 + ((a - C0) / 64 + 1) * 64;
+            const uint32_t tail = min(b, wave_end) - 1;
+#pragma unroll
+            for (int c = 0; c < GRAD_ROW; ++c) acc[c] += s_scan[tail - C0][c];
+            a = min(b, wave_end);
+        }
+        __syncthreads();
+    }
+    if (t < nr && my_hi > my_lo) {
+        float* out = grad_sum + (size_t)order[r0 + t] * GRAD_ROW;
+#pragma unroll
+        for (int c = 0; c < GRAD_ROW; ++c) out[c] = acc[c];
+    }
+}
+
 }  // namespace
+
+void launch_instance_reduce(int P, const uint32_t* order, const uint32_t* offsets, const float* inst_grad,
+                            float* grad_sum, hipStream_t s)
+{
+    if (P <= 0) return;
+    instance_reduce_kernel<<<div_up(P, RED_THREADS), RED_THREADS, 0, s>>>(P, order, offsets, inst_grad, grad_sum);
+}
 
 void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s)
 {

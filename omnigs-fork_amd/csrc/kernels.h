@@ -39,8 +39,8 @@ size_t radix_hist_size(size_t n);
 // stable LSD radix sort of (key, value) over bits [0, 8*passes); returns which buffer holds the result (0: a, 1: b)
 int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* hist,
                      uint32_t* scan_partials, size_t n, int first_pass, int passes, hipStream_t s);
-void launch_emit_instances(int P, const GeomState& g, const int* radii, uint32_t gx, uint32_t gy, uint32_t* tile_keys,
-                           uint32_t* gauss_vals, hipStream_t s);
+void launch_emit_instances(int P, size_t L, const GeomState& g, const int* radii, uint32_t gx, uint32_t gy,
+                           uint32_t* tile_keys, uint32_t* gauss_vals, hipStream_t s);
 void launch_tile_ranges(size_t L, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s);
 
 // render_fwd.hip
@@ -94,9 +94,7 @@ struct GaussBwdArgs {
     const float* campos;
     float tan_fovx, tan_fovy, focal_x, focal_y;
     const uint8_t* clamped;
-    const uint32_t* emit_off;
-    const uint32_t* tiles_touched;
-    const float* inst_grad;
+    const float* grad_sum;  // [P][GRAD_ROW] per-Gaussian sums of the instance rows (instance_reduce)
     float* dL_dmean2D;   // [P,3]
     float* dL_dconic;    // [P,4] optional (may be null)
     float* dL_dopacity;  // [P]
@@ -110,5 +108,8 @@ struct GaussBwdArgs {
     float* dpy_dt;       // [P,3] optional
 };
 void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s);
+// sums each Gaussian's instance rows (slots [offsets[r-1], offsets[r]) of depth rank r) into grad_sum[order[r]]
+void launch_instance_reduce(int P, const uint32_t* order, const uint32_t* offsets, const float* inst_grad,
+                            float* grad_sum, hipStream_t s);
 
 }  // namespace omr

@@ -72,6 +72,7 @@ struct GeomState {
     uint32_t* counters;       // [0] = num_rendered
     uint32_t* order;          // depth order (points at val_a or val_b after the sort)
     int* internal_radii;      // used when the caller passes radii == NULL (rasterizer_impl.cu:284-287)
+    float* grad_sum;          // [P][GRAD_ROW] backward: per-Gaussian sums of its instance rows
 
     static size_t carve(char* base, size_t P, GeomState* s);
 };
@@ -145,6 +146,31 @@ __device__ __forceinline__ void getRect(float2 p, int max_radius, uint32_t gx, u
     // ((p.x + r) + 16) - 1: the reference's macro arithmetic, evaluated left to right in float
     x1 = min(gx, (uint32_t)max(0, (int)((p.x + r + (float)BLOCK_X - 1.0f) / (float)BLOCK_X)));
     y1 = min(gy, (uint32_t)max(0, (int)((p.y + r + (float)BLOCK_Y - 1.0f) / (float)BLOCK_Y)));
+}
+
+// Which of the four 16x4-pixel bands of tile (tx, ty) (band b = rows 4b..4b+3 = the pixels of wave b of the
+// 256-thread tile workgroup) can see alpha = min(0.99, o * exp(power)) >= 1/255 from this Gaussian.
+// alpha >= 1/255  <=>  q(d) = a dx^2 + 2 b dx dy + c dy^2 <= t = 2 ln(255 o), an ellipse whose half extents are
+// sqrt(t * Sigma_xx), sqrt(t * Sigma_yy) with Sigma = conic^-1. The bound is widened by 1% + 0.01 px so that
+// float rounding of the per-pixel test can never make the mask drop a pixel the reference would blend; a
+// wave whose band is not in the mask provably skips every pixel, so skipping it is result-identical.
+__device__ __forceinline__ uint32_t band_mask(float2 xy, float4 co, uint32_t tx, uint32_t ty)
+{
+    if (!(co.w * 255.0f >= 1.0f)) return 0u;  // even G = 1 gives alpha < 1/255
+    const float det = co.x * co.z - co.y * co.y;
+    if (!(det > 0.0f)) return 0xFu;
+    const float t = 2.0f * __logf(255.0f * co.w);
+    const float ex = sqrtf(fmaxf(t, 0.0f) * (co.z / det)) * 1.01f + 0.01f;
+    const float ey = sqrtf(fmaxf(t, 0.0f) * (co.x / det)) * 1.01f + 0.01f;
+    const float x0 = (float)(tx * BLOCK_X), y0 = (float)(ty * BLOCK_Y);
+    if (xy.x + ex < x0 || xy.x - ex > x0 + (float)(BLOCK_X - 1)) return 0u;
+    uint32_t m = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const float lo = y0 + (float)(4 * b), hi = lo + 3.0f;
+        if (!(xy.y + ey < lo || xy.y - ey > hi)) m |= 1u << b;
+    }
+    return m;
 }
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }

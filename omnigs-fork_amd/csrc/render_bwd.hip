@@ -76,6 +76,7 @@ __global__ __launch_bounds__(BLOCK_SIZE) void render_bwd_kernel(RenderBwdArgs a)
     __shared__ float4 s_co[BATCH];
     __shared__ float4 s_rgb[BATCH];
     __shared__ uint32_t s_slot[BATCH];
+    __shared__ uint32_t s_mask[BATCH];
     __shared__ float s_part[WAVES][BATCH][GRAD_ROW];
     __shared__ uint32_t s_tmp[WAVES];
 
@@ -106,6 +107,10 @@ __global__ __launch_bounds__(BLOCK_SIZE) void render_bwd_kernel(RenderBwdArgs a)
 
     // instances at positions >= max_c are behind every pixel's last contributor
     const uint32_t max_c = min(n, block_max(last_contributor, s_tmp));
+    uint32_t wave_max_c = last_contributor;  // positions >= wave_max_c are skipped by every pixel of this wave
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) wave_max_c = max(wave_max_c, (uint32_t)__shfl_xor((int)wave_max_c, o, 64));
+    const uint32_t wave_bit = 1u << w;
     for (uint32_t k = max_c + t; k < n; k += BLOCK_SIZE) {
         const uint32_t gid = a.point_list[range.x + k];
         float* row = a.inst_grad + (size_t)instance_slot(a, gid, tx, ty) * GRAD_ROW;
@@ -126,14 +131,24 @@ __global__ __launch_bounds__(BLOCK_SIZE) void render_bwd_kernel(RenderBwdArgs a)
         if ((int)t < cnt) {
             const uint32_t pos = (uint32_t)(hi - 1 - (int)t);
             const uint32_t gid = a.point_list[range.x + pos];
-            s_xy[t] = a.means2D[gid];
-            s_co[t] = a.conic_opacity[gid];
+            const float2 xy = a.means2D[gid];
+            const float4 co = a.conic_opacity[gid];
+            s_xy[t] = xy;
+            s_co[t] = co;
             s_rgb[t] = a.rgb[gid];
             s_slot[t] = instance_slot(a, gid, tx, ty);
+            s_mask[t] = band_mask(xy, co, tx, ty);
         }
         __syncthreads();
         for (int j = 0; j < cnt; ++j) {
             const uint32_t pos = (uint32_t)(hi - 1 - j);
+            if (!(s_mask[j] & wave_bit) || pos >= wave_max_c) {  // wave-uniform: nothing of this wave contributes
+                if (lane == 63) {
+#pragma unroll
+                    for (int c = 0; c < GRAD_ROW; ++c) s_part[w][j][c] = 0.f;
+                }
+                continue;
+            }
             float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f;
             bool contrib = false;
             if (pos < last_contributor) {  // reference: skip if contributor >= last_contributor

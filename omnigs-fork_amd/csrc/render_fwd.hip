@@ -9,7 +9,9 @@
 //    features[] from global memory inside the per-pixel loop, forward.cu:447-448);
 //  * blockIdx is remapped so that consecutive tiles (which share most of their Gaussians) run on the same
 //    XCD and hit the same L2 (MI355X: 8 XCDs, blocks b and b+8 share one);
-//  * exp uses the hardware v_exp_f32 path (__expf).
+//  * exp uses the hardware v_exp_f32 path (__expf);
+//  * each staged instance carries a 4-bit mask of the 16x4 wave bands its alpha >= 1/255 ellipse reaches
+//    (band_mask, raster_common.h); a wave skips instances outside its band with one uniform branch.
 // HBM per tile instance: 4 (point_list) + 8 (xy) + 16 (conic/opacity) + 16 (rgb) = 44 B gathered;
 // per pixel: 12 (colour) + 4 (final_T) + 4 (n_contrib) = 20 B written.
 #include "kernels.h"
@@ -31,6 +33,7 @@ __global__ __launch_bounds__(BLOCK_SIZE) void render_fwd_kernel(RenderFwdArgs a)
     __shared__ float2 s_xy[BLOCK_SIZE];
     __shared__ float4 s_co[BLOCK_SIZE];
     __shared__ float4 s_rgb[BLOCK_SIZE];
+    __shared__ uint32_t s_mask[BLOCK_SIZE];
 
     const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
     const uint32_t tx = tile % a.gx, ty = tile / a.gx;
@@ -46,15 +49,19 @@ __global__ __launch_bounds__(BLOCK_SIZE) void render_fwd_kernel(RenderFwdArgs a)
     bool done = !inside;
     float T = 1.0f;
     float C0 = 0.f, C1 = 0.f, C2 = 0.f;
-    uint32_t contributor = 0, last_contributor = 0;
+    uint32_t last_contributor = 0;
+    const uint32_t wave_bit = 1u << (t >> 6);
 
     for (int start = 0; start < n; start += BLOCK_SIZE) {
         if (__syncthreads_count(done) == BLOCK_SIZE) break;
         const int k = start + (int)t;
         if (k < n) {
             const uint32_t gid = a.point_list[range.x + k];
-            s_xy[t] = a.means2D[gid];
-            s_co[t] = a.conic_opacity[gid];
+            const float2 xy = a.means2D[gid];
+            const float4 co = a.conic_opacity[gid];
+            s_xy[t] = xy;
+            s_co[t] = co;
+            s_mask[t] = band_mask(xy, co, tx, ty);
             if (DEPTH) {
                 const float d = a.depths[gid];
                 s_rgb[t] = make_float4(d, d, d, 0.f);
@@ -65,7 +72,7 @@ __global__ __launch_bounds__(BLOCK_SIZE) void render_fwd_kernel(RenderFwdArgs a)
         __syncthreads();
         const int cnt = min(BLOCK_SIZE, n - start);
         for (int j = 0; !done && j < cnt; ++j) {
-            contributor++;
+            if (!(s_mask[j] & wave_bit)) continue;  // wave-uniform: no pixel of this wave can be reached
             const float2 xy = s_xy[j];
             const float4 co = s_co[j];
             const float dx = xy.x - pxf, dy = xy.y - pyf;
@@ -84,7 +91,7 @@ __global__ __launch_bounds__(BLOCK_SIZE) void render_fwd_kernel(RenderFwdArgs a)
             C1 += c.y * w;
             C2 += c.z * w;
             T = test_T;
-            last_contributor = contributor;
+            last_contributor = (uint32_t)(start + j + 1);  // the reference's running contributor count
         }
     }
     if (inside) {

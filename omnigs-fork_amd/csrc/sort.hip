@@ -197,27 +197,47 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_downsweep_kernel(const uin
 }
 
 // ---- instances -------------------------------------------------------------------------------------------
+// first index r in [lo, hi) with offsets[r] > e (offsets = inclusive scan, non-decreasing)
+__device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* offsets, uint32_t lo, uint32_t hi, uint32_t e)
+{
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (offsets[mid] > e) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
 // duplicateWithKeys (rasterizer_impl.cu:94-140) in depth order: Gaussian order[r] owns slots
-// [offsets[r-1], offsets[r]); its tiles are emitted row-major like the reference.
-__global__ __launch_bounds__(256) void emit_kernel(int P, const uint32_t* order, const uint32_t* offsets,
+// [offsets[r-1], offsets[r]) and its tiles are emitted row-major like the reference. One thread per INSTANCE
+// (not per Gaussian as in the reference): writes are fully coalesced and a polar Gaussian spanning hundreds
+// of tiles no longer serialises its wave. The owner of each slot is found by binary search over the scan,
+// narrowed per block to the few Gaussians that own the block's 256 slots.
+__global__ __launch_bounds__(256) void emit_kernel(int P, size_t L, const uint32_t* order, const uint32_t* offsets,
                                                    const float2* means2D, const int* radii, uint32_t gx, uint32_t gy,
                                                    uint32_t* tile_keys, uint32_t* gauss_vals, uint32_t* emit_off)
 {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= P) return;
+    __shared__ uint32_t s_lo, s_hi;
+    const size_t e0 = (size_t)blockIdx.x * blockDim.x;
+    const size_t e = e0 + threadIdx.x;
+    if (threadIdx.x == 0) {
+        const size_t elast = min(L, e0 + blockDim.x) - 1;
+        s_lo = upper_bound_u32(offsets, 0, (uint32_t)P, (uint32_t)e0);
+        s_hi = upper_bound_u32(offsets, s_lo, (uint32_t)P, (uint32_t)elast) + 1;
+    }
+    __syncthreads();
+    if (e >= L) return;
+    const uint32_t r = upper_bound_u32(offsets, s_lo, min(s_hi, (uint32_t)P), (uint32_t)e);
     const uint32_t gid = order[r];
-    uint32_t off = r == 0 ? 0u : offsets[r - 1];
-    emit_off[gid] = off;
-    const int rad = radii[gid];
-    if (rad <= 0) return;
+    const uint32_t start = r == 0 ? 0u : offsets[r - 1];
+    const uint32_t k = (uint32_t)e - start;
+    if (k == 0) emit_off[gid] = start;
     uint32_t x0, y0, x1, y1;
-    getRect(means2D[gid], rad, gx, gy, x0, y0, x1, y1);
-    for (uint32_t y = y0; y < y1; ++y)
-        for (uint32_t x = x0; x < x1; ++x) {
-            tile_keys[off] = y * gx + x;
-            gauss_vals[off] = gid;
-            ++off;
-        }
+    getRect(means2D[gid], radii[gid], gx, gy, x0, y0, x1, y1);
+    const uint32_t w = x1 - x0;
+    const uint32_t ky = k / w;
+    tile_keys[e] = (y0 + ky) * gx + (x0 + (k - ky * w));
+    gauss_vals[e] = gid;
 }
 
 // identifyTileRanges (rasterizer_impl.cu:145-167)
@@ -281,12 +301,12 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
     return cur;
 }
 
-void launch_emit_instances(int P, const GeomState& g, const int* radii, uint32_t gx, uint32_t gy, uint32_t* tile_keys,
-                           uint32_t* gauss_vals, hipStream_t s)
+void launch_emit_instances(int P, size_t L, const GeomState& g, const int* radii, uint32_t gx, uint32_t gy,
+                           uint32_t* tile_keys, uint32_t* gauss_vals, hipStream_t s)
 {
-    if (P <= 0) return;
-    emit_kernel<<<div_up(P, 256), 256, 0, s>>>(P, g.order, g.offsets, g.means2D, radii, gx, gy, tile_keys, gauss_vals,
-                                               g.emit_off);
+    if (P <= 0 || L == 0) return;
+    emit_kernel<<<div_up(L, 256), 256, 0, s>>>(P, L, g.order, g.offsets, g.means2D, radii, gx, gy, tile_keys,
+                                               gauss_vals, g.emit_off);
 }
 
 void launch_tile_ranges(size_t L, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s)

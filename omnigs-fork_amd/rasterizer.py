@@ -356,7 +356,7 @@ def debug_state(P, R, width, height, geomBuffer, binningBuffer, imgBuffer):
 # --------------------------------------------------------------------------------------------------------------
 # Stage timing: HIP events recorded by the library on the launch stream (omr_profile_*)
 # --------------------------------------------------------------------------------------------------------------
-NUM_STAGES = 9
+NUM_STAGES = 10
 
 
 def profile_enable(on: bool = True):
