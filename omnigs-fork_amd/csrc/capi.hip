@@ -14,10 +14,23 @@
 
 #include "../../include/omnigs_raster.h"
 #include "kernels.h"
+#include "wave_ops.h"
 
 namespace omr {
 
 namespace {
+
+// one wave: in [64][9] -> out[9] through the render backward's transposed wave reduction
+__global__ __launch_bounds__(64) void debug_wave_sum_kernel(const float* in, float* out)
+{
+    const uint32_t lane = threadIdx.x;
+    float v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = in[lane * 9 + c];
+    float t8;
+    const float tv = wave_sum8_transposed(v, in[lane * 9 + 8], lane, &t8);
+    if (lane < 9) out[transposed_slot_of_lane(lane)] = lane < 8 ? tv : t8;
+}
 
 thread_local std::string g_last_error;
 
@@ -460,6 +473,13 @@ size_t omr_binning_bytes(int num_rendered, int width, int height)
 {
     const Dims d = dims(width, height);
     return BinningState::carve(nullptr, (size_t)std::max(num_rendered, 0), nullptr, nullptr, tile_sort_passes(d.T));
+}
+
+int omr_debug_wave_sum(const float* in, float* out, void* stream)
+{
+    g_last_error.clear();
+    debug_wave_sum_kernel<<<1, 64, 0, (hipStream_t)stream>>>(in, out);
+    return hip_check("debug_wave_sum");
 }
 
 void omr_profile_enable(int on) { g_prof.on = on != 0; }

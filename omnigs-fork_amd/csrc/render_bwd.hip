@@ -8,15 +8,19 @@
 //  * The reference issues 9 float atomicAdds per contributing (pixel, Gaussian) pair into per-Gaussian
 //    arrays. On MI355X float atomics run at ~1.3 TB/s chip-wide and ~17x slower still when the 64 lanes of
 //    an instruction hit 64 different rows (MI355X_MICROARCH.md, Global float atomics) — that would bound the
-//    kernel. Here each wave64 sums its 64 pixels' contributions with a 6-step DPP reduction (only when at
-//    least one lane contributes), the 4 waves' partials are combined in LDS, and ONE 36-B row per
-//    (tile, Gaussian) instance is stored with plain stores, indexed by the instance's emission slot. The
-//    per-Gaussian kernel (gaussian_bwd.hip) then sums each Gaussian's rows in a fixed order. No atomics:
+//    kernel. Here each wave64 sums its 64 pixels' 9 gradient values in registers: a transposed butterfly
+//    inside each 16-lane DPP row (8 values in 22 DPP-fused VALU ops: each step halves the values a lane
+//    holds), then v_permlane16_swap / v_permlane32_swap across rows (gfx950). The 4 waves' partials are
+//    combined in LDS and ONE 36-B row per (tile, Gaussian) instance is stored with plain stores, indexed by
+//    the instance's emission slot; gaussian_bwd.hip sums each Gaussian's rows in a fixed order. No atomics:
 //    gradients are bitwise reproducible run to run.
-//  * Instances behind the last contributor of every pixel in the tile are skipped outright (the reference
-//    walks them and skips per pixel: contributor >= last_contributor); their rows are zero-filled.
+//  * Per pair the math is predicated (no divergent branches), T is recovered with v_rcp_f32 instead of an
+//    IEEE division sequence, and a wave skips an instance outright when its 16x4 band is outside the
+//    instance's alpha >= 1/255 ellipse (band_mask) or lies behind every pixel's last contributor.
+//  * Instances behind the last contributor of every pixel in the tile are skipped (their rows zero-filled).
 //  * XCD-aware tile order, as in the forward.
 #include "kernels.h"
+#include "wave_ops.h"
 
 namespace omr {
 
@@ -29,24 +33,6 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t orig, uint32_t nwg)
 {
     const uint32_t q = nwg / 8, r = nwg % 8, xcd = orig % 8;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
-}
-
-template <int CTRL, int ROW_MASK = 0xf>
-__device__ __forceinline__ float dpp(float v)
-{
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf, false));
-}
-
-// sum over the 64 lanes; the total lands in lane 63 (other lanes hold partial sums)
-__device__ __forceinline__ float wave_sum_lane63(float v)
-{
-    v += dpp<0xb1>(v);        // quad_perm [1,0,3,2]
-    v += dpp<0x4e>(v);        // quad_perm [2,3,0,1]
-    v += dpp<0x114>(v);       // row_shr:4
-    v += dpp<0x118>(v);       // row_shr:8
-    v += dpp<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
-    v += dpp<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
-    return v;
 }
 
 __device__ __forceinline__ uint32_t block_max(uint32_t v, uint32_t* s_tmp)
@@ -104,6 +90,8 @@ __global__ __launch_bounds__(BLOCK_SIZE) void render_bwd_kernel(RenderBwdArgs a)
     const float bg_dot = a.bg[0] * dpix0 + a.bg[1] * dpix1 + a.bg[2] * dpix2;
     const float ddelx_dx = (float)(0.5 * a.W);
     const float ddely_dy = (float)(0.5 * a.H);
+    // lane (l < 9) of a wave writes value slot slot_of_lane of the wave partial
+    const uint32_t slot_of_lane = transposed_slot_of_lane(lane);
 
     // instances at positions >= max_c are behind every pixel's last contributor
     const uint32_t max_c = min(n, block_max(last_contributor, s_tmp));
@@ -111,6 +99,7 @@ __global__ __launch_bounds__(BLOCK_SIZE) void render_bwd_kernel(RenderBwdArgs a)
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) wave_max_c = max(wave_max_c, (uint32_t)__shfl_xor((int)wave_max_c, o, 64));
     const uint32_t wave_bit = 1u << w;
+
     for (uint32_t k = max_c + t; k < n; k += BLOCK_SIZE) {
         const uint32_t gid = a.point_list[range.x + k];
         float* row = a.inst_grad + (size_t)instance_slot(a, gid, tx, ty) * GRAD_ROW;
@@ -142,75 +131,59 @@ __global__ __launch_bounds__(BLOCK_SIZE) void render_bwd_kernel(RenderBwdArgs a)
         __syncthreads();
         for (int j = 0; j < cnt; ++j) {
             const uint32_t pos = (uint32_t)(hi - 1 - j);
+            float* part = s_part[w][j];
             if (!(s_mask[j] & wave_bit) || pos >= wave_max_c) {  // wave-uniform: nothing of this wave contributes
-                if (lane == 63) {
-#pragma unroll
-                    for (int c = 0; c < GRAD_ROW; ++c) s_part[w][j][c] = 0.f;
-                }
+                if (lane < GRAD_ROW) part[lane] = 0.f;
                 continue;
             }
-            float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f;
-            bool contrib = false;
-            if (pos < last_contributor) {  // reference: skip if contributor >= last_contributor
-                const float2 xy = s_xy[j];
-                const float4 co = s_co[j];
-                const float dx = xy.x - pxf, dy = xy.y - pyf;
-                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                if (power <= 0.0f) {
-                    const float G = __expf(power);
-                    const float alpha = fminf(0.99f, co.w * G);
-                    if (alpha >= 1.0f / 255.0f) {
-                        contrib = true;
-                        const float one_m_a = 1.f - alpha;
-                        T = __fdividef(T, one_m_a);
-                        const float dchannel_dcolor = alpha * T;
-                        const float4 c = s_rgb[j];
-                        acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
-                        acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
-                        acc2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
-                        lc0 = c.x;
-                        lc1 = c.y;
-                        lc2 = c.z;
-                        float dL_dalpha = (c.x - acc0) * dpix0 + (c.y - acc1) * dpix1 + (c.z - acc2) * dpix2;
-                        g6 = dchannel_dcolor * dpix0;
-                        g7 = dchannel_dcolor * dpix1;
-                        g8 = dchannel_dcolor * dpix2;
-                        dL_dalpha *= T;
-                        last_alpha = alpha;
-                        dL_dalpha += __fdividef(-T_final, one_m_a) * bg_dot;
-                        const float dL_dG = co.w * dL_dalpha;
-                        const float gdx = G * dx;
-                        const float gdy = G * dy;
-                        const float dG_ddelx = -gdx * co.x - gdy * co.y;
-                        const float dG_ddely = -gdy * co.z - gdx * co.y;
-                        g0 = dL_dG * dG_ddelx * ddelx_dx;
-                        g1 = dL_dG * dG_ddely * ddely_dy;
-                        g2 = -0.5f * gdx * dx * dL_dG;
-                        g3 = -0.5f * gdx * dy * dL_dG;
-                        g4 = -0.5f * gdy * dy * dL_dG;
-                        g5 = G * dL_dalpha;
-                    }
-                }
+            const float2 xy = s_xy[j];
+            const float4 co = s_co[j];
+            const float dx = xy.x - pxf, dy = xy.y - pyf;
+            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+            const float G = __expf(power);
+            const float alpha = fminf(0.99f, co.w * G);
+            // reference: skip if contributor >= last_contributor, power > 0 or alpha < 1/255
+            const bool contrib = pos < last_contributor && power <= 0.0f && alpha >= 1.0f / 255.0f;
+            if (__ballot(contrib) == 0ull) {
+                if (lane < GRAD_ROW) part[lane] = 0.f;
+                continue;
             }
-            float* part = s_part[w][j];
-            if (__ballot(contrib) != 0ull) {
-                g0 = wave_sum_lane63(g0);
-                g1 = wave_sum_lane63(g1);
-                g2 = wave_sum_lane63(g2);
-                g3 = wave_sum_lane63(g3);
-                g4 = wave_sum_lane63(g4);
-                g5 = wave_sum_lane63(g5);
-                g6 = wave_sum_lane63(g6);
-                g7 = wave_sum_lane63(g7);
-                g8 = wave_sum_lane63(g8);
-                if (lane == 63) {
-                    part[0] = g0; part[1] = g1; part[2] = g2; part[3] = g3; part[4] = g4;
-                    part[5] = g5; part[6] = g6; part[7] = g7; part[8] = g8;
-                }
-            } else if (lane == 63) {
+            const float4 c = s_rgb[j];
+            const float inv = __builtin_amdgcn_rcpf(1.f - alpha);
+            const float Tn = T * inv;
+            const float dchannel_dcolor = alpha * Tn;
+            const float n0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
+            const float n1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
+            const float n2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
+            float dL_dalpha = ((c.x - n0) * dpix0 + (c.y - n1) * dpix1 + (c.z - n2) * dpix2) * Tn;
+            dL_dalpha += (-T_final * inv) * bg_dot;
+            const float dL_dG = co.w * dL_dalpha;
+            const float gdx = G * dx;
+            const float gdy = G * dy;
+            float v[8];
+            v[0] = dL_dG * (-gdx * co.x - gdy * co.y) * ddelx_dx;
+            v[1] = dL_dG * (-gdy * co.z - gdx * co.y) * ddely_dy;
+            v[2] = -0.5f * gdx * dx * dL_dG;
+            v[3] = -0.5f * gdx * dy * dL_dG;
+            v[4] = -0.5f * gdy * dy * dL_dG;
+            v[5] = G * dL_dalpha;
+            v[6] = dchannel_dcolor * dpix0;
+            v[7] = dchannel_dcolor * dpix1;
+            float v8 = dchannel_dcolor * dpix2;
 #pragma unroll
-                for (int c = 0; c < GRAD_ROW; ++c) part[c] = 0.f;
-            }
+            for (int q = 0; q < 8; ++q) v[q] = contrib ? v[q] : 0.f;
+            v8 = contrib ? v8 : 0.f;
+            T = contrib ? Tn : T;
+            acc0 = contrib ? n0 : acc0;
+            acc1 = contrib ? n1 : acc1;
+            acc2 = contrib ? n2 : acc2;
+            lc0 = contrib ? c.x : lc0;
+            lc1 = contrib ? c.y : lc1;
+            lc2 = contrib ? c.z : lc2;
+            last_alpha = contrib ? alpha : last_alpha;
+            float t8;
+            const float tv = wave_sum8_transposed(v, v8, lane, &t8);
+            if (lane < GRAD_ROW) part[slot_of_lane] = lane < 8 ? tv : t8;
         }
         __syncthreads();
         if ((int)t < cnt) {

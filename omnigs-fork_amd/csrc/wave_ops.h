@@ -1,0 +1,66 @@
+// wave_ops.h — wave64 cross-lane reductions for gfx950 (DPP + v_permlane{16,32}_swap).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace omr {
+
+// v + (value of lane given by the DPP control); bound_ctrl: out-of-row sources read 0
+template <int CTRL>
+__device__ __forceinline__ float add_dpp(float keep, float send)
+{
+    return keep + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), CTRL, 0xf, 0xf, true));
+}
+constexpr int DPP_XOR1 = 0xb1;   // quad_perm [1,0,3,2]
+constexpr int DPP_XOR2 = 0x4e;   // quad_perm [2,3,0,1]
+constexpr int DPP_ROR4 = 0x124;  // row_ror:4
+constexpr int DPP_ROR8 = 0x128;  // row_ror:8
+
+// Sum over the four 16-lane rows: x(lane) + x(lane^16) + x(lane^32) + x(lane^48). v_permlane16_swap swaps the
+// odd rows of its first operand with the even rows of its second; with both operands = x, vdst' + src' =
+// own + partner on every lane (likewise v_permlane32_swap for the two halves). Inline asm: ROCm 7.2 folds
+// __builtin_amdgcn_permlane16_swap(x, x) into "2 * first result" (seen in the .s), which is wrong. The
+// s_nop 1 covers the VALU-write -> permlane-read hazard, which hipcc does not pad inside asm.
+__device__ __forceinline__ float cross_row_sum(float x)
+{
+    float a = x, b = x;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    x = a + b;
+    a = x;
+    b = x;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    return a + b;
+}
+
+// Wave-sum of v[0..7] and v8. Returns, in lane l (l < 8), the wave total of value index bitrev3(l); v8 total
+// is returned in *t8 on every lane.
+__device__ __forceinline__ float wave_sum8_transposed(const float v[8], float v8, uint32_t lane, float* t8)
+{
+    const bool b0 = lane & 1, b1 = (lane >> 1) & 1, b2 = (lane >> 2) & 1;
+    float a[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = add_dpp<DPP_XOR1>(b0 ? v[i + 4] : v[i], b0 ? v[i] : v[i + 4]);
+    float b[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) b[i] = add_dpp<DPP_XOR2>(b1 ? a[i + 2] : a[i], b1 ? a[i] : a[i + 2]);
+    // lane i receives lane (i - 4) mod 16, whose bit 2 is flipped: each lane adds its partner's copy of the
+    // value index it keeps; after ror:8 every lane holds the row total of index 4*b0 + 2*b1 + b2
+    float c = add_dpp<DPP_ROR4>(b2 ? b[1] : b[0], b2 ? b[0] : b[1]);
+    c = add_dpp<DPP_ROR8>(c, c);
+    float w8 = add_dpp<DPP_XOR1>(v8, v8);
+    w8 = add_dpp<DPP_XOR2>(w8, w8);
+    w8 = add_dpp<DPP_ROR4>(w8, w8);
+    w8 = add_dpp<DPP_ROR8>(w8, w8);
+    *t8 = cross_row_sum(w8);
+    return cross_row_sum(c);
+}
+
+
+// lane l < 8 holds value index bitrev3(l) after wave_sum8_transposed; lane 8 is used for the 9th value
+__device__ __forceinline__ uint32_t transposed_slot_of_lane(uint32_t lane)
+{
+    return lane < 8 ? (((lane & 1) << 2) | (lane & 2) | ((lane >> 2) & 1)) : 8u;
+}
+
+}  // namespace omr

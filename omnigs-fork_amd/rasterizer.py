@@ -63,6 +63,7 @@ def lib() -> C.CDLL:
         L.omr_debug_ranges.argtypes = [vp, i, i, vp, vp]
         L.omr_debug_image_state.argtypes = [vp, i, i, vp, vp, vp]
         L.omr_debug_geometry.argtypes = [vp, i, vp, vp, vp, vp, vp, vp]
+        L.omr_debug_wave_sum.argtypes = [vp, vp, vp]
         L.omr_profile_enable.argtypes = [i]
         L.omr_profile_read.restype = i
         L.omr_profile_read.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_uint64), i]
@@ -373,3 +374,12 @@ def profile_read() -> dict:
     cnt = (C.c_uint64 * NUM_STAGES)()
     n = lib().omr_profile_read(tot, cnt, NUM_STAGES)
     return {lib().omr_profile_stage_name(i).decode(): (float(tot[i]), int(cnt[i])) for i in range(n)}
+
+
+def debug_wave_sum(x: torch.Tensor) -> torch.Tensor:
+    """Column sums of a [64, 9] float32 device tensor through the render backward's wave reduction."""
+    x = _dev_f32(x, "x")
+    assert tuple(x.shape) == (64, 9)
+    out = torch.empty(9, dtype=torch.float32, device=x.device)
+    _check(lib().omr_debug_wave_sum(x.data_ptr(), out.data_ptr(), _stream(x.device)), "debug_wave_sum")
+    return out
