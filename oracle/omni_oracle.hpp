@@ -570,8 +570,18 @@ template <typename R> int forward(State<R>& s, const Args<R>& in)
     const R focal_y = (R)a.height / (R(2) * a.tan_fovy);  // rasterizer_impl.cu:275-276
     const R focal_x = (R)a.width / (R(2) * a.tan_fovx);
 
-#pragma omp parallel for schedule(static)
-    for (int i = 0; i < P; ++i) preprocess_one(s, i, focal_x, focal_y);
+    // exceptions must not escape an OpenMP region: record and rethrow after it
+    int prefiltered_violation = 0;
+#pragma omp parallel for schedule(static) reduction(| : prefiltered_violation)
+    for (int i = 0; i < P; ++i) {
+        try {
+            preprocess_one(s, i, focal_x, focal_y);
+        } catch (const std::runtime_error&) {
+            prefiltered_violation |= 1;
+        }
+    }
+    if (prefiltered_violation)
+        throw std::runtime_error("Point is filtered although prefiltered is set. This shouldn't happen!");
 
     // InclusiveSum (rasterizer_impl.cu:622)
     uint64_t acc = 0;

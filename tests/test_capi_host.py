@@ -1,0 +1,94 @@
+"""C-ABI library checks that need no GPU: the library loads, exports every entry point include/omnigs_raster.h
+declares, and the host-side logic (argument validation, scratch sizing, P = 0 early return) behaves."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "omnigs_raster.h")
+
+
+def _declared():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(omr_[a-z0-9_]+)\s*\(", text)) - {"omr_alloc_fn"})
+
+
+def test_header_declares_reference_entry_points():
+    names = _declared()
+    for n in ["omr_rasterizer_mark_visible", "omr_rasterizer_forward", "omr_rasterizer_backward",
+              "omr_lonlat_mark_visible", "omr_lonlat_forward", "omr_lonlat_backward"]:
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol(omr):
+    lib = omr.rasterizer.lib()
+    out = subprocess.run(["nm", "-D", "--defined-only", omr.rasterizer.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r" T (omr_\w+)", out))
+    for n in _declared():
+        assert n in exported, n
+        assert getattr(lib, n) is not None
+
+
+def test_abi_version_and_sizes(omr):
+    lib = omr.rasterizer.lib()
+    assert lib.omr_abi_version() == 1
+    g0, g1 = lib.omr_geometry_bytes(1000), lib.omr_geometry_bytes(2000)
+    assert g1 > g0 > 1000 * 100  # SoA state of ~100+ B per Gaussian
+    assert lib.omr_image_bytes(64, 32) >= 64 * 32 * 8 + 8 * 8
+    b0, b1 = lib.omr_binning_bytes(0, 64, 32), lib.omr_binning_bytes(1000, 64, 32)
+    assert b1 - b0 >= 1000 * (16 + 36)  # keys/values ping-pong + one gradient row per instance
+
+
+def test_invalid_camera_type_and_empty_scene_without_gpu(omr):
+    lib = omr.rasterizer.lib()
+    nr = C.c_int(-1)
+    alloc = omr.rasterizer._ALLOC_FN(lambda ctx, n: None)
+    # P = 0 returns before touching the device (rasterize_points.cu:97)
+    rc = lib.omr_lonlat_forward(alloc, None, alloc, None, alloc, None, 0, 3, 16, None, 64, 32, None, None, None, None,
+                                None, 1.0, None, None, None, None, False, None, None, None, C.byref(nr))
+    assert rc == 0 and nr.value == 0
+    # missing inputs are rejected by the host validation, before any allocation or launch
+    rc = lib.omr_lonlat_forward(alloc, None, alloc, None, alloc, None, 10, 3, 16, None, 64, 32, None, None, None, None,
+                                None, 1.0, None, None, None, None, False, None, None, None, C.byref(nr))
+    assert rc == 1
+    assert b"missing" in lib.omr_last_error()
+    rc = lib.omr_lonlat_backward(10, 3, 16, 0, None, 64, 32, None, None, None, None, 1.0, None, None, None, None,
+                                 None, None, None, None, None, None, None, None, None, None, None, None, None, None,
+                                 None, None, None)
+    assert rc == 1
+
+
+def test_python_boundary_rejects_cpu_tensors(omr):
+    import torch
+
+    R = omr.rasterizer
+    t = torch.zeros(4, 3)
+    with pytest.raises(R.RasterizerError, match="HIP device"):
+        R.RasterizeGaussiansCUDA(torch.zeros(3), t, torch.empty(0), torch.ones(4, 1), torch.ones(4, 3),
+                                 torch.ones(4, 4), 1.0, torch.empty(0), torch.eye(4), torch.eye(4), 0.0, 0.0, 32, 64,
+                                 torch.zeros(4, 16, 3), 3, torch.zeros(3), False, 3)
+    with pytest.raises(R.RasterizerError, match="num_points, 3"):
+        R.RasterizeGaussiansCUDA(torch.zeros(3), torch.zeros(4, 2), None, None, None, None, 1.0, None, None, None,
+                                 0.0, 0.0, 32, 64, None, 3, None, False, 3)
+    with pytest.raises(R.RasterizerError, match="Invalid camera_type"):
+        R.RasterizeGaussiansCUDA(torch.zeros(3), t, None, None, None, None, 1.0, None, None, None, 0.0, 0.0, 32, 64,
+                                 None, 3, None, False, 2)
+
+
+def test_autograd_wrapper_argument_rules(omr):
+    import torch
+
+    R = omr.rasterizer
+    s = R.GaussianRasterizationSettings(32, 64, 0.0, 0.0, torch.zeros(3), 1.0, torch.eye(4), torch.eye(4), None, 3,
+                                        torch.zeros(3), False, R.CAMERA_LONLAT)
+    rast = R.GaussianRasterizer(s)
+    m = torch.zeros(4, 3)
+    with pytest.raises(R.RasterizerError, match="excatly one of either SHs"):
+        rast(m, m, torch.ones(4, 1), scales=torch.ones(4, 3), rotations=torch.ones(4, 4))
+    with pytest.raises(R.RasterizerError, match="scale/rotation pair"):
+        rast(m, m, torch.ones(4, 1), shs=torch.zeros(4, 16, 3), scales=torch.ones(4, 3))
