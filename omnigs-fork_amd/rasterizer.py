@@ -73,6 +73,21 @@ def lib() -> C.CDLL:
     return _lib
 
 
+def libtorch_boundary():
+    """The LibTorch drop-in (lib/librasterize_points.so: the reference's rasterize_points.h C++ symbols) through
+    its pybind11 module — the same functions a C++ LibTorch host links against."""
+    import importlib
+    import sys
+
+    libdir = os.path.join(_HERE, "lib")
+    if libdir not in sys.path:
+        sys.path.insert(0, libdir)
+    try:
+        return importlib.import_module("_rasterize_points")
+    except ImportError as e:
+        raise RasterizerError(f"LibTorch drop-in not built ({e}); run __graft_entry__.build()") from e
+
+
 def _check(rc: int, what: str):
     if rc != 0:
         msg = lib().omr_last_error().decode(errors="replace")

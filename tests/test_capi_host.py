@@ -92,3 +92,22 @@ def test_autograd_wrapper_argument_rules(omr):
         rast(m, m, torch.ones(4, 1), scales=torch.ones(4, 3), rotations=torch.ones(4, 4))
     with pytest.raises(R.RasterizerError, match="scale/rotation pair"):
         rast(m, m, torch.ones(4, 1), shs=torch.zeros(4, 16, 3), scales=torch.ones(4, 3))
+
+
+def test_libtorch_dropin_exports_reference_symbols(omr):
+    """librasterize_points.so exports the reference's three C++ functions with identical signatures
+    (include/rasterize_points.h:29-80 of the reference), so a LibTorch host links it unchanged."""
+    path = os.path.join(os.path.dirname(omr.rasterizer.LIB_PATH), "librasterize_points.so")
+    out = subprocess.run(["nm", "-DC", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    T, F = "at::Tensor const&", "float"
+    expect = [
+        f"RasterizeGaussiansCUDA({T}, {T}, {T}, {T}, {T}, {T}, {F}, {T}, {T}, {T}, {F}, {F}, int, int, {T}, int, {T}, "
+        "bool, int, bool)",
+        f"RasterizeGaussiansBackwardCUDA({T}, {T}, {T}, {T}, {T}, {T}, {F}, {T}, {T}, {T}, {F}, {F}, {T}, {T}, int, "
+        f"{T}, {T}, int, {T}, {T}, int)",
+        "markVisible(at::Tensor&, at::Tensor&, at::Tensor&, int)",
+    ]
+    for sig in expect:
+        assert sig in out, sig
+    m = omr.rasterizer.libtorch_boundary()
+    assert hasattr(m, "RasterizeGaussiansCUDA") and hasattr(m, "markVisible")
