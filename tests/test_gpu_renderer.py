@@ -75,7 +75,8 @@ def test_render_end_to_end_raw_param_grads(cam_type):
                                   tanfovx=tanfov[0], tanfovy=tanfov[1])
     o, L, og = oracle_run(act, cam_o, dL, bg=(0.1, 0.2, 0.3))
     assert np.abs(to_np(image) - o.get("out_color").reshape(3, H, W)).max() <= 1e-4
-    assert vis.sum().item() > 0.3 * g.P
+    # Gaussians surround the camera: the 360° view sees most, the 90° pinhole about a sixth
+    assert vis.sum().item() > (0.3 if cam_type == scene.CAMERA_LONLAT else 0.1) * g.P
     ok, emax, nbad = grad_close(to_np(vsp.grad), og["dmean2D"])
     assert ok, ("viewspace_points", emax, nbad)
     want = _chain_to_raw(pc, og)
