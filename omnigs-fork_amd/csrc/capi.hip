@@ -122,10 +122,7 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s)
 {
     Carver c(base);
     GeomState g;
-    g.means2D = c.take<float2>(P);
-    g.conic_opacity = c.take<float4>(P);
-    g.rgb = c.take<float4>(P);
-    g.depths = c.take<float>(P);
+    g.splat = c.take<float4>(P * SPLAT_F4);
     g.clamped = c.take<uint8_t>(P);
     g.tiles_touched = c.take<uint32_t>(P);
     g.key_a = c.take<uint32_t>(P);
@@ -136,7 +133,6 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s)
     g.hist = c.take<uint32_t>(nh);
     g.scan_partials = c.take<uint32_t>(std::max(scan_partials_size(P), scan_partials_size(nh)));
     g.offsets = c.take<uint32_t>(P);
-    g.emit_off = c.take<uint32_t>(P);
     g.counters = c.take<uint32_t>(4);
     g.internal_radii = c.take<int>(P);
     g.grad_sum = c.take<float>(P * GRAD_ROW);
@@ -288,7 +284,7 @@ int forward_impl(const ForwardIn& in)
     BinningState b;
     BinningState::carve(bin_base, L, nullptr, &b, tile_passes);
 
-    { StageScope st_(ST_EMIT, s); launch_emit_instances(in.P, L, g, radii, d.gx, d.gy, b.key_a, b.val_a, s); }
+    { StageScope st_(ST_EMIT, s); launch_emit_instances(in.P, L, g, d.gx, b.key_a, b.val_a, s); }
     { StageScope st_(ST_TILE_SORT, s); radix_sort_pairs(b.key_a, b.key_b, b.val_a, b.val_b, b.hist, b.scan_partials, L, 0, tile_passes, s); }
     OMR_HIP(hipMemsetAsync(im.ranges, 0, d.T * sizeof(uint2), s));
     { StageScope st_(ST_RANGES, s); launch_tile_ranges(L, b.point_keys, im.ranges, s); }
@@ -296,7 +292,7 @@ int forward_impl(const ForwardIn& in)
     RenderFwdArgs ra;
     ra.W = in.width; ra.H = in.height; ra.gx = d.gx; ra.gy = d.gy;
     ra.ranges = im.ranges; ra.point_list = b.point_list;
-    ra.means2D = g.means2D; ra.conic_opacity = g.conic_opacity; ra.rgb = g.rgb; ra.depths = g.depths;
+    ra.splat = g.splat;
     ra.bg = in.background; ra.final_T = im.final_T; ra.n_contrib = im.n_contrib; ra.out_color = in.out_color;
     // lonlat never renders depth (rasterize_points.cu:133-156 passes render_depth to the pinhole path only)
     { StageScope st_(ST_RENDER_FWD, s); launch_render_forward(ra, in.render_depth && in.camera_type == CAM_PINHOLE, s); }
@@ -348,8 +344,7 @@ int backward_impl(const BackwardIn& in)
 
     RenderBwdArgs rb;
     rb.W = in.width; rb.H = in.height; rb.gx = d.gx; rb.gy = d.gy;
-    rb.ranges = im.ranges; rb.point_list = b.point_list; rb.means2D = g.means2D; rb.conic_opacity = g.conic_opacity;
-    rb.rgb = g.rgb; rb.radii = radii; rb.emit_off = g.emit_off; rb.bg = in.background;
+    rb.ranges = im.ranges; rb.point_list = b.point_list; rb.splat = g.splat; rb.bg = in.background;
     rb.final_T = im.final_T; rb.n_contrib = im.n_contrib; rb.dL_dpix = in.dL_dpix; rb.inst_grad = b.inst_grad;
     { StageScope st_(ST_RENDER_BWD, s); launch_render_backward(rb, s); }
 
@@ -561,10 +556,16 @@ int omr_debug_geometry(char* geom_buffer, int P, float* means2D, float* conic_op
     GeomState g;
     GeomState::carve(geom_buffer, (size_t)P, &g);
     const hipStream_t s = (hipStream_t)stream;
-    if (means2D) OMR_HIP(hipMemcpyAsync(means2D, g.means2D, P * sizeof(float2), hipMemcpyDeviceToDevice, s));
-    if (conic_opacity) OMR_HIP(hipMemcpyAsync(conic_opacity, g.conic_opacity, P * sizeof(float4), hipMemcpyDeviceToDevice, s));
-    if (rgb) OMR_HIP(hipMemcpy2DAsync(rgb, 3 * sizeof(float), g.rgb, sizeof(float4), 3 * sizeof(float), P, hipMemcpyDeviceToDevice, s));
-    if (depths) OMR_HIP(hipMemcpyAsync(depths, g.depths, P * sizeof(float), hipMemcpyDeviceToDevice, s));
+    // strided copies out of the 64-B render records (raster_common.h)
+    const size_t pitch = SPLAT_F4 * sizeof(float4);
+    const char* rec = reinterpret_cast<const char*>(g.splat);
+    auto col = [&](void* dst, size_t off, size_t bytes) {
+        return hipMemcpy2DAsync(dst, bytes, rec + off, pitch, bytes, P, hipMemcpyDeviceToDevice, s);
+    };
+    if (means2D) OMR_HIP(col(means2D, 0, 2 * sizeof(float)));
+    if (conic_opacity) OMR_HIP(col(conic_opacity, sizeof(float4), sizeof(float4)));
+    if (rgb) OMR_HIP(col(rgb, 2 * sizeof(float4), 3 * sizeof(float)));
+    if (depths) OMR_HIP(col(depths, 2 * sizeof(float), sizeof(float)));
     if (tiles_touched) OMR_HIP(hipMemcpyAsync(tiles_touched, g.tiles_touched, P * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     return OMR_OK;
 }

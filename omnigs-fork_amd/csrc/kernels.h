@@ -39,8 +39,8 @@ size_t radix_hist_size(size_t n);
 // stable LSD radix sort of (key, value) over bits [0, 8*passes); returns which buffer holds the result (0: a, 1: b)
 int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* hist,
                      uint32_t* scan_partials, size_t n, int first_pass, int passes, hipStream_t s);
-void launch_emit_instances(int P, size_t L, const GeomState& g, const int* radii, uint32_t gx, uint32_t gy,
-                           uint32_t* tile_keys, uint32_t* gauss_vals, hipStream_t s);
+void launch_emit_instances(int P, size_t L, const GeomState& g, uint32_t gx, uint32_t* tile_keys,
+                           uint32_t* gauss_vals, hipStream_t s);
 void launch_tile_ranges(size_t L, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s);
 
 // render_fwd.hip
@@ -49,10 +49,7 @@ struct RenderFwdArgs {
     uint32_t gx, gy;
     const uint2* ranges;
     const uint32_t* point_list;
-    const float2* means2D;
-    const float4* conic_opacity;
-    const float4* rgb;
-    const float* depths;
+    const float4* splat;  // [P][SPLAT_F4] render records
     const float* bg;
     float* final_T;
     uint32_t* n_contrib;
@@ -66,11 +63,7 @@ struct RenderBwdArgs {
     uint32_t gx, gy;
     const uint2* ranges;
     const uint32_t* point_list;
-    const float2* means2D;
-    const float4* conic_opacity;
-    const float4* rgb;
-    const int* radii;
-    const uint32_t* emit_off;
+    const float4* splat;  // [P][SPLAT_F4] render records
     const float* bg;
     const float* final_T;
     const uint32_t* n_contrib;

@@ -224,12 +224,14 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
         rgb[1] = a.colors_precomp[3 * idx + 1];
         rgb[2] = a.colors_precomp[3 * idx + 2];
     }
-    g.rgb[idx] = {rgb[0], rgb[1], rgb[2], 0.0f};
+    float4* rec = g.splat + (size_t)idx * SPLAT_F4;
+    rec[0] = {point_image.x, point_image.y, depth, 0.0f};  // .w (slot base) is written by emit
+    rec[1] = {conic.x, conic.y, conic.z, a.opacities[idx]};
+    rec[2] = {rgb[0], rgb[1], rgb[2], __builtin_bit_cast(float, x1 - x0)};
+    rec[3] = {__builtin_bit_cast(float, x0), __builtin_bit_cast(float, y0), __builtin_bit_cast(float, x1),
+              __builtin_bit_cast(float, y1)};
     g.clamped[idx] = clamp_bits;
-    g.depths[idx] = depth;
     a.radii[idx] = rad;
-    g.means2D[idx] = point_image;
-    g.conic_opacity[idx] = {conic.x, conic.y, conic.z, a.opacities[idx]};
     g.tiles_touched[idx] = area;
     g.key_a[idx] = __float_as_uint(depth);
 }

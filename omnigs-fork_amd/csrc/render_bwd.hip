@@ -48,13 +48,6 @@ __device__ __forceinline__ uint32_t block_max(uint32_t v, uint32_t* s_tmp)
     return m;
 }
 
-// emission slot of Gaussian gid's instance on tile (tx, ty): slots are emitted row-major over its rect
-__device__ __forceinline__ uint32_t instance_slot(const RenderBwdArgs& a, uint32_t gid, uint32_t tx, uint32_t ty)
-{
-    uint32_t x0, y0, x1, y1;
-    getRect(a.means2D[gid], a.radii[gid], a.gx, a.gy, x0, y0, x1, y1);
-    return a.emit_off[gid] + (ty - y0) * (x1 - x0) + (tx - x0);
-}
 
 __global__ __launch_bounds__(BLOCK_SIZE) void render_bwd_kernel(RenderBwdArgs a)
 {
@@ -101,8 +94,8 @@ __global__ __launch_bounds__(BLOCK_SIZE) void render_bwd_kernel(RenderBwdArgs a)
     const uint32_t wave_bit = 1u << w;
 
     for (uint32_t k = max_c + t; k < n; k += BLOCK_SIZE) {
-        const uint32_t gid = a.point_list[range.x + k];
-        float* row = a.inst_grad + (size_t)instance_slot(a, gid, tx, ty) * GRAD_ROW;
+        const float4* rec = a.splat + (size_t)a.point_list[range.x + k] * SPLAT_F4;
+        float* row = a.inst_grad + (size_t)splat_slot(rec[0], rec[2], tx, ty) * GRAD_ROW;
 #pragma unroll
         for (int c = 0; c < GRAD_ROW; ++c) row[c] = 0.f;
     }
@@ -119,13 +112,15 @@ __global__ __launch_bounds__(BLOCK_SIZE) void render_bwd_kernel(RenderBwdArgs a)
         // batch entry j <-> position hi-1-j
         if ((int)t < cnt) {
             const uint32_t pos = (uint32_t)(hi - 1 - (int)t);
-            const uint32_t gid = a.point_list[range.x + pos];
-            const float2 xy = a.means2D[gid];
-            const float4 co = a.conic_opacity[gid];
+            const float4* rec = a.splat + (size_t)a.point_list[range.x + pos] * SPLAT_F4;  // one 64-B line
+            const float4 p = rec[0];
+            const float4 co = rec[1];
+            const float4 c = rec[2];
+            const float2 xy = {p.x, p.y};
             s_xy[t] = xy;
             s_co[t] = co;
-            s_rgb[t] = a.rgb[gid];
-            s_slot[t] = instance_slot(a, gid, tx, ty);
+            s_rgb[t] = c;
+            s_slot[t] = splat_slot(p, c, tx, ty);
             s_mask[t] = band_mask(xy, co, tx, ty);
         }
         __syncthreads();

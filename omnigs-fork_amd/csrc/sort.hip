@@ -214,8 +214,8 @@ __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* offsets, uin
 // of tiles no longer serialises its wave. The owner of each slot is found by binary search over the scan,
 // narrowed per block to the few Gaussians that own the block's 256 slots.
 __global__ __launch_bounds__(256) void emit_kernel(int P, size_t L, const uint32_t* order, const uint32_t* offsets,
-                                                   const float2* means2D, const int* radii, uint32_t gx, uint32_t gy,
-                                                   uint32_t* tile_keys, uint32_t* gauss_vals, uint32_t* emit_off)
+                                                   float4* splat, uint32_t gx, uint32_t* tile_keys,
+                                                   uint32_t* gauss_vals)
 {
     __shared__ uint32_t s_lo, s_hi;
     const size_t e0 = (size_t)blockIdx.x * blockDim.x;
@@ -231,10 +231,12 @@ __global__ __launch_bounds__(256) void emit_kernel(int P, size_t L, const uint32
     const uint32_t gid = order[r];
     const uint32_t start = r == 0 ? 0u : offsets[r - 1];
     const uint32_t k = (uint32_t)e - start;
-    if (k == 0) emit_off[gid] = start;
-    uint32_t x0, y0, x1, y1;
-    getRect(means2D[gid], radii[gid], gx, gy, x0, y0, x1, y1);
-    const uint32_t w = x1 - x0;
+    float4* rec = splat + (size_t)gid * SPLAT_F4;
+    const float4 rect = rec[3];  // {x0, y0, x1, y1} from preprocess (getRect)
+    const uint32_t x0 = __builtin_bit_cast(uint32_t, rect.x), y0 = __builtin_bit_cast(uint32_t, rect.y);
+    const uint32_t w = __builtin_bit_cast(uint32_t, rect.z) - x0;
+    // slot of tile (tx, ty) = start + (ty - y0) * w + (tx - x0) = slot_base + ty * w + tx  (mod 2^32)
+    if (k == 0) rec[0].w = __builtin_bit_cast(float, start - (y0 * w + x0));
     const uint32_t ky = k / w;
     tile_keys[e] = (y0 + ky) * gx + (x0 + (k - ky * w));
     gauss_vals[e] = gid;
@@ -301,12 +303,11 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
     return cur;
 }
 
-void launch_emit_instances(int P, size_t L, const GeomState& g, const int* radii, uint32_t gx, uint32_t gy,
-                           uint32_t* tile_keys, uint32_t* gauss_vals, hipStream_t s)
+void launch_emit_instances(int P, size_t L, const GeomState& g, uint32_t gx, uint32_t* tile_keys,
+                           uint32_t* gauss_vals, hipStream_t s)
 {
     if (P <= 0 || L == 0) return;
-    emit_kernel<<<div_up(L, 256), 256, 0, s>>>(P, L, g.order, g.offsets, g.means2D, radii, gx, gy, tile_keys,
-                                               gauss_vals, g.emit_off);
+    emit_kernel<<<div_up(L, 256), 256, 0, s>>>(P, L, g.order, g.offsets, g.splat, gx, tile_keys, gauss_vals);
 }
 
 void launch_tile_ranges(size_t L, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s)

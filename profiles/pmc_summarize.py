@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Summarise the rocprofv3 runs of profiles/collect.sh (CPU side, after gpurun merged gpurun_out/).
+
+    python profiles/pmc_summarize.py r01e
+
+Writes profiles/<tag>_kernel_stats.csv (copy of the --stats summary), profiles/<tag>_pmc.csv (per-kernel FETCH_SIZE /
+WRITE_SIZE averages) and profiles/pmc_latest.json, which bench.py reads for roofline.traffic.
+
+HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: rocprofv3 reports both in KiB, and on gfx950
+FETCH_SIZE counts half the bytes of wide coalesced reads (MI355X_MICROARCH.md § HBM), so it is doubled.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+OUT = os.path.join(ROOT, "gpurun_out")
+
+# kernel-name fragment -> bench.py stage name (kernels launched once per stage)
+STAGES = {
+    "preprocess_kernel": "preprocess",
+    "emit_kernel": "emit",
+    "tile_ranges_kernel": "tile_ranges",
+    "render_fwd_kernel": "render_forward",
+    "render_bwd_kernel": "render_backward",
+    "instance_reduce_kernel": "instance_reduce",
+    "gaussian_bwd_kernel": "gaussian_backward",
+}
+
+
+def _col(row, *names):
+    for n in names:
+        if n in row:
+            return row[n]
+    raise KeyError(names)
+
+
+def per_kernel(counter_dir, counter):
+    files = glob.glob(os.path.join(counter_dir, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise FileNotFoundError(f"no counter_collection.csv under {counter_dir}")
+    acc = {}
+    for fn in files:
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                if _col(row, "Counter_Name", "Counter-Name") != counter:
+                    continue
+                name = _col(row, "Kernel_Name", "Kernel-Name", "KernelName")
+                disp = _col(row, "Dispatch_Id", "Dispatch-Id", "Correlation_Id")
+                v = float(_col(row, "Counter_Value", "Counter-Value"))
+                acc.setdefault(name, {}).setdefault(disp, 0.0)
+                acc[name][disp] += v  # a counter may be split over rows (per XCD/instance)
+    return {k: (sum(d.values()) / len(d), len(d)) for k, d in acc.items()}
+
+
+def main():
+    tag = sys.argv[1]
+    stats = glob.glob(os.path.join(OUT, f"prof_{tag}", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(HERE, f"{tag}_kernel_stats.csv"))
+    fetch = per_kernel(os.path.join(OUT, f"pmc_fetch_{tag}"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(OUT, f"pmc_write_{tag}"), "WRITE_SIZE")
+    with open(os.path.join(OUT, f"bench_pmc_fetch_{tag}.json")) as f:
+        bench = json.loads([ln for ln in f if ln.startswith("{")][-1])
+    cfg = bench["config"]["workload"].split(":")[0]
+    rows, kernels = [], {}
+    for name in sorted(set(fetch) | set(write)):
+        fk, n = fetch.get(name, (0.0, 0))
+        wk, _ = write.get(name, (0.0, 0))
+        hbm = (2.0 * fk + wk) * 1024.0
+        rows.append([name, n, round(fk, 1), round(wk, 1), int(hbm)])
+        for frag, stage in STAGES.items():
+            if frag in name:
+                kernels[stage] = {"kernel": name, "fetch_kib_raw": round(fk, 1), "write_kib": round(wk, 1),
+                                  "hbm_bytes_per_launch": int(hbm), "dispatches": n}
+    with open(os.path.join(HERE, f"{tag}_pmc.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "dispatches", "FETCH_SIZE_KiB_avg", "WRITE_SIZE_KiB_avg", "hbm_bytes_per_launch"])
+        w.writerows(rows)
+    latest = {"tag": tag, "config": cfg, "P": bench["config"]["P"], "L": bench["config"]["L"],
+              "method": "(2*FETCH_SIZE + WRITE_SIZE) KiB * 1024, separate --pmc passes, gfx950 FETCH x2 correction",
+              "kernels": kernels}
+    with open(os.path.join(HERE, "pmc_latest.json"), "w") as f:
+        json.dump(latest, f, indent=1)
+    print(json.dumps(latest, indent=1))
+
+
+if __name__ == "__main__":
+    main()
