@@ -15,10 +15,12 @@
 //    the instance's emission slot; gaussian_bwd.hip sums each Gaussian's rows in a fixed order. No atomics:
 //    gradients are bitwise reproducible run to run.
 //  * Per pair the math is predicated (no divergent branches), T is recovered with v_rcp_f32 instead of an
-//    IEEE division sequence, and a wave skips an instance outright when its 16x4 band is outside the
-//    instance's alpha >= 1/255 ellipse (band_mask) or lies behind every pixel's last contributor.
+//    IEEE division sequence, and each wave walks only the instances whose alpha >= 1/255 ellipse reaches
+//    its 16x4 band (band_mask) and that lie in front of some pixel's last contributor: every staged batch
+//    is compacted into one ordered list per wave (band_lists.h). Built with FMA contraction.
 //  * Instances behind the last contributor of every pixel in the tile are skipped (their rows zero-filled).
 //  * XCD-aware tile order, as in the forward.
+#include "band_lists.h"
 #include "kernels.h"
 #include "wave_ops.h"
 
@@ -57,7 +59,9 @@ __global__ __launch_bounds__(BLOCK_SIZE) void render_bwd_kernel(RenderBwdArgs a)
     __shared__ uint32_t s_slot[BATCH];
     __shared__ uint32_t s_mask[BATCH];
     __shared__ float s_part[WAVES][BATCH][GRAD_ROW];
+    __shared__ BandLists<BATCH> s_lists;
     __shared__ uint32_t s_tmp[WAVES];
+    __shared__ uint32_t s_wave_max_c[WAVES];
 
     const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
     const uint32_t tx = tile % a.gx, ty = tile / a.gx;
@@ -86,12 +90,13 @@ __global__ __launch_bounds__(BLOCK_SIZE) void render_bwd_kernel(RenderBwdArgs a)
     // lane (l < 9) of a wave writes value slot slot_of_lane of the wave partial
     const uint32_t slot_of_lane = transposed_slot_of_lane(lane);
 
-    // instances at positions >= max_c are behind every pixel's last contributor
-    const uint32_t max_c = min(n, block_max(last_contributor, s_tmp));
-    uint32_t wave_max_c = last_contributor;  // positions >= wave_max_c are skipped by every pixel of this wave
+    // positions >= wave_max_c are behind the last contributor of every pixel of the wave
+    uint32_t wave_max_c = last_contributor;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) wave_max_c = max(wave_max_c, (uint32_t)__shfl_xor((int)wave_max_c, o, 64));
-    const uint32_t wave_bit = 1u << w;
+    if (lane == 0) s_wave_max_c[w] = wave_max_c;
+    // instances at positions >= max_c are behind every pixel's last contributor
+    const uint32_t max_c = min(n, block_max(last_contributor, s_tmp));  // (its barriers publish s_wave_max_c)
 
     for (uint32_t k = max_c + t; k < n; k += BLOCK_SIZE) {
         const float4* rec = a.splat + (size_t)a.point_list[range.x + k] * SPLAT_F4;
@@ -110,6 +115,7 @@ __global__ __launch_bounds__(BLOCK_SIZE) void render_bwd_kernel(RenderBwdArgs a)
         const int lo = max(0, hi - BATCH);
         const int cnt = hi - lo;
         // batch entry j <-> position hi-1-j
+        uint32_t m = 0;
         if ((int)t < cnt) {
             const uint32_t pos = (uint32_t)(hi - 1 - (int)t);
             const float4* rec = a.splat + (size_t)a.point_list[range.x + pos] * SPLAT_F4;  // one 64-B line
@@ -121,73 +127,83 @@ __global__ __launch_bounds__(BLOCK_SIZE) void render_bwd_kernel(RenderBwdArgs a)
             s_co[t] = co;
             s_rgb[t] = c;
             s_slot[t] = splat_slot(p, c, tx, ty);
-            s_mask[t] = band_mask(xy, co, tx, ty);
-        }
-        __syncthreads();
-        for (int j = 0; j < cnt; ++j) {
-            const uint32_t pos = (uint32_t)(hi - 1 - j);
-            float* part = s_part[w][j];
-            if (!(s_mask[j] & wave_bit) || pos >= wave_max_c) {  // wave-uniform: nothing of this wave contributes
-                if (lane < GRAD_ROW) part[lane] = 0.f;
-                continue;
-            }
-            const float2 xy = s_xy[j];
-            const float4 co = s_co[j];
-            const float dx = xy.x - pxf, dy = xy.y - pyf;
-            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-            const float G = __expf(power);
-            const float alpha = fminf(0.99f, co.w * G);
-            // reference: skip if contributor >= last_contributor, power > 0 or alpha < 1/255
-            const bool contrib = pos < last_contributor && power <= 0.0f && alpha >= 1.0f / 255.0f;
-            if (__ballot(contrib) == 0ull) {
-                if (lane < GRAD_ROW) part[lane] = 0.f;
-                continue;
-            }
-            const float4 c = s_rgb[j];
-            const float inv = __builtin_amdgcn_rcpf(1.f - alpha);
-            const float Tn = T * inv;
-            const float dchannel_dcolor = alpha * Tn;
-            const float n0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
-            const float n1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
-            const float n2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
-            float dL_dalpha = ((c.x - n0) * dpix0 + (c.y - n1) * dpix1 + (c.z - n2) * dpix2) * Tn;
-            dL_dalpha += (-T_final * inv) * bg_dot;
-            const float dL_dG = co.w * dL_dalpha;
-            const float gdx = G * dx;
-            const float gdy = G * dy;
-            float v[8];
-            v[0] = dL_dG * (-gdx * co.x - gdy * co.y) * ddelx_dx;
-            v[1] = dL_dG * (-gdy * co.z - gdx * co.y) * ddely_dy;
-            v[2] = -0.5f * gdx * dx * dL_dG;
-            v[3] = -0.5f * gdx * dy * dL_dG;
-            v[4] = -0.5f * gdy * dy * dL_dG;
-            v[5] = G * dL_dalpha;
-            v[6] = dchannel_dcolor * dpix0;
-            v[7] = dchannel_dcolor * dpix1;
-            float v8 = dchannel_dcolor * dpix2;
+            m = band_mask(xy, co, tx, ty);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) v[q] = contrib ? v[q] : 0.f;
-            v8 = contrib ? v8 : 0.f;
-            T = contrib ? Tn : T;
-            acc0 = contrib ? n0 : acc0;
-            acc1 = contrib ? n1 : acc1;
-            acc2 = contrib ? n2 : acc2;
-            lc0 = contrib ? c.x : lc0;
-            lc1 = contrib ? c.y : lc1;
-            lc2 = contrib ? c.z : lc2;
-            last_alpha = contrib ? alpha : last_alpha;
-            float t8;
-            const float tv = wave_sum8_transposed(v, v8, lane, &t8);
-            if (lane < GRAD_ROW) part[slot_of_lane] = lane < 8 ? tv : t8;
+            for (int b = 0; b < WAVES; ++b)
+                if (pos >= s_wave_max_c[b]) m &= ~(1u << b);
+            s_mask[t] = m;
+        }
+        s_lists.build(m, t);
+        const uint32_t lcnt = s_lists.count(w);
+        const uint8_t* list = s_lists.idx[w];
+        for (uint32_t k4 = 0; k4 < lcnt; k4 += 4) {
+            const uint32_t packed = *reinterpret_cast<const uint32_t*>(list + k4);
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                if (k4 + u >= lcnt) break;
+                const uint32_t j = (packed >> (8 * u)) & 0xffu;
+                const uint32_t pos = (uint32_t)(hi - 1) - j;
+                float* part = s_part[w][j];
+                const float2 xy = s_xy[j];
+                const float4 co = s_co[j];
+                const float dx = xy.x - pxf, dy = xy.y - pyf;
+                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                const float G = __expf(power);
+                const float alpha = fminf(0.99f, co.w * G);
+                // reference: skip if contributor >= last_contributor, power > 0 or alpha < 1/255
+                const bool contrib = pos < last_contributor && power <= 0.0f && alpha >= 1.0f / 255.0f;
+                if (__ballot(contrib) == 0ull) {
+                    if (lane < GRAD_ROW) part[lane] = 0.f;
+                    continue;
+                }
+                const float4 c = s_rgb[j];
+                const float inv = __builtin_amdgcn_rcpf(1.f - alpha);
+                const float Tn = T * inv;
+                const float dchannel_dcolor = alpha * Tn;
+                const float n0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
+                const float n1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
+                const float n2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
+                float dL_dalpha = ((c.x - n0) * dpix0 + (c.y - n1) * dpix1 + (c.z - n2) * dpix2) * Tn;
+                dL_dalpha += (-T_final * inv) * bg_dot;
+                const float dL_dG = co.w * dL_dalpha;
+                const float gdx = G * dx;
+                const float gdy = G * dy;
+                float v[8];
+                v[0] = dL_dG * (-gdx * co.x - gdy * co.y) * ddelx_dx;
+                v[1] = dL_dG * (-gdy * co.z - gdx * co.y) * ddely_dy;
+                v[2] = -0.5f * gdx * dx * dL_dG;
+                v[3] = -0.5f * gdx * dy * dL_dG;
+                v[4] = -0.5f * gdy * dy * dL_dG;
+                v[5] = G * dL_dalpha;
+                v[6] = dchannel_dcolor * dpix0;
+                v[7] = dchannel_dcolor * dpix1;
+                float v8 = dchannel_dcolor * dpix2;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[q] = contrib ? v[q] : 0.f;
+                v8 = contrib ? v8 : 0.f;
+                T = contrib ? Tn : T;
+                acc0 = contrib ? n0 : acc0;
+                acc1 = contrib ? n1 : acc1;
+                acc2 = contrib ? n2 : acc2;
+                lc0 = contrib ? c.x : lc0;
+                lc1 = contrib ? c.y : lc1;
+                lc2 = contrib ? c.z : lc2;
+                last_alpha = contrib ? alpha : last_alpha;
+                float t8;
+                const float tv = wave_sum8_transposed(v, v8, lane, &t8);
+                if (lane < GRAD_ROW) part[slot_of_lane] = lane < 8 ? tv : t8;
+            }
         }
         __syncthreads();
+        // one row per instance: the sum of the partials of the waves whose list held it
         if ((int)t < cnt) {
+            const uint32_t mt = s_mask[t];
             float* row = a.inst_grad + (size_t)s_slot[t] * GRAD_ROW;
 #pragma unroll
             for (int c = 0; c < GRAD_ROW; ++c) {
-                float v = s_part[0][t][c];
+                float v = 0.f;
 #pragma unroll
-                for (int q = 1; q < WAVES; ++q) v += s_part[q][t][c];
+                for (int q = 0; q < WAVES; ++q) v += (mt >> q) & 1u ? s_part[q][t][c] : 0.f;
                 row[c] = v;
             }
         }

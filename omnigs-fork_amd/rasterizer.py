@@ -22,7 +22,8 @@ CAMERA_PINHOLE = 1
 CAMERA_LONLAT = 3
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libomnigs_raster.so")
+# OMR_LIB_PATH selects another build of the same C ABI (kernel experiments); default: the in-tree library
+LIB_PATH = os.environ.get("OMR_LIB_PATH") or os.path.join(_HERE, "lib", "libomnigs_raster.so")
 _ALLOC_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_size_t)
 _lib = None
 
