@@ -155,6 +155,8 @@ size_t ImageState::carve(char* base, size_t N, size_t T, ImageState* s)
     im.final_T = c.take<float>(N);
     im.n_contrib = c.take<uint32_t>(N);
     im.ranges = c.take<uint2>(T);
+    im.tile_order = c.take<uint32_t>(T);
+    im.tile_cost = c.take<uint32_t>(T);
     if (s) *s = im;
     return c.size();
 }
@@ -287,13 +289,18 @@ int forward_impl(const ForwardIn& in)
     { StageScope st_(ST_EMIT, s); launch_emit_instances(in.P, L, g, d.gx, b.key_a, b.val_a, s); }
     { StageScope st_(ST_TILE_SORT, s); radix_sort_pairs(b.key_a, b.key_b, b.val_a, b.val_b, b.hist, b.scan_partials, L, 0, tile_passes, s); }
     OMR_HIP(hipMemsetAsync(im.ranges, 0, d.T * sizeof(uint2), s));
-    { StageScope st_(ST_RANGES, s); launch_tile_ranges(L, b.point_keys, im.ranges, s); }
+    {
+        StageScope st_(ST_RANGES, s);
+        launch_tile_ranges(L, b.point_keys, im.ranges, s);
+        launch_tile_order(im.ranges, nullptr, d.T, im.tile_order, s);
+    }
+    OMR_HIP(hipMemsetAsync(im.tile_cost, 0, d.T * sizeof(uint32_t), s));
 
     RenderFwdArgs ra;
     ra.W = in.width; ra.H = in.height; ra.gx = d.gx; ra.gy = d.gy;
-    ra.ranges = im.ranges; ra.point_list = b.point_list;
+    ra.ranges = im.ranges; ra.tile_order = im.tile_order; ra.point_list = b.point_list;
     ra.splat = g.splat;
-    ra.bg = in.background; ra.final_T = im.final_T; ra.n_contrib = im.n_contrib; ra.out_color = in.out_color;
+    ra.bg = in.background; ra.tile_cost = im.tile_cost; ra.final_T = im.final_T; ra.n_contrib = im.n_contrib; ra.out_color = in.out_color;
     // lonlat never renders depth (rasterize_points.cu:133-156 passes render_depth to the pinhole path only)
     { StageScope st_(ST_RENDER_FWD, s); launch_render_forward(ra, in.render_depth && in.camera_type == CAM_PINHOLE, s); }
     if (int e = hip_check("emit/sort/render")) return e;
@@ -344,9 +351,13 @@ int backward_impl(const BackwardIn& in)
 
     RenderBwdArgs rb;
     rb.W = in.width; rb.H = in.height; rb.gx = d.gx; rb.gy = d.gy;
-    rb.ranges = im.ranges; rb.point_list = b.point_list; rb.splat = g.splat; rb.bg = in.background;
+    rb.ranges = im.ranges; rb.tile_order = im.tile_order; rb.point_list = b.point_list; rb.splat = g.splat; rb.bg = in.background;
     rb.final_T = im.final_T; rb.n_contrib = im.n_contrib; rb.dL_dpix = in.dL_dpix; rb.inst_grad = b.inst_grad;
-    { StageScope st_(ST_RENDER_BWD, s); launch_render_backward(rb, s); }
+    {
+        StageScope st_(ST_RENDER_BWD, s);
+        launch_tile_order(im.ranges, im.tile_cost, d.T, im.tile_order, s);  // costliest tiles first
+        launch_render_backward(rb, s);
+    }
 
     GaussBwdArgs ga;
     ga.P = in.P; ga.D = in.D; ga.M = in.M; ga.W = in.width; ga.H = in.height;

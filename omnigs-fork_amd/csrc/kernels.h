@@ -42,15 +42,20 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
 void launch_emit_instances(int P, size_t L, const GeomState& g, uint32_t gx, uint32_t* tile_keys,
                            uint32_t* gauss_vals, hipStream_t s);
 void launch_tile_ranges(size_t L, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s);
+// render schedule: within each of 8 contiguous shares of the tiles (one per XCD), tiles by descending cost
+// (cost[t] if cost != NULL, else the instance count ranges[t].y - ranges[t].x)
+void launch_tile_order(const uint2* ranges, const uint32_t* cost, uint32_t T, uint32_t* order, hipStream_t s);
 
 // render_fwd.hip
 struct RenderFwdArgs {
     int W, H;
     uint32_t gx, gy;
     const uint2* ranges;
+    const uint32_t* tile_order;  // [T] schedule (launch_tile_order)
     const uint32_t* point_list;
     const float4* splat;  // [P][SPLAT_F4] render records
     const float* bg;
+    uint32_t* tile_cost;  // [T] zeroed; receives the (instance, band) pairs each tile evaluated (backward schedule)
     float* final_T;
     uint32_t* n_contrib;
     float* out_color;
@@ -62,6 +67,7 @@ struct RenderBwdArgs {
     int W, H;
     uint32_t gx, gy;
     const uint2* ranges;
+    const uint32_t* tile_order;  // [T] schedule (launch_tile_order)
     const uint32_t* point_list;
     const float4* splat;  // [P][SPLAT_F4] render records
     const float* bg;
@@ -71,6 +77,9 @@ struct RenderBwdArgs {
     float* inst_grad;
 };
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
+#ifdef OMR_STAMPS
+int omr_debug_stamps_bwd(uint64_t* dst, size_t bytes);  // diagnostic builds only (tile_wave.h)
+#endif
 
 // gaussian_bwd.hip
 struct GaussBwdArgs {

@@ -94,6 +94,8 @@ struct ImageState {
     float* final_T;     // accum_alpha in the reference (rasterizer_impl.cu:222)
     uint32_t* n_contrib;
     uint2* ranges;      // [T] (the reference allocates N, uses T)
+    uint32_t* tile_order;  // [T] render schedule: tiles by descending cost within each XCD's share (launch_tile_order)
+    uint32_t* tile_cost;   // [T] (instance, band) pairs the forward evaluated per tile: the backward's schedule key
     static size_t carve(char* base, size_t N, size_t T, ImageState* s);
 };
 

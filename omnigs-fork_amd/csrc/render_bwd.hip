@@ -1,223 +1,244 @@
 // render_bwd.hip — per-tile back-to-front gradient replay, gfx950.
 //
-// Follows cuda_rasterizer/backward.cu:671-843 (renderCUDA backward) for the per-pixel arithmetic: T is
-// recovered by division, accum_rec / last_alpha / last_color carry the colour behind each instance, and the
-// background term uses T_final.
+// Follows cuda_rasterizer/backward.cu:671-843 (renderCUDA backward). Per pixel, the tile's instances are replayed
+// back to front from the last contributor; for each contributing instance the reference accumulates, with nine
+// float atomics into per-Gaussian arrays, dL/dmean2D.xy, dL/dconic.{x,y,w}, dL/dopacity and dL/dcolour.
 //
-// What is different, and why (MI355X):
-//  * The reference issues 9 float atomicAdds per contributing (pixel, Gaussian) pair into per-Gaussian
-//    arrays. On MI355X float atomics run at ~1.3 TB/s chip-wide and ~17x slower still when the 64 lanes of
-//    an instruction hit 64 different rows (MI355X_MICROARCH.md, Global float atomics) — that would bound the
-//    kernel. Here each wave64 sums its 64 pixels' 9 gradient values in registers: a transposed butterfly
-//    inside each 16-lane DPP row (8 values in 22 DPP-fused VALU ops: each step halves the values a lane
-//    holds), then v_permlane16_swap / v_permlane32_swap across rows (gfx950). The 4 waves' partials are
-//    combined in LDS and ONE 36-B row per (tile, Gaussian) instance is stored with plain stores, indexed by
-//    the instance's emission slot; gaussian_bwd.hip sums each Gaussian's rows in a fixed order. No atomics:
-//    gradients are bitwise reproducible run to run.
-//  * Per pair the math is predicated (no divergent branches), T is recovered with v_rcp_f32 instead of an
-//    IEEE division sequence, and each wave walks only the instances whose alpha >= 1/255 ellipse reaches
-//    its 16x4 band (band_mask) and that lie in front of some pixel's last contributor: every staged batch
-//    is compacted into one ordered list per wave (band_lists.h). Built with FMA contraction.
-//  * Instances behind the last contributor of every pixel in the tile are skipped (their rows zero-filled).
-//  * XCD-aware tile order, as in the forward.
-#include "band_lists.h"
+// Structure (MI355X): ONE wave64 per 16x16 tile, four pixels per lane (one per 16x4 band, tile_wave.h), as in
+// render_fwd.hip. For each instance the wave accumulates, per lane and over the bands the instance reaches,
+// nine moments of the pixel weights u = G * dL/dalpha and the colour weights alpha * T:
+//     S_u, S_u dx, S_u dy, S_u dx^2, S_u dx dy, S_u dy^2, S_aT dpix_{r,g,b}
+// The per-Gaussian constants of the reference's expressions (conic, opacity, 0.5 W, 0.5 H, -1/2) are linear
+// factors, so they are applied once per instance to the lane's sums — not once per pixel — and the nine values
+// are then summed over the wave in registers (DPP transposed butterfly + v_permlane{16,32}_swap, wave_ops.h).
+// Lanes 0..8 store the instance's 36-B gradient row, indexed by its emission slot, with plain stores;
+// gaussian_bwd.hip sums each Gaussian's rows in a fixed order. No atomics: gradients are bitwise reproducible.
+//
+// The per-pixel recurrence keeps two numbers instead of the reference's seven (T, accum_rec[3], last_alpha,
+// last_color[3]): T and s = bg . dL/dpix * T_final + sum over the contributors j behind the current instance of
+// (c_j . dL/dpix) alpha_j T_j. Since T_i (1 - alpha_i) accum_rec_i = sum_j c_j alpha_j T_j (unroll
+// backward.cu:790-797), the reference's
+//     dL/dalpha_i = T_i (c_i - accum_rec_i) . dL/dpix - T_final / (1 - alpha_i) bg . dL/dpix
+// equals T_i c_i . dL/dpix - s / (1 - alpha_i): the same quantity, rounded differently.
+// T_i is recovered with v_rcp_f32 (T_{i+1} / (1 - alpha_i)), as the reference divides (backward.cu:782).
+// Instances at or behind every band's last contributor are skipped (their rows are zero).
 #include "kernels.h"
+#include "tile_wave.h"
 #include "wave_ops.h"
 
 namespace omr {
 
 namespace {
 
-constexpr int BATCH = 128;
-constexpr int WAVES = BLOCK_SIZE / 64;
-
-__device__ __forceinline__ uint32_t xcd_remap(uint32_t orig, uint32_t nwg)
+__device__ __forceinline__ void zero_row(float* inst_grad, uint32_t slot)
 {
-    const uint32_t q = nwg / 8, r = nwg % 8, xcd = orig % 8;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+    float* row = inst_grad + (size_t)slot * GRAD_ROW;
+#pragma unroll
+    for (int c = 0; c < GRAD_ROW; ++c) row[c] = 0.f;
 }
 
-__device__ __forceinline__ uint32_t block_max(uint32_t v, uint32_t* s_tmp)
+OMR_STAMP_DECL(g_stamps_bwd)
+
+#ifndef OMR_BWD_MINW
+#define OMR_BWD_MINW 1
+#endif
+// keep each pixel's dL/dpix and last contributor in LDS (read per instance and band) instead of 16 VGPRs
+#ifndef OMR_BWD_PIX_LDS
+#define OMR_BWD_PIX_LDS 0
+#endif
+
+__global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel(RenderBwdArgs a)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    if ((threadIdx.x & 63) == 0) s_tmp[threadIdx.x >> 6] = v;
-    __syncthreads();
-    uint32_t m = s_tmp[0];
-#pragma unroll
-    for (int k = 1; k < WAVES; ++k) m = max(m, s_tmp[k]);
-    __syncthreads();
-    return m;
-}
+    OMR_STAMP_BEGIN
+    __shared__ float4 s_geo_all[TW_WAVES][TW_BATCH];   // x, y, position in range (u32 bits), band mask (u32 bits)
+    __shared__ float4 s_quad_all[TW_WAVES][TW_BATCH];  // qa, qb, qc, opacity
+    __shared__ float4 s_rgb_all[TW_WAVES][TW_BATCH];   // colour, emission slot (u32 bits)
+#if OMR_BWD_PIX_LDS
+    __shared__ float4 s_pix_all[TW_WAVES][TW_BANDS][64];  // dL/dpix rgb, last contributor (u32 bits)
+#endif
 
-
-__global__ __launch_bounds__(BLOCK_SIZE) void render_bwd_kernel(RenderBwdArgs a)
-{
-    __shared__ float2 s_xy[BATCH];
-    __shared__ float4 s_co[BATCH];
-    __shared__ float4 s_rgb[BATCH];
-    __shared__ uint32_t s_slot[BATCH];
-    __shared__ uint32_t s_mask[BATCH];
-    __shared__ float s_part[WAVES][BATCH][GRAD_ROW];
-    __shared__ BandLists<BATCH> s_lists;
-    __shared__ uint32_t s_tmp[WAVES];
-    __shared__ uint32_t s_wave_max_c[WAVES];
-
-    const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
-    const uint32_t tx = tile % a.gx, ty = tile / a.gx;
-    const uint32_t t = threadIdx.x;
-    const uint32_t lane = t & 63, w = t >> 6;
-    const uint32_t px = tx * BLOCK_X + (t & (BLOCK_X - 1));
-    const uint32_t py = ty * BLOCK_Y + (t / BLOCK_X);
-    const bool inside = px < (uint32_t)a.W && py < (uint32_t)a.H;
-    const uint32_t pix_id = a.W * py + px;
-    const float pxf = (float)px, pyf = (float)py;
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t rank = xcd_remap(blockIdx.x, gridDim.x) * TW_WAVES + wv;
+    if (rank >= a.gx * a.gy) return;  // wave-uniform; the block's waves never synchronise with each other
+#ifdef OMR_NO_TILE_ORDER
+    const uint32_t tile = rank;
+#else
+    const uint32_t tile = a.tile_order[rank];
+#endif
+    float4* s_geo = s_geo_all[wv];
+    float4* s_quad = s_quad_all[wv];
+    float4* s_rgb = s_rgb_all[wv];
+    const TileLane tl(tile, a.gx);
+    const uint32_t lane = tl.lane;
+    const float pxf = (float)tl.px;
     const size_t plane = (size_t)a.H * a.W;
 
+    float T[TW_BANDS], s[TW_BANDS];
+#if OMR_BWD_PIX_LDS
+    float4* s_pix = &s_pix_all[wv][0][0];
+#else
+    float dp0[TW_BANDS], dp1[TW_BANDS], dp2[TW_BANDS];
+    uint32_t last[TW_BANDS];
+#endif
+    uint32_t band_end[TW_BANDS];  // wave-uniform: max last contributor of the band
+    uint32_t max_c = 0;
+#pragma unroll
+    for (int b = 0; b < TW_BANDS; ++b) {
+        const uint32_t py = tl.py(b);
+        const bool inside = tl.px < (uint32_t)a.W && py < (uint32_t)a.H;
+        const uint32_t pix = a.W * py + tl.px;
+        const float Tf = inside ? a.final_T[pix] : 0.f;
+        const uint32_t lc = inside ? a.n_contrib[pix] : 0u;
+        const float d0 = inside ? a.dL_dpix[pix] : 0.f;
+        const float d1 = inside ? a.dL_dpix[plane + pix] : 0.f;
+        const float d2 = inside ? a.dL_dpix[2 * plane + pix] : 0.f;
+#if OMR_BWD_PIX_LDS
+        s_pix[b * 64 + lane] = make_float4(d0, d1, d2, __builtin_bit_cast(float, lc));
+#else
+        last[b] = lc;
+        dp0[b] = d0;
+        dp1[b] = d1;
+        dp2[b] = d2;
+#endif
+        T[b] = Tf;
+        s[b] = Tf * (a.bg[0] * d0 + a.bg[1] * d1 + a.bg[2] * d2);
+        band_end[b] = uniform(wave_max_u32(lc));
+        max_c = max(max_c, band_end[b]);
+    }
     const uint2 range = a.ranges[tile];
     const uint32_t n = range.y - range.x;
-    const float T_final = inside ? a.final_T[pix_id] : 0.f;
-    const uint32_t last_contributor = inside ? a.n_contrib[pix_id] : 0u;
-    float dpix0 = 0.f, dpix1 = 0.f, dpix2 = 0.f;
-    if (inside) {
-        dpix0 = a.dL_dpix[pix_id];
-        dpix1 = a.dL_dpix[plane + pix_id];
-        dpix2 = a.dL_dpix[2 * plane + pix_id];
+    max_c = min(max_c, n);
+
+    // instances behind every pixel's last contributor: zero rows
+    for (uint32_t k = max_c + lane; k < n; k += TW_BATCH) {
+        const float4* rec = a.splat + (size_t)a.point_list[range.x + k] * SPLAT_F4;
+        zero_row(a.inst_grad, splat_slot(rec[0], rec[2], tl.tx, tl.ty));
     }
-    const float bg_dot = a.bg[0] * dpix0 + a.bg[1] * dpix1 + a.bg[2] * dpix2;
-    const float ddelx_dx = (float)(0.5 * a.W);
-    const float ddely_dy = (float)(0.5 * a.H);
-    // lane (l < 9) of a wave writes value slot slot_of_lane of the wave partial
+
+    const float half_w = 0.5f * (float)a.W, half_h = 0.5f * (float)a.H;  // ddelx_dx, ddely_dy (backward.cu:700-701)
     const uint32_t slot_of_lane = transposed_slot_of_lane(lane);
 
-    // positions >= wave_max_c are behind the last contributor of every pixel of the wave
-    uint32_t wave_max_c = last_contributor;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) wave_max_c = max(wave_max_c, (uint32_t)__shfl_xor((int)wave_max_c, o, 64));
-    if (lane == 0) s_wave_max_c[w] = wave_max_c;
-    // instances at positions >= max_c are behind every pixel's last contributor
-    const uint32_t max_c = min(n, block_max(last_contributor, s_tmp));  // (its barriers publish s_wave_max_c)
-
-    for (uint32_t k = max_c + t; k < n; k += BLOCK_SIZE) {
-        const float4* rec = a.splat + (size_t)a.point_list[range.x + k] * SPLAT_F4;
-        float* row = a.inst_grad + (size_t)splat_slot(rec[0], rec[2], tx, ty) * GRAD_ROW;
-#pragma unroll
-        for (int c = 0; c < GRAD_ROW; ++c) row[c] = 0.f;
-    }
-
-    float T = T_final;
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;  // accum_rec
-    float last_alpha = 0.f;
-    float lc0 = 0.f, lc1 = 0.f, lc2 = 0.f;  // last_color
-
-    // walk positions max_c-1 .. 0 in batches of BATCH, back to front
-    for (int hi = (int)max_c; hi > 0; hi -= BATCH) {
-        const int lo = max(0, hi - BATCH);
-        const int cnt = hi - lo;
-        // batch entry j <-> position hi-1-j
+    // positions max_c-1 .. 0, 64 per batch, back to front: batch entry `lane` <-> position hi-1-lane
+    for (int hi = (int)max_c; hi > 0; hi -= TW_BATCH) {
+        const int cnt = min(hi, TW_BATCH);
         uint32_t m = 0;
-        if ((int)t < cnt) {
-            const uint32_t pos = (uint32_t)(hi - 1 - (int)t);
+        float4 p, co, c;
+        uint32_t pos = 0, slot = 0;
+        if ((int)lane < cnt) {
+            pos = (uint32_t)(hi - 1 - (int)lane);
             const float4* rec = a.splat + (size_t)a.point_list[range.x + pos] * SPLAT_F4;  // one 64-B line
-            const float4 p = rec[0];
-            const float4 co = rec[1];
-            const float4 c = rec[2];
-            const float2 xy = {p.x, p.y};
-            s_xy[t] = xy;
-            s_co[t] = co;
-            s_rgb[t] = c;
-            s_slot[t] = splat_slot(p, c, tx, ty);
-            m = band_mask(xy, co, tx, ty);
+            p = rec[0];
+            co = rec[1];
+            c = rec[2];
+            slot = splat_slot(p, c, tl.tx, tl.ty);
+            m = band_mask(make_float2(p.x, p.y), co, tl.tx, tl.ty);
 #pragma unroll
-            for (int b = 0; b < WAVES; ++b)
-                if (pos >= s_wave_max_c[b]) m &= ~(1u << b);
-            s_mask[t] = m;
+            for (int b = 0; b < TW_BANDS; ++b)
+                if (pos >= band_end[b]) m &= ~(1u << b);
+            if (m == 0) zero_row(a.inst_grad, slot);
         }
-        s_lists.build(m, t);
-        const uint32_t lcnt = s_lists.count(w);
-        const uint8_t* list = s_lists.idx[w];
-        for (uint32_t k4 = 0; k4 < lcnt; k4 += 4) {
-            const uint32_t packed = *reinterpret_cast<const uint32_t*>(list + k4);
+        const uint64_t useful = __ballot(m != 0);
+        if (m != 0) {
+            const uint32_t r = mask_rank(useful);
+            const Quad q = quad_of_conic(co);
+            s_geo[r] = make_float4(p.x, p.y, __builtin_bit_cast(float, pos), __builtin_bit_cast(float, m));
+            s_quad[r] = make_float4(q.qa, q.qb, q.qc, co.w);
+            s_rgb[r] = make_float4(c.x, c.y, c.z, __builtin_bit_cast(float, slot));
+        }
+        wave_sync();  // orders this wave's LDS stores before its reads below
+        const uint32_t nuse = (uint32_t)__popcll(useful);
+        for (uint32_t j = 0; j < nuse; ++j) {
+            const float4 g = s_geo[j];
+            const float4 qo = s_quad[j];
+            const float4 f = s_rgb[j];
+            const uint32_t mb = uniform(__builtin_bit_cast(uint32_t, g.w));
+            const uint32_t ipos = __builtin_bit_cast(uint32_t, g.z);
+            const Quad q = {qo.x, qo.y, qo.z};
+            const float dx = g.x - pxf;
+            const float dy0 = g.y - (float)tl.py0;
+            float su = 0.f, sux = 0.f, suy = 0.f, suxx = 0.f, suxy = 0.f, suyy = 0.f;
+            float sc0 = 0.f, sc1 = 0.f, sc2 = 0.f;
+            bool any = false;
 #pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) {
-                if (k4 + u >= lcnt) break;
-                const uint32_t j = (packed >> (8 * u)) & 0xffu;
-                const uint32_t pos = (uint32_t)(hi - 1) - j;
-                float* part = s_part[w][j];
-                const float2 xy = s_xy[j];
-                const float4 co = s_co[j];
-                const float dx = xy.x - pxf, dy = xy.y - pyf;
-                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                const float G = __expf(power);
-                const float alpha = fminf(0.99f, co.w * G);
-                // reference: skip if contributor >= last_contributor, power > 0 or alpha < 1/255
-                const bool contrib = pos < last_contributor && power <= 0.0f && alpha >= 1.0f / 255.0f;
-                if (__ballot(contrib) == 0ull) {
-                    if (lane < GRAD_ROW) part[lane] = 0.f;
-                    continue;
-                }
-                const float4 c = s_rgb[j];
-                const float inv = __builtin_amdgcn_rcpf(1.f - alpha);
-                const float Tn = T * inv;
-                const float dchannel_dcolor = alpha * Tn;
-                const float n0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
-                const float n1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
-                const float n2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
-                float dL_dalpha = ((c.x - n0) * dpix0 + (c.y - n1) * dpix1 + (c.z - n2) * dpix2) * Tn;
-                dL_dalpha += (-T_final * inv) * bg_dot;
-                const float dL_dG = co.w * dL_dalpha;
-                const float gdx = G * dx;
-                const float gdy = G * dy;
-                float v[8];
-                v[0] = dL_dG * (-gdx * co.x - gdy * co.y) * ddelx_dx;
-                v[1] = dL_dG * (-gdy * co.z - gdx * co.y) * ddely_dy;
-                v[2] = -0.5f * gdx * dx * dL_dG;
-                v[3] = -0.5f * gdx * dy * dL_dG;
-                v[4] = -0.5f * gdy * dy * dL_dG;
-                v[5] = G * dL_dalpha;
-                v[6] = dchannel_dcolor * dpix0;
-                v[7] = dchannel_dcolor * dpix1;
-                float v8 = dchannel_dcolor * dpix2;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) v[q] = contrib ? v[q] : 0.f;
-                v8 = contrib ? v8 : 0.f;
-                T = contrib ? Tn : T;
-                acc0 = contrib ? n0 : acc0;
-                acc1 = contrib ? n1 : acc1;
-                acc2 = contrib ? n2 : acc2;
-                lc0 = contrib ? c.x : lc0;
-                lc1 = contrib ? c.y : lc1;
-                lc2 = contrib ? c.z : lc2;
-                last_alpha = contrib ? alpha : last_alpha;
-                float t8;
-                const float tv = wave_sum8_transposed(v, v8, lane, &t8);
-                if (lane < GRAD_ROW) part[slot_of_lane] = lane < 8 ? tv : t8;
+            for (int b = 0; b < TW_BANDS; ++b) {
+                if (!(mb & (1u << b))) continue;  // scalar branch
+#if OMR_BWD_PIX_LDS
+                const float4 pxd = s_pix[b * 64 + lane];
+                const float dp0b = pxd.x, dp1b = pxd.y, dp2b = pxd.z;
+                const uint32_t lastb = __builtin_bit_cast(uint32_t, pxd.w);
+#else
+                const float dp0b = dp0[b], dp1b = dp1[b], dp2b = dp2[b];
+                const uint32_t lastb = last[b];
+#endif
+                const float dy = dy0 - (float)(4 * b);
+                const float p2 = falloff_p2(q, dx, dy);
+                const float G = __builtin_amdgcn_exp2f(p2);
+                const float alpha = fminf(0.99f, qo.w * G);
+                // backward.cu:770-781: skip positions at/after the pixel's last contributor, power > 0, alpha < 1/255
+                const bool contrib = ipos < lastb && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
+                if (!__ballot(contrib)) continue;
+                any = true;
+                const float inv = __builtin_amdgcn_rcpf(1.0f - alpha);
+                const float Ti = T[b] * inv;
+                const float cdot = __builtin_fmaf(f.x, dp0b, __builtin_fmaf(f.y, dp1b, f.z * dp2b));
+                const float dL_dalpha = contrib ? __builtin_fmaf(Ti, cdot, -s[b] * inv) : 0.0f;
+                const float wc = contrib ? alpha * Ti : 0.0f;  // dchannel/dcolour (backward.cu:800)
+                s[b] = __builtin_fmaf(cdot, wc, s[b]);
+                T[b] = contrib ? Ti : T[b];
+                const float u = G * dL_dalpha;  // = dL/dopacity contribution; dL/dG * G = opacity * u
+                const float ux = u * dx, uy = u * dy;
+                su += u;
+                sux += ux;
+                suy += uy;
+                suxx = __builtin_fmaf(ux, dx, suxx);
+                suxy = __builtin_fmaf(ux, dy, suxy);
+                suyy = __builtin_fmaf(uy, dy, suyy);
+                sc0 = __builtin_fmaf(wc, dp0b, sc0);
+                sc1 = __builtin_fmaf(wc, dp1b, sc1);
+                sc2 = __builtin_fmaf(wc, dp2b, sc2);
             }
-        }
-        __syncthreads();
-        // one row per instance: the sum of the partials of the waves whose list held it
-        if ((int)t < cnt) {
-            const uint32_t mt = s_mask[t];
-            float* row = a.inst_grad + (size_t)s_slot[t] * GRAD_ROW;
-#pragma unroll
-            for (int c = 0; c < GRAD_ROW; ++c) {
-                float v = 0.f;
-#pragma unroll
-                for (int q = 0; q < WAVES; ++q) v += (mt >> q) & 1u ? s_part[q][t][c] : 0.f;
-                row[c] = v;
+            const uint32_t slot_j = __builtin_bit_cast(uint32_t, f.w);
+            float* row = a.inst_grad + (size_t)slot_j * GRAD_ROW;
+            if (!uniform(any)) {
+                if (lane < GRAD_ROW) row[lane] = 0.f;
+                continue;
             }
+            // per-instance factors of backward.cu:805-840 (dG/ddelx = -G (dx a + dy b), ...)
+            // conic (a, b, c) back from the staged quadratic form: q = (-a/2, -b, -c/2) log2(e)
+            const float ca = q.qa * (-2.0f / LOG2E), cb = q.qb * (-1.0f / LOG2E), cc = q.qc * (-2.0f / LOG2E);
+            const float o = qo.w;
+            float v[8];
+            v[0] = -o * half_w * (ca * sux + cb * suy);  // dL/dmean2D.x
+            v[1] = -o * half_h * (cc * suy + cb * sux);  // dL/dmean2D.y
+            v[2] = -0.5f * o * suxx;                           // dL/dconic.x
+            v[3] = -0.5f * o * suxy;                           // dL/dconic.y (the reference's half-weight slot)
+            v[4] = -0.5f * o * suyy;                           // dL/dconic.w
+            v[5] = su;                                         // dL/dopacity
+            v[6] = sc0;                                        // dL/dcolour
+            v[7] = sc1;
+            float t8;
+            const float tv = wave_sum8_transposed(v, sc2, lane, &t8);
+            if (lane < GRAD_ROW) row[slot_of_lane] = lane < 8 ? tv : t8;
         }
-        __syncthreads();
+        wave_sync();  // the next batch overwrites the staging arrays
     }
+    OMR_STAMP_END(g_stamps_bwd, tile);
 }
 
 }  // namespace
+
+#ifdef OMR_STAMPS
+int omr_debug_stamps_bwd(uint64_t* dst, size_t bytes)
+{
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps_bwd), bytes);
+}
+#endif
 
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s)
 {
     const uint32_t T = a.gx * a.gy;
     if (T == 0) return;
-    render_bwd_kernel<<<T, BLOCK_SIZE, 0, s>>>(a);
+    render_bwd_kernel<<<div_up(T, TW_WAVES), 64 * TW_WAVES, 0, s>>>(a);
 }
 
 }  // namespace omr

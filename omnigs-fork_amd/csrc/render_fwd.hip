@@ -1,121 +1,175 @@
 // render_fwd.hip — per-tile front-to-back alpha blending, gfx950.
 //
-// Follows cuda_rasterizer/forward.cu:346-467 (renderCUDA) and :472-590 (renderDepthCUDA): one 16x16 tile per
-// 256-thread workgroup (four wave64s, each 16 px x 4 rows), one pixel per thread, instances of the tile's
-// sorted range fetched 256 at a time into LDS, block-vote early exit when every pixel saturated.
+// Follows cuda_rasterizer/forward.cu:346-467 (renderCUDA) and :472-590 (renderDepthCUDA): per pixel, walk the
+// tile's depth-sorted instances front to back; skip power > 0 and alpha < 1/255; stop (without blending) once
+// T * (1 - alpha) < 1e-4; C += feature * alpha * T; record the last contributor; out = C + T * bg.
 //
-// Differences from the reference kernel (results identical up to the exp() implementation):
-//  * the colour of each instance is staged in LDS with its centre and conic (the reference re-reads
-//    features[] from global memory inside the per-pixel loop, forward.cu:447-448);
-//  * blockIdx is remapped so that consecutive tiles (which share most of their Gaussians) run on the same
-//    XCD and hit the same L2 (MI355X: 8 XCDs, blocks b and b+8 share one);
-//  * exp uses the hardware v_exp_f32 path (__expf);
-//  * each staged instance carries a 4-bit mask of the 16x4 wave bands its alpha >= 1/255 ellipse reaches
-//    (band_mask, raster_common.h); the batch is compacted into one ordered list per band (band_lists.h) and
-//    each wave walks only its own list, four instances per step with predicated (branch-free) blending.
-// HBM per tile instance: 4 (point_list) + 40 of the Gaussian's 64-B render record (xy, conic/opacity, rgb:
-// one random line, raster_common.h) gathered;
+// Structure (MI355X): ONE wave64 per 16x16 tile, four pixels per lane (one per 16x4 band, tile_wave.h).
+//  * Batches of 64 instances: each lane gathers one instance (point_list entry + the Gaussian's 64-B render
+//    record, raster_common.h), computes the bands its alpha >= 1/255 ellipse can reach (band_mask) and, if any,
+//    stages it in LDS at its ballot rank — a compacted, order-preserving list of the batch's useful instances.
+//  * The wave then walks that list; for each instance the band mask is wave-uniform (readfirstlane), so
+//    unreachable bands cost one scalar branch and reachable ones ~20 VALU per lane.
+//  * A band whose 64 pixels are all saturated leaves the active set; the tile exits when none is left.
+//  * No workgroup barriers (the block is one wave); XCD-aware tile order (tile_wave.h).
+// Results are those of the reference up to the exp implementation (v_exp_f32 on log2(e)-scaled powers).
+// HBM per tile instance: 4 (point_list) + 48 of the Gaussian's 64-B record (one random line);
 // per pixel: 12 (colour) + 4 (final_T) + 4 (n_contrib) = 20 B written.
-#include "band_lists.h"
+#include <algorithm>
+
 #include "kernels.h"
+#include "tile_wave.h"
 
 namespace omr {
 
 namespace {
 
-// bijective XCD-aware remap: blocks that share an XCD (orig % 8 equal) get consecutive logical ids
-__device__ __forceinline__ uint32_t xcd_remap(uint32_t orig, uint32_t nwg)
-{
-    const uint32_t q = nwg / 8, r = nwg % 8, xcd = orig % 8;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
-}
+#ifndef OMR_FWD_BANDS
+#define OMR_FWD_BANDS 2
+#endif
+// bands per wave: 4 = one wave per tile; 2 or 1 split a tile over 2 or 4 independent waves (shorter work
+// units for load balance; each wave stages the tile's instances itself)
+#ifndef OMR_FWD_MINW
+#define OMR_FWD_MINW 8
+#endif
+#ifndef OMR_FWD_PREFETCH
+#define OMR_FWD_PREFETCH 0
+#endif
+constexpr int FWD_BANDS = OMR_FWD_BANDS;
+constexpr int FWD_GROUPS = TW_BANDS / FWD_BANDS;
+
+OMR_STAMP_DECL(g_stamps_fwd)
 
 template <bool DEPTH>
-__global__ __launch_bounds__(BLOCK_SIZE) void render_fwd_kernel(RenderFwdArgs a)
+__global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel(RenderFwdArgs a)
 {
-    __shared__ float2 s_xy[BLOCK_SIZE];
-    __shared__ float4 s_co[BLOCK_SIZE];
-    __shared__ float4 s_rgb[BLOCK_SIZE];
-    __shared__ BandLists<BLOCK_SIZE> s_lists;
+    __shared__ float4 s_geo_all[TW_WAVES][TW_BATCH];  // x, y, position in range (u32 bits), band mask (u32 bits)
+    __shared__ float4 s_quad_all[TW_WAVES][TW_BATCH]; // qa, qb, qc, opacity
+    __shared__ float4 s_rgb_all[TW_WAVES][TW_BATCH];  // feature (colour, or depth for DEPTH)
 
-    const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
-    const uint32_t tx = tile % a.gx, ty = tile / a.gx;
-    const uint32_t t = threadIdx.x;
-    const uint32_t w = t >> 6;
-    const uint32_t px = tx * BLOCK_X + (t & (BLOCK_X - 1));
-    const uint32_t py = ty * BLOCK_Y + (t / BLOCK_X);
-    const bool inside = px < (uint32_t)a.W && py < (uint32_t)a.H;
-    const uint32_t pix_id = a.W * py + px;
-    const float pxf = (float)px, pyf = (float)py;
+    OMR_STAMP_BEGIN
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t unit = xcd_remap(blockIdx.x, gridDim.x) * TW_WAVES + wv;
+    if (unit >= a.gx * a.gy * FWD_GROUPS) return;  // wave-uniform; the block's waves never synchronise
+    float4* s_geo = s_geo_all[wv];
+    float4* s_quad = s_quad_all[wv];
+    float4* s_rgb = s_rgb_all[wv];
+#ifdef OMR_NO_TILE_ORDER
+    const uint32_t tile = unit / FWD_GROUPS;
+#else
+    const uint32_t tile = a.tile_order[unit / FWD_GROUPS];
+#endif
+    const uint32_t band0 = (unit % FWD_GROUPS) * FWD_BANDS;  // this wave's bands: band0 .. band0 + FWD_BANDS - 1
+    const TileLane tl(tile, a.gx);
+    const uint32_t lane = tl.lane;
+    const float pxf = (float)tl.px;
+
+    bool done[FWD_BANDS];
+    float T[FWD_BANDS], C0[FWD_BANDS], C1[FWD_BANDS], C2[FWD_BANDS];
+    uint32_t last[FWD_BANDS];
+    uint32_t active = 0;  // local bands with at least one unsaturated in-image pixel (wave-uniform)
+    uint32_t work = 0;    // (instance, band) pairs evaluated: the backward's schedule key
+#pragma unroll
+    for (int b = 0; b < FWD_BANDS; ++b) {
+        const bool inside = tl.px < (uint32_t)a.W && tl.py(band0 + b) < (uint32_t)a.H;
+        done[b] = !inside;
+        T[b] = 1.0f;
+        C0[b] = C1[b] = C2[b] = 0.f;
+        last[b] = 0;
+        if (__ballot(inside)) active |= 1u << b;
+    }
 
     const uint2 range = a.ranges[tile];
-    const int n = (int)(range.y - range.x);
-    bool done = !inside;
-    float T = 1.0f;
-    float C0 = 0.f, C1 = 0.f, C2 = 0.f;
-    uint32_t last_contributor = 0;
-
-    for (int start = 0; start < n; start += BLOCK_SIZE) {
-        if (__syncthreads_count(done) == BLOCK_SIZE) break;
-        const int k = start + (int)t;
+    const uint32_t n = range.y - range.x;
+    for (uint32_t start = 0; start < n && active; start += TW_BATCH) {
+        const uint32_t k = start + lane;
         uint32_t m = 0;
+        float4 pos, co, c;
         if (k < n) {
             const uint32_t gid = a.point_list[range.x + k];
             const float4* rec = a.splat + (size_t)gid * SPLAT_F4;  // one 64-B record per instance
-            const float4 pos = rec[0];
-            const float4 co = rec[1];
-            const float2 xy = {pos.x, pos.y};
-            s_xy[t] = xy;
-            s_co[t] = co;
-            m = band_mask(xy, co, tx, ty);
-            if (DEPTH) {
-                s_rgb[t] = make_float4(pos.z, pos.z, pos.z, 0.f);
-            } else {
-                s_rgb[t] = rec[2];
-            }
+            pos = rec[0];
+            co = rec[1];
+            c = DEPTH ? make_float4(pos.z, pos.z, pos.z, 0.f) : rec[2];
+            m = (band_mask(make_float2(pos.x, pos.y), co, tl.tx, tl.ty) >> band0) & active;
         }
-        s_lists.build(m, t);
-        // this wave's instances, in front-to-back order, 4 per step; the math is predicated (no per-lane
-        // branches): a lane that is done, or an entry past the end of the list, changes nothing
-        const uint32_t cnt = s_lists.count(w);
-        const uint8_t* list = s_lists.idx[w];
-        for (uint32_t k4 = 0; k4 < cnt; k4 += 4) {
-            if (__ballot(!done) == 0ull) break;  // every pixel of the wave saturated
-            const uint32_t packed = *reinterpret_cast<const uint32_t*>(list + k4);
+        const uint64_t useful = __ballot(m != 0);
+        if (m != 0) {
+            const uint32_t r = mask_rank(useful);
+            const Quad q = quad_of_conic(co);
+            s_geo[r] = make_float4(pos.x, pos.y, __builtin_bit_cast(float, k), __builtin_bit_cast(float, m));
+            s_quad[r] = make_float4(q.qa, q.qb, q.qc, co.w);
+            s_rgb[r] = c;
+        }
+        wave_sync();  // orders this wave's LDS stores before its reads below
+        const uint32_t cnt = (uint32_t)__popcll(useful);
+        float4 g = s_geo[0], qo = s_quad[0], f = s_rgb[0];
+        for (uint32_t j = 0; j < cnt; ++j) {
+#if OMR_FWD_PREFETCH
+            // prefetch the next entry (index 63 at most; an entry past cnt is read but never used)
+            const uint32_t jn = min(j + 1, (uint32_t)TW_BATCH - 1);
+            const float4 gn = s_geo[jn], qn = s_quad[jn], fn = s_rgb[jn];
+#else
+            g = s_geo[j];
+            qo = s_quad[j];
+            f = s_rgb[j];
+#endif
+            const uint32_t mb = uniform(__builtin_bit_cast(uint32_t, g.w)) & active;
+            work += (uint32_t)__builtin_popcount(mb);
+            const uint32_t contributor = __builtin_bit_cast(uint32_t, g.z) + 1u;
+            const Quad q = {qo.x, qo.y, qo.z};
+            const float dx = g.x - pxf;
+            const float dy0 = g.y - (float)tl.py(band0);
+            bool sat_any = false;
 #pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) {
-                const uint32_t j = (packed >> (8 * u)) & 0xffu;
-                const float2 xy = s_xy[j];
-                const float4 co = s_co[j];
-                const float4 c = s_rgb[j];
-                const float dx = xy.x - pxf, dy = xy.y - pyf;
-                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                const float alpha = fminf(0.99f, co.w * __expf(power));
-                // forward.cu:424-452: skip power > 0 and alpha < 1/255; stop (without blending) when
-                // T * (1 - alpha) < 1e-4
-                bool ok = !done && k4 + u < cnt && power <= 0.0f && alpha >= 1.0f / 255.0f;
-                const float test_T = T * (1.0f - alpha);
+            for (int b = 0; b < FWD_BANDS; ++b) {
+                if (!(mb & (1u << b))) continue;  // scalar branch
+                const float dy = dy0 - (float)(4 * b);
+                const float p2 = falloff_p2(q, dx, dy);
+                const float alpha = fminf(0.99f, qo.w * __builtin_amdgcn_exp2f(p2));
+                bool ok = !done[b] && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
+                const float test_T = T[b] * (1.0f - alpha);
                 const bool sat = ok && test_T < 0.0001f;
-                done = done || sat;
+                done[b] = done[b] || sat;
+                sat_any = sat_any || sat;
                 ok = ok && !sat;
-                // selects, not multiplies by 0: entries past the end of the list may hold stale LDS words
-                const float wgt = alpha * T;
-                C0 = ok ? C0 + c.x * wgt : C0;
-                C1 = ok ? C1 + c.y * wgt : C1;
-                C2 = ok ? C2 + c.z * wgt : C2;
-                T = ok ? test_T : T;
-                last_contributor = ok ? (uint32_t)(start + (int)j + 1) : last_contributor;
+                const float wgt = ok ? alpha * T[b] : 0.0f;
+                C0[b] = __builtin_fmaf(f.x, wgt, C0[b]);
+                C1[b] = __builtin_fmaf(f.y, wgt, C1[b]);
+                C2[b] = __builtin_fmaf(f.z, wgt, C2[b]);
+                T[b] = ok ? test_T : T[b];
+                last[b] = ok ? contributor : last[b];
             }
+            if (__ballot(sat_any)) {  // some pixel saturated: drop bands with no live pixel left
+#pragma unroll
+                for (int b = 0; b < FWD_BANDS; ++b)
+                    if (!__ballot(!done[b])) active &= ~(1u << b);
+                if (!active) break;
+            }
+#if OMR_FWD_PREFETCH
+            g = gn;
+            qo = qn;
+            f = fn;
+#endif
+        }
+        wave_sync();  // the next batch overwrites the staging arrays
+    }
+
+    const size_t plane = (size_t)a.H * a.W;
+#pragma unroll
+    for (int b = 0; b < FWD_BANDS; ++b) {
+        const uint32_t py = tl.py(band0 + b);
+        if (tl.px < (uint32_t)a.W && py < (uint32_t)a.H) {
+            const uint32_t pix = a.W * py + tl.px;
+            a.final_T[pix] = T[b];
+            a.n_contrib[pix] = last[b];
+            a.out_color[pix] = C0[b] + T[b] * a.bg[0];
+            a.out_color[plane + pix] = C1[b] + T[b] * a.bg[1];
+            a.out_color[2 * plane + pix] = C2[b] + T[b] * a.bg[2];
         }
     }
-    if (inside) {
-        a.final_T[pix_id] = T;
-        a.n_contrib[pix_id] = last_contributor;
-        const size_t plane = (size_t)a.H * a.W;
-        a.out_color[pix_id] = C0 + T * a.bg[0];
-        a.out_color[plane + pix_id] = C1 + T * a.bg[1];
-        a.out_color[2 * plane + pix_id] = C2 + T * a.bg[2];
-    }
+    if (lane == 0 && work) atomicAdd(&a.tile_cost[tile], work);
+    OMR_STAMP_END(g_stamps_fwd, unit);
 }
 
 }  // namespace
@@ -124,8 +178,19 @@ void launch_render_forward(const RenderFwdArgs& a, bool depth_mode, hipStream_t 
 {
     const uint32_t T = a.gx * a.gy;
     if (T == 0) return;
-    if (depth_mode) render_fwd_kernel<true><<<T, BLOCK_SIZE, 0, s>>>(a);
-    else render_fwd_kernel<false><<<T, BLOCK_SIZE, 0, s>>>(a);
+    const uint32_t units = T * FWD_GROUPS;
+    const uint32_t blocks = div_up(units, TW_WAVES);
+    if (depth_mode) render_fwd_kernel<true><<<blocks, 64 * TW_WAVES, 0, s>>>(a);
+    else render_fwd_kernel<false><<<blocks, 64 * TW_WAVES, 0, s>>>(a);
 }
+
+#ifdef OMR_STAMPS
+extern "C" int omr_debug_stamps(int which, uint64_t* dst, int n)
+{
+    const size_t bytes = (size_t)std::min(n, STAMP_CAP) * 4 * sizeof(uint64_t);
+    return which == 0 ? (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps_fwd), bytes)
+                      : (int)omr_debug_stamps_bwd(dst, bytes);
+}
+#endif
 
 }  // namespace omr

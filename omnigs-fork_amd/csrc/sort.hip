@@ -259,7 +259,57 @@ __global__ __launch_bounds__(256) void tile_ranges_kernel(size_t L, const uint32
     if (idx == L - 1) ranges[curr].y = (uint32_t)L;
 }
 
+// Longest-first render schedule. The render kernels run one wave per tile (or half tile) and launch more waves
+// than the chip holds at once; dispatching the costly tiles first keeps the SIMDs busy to the end instead of
+// leaving a tail of late heavy tiles. Block c sorts the c-th of 8 contiguous shares of [0, T) — the share the
+// render kernels' xcd_remap places on XCD c, so L2 locality is unchanged — by a 256-bucket counting sort on the
+// cost, descending. Cost = the tile's instance count (forward) or the (instance, band) work the forward measured
+// (backward). The order of equal-bucket tiles depends on LDS atomics, which is harmless: every tile is rendered
+// the same way whenever it runs.
+constexpr int ORDER_THREADS = 1024;
+__device__ __forceinline__ uint32_t tile_cost(const uint2* ranges, const uint32_t* cost, uint32_t i)
+{
+    return cost ? cost[i] : ranges[i].y - ranges[i].x;
+}
+__global__ __launch_bounds__(ORDER_THREADS) void tile_order_kernel(const uint2* ranges, const uint32_t* cost, uint32_t T,
+                                                                   uint32_t* order)
+{
+    __shared__ uint32_t s_hist[RADIX];
+    __shared__ uint32_t s_max;
+    const uint32_t lo = (uint32_t)(((uint64_t)T * blockIdx.x) / gridDim.x);
+    const uint32_t hi = (uint32_t)(((uint64_t)T * (blockIdx.x + 1)) / gridDim.x);
+    if (threadIdx.x < RADIX) s_hist[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_max = 0;
+    __syncthreads();
+    uint32_t mx = 0;
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += ORDER_THREADS) mx = max(mx, tile_cost(ranges, cost, i));
+    atomicMax(&s_max, mx);
+    __syncthreads();
+    const uint64_t scale = (uint64_t)s_max + 1;
+    auto bucket = [&](uint32_t i) {  // 0 = costliest
+        return (uint32_t)(RADIX - 1) - (uint32_t)(((uint64_t)tile_cost(ranges, cost, i) * RADIX) / scale);
+    };
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += ORDER_THREADS) atomicAdd(&s_hist[bucket(i)], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {  // 256-entry exclusive scan
+        uint32_t run = lo;
+        for (int b = 0; b < RADIX; ++b) {
+            const uint32_t c = s_hist[b];
+            s_hist[b] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += ORDER_THREADS) order[atomicAdd(&s_hist[bucket(i)], 1u)] = i;
+}
+
 }  // namespace
+
+void launch_tile_order(const uint2* ranges, const uint32_t* cost, uint32_t T, uint32_t* order, hipStream_t s)
+{
+    if (T == 0) return;
+    tile_order_kernel<<<min(T, 8u), ORDER_THREADS, 0, s>>>(ranges, cost, T, order);
+}
 
 size_t scan_partials_size(size_t n) { return div_up(n, SCAN_TILE) + 1; }
 

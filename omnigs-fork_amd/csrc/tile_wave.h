@@ -1,0 +1,107 @@
+// tile_wave.h — shared pieces of the one-wave-per-tile render kernels (render_fwd.hip, render_bwd.hip).
+//
+// Layout: one wave64 owns one 16x16 tile. Lane l owns pixel column l % 16 and, in each of the four 16x4 bands
+// b = 0..3 of the tile, the pixel row 4b + l / 16: four pixels per lane, one per band. An instance's band mask
+// (band_mask, raster_common.h) is therefore wave-uniform, and a band the instance cannot reach is skipped with a
+// scalar branch. Per instance, the per-lane work is amortised over up to four pixels and, in the backward, the
+// wave reduction of the gradient row over up to 256 pixels happens once.
+#pragma once
+
+#include "raster_common.h"
+
+namespace omr {
+
+constexpr int TW_BANDS = 4;       // 16x4 bands per 16x16 tile = pixels per lane
+constexpr int TW_BATCH = 64;      // instances staged per batch (one per lane)
+constexpr float LOG2E = 1.4426950408889634f;
+
+// Gaussian falloff in base 2: p2 = log2(e) * power, power = -1/2 (a dx^2 + c dy^2) - b dx dy
+// (forward.cu:434 / backward.cu:774). The staging lane folds -1/2 and log2(e) into q = {qa, qb, qc} once per
+// instance, so each (pixel, instance) pair costs four VALU ops before v_exp_f32. Forward and backward evaluate
+// exactly this expression, so they take identical contribute / skip decisions.
+struct Quad {
+    float qa, qb, qc;
+};
+__device__ __forceinline__ Quad quad_of_conic(float4 co)
+{
+    return {-0.5f * LOG2E * co.x, -LOG2E * co.y, -0.5f * LOG2E * co.z};
+}
+__device__ __forceinline__ float falloff_p2(const Quad& q, float dx, float dy)
+{
+    return __builtin_fmaf(dx, __builtin_fmaf(q.qa, dx, q.qb * dy), q.qc * dy * dy);
+}
+
+// one lane's view of a tile: pixel coordinates of its band pixels; band b of the tile = rows 4b..4b+3
+struct TileLane {
+    uint32_t tx, ty, lane;
+    uint32_t px, py0;  // band b pixel = (px, py0 + 4b)
+    __device__ __forceinline__ TileLane(uint32_t tile, uint32_t gx)
+    {
+        tx = tile % gx;
+        ty = tile / gx;
+        lane = threadIdx.x & 63u;
+        px = tx * BLOCK_X + (lane & (BLOCK_X - 1));
+        py0 = ty * BLOCK_Y + (lane / BLOCK_X);
+    }
+    __device__ __forceinline__ uint32_t py(int b) const { return py0 + 4u * (uint32_t)b; }
+};
+
+// bijective XCD-aware remap: blocks that share an XCD (orig % 8 equal) get consecutive logical ids, so
+// neighbouring tiles (which share most of their Gaussians) hit the same L2 (MI355X: 8 XCDs, block b -> XCD b % 8)
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t orig, uint32_t nwg)
+{
+    const uint32_t q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// ---- diagnostic wave timeline (build with -DOMR_STAMPS only; profiles/wave_timeline.py) ---------------------
+// per wave: [0] s_memrealtime at start (100 MHz), [1] at end, [2] HW_ID | XCC_ID << 32, [3] unit index
+#ifdef OMR_STAMPS
+constexpr int STAMP_CAP = 1 << 17;
+#define OMR_STAMP_DECL(name) __device__ uint64_t name[STAMP_CAP][4];
+#define OMR_STAMP_BEGIN const uint64_t stamp_t0_ = __builtin_amdgcn_s_memrealtime();
+#define OMR_STAMP_END(arr, unit)                                                                          \
+    do {                                                                                                 \
+        const uint64_t t1_ = __builtin_amdgcn_s_memrealtime();                                            \
+        if ((threadIdx.x & 63) == 0 && (unit) < (uint32_t)STAMP_CAP) {                                    \
+            arr[unit][0] = stamp_t0_;                                                                     \
+            arr[unit][1] = t1_;                                                                           \
+            arr[unit][2] = (uint64_t)__builtin_amdgcn_s_getreg(63492) |                                   \
+                           ((uint64_t)__builtin_amdgcn_s_getreg(63508) << 32);                            \
+            arr[unit][3] = (unit);                                                                        \
+        }                                                                                                \
+    } while (0)
+#else
+#define OMR_STAMP_DECL(name)
+#define OMR_STAMP_BEGIN
+#define OMR_STAMP_END(arr, unit) \
+    do {                         \
+    } while (0)
+#endif
+
+// Several independent waves share one workgroup (TW_WAVES tiles per block): gfx950 caps resident workgroups per
+// CU, so one-wave workgroups would cap occupancy at a few waves per SIMD. The waves never synchronise with each
+// other; each orders its own LDS staging with wave_sync().
+#ifndef OMR_TW_WAVES
+#define OMR_TW_WAVES 1
+#endif
+constexpr int TW_WAVES = OMR_TW_WAVES;
+__device__ __forceinline__ void wave_sync()
+{
+    // LDS operations of one wave complete in issue order; this keeps the compiler from moving LDS accesses
+    // across the staging boundary
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+}  // namespace omr
