@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, Chip-level parameters)
+DOMINANT = "render_backward"  # the kernel the roofline reports (largest stage at every config)
 
 
 def parse():
@@ -39,6 +40,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-oracle sample budget")
     p.add_argument("--cpu-threads", type=int, default=None)
     p.add_argument("--bucket-mb", type=float, default=0.0, help="all-reduce bucket size (0 = one collective)")
+    p.add_argument("--boundary", choices=["ctypes", "libtorch"], default="ctypes",
+                   help="ctypes: Python host on the C ABI (writes grads into the flat all-reduce buffer); libtorch: "
+                        "the rasterize_points.h drop-in (librasterize_points.so) through its pybind module")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     return p.parse_args()
 
@@ -127,7 +131,26 @@ def main():
     bucket = int(args.bucket_mb * 1024 * 1024)
     stats = {}
 
+    LT = R.libtorch_boundary() if args.boundary == "libtorch" else None
+
+    def step_libtorch():
+        nr, color, radii, gb, bb, ib = LT.RasterizeGaussiansCUDA(
+            bg, means3D, empty, opacity, scales, rots, 1.0, empty, view, proj, cam.tanfovx, cam.tanfovy, H, W, shs,
+            g.sh_degree, campos, False, cam.camera_type, False)
+        gr = LT.RasterizeGaussiansBackwardCUDA(bg, means3D, radii, empty, scales, rots, 1.0, empty, view, proj,
+                                               cam.tanfovx, cam.tanfovy, dL_dout, shs, g.sh_degree, campos, gb, nr, bb,
+                                               ib, cam.camera_type)
+        if world > 1:  # the drop-in allocates its own gradient tensors: gather them into the flat buffer
+            for name, idx in (("dL_dmeans3D", 3), ("dL_dsh", 5), ("dL_dopacity", 2), ("dL_dscales", 6),
+                              ("dL_drotations", 7)):
+                grads.views[name].copy_(gr[idx])
+        par.allreduce_(grads, info, average=False, bucket_bytes=bucket)
+        stats["L"] = nr
+        stats["radii"] = radii
+
     def step():
+        if LT is not None:
+            return step_libtorch()
         nr, color, radii, gb, bb, ib = R.RasterizeGaussiansCUDA(
             bg, means3D, empty, opacity, scales, rots, 1.0, empty, view, proj, cam.tanfovx, cam.tanfovy, H, W, shs,
             g.sh_degree, campos, False, cam.camera_type, False)
@@ -145,8 +168,11 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    # timed region: HIP events around the dominant kernel only (the roofline's live launch duration); events at
+    # every stage boundary would add a few us of GPU idle each, so the full per-stage breakdown comes from a
+    # separate pass after the timed one
     R.profile_reset()
-    R.profile_enable(True)
+    R.profile_enable(True, stages=[DOMINANT])
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -155,6 +181,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    R.profile_enable(False)
+    live = R.profile_read()
+    R.profile_reset()
+    R.profile_enable(True)
+    for _ in range(min(args.steps, 10)):
+        step()
+    torch.cuda.synchronize(dev)
     R.profile_enable(False)
     prof = R.profile_read()
     if V is None:
@@ -171,10 +204,10 @@ def main():
 
     # dominant kernel from the live stage timings (HIP events on the launch stream)
     stage_avg = {k: (ms / c if c else 0.0) for k, (ms, c) in prof.items()}
-    kernel_stages = ["render_forward", "render_backward", "gaussian_backward", "preprocess", "instance_reduce", "emit"]
-    dom = max(kernel_stages, key=lambda k: stage_avg.get(k, 0.0))
+    dom = DOMINANT
     dom_bytes = stage_bytes(dom, P, V, L, N, T, M, g.sh_degree)
-    dom_ms = stage_avg[dom]
+    ms, cnt = live.get(dom, (0.0, 0))
+    dom_ms = ms / cnt if cnt else stage_avg[dom]
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     traffic = None
     try:
@@ -202,7 +235,7 @@ def main():
                                f"{g.sh_degree}, one view per GPU" + (", RCCL sum all-reduce of 236 B/Gaussian "
                                                                     "gradients" if world > 1 else ""),
                    "P": P, "V": V, "L": L, "N": N, "T": T, "width": W, "height": H,
-                   "parallelism": f"view-parallel dp{world}"},
+                   "parallelism": f"view-parallel dp{world}", "boundary": args.boundary},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 4),

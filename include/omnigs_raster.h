@@ -114,6 +114,9 @@ size_t omr_binning_bytes(int num_rendered, int width, int height);
  *         7 render_backward, 8 gaussian_backward, 9 instance_reduce                                */
 #define OMR_NUM_STAGES 10
 void omr_profile_enable(int on);
+/* restrict recording to the stages whose bit (1 << stage) is set (default: all); each recorded stage costs a
+ * few microseconds of GPU idle at its boundaries, so a timed run records only the kernel it reports */
+void omr_profile_set_mask(uint32_t mask);
 void omr_profile_reset(void);
 /* waits for the recorded events; fills total milliseconds and launch counts per stage since the last reset;
  * returns the number of stages written (<= n) */

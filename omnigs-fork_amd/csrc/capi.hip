@@ -61,6 +61,7 @@ const char* kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "scan", "emit",
 
 struct Profiler {
     bool on = false;
+    uint32_t mask = ~0u;
     struct Rec {
         int stage;
         hipEvent_t a, b;
@@ -89,7 +90,7 @@ struct StageScope {
     hipEvent_t a = nullptr;
     StageScope(int st, hipStream_t stream) : stage(st), s(stream)
     {
-        if (g_prof.on) {
+        if (g_prof.on && (g_prof.mask >> st) & 1u) {
             a = g_prof.get();
             if (a) (void)hipEventRecord(a, s);
         }
@@ -114,6 +115,29 @@ uint32_t* pinned_words()
         if (hipHostMalloc(reinterpret_cast<void**>(&p), 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) p = nullptr;
     }
     return p;
+}
+
+// event recorded after the num_rendered copy (one per thread; the forward waits on it at most once per call)
+hipEvent_t count_event()
+{
+    thread_local hipEvent_t e = nullptr;
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    return e;
+}
+
+// per-thread capacity hint for the binning buffer, by view shape (L depends mostly on the resolution and camera)
+size_t& capacity_hint(int W, int H, int camera_type)
+{
+    struct Entry {
+        int W, H, cam;
+        size_t hint;
+    };
+    thread_local std::vector<Entry> table;
+    for (auto& e : table)
+        if (e.W == W && e.H == H && e.cam == camera_type) return e.hint;
+    if (table.size() >= 16) table.erase(table.begin());
+    table.push_back({W, H, camera_type, 0});
+    return table.back().hint;
 }
 
 }  // namespace
@@ -161,21 +185,21 @@ size_t ImageState::carve(char* base, size_t N, size_t T, ImageState* s)
     return c.size();
 }
 
-size_t BinningState::carve(char* base, size_t L, GeomState*, BinningState* s, int tile_passes)
+size_t BinningState::carve(char* base, size_t cap, BinningState* s, int tile_passes)
 {
     Carver c(base);
     BinningState b;
-    b.key_a = c.take<uint32_t>(L);
-    b.key_b = c.take<uint32_t>(L);
-    b.val_a = c.take<uint32_t>(L);
-    b.val_b = c.take<uint32_t>(L);
-    const size_t nh = radix_hist_size(L);
+    b.inst_grad = c.take<float>(cap * GRAD_ROW);
+    c.take<uint32_t>(cap);  // room for the canonical point list when L < cap (raster_common.h)
+    b.point_list = base ? reinterpret_cast<uint32_t*>(base + canonical_list_offset(cap)) : nullptr;
+    b.key_a = c.take<uint32_t>(cap);
+    b.key_b = c.take<uint32_t>(cap);
+    b.val_a = c.take<uint32_t>(cap);
+    b.val_b = c.take<uint32_t>(cap);
+    const size_t nh = radix_hist_size(cap);
     b.hist = c.take<uint32_t>(nh);
     b.scan_partials = c.take<uint32_t>(scan_partials_size(nh));
-    b.inst_grad = c.take<float>(L * GRAD_ROW);
-    const bool in_b = (tile_passes & 1) != 0;  // result buffer of the ping-pong
-    b.point_list = in_b ? b.val_b : b.val_a;
-    b.point_keys = in_b ? b.key_b : b.key_a;
+    b.point_keys = (tile_passes & 1) != 0 ? b.key_b : b.key_a;  // result buffer of the key ping-pong
     if (s) *s = b;
     return c.size();
 }
@@ -265,44 +289,77 @@ int forward_impl(const ForwardIn& in)
     { StageScope st_(ST_PREPROCESS, s); launch_preprocess(in.camera_type, pa, s); }
 
     // depth order of the Gaussians (stable: ties keep index order)
-    int which; { StageScope st_(ST_DEPTH_SORT, s); which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, 0, 4, s); }
+    int which; { StageScope st_(ST_DEPTH_SORT, s); which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr, nullptr, 0, 4, s); }
     g.order = which ? g.val_b : g.val_a;
     { StageScope st_(ST_SCAN, s); launch_inclusive_scan(g.tiles_touched, g.order, g.offsets, g.scan_partials, P, s); }
 
+    // num_rendered = offsets[P-1] (+ the prefiltered error flag) to pinned host memory, without waiting for it:
+    // the binning buffer is sized from a capacity hint and everything after the scan reads the count on the device,
+    // so the GPU never idles on this host round trip (the reference synchronises here, rasterizer_impl.cu:628).
+    // The host checks the count once the rest of the forward is queued; a hint that was too small costs one
+    // re-run of the back half with the exact size.
     uint32_t* host = pinned_words();
-    if (!host) return fail(OMR_ERR_HIP, "hipHostMalloc failed");
-    OMR_HIP(hipMemcpyAsync(host, g.offsets + (P - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    hipEvent_t ev_count = count_event();
+    if (!host || !ev_count) return fail(OMR_ERR_HIP, "pinned host memory / event allocation failed");
+    const uint32_t* count_dev = g.offsets + (P - 1);
+    OMR_HIP(hipMemcpyAsync(host, count_dev, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     OMR_HIP(hipMemcpyAsync(host + 1, g.counters + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    OMR_HIP(hipStreamSynchronize(s));
-    if (int e = hip_check("preprocess/sort/scan")) return e;
-    if (host[1] != 0)
-        return fail(OMR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
-    const size_t L = host[0];
+    OMR_HIP(hipEventRecord(ev_count, s));
 
     const int tile_passes = tile_sort_passes(d.T);
-    char* bin_base = static_cast<char*>(
-        in.binning_alloc(in.binning_ctx, BinningState::carve(nullptr, L, nullptr, nullptr, tile_passes)));
-    if (!bin_base) return fail(OMR_ERR_ALLOCATION, "binning allocation failed");
-    BinningState b;
-    BinningState::carve(bin_base, L, nullptr, &b, tile_passes);
+    size_t& hint = capacity_hint(in.width, in.height, in.camera_type);
+    bool known = false;
+    size_t L = 0;
+    auto wait_count = [&]() -> int {
+        OMR_HIP(hipEventSynchronize(ev_count));
+        if (int e = hip_check("preprocess/sort/scan")) return e;
+        if (host[1] != 0)
+            return fail(OMR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+        L = host[0];
+        known = true;
+        return OMR_OK;
+    };
+    if (hint == 0)  // first call for this view shape: learn L the reference's way
+        if (int e = wait_count()) return e;
+    size_t cap = known ? L : hint;
 
-    { StageScope st_(ST_EMIT, s); launch_emit_instances(in.P, L, g, d.gx, b.key_a, b.val_a, s); }
-    { StageScope st_(ST_TILE_SORT, s); radix_sort_pairs(b.key_a, b.key_b, b.val_a, b.val_b, b.hist, b.scan_partials, L, 0, tile_passes, s); }
-    OMR_HIP(hipMemsetAsync(im.ranges, 0, d.T * sizeof(uint2), s));
-    {
-        StageScope st_(ST_RANGES, s);
-        launch_tile_ranges(L, b.point_keys, im.ranges, s);
-        launch_tile_order(im.ranges, nullptr, d.T, im.tile_order, s);
+    auto back_half = [&](size_t capacity) -> int {
+        char* bin_base = static_cast<char*>(
+            in.binning_alloc(in.binning_ctx, BinningState::carve(nullptr, capacity, nullptr, tile_passes)));
+        if (!bin_base) return fail(OMR_ERR_ALLOCATION, "binning allocation failed");
+        BinningState b;
+        BinningState::carve(bin_base, capacity, &b, tile_passes);
+        { StageScope st_(ST_EMIT, s); launch_emit_instances(in.P, capacity, count_dev, g, d.gx, b.key_a, b.val_a, s); }
+        {
+            StageScope st_(ST_TILE_SORT, s);
+            radix_sort_pairs(b.key_a, b.key_b, b.val_a, b.val_b, b.hist, b.scan_partials, capacity, count_dev,
+                             bin_base, 0, tile_passes, s);
+        }
+        OMR_HIP(hipMemsetAsync(im.ranges, 0, d.T * sizeof(uint2), s));
+        {
+            StageScope st_(ST_RANGES, s);
+            launch_tile_ranges(capacity, count_dev, b.point_keys, im.ranges, s);
+            launch_tile_order(im.ranges, nullptr, d.T, im.tile_order, s);
+        }
+        OMR_HIP(hipMemsetAsync(im.tile_cost, 0, d.T * sizeof(uint32_t), s));
+        RenderFwdArgs ra;
+        ra.W = in.width; ra.H = in.height; ra.gx = d.gx; ra.gy = d.gy;
+        ra.ranges = im.ranges; ra.tile_order = im.tile_order; ra.binning = bin_base; ra.count = count_dev;
+        ra.splat = g.splat;
+        ra.bg = in.background; ra.tile_cost = im.tile_cost; ra.final_T = im.final_T; ra.n_contrib = im.n_contrib;
+        ra.out_color = in.out_color;
+        // lonlat never renders depth (rasterize_points.cu:133-156 passes render_depth to the pinhole path only)
+        { StageScope st_(ST_RENDER_FWD, s); launch_render_forward(ra, in.render_depth && in.camera_type == CAM_PINHOLE, s); }
+        return OMR_OK;
+    };
+    if (int e = back_half(cap)) return e;
+    if (!known)
+        if (int e = wait_count()) return e;
+    if (L > cap) {  // the hint was too small: redo the back half at the exact size (outputs are overwritten)
+        cap = L;
+        if (int e = back_half(cap)) return e;
     }
-    OMR_HIP(hipMemsetAsync(im.tile_cost, 0, d.T * sizeof(uint32_t), s));
-
-    RenderFwdArgs ra;
-    ra.W = in.width; ra.H = in.height; ra.gx = d.gx; ra.gy = d.gy;
-    ra.ranges = im.ranges; ra.tile_order = im.tile_order; ra.point_list = b.point_list;
-    ra.splat = g.splat;
-    ra.bg = in.background; ra.tile_cost = im.tile_cost; ra.final_T = im.final_T; ra.n_contrib = im.n_contrib; ra.out_color = in.out_color;
-    // lonlat never renders depth (rasterize_points.cu:133-156 passes render_depth to the pinhole path only)
-    { StageScope st_(ST_RENDER_FWD, s); launch_render_forward(ra, in.render_depth && in.camera_type == CAM_PINHOLE, s); }
+    hint = L + L / 8 + 4096;
     if (int e = hip_check("emit/sort/render")) return e;
     if (in.num_rendered) *in.num_rendered = (int)L;
     return OMR_OK;
@@ -344,7 +401,7 @@ int backward_impl(const BackwardIn& in)
     GeomState g;
     GeomState::carve(in.geom_buffer, P, &g);
     BinningState b;
-    BinningState::carve(in.binning_buffer, (size_t)in.R, nullptr, &b, tile_sort_passes(d.T));
+    BinningState::carve(in.binning_buffer, (size_t)in.R, &b, tile_sort_passes(d.T));
     ImageState im;
     ImageState::carve(in.image_buffer, d.N, d.T, &im);
     const int* radii = in.radii ? in.radii : geom_internal_radii(in.geom_buffer, P);
@@ -478,7 +535,7 @@ size_t omr_image_bytes(int width, int height)
 size_t omr_binning_bytes(int num_rendered, int width, int height)
 {
     const Dims d = dims(width, height);
-    return BinningState::carve(nullptr, (size_t)std::max(num_rendered, 0), nullptr, nullptr, tile_sort_passes(d.T));
+    return BinningState::carve(nullptr, (size_t)std::max(num_rendered, 0), nullptr, tile_sort_passes(d.T));
 }
 
 int omr_debug_wave_sum(const float* in, float* out, void* stream)
@@ -489,6 +546,7 @@ int omr_debug_wave_sum(const float* in, float* out, void* stream)
 }
 
 void omr_profile_enable(int on) { g_prof.on = on != 0; }
+void omr_profile_set_mask(uint32_t mask) { g_prof.mask = mask; }
 
 void omr_profile_reset(void)
 {
@@ -533,7 +591,7 @@ int omr_debug_point_list(char* binning_buffer, int R, int width, int height, uin
     if (R <= 0) return OMR_OK;
     const Dims d = dims(width, height);
     BinningState b;
-    BinningState::carve(binning_buffer, (size_t)R, nullptr, &b, tile_sort_passes(d.T));
+    BinningState::carve(binning_buffer, (size_t)R, &b, tile_sort_passes(d.T));
     OMR_HIP(hipMemcpyAsync(dst, b.point_list, (size_t)R * sizeof(uint32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
     return OMR_OK;
 }

@@ -36,12 +36,16 @@ void launch_mark_visible(int camera_type, int P, const float* means3D, const flo
 size_t scan_partials_size(size_t n);
 void launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, uint32_t* partials, size_t n, hipStream_t s);
 size_t radix_hist_size(size_t n);
-// stable LSD radix sort of (key, value) over bits [0, 8*passes); returns which buffer holds the result (0: a, 1: b)
+// stable LSD radix sort of (key, value) over bits [0, 8*passes); returns which buffer holds the result (0: a, 1: b).
+// n = capacity; count (device, may be NULL) = live element count <= n. canon != NULL: the last pass writes the
+// values to the canonical point list of the binning buffer at canon (raster_common.h) instead of val_a / val_b.
 int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* hist,
-                     uint32_t* scan_partials, size_t n, int first_pass, int passes, hipStream_t s);
-void launch_emit_instances(int P, size_t L, const GeomState& g, uint32_t gx, uint32_t* tile_keys,
-                           uint32_t* gauss_vals, hipStream_t s);
-void launch_tile_ranges(size_t L, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s);
+                     uint32_t* scan_partials, size_t n, const uint32_t* count, char* canon, int first_pass, int passes,
+                     hipStream_t s);
+// duplicateWithKeys; L_cap = capacity, *count (device) = num_rendered
+void launch_emit_instances(int P, size_t L_cap, const uint32_t* count, const GeomState& g, uint32_t gx,
+                           uint32_t* tile_keys, uint32_t* gauss_vals, hipStream_t s);
+void launch_tile_ranges(size_t L_cap, const uint32_t* count, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s);
 // render schedule: within each of 8 contiguous shares of the tiles (one per XCD), tiles by descending cost
 // (cost[t] if cost != NULL, else the instance count ranges[t].y - ranges[t].x)
 void launch_tile_order(const uint2* ranges, const uint32_t* cost, uint32_t T, uint32_t* order, hipStream_t s);
@@ -52,7 +56,8 @@ struct RenderFwdArgs {
     uint32_t gx, gy;
     const uint2* ranges;
     const uint32_t* tile_order;  // [T] schedule (launch_tile_order)
-    const uint32_t* point_list;
+    const char* binning;         // binning buffer: the point list is at binning + canonical_list_offset(*count)
+    const uint32_t* count;       // num_rendered (device)
     const float4* splat;  // [P][SPLAT_F4] render records
     const float* bg;
     uint32_t* tile_cost;  // [T] zeroed; receives the (instance, band) pairs each tile evaluated (backward schedule)

@@ -100,17 +100,27 @@ struct ImageState {
 };
 
 // ---- binning state: L instances ----------------------------------------------------------------------------
+// The forward sizes this buffer BEFORE it knows L (capacity `cap` >= L from a hint, see capi.hip) so that it never
+// waits for the host; the backward only learns R = L. So the two arrays the backward reads sit at offsets that
+// depend on L alone: inst_grad at 0 and the sorted point list right after R rows of it (canonical_list_offset).
+// In the forward, the region [0, align(cap * 36) + align(cap * 4)) is reserved for them; the final tile-sort pass
+// writes the point list to base + canonical_list_offset(L) with L read on the device.
+__host__ __device__ inline size_t canonical_list_offset(size_t L)
+{
+    return (L * GRAD_ROW * sizeof(float) + ALIGN - 1) & ~(ALIGN - 1);
+}
 struct BinningState {
+    float* inst_grad;      // [L][GRAD_ROW] backward scratch, indexed by emission slot (offset 0)
+    uint32_t* point_list;  // sorted Gaussian indices at base + canonical_list_offset(L) (host-known only when L is)
     uint32_t* key_a;       // tile id ping-pong
     uint32_t* key_b;
     uint32_t* val_a;       // Gaussian index ping-pong
     uint32_t* val_b;
     uint32_t* hist;        // radix histograms
     uint32_t* scan_partials;
-    float* inst_grad;      // [L][GRAD_ROW] backward scratch, indexed by emission slot
-    uint32_t* point_list;  // sorted Gaussian indices (points at val_a or val_b)
-    uint32_t* point_keys;  // sorted tile ids
-    static size_t carve(char* base, size_t L, GeomState* unused, BinningState* s, int tile_passes);
+    uint32_t* point_keys;  // sorted tile ids (points at key_a or key_b)
+    // carve for capacity cap; point_list is set for L = cap (exact sizing: backward, debug, omr_binning_bytes)
+    static size_t carve(char* base, size_t cap, BinningState* s, int tile_passes);
 };
 
 // number of 8-bit passes needed for tile ids < T (rasterizer_impl.cu:651: sort end bit = 32 + getHigherMsb(T))

@@ -79,6 +79,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
         if (__ballot(inside)) active |= 1u << b;
     }
 
+    const uint32_t* point_list = reinterpret_cast<const uint32_t*>(a.binning + canonical_list_offset(*a.count));
     const uint2 range = a.ranges[tile];
     const uint32_t n = range.y - range.x;
     for (uint32_t start = 0; start < n && active; start += TW_BATCH) {
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
         uint32_t m = 0;
         float4 pos, co, c;
         if (k < n) {
-            const uint32_t gid = a.point_list[range.x + k];
+            const uint32_t gid = point_list[range.x + k];
             const float4* rec = a.splat + (size_t)gid * SPLAT_F4;  // one 64-B record per instance
             pos = rec[0];
             co = rec[1];

@@ -129,9 +129,17 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_downsweep_kernel(const uint
 }
 
 // ---- radix sort ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(SORT_THREADS) void radix_upsweep_kernel(const uint32_t* keys, size_t n, int shift,
-                                                                     uint32_t* hist, uint32_t nblocks)
+// element count: the host's n, or min(*count, n) when the count lives on the device (binning, capi.hip)
+__device__ __forceinline__ size_t live_count(size_t n, const uint32_t* count)
 {
+    return count ? min(n, (size_t)*count) : n;
+}
+
+__global__ __launch_bounds__(SORT_THREADS) void radix_upsweep_kernel(const uint32_t* keys, size_t n_cap,
+                                                                     const uint32_t* count, int shift, uint32_t* hist,
+                                                                     uint32_t nblocks)
+{
+    const size_t n = live_count(n_cap, count);
     __shared__ uint32_t s_hist[RADIX];
     s_hist[threadIdx.x] = 0;
     __syncthreads();
@@ -145,11 +153,15 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_upsweep_kernel(const uint3
     hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = s_hist[threadIdx.x];
 }
 
+// canon != NULL: values go to the canonical point list of the binning buffer at canon (raster_common.h)
 __global__ __launch_bounds__(SORT_THREADS) void radix_downsweep_kernel(const uint32_t* keys_in, const uint32_t* vals_in,
-                                                                       uint32_t* keys_out, uint32_t* vals_out, size_t n,
+                                                                       uint32_t* keys_out, uint32_t* vals_out,
+                                                                       size_t n_cap, const uint32_t* count, char* canon,
                                                                        int shift, const uint32_t* hist_scanned,
                                                                        uint32_t nblocks)
 {
+    const size_t n = live_count(n_cap, count);
+    if (canon) vals_out = reinterpret_cast<uint32_t*>(canon + canonical_list_offset(n));
     constexpr int WAVES = SORT_THREADS / 64;
     __shared__ uint32_t s_offset[RADIX];
     __shared__ uint32_t s_cnt[WAVES][RADIX];
@@ -213,13 +225,15 @@ __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* offsets, uin
 // (not per Gaussian as in the reference): writes are fully coalesced and a polar Gaussian spanning hundreds
 // of tiles no longer serialises its wave. The owner of each slot is found by binary search over the scan,
 // narrowed per block to the few Gaussians that own the block's 256 slots.
-__global__ __launch_bounds__(256) void emit_kernel(int P, size_t L, const uint32_t* order, const uint32_t* offsets,
-                                                   float4* splat, uint32_t gx, uint32_t* tile_keys,
-                                                   uint32_t* gauss_vals)
+__global__ __launch_bounds__(256) void emit_kernel(int P, size_t L_cap, const uint32_t* count, const uint32_t* order,
+                                                   const uint32_t* offsets, float4* splat, uint32_t gx,
+                                                   uint32_t* tile_keys, uint32_t* gauss_vals)
 {
+    const size_t L = live_count(L_cap, count);
     __shared__ uint32_t s_lo, s_hi;
     const size_t e0 = (size_t)blockIdx.x * blockDim.x;
     const size_t e = e0 + threadIdx.x;
+    if (e0 >= L) return;  // block-uniform
     if (threadIdx.x == 0) {
         const size_t elast = min(L, e0 + blockDim.x) - 1;
         s_lo = upper_bound_u32(offsets, 0, (uint32_t)P, (uint32_t)e0);
@@ -243,8 +257,10 @@ __global__ __launch_bounds__(256) void emit_kernel(int P, size_t L, const uint32
 }
 
 // identifyTileRanges (rasterizer_impl.cu:145-167)
-__global__ __launch_bounds__(256) void tile_ranges_kernel(size_t L, const uint32_t* tiles, uint2* ranges)
+__global__ __launch_bounds__(256) void tile_ranges_kernel(size_t L_cap, const uint32_t* count, const uint32_t* tiles,
+                                                          uint2* ranges)
 {
+    const size_t L = live_count(L_cap, count);
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= L) return;
     const uint32_t curr = tiles[idx];
@@ -335,7 +351,8 @@ static void launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t* p
 size_t radix_hist_size(size_t n) { return (size_t)RADIX * div_up(n, SORT_TILE); }
 
 int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* hist,
-                     uint32_t* scan_partials, size_t n, int first_pass, int passes, hipStream_t s)
+                     uint32_t* scan_partials, size_t n, const uint32_t* count, char* canon, int first_pass, int passes,
+                     hipStream_t s)
 {
     if (n == 0 || passes <= 0) return 0;
     const uint32_t nb = div_up(n, SORT_TILE);
@@ -343,9 +360,11 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
     int cur = 0;
     for (int p = first_pass; p < first_pass + passes; ++p) {
         const int shift = p * RADIX_BITS;
-        radix_upsweep_kernel<<<nb, SORT_THREADS, 0, s>>>(ki, n, shift, hist, nb);
+        const bool last = p == first_pass + passes - 1;
+        radix_upsweep_kernel<<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb);
         launch_exclusive_scan(hist, hist, scan_partials, (size_t)RADIX * nb, s);
-        radix_downsweep_kernel<<<nb, SORT_THREADS, 0, s>>>(ki, vi, ko, vo, n, shift, hist, nb);
+        radix_downsweep_kernel<<<nb, SORT_THREADS, 0, s>>>(ki, vi, ko, vo, n, count, last ? canon : nullptr, shift,
+                                                           hist, nb);
         std::swap(ki, ko);
         std::swap(vi, vo);
         cur ^= 1;
@@ -353,17 +372,18 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
     return cur;
 }
 
-void launch_emit_instances(int P, size_t L, const GeomState& g, uint32_t gx, uint32_t* tile_keys,
-                           uint32_t* gauss_vals, hipStream_t s)
+void launch_emit_instances(int P, size_t L_cap, const uint32_t* count, const GeomState& g, uint32_t gx,
+                           uint32_t* tile_keys, uint32_t* gauss_vals, hipStream_t s)
 {
-    if (P <= 0 || L == 0) return;
-    emit_kernel<<<div_up(L, 256), 256, 0, s>>>(P, L, g.order, g.offsets, g.splat, gx, tile_keys, gauss_vals);
+    if (P <= 0 || L_cap == 0) return;
+    emit_kernel<<<div_up(L_cap, 256), 256, 0, s>>>(P, L_cap, count, g.order, g.offsets, g.splat, gx, tile_keys,
+                                                   gauss_vals);
 }
 
-void launch_tile_ranges(size_t L, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s)
+void launch_tile_ranges(size_t L_cap, const uint32_t* count, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s)
 {
-    if (L == 0) return;
-    tile_ranges_kernel<<<div_up(L, 256), 256, 0, s>>>(L, sorted_tiles, ranges);
+    if (L_cap == 0) return;
+    tile_ranges_kernel<<<div_up(L_cap, 256), 256, 0, s>>>(L_cap, count, sorted_tiles, ranges);
 }
 
 }  // namespace omr

@@ -66,6 +66,7 @@ def lib() -> C.CDLL:
         L.omr_debug_geometry.argtypes = [vp, i, vp, vp, vp, vp, vp, vp]
         L.omr_debug_wave_sum.argtypes = [vp, vp, vp]
         L.omr_profile_enable.argtypes = [i]
+        L.omr_profile_set_mask.argtypes = [C.c_uint32]
         L.omr_profile_read.restype = i
         L.omr_profile_read.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_uint64), i]
         L.omr_profile_stage_name.restype = C.c_char_p
@@ -376,7 +377,13 @@ def debug_state(P, R, width, height, geomBuffer, binningBuffer, imgBuffer):
 NUM_STAGES = 10
 
 
-def profile_enable(on: bool = True):
+def profile_enable(on: bool = True, stages=None):
+    """Record per-stage HIP events; `stages` (names) limits recording to those stages (None = all)."""
+    mask = 0xFFFFFFFF
+    if stages is not None:
+        names = [lib().omr_profile_stage_name(i).decode() for i in range(NUM_STAGES)]
+        mask = sum(1 << names.index(s) for s in stages)
+    lib().omr_profile_set_mask(mask)
     lib().omr_profile_enable(1 if on else 0)
 
 
