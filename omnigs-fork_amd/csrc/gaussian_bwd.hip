@@ -14,6 +14,7 @@
 // caller needs no zero-initialised gradient tensors (the reference zero-fills ~324 B/Gaussian first,
 // rasterize_points.cu:200-208).
 #include "kernels.h"
+#include "wave_ops.h"
 
 namespace omr {
 
@@ -416,76 +417,79 @@ __global__ __launch_bounds__(256) void gaussian_bwd_kernel(GaussBwdArgs a)
 }
 
 // Segmented sum of the per-instance rows. Gaussian order[r] (depth rank r) owns the contiguous emission slots
-// [offsets[r-1], offsets[r]). A 256-thread block owns 256 consecutive ranks and streams their rows in chunks of
-// 256 rows: one row per thread (coalesced 36-B rows), owner found by binary search of the block's offsets in
-// LDS, a wave64 segmented inclusive scan keyed by owner, and each Gaussian adds the scan value at the last row
-// of its segment in every wave it touches — in row order, so the sum is deterministic. Balanced however many
-// tiles a (polar) Gaussian covers. Culled Gaussians are not written (never read downstream).
+// [offsets[r-1], offsets[r]); lane r of the grid sums the rows of rank r.
+//  * Short segments (<= RED_SHORT rows, ~95 % of the Gaussians, median 4 rows at config C): the lane adds its rows
+//    in order straight from global memory. The 64 lanes of a wave own consecutive ranks, hence one contiguous
+//    span of rows, so the loads stay within a few KB that L1/L2 serve after the first touch.
+//  * Long segments (polar Gaussians span up to every tile of the image): the whole wave takes them one at a
+//    time, 64 rows per step (one per lane, coalesced), and reduces the 9 sums over the wave (wave_ops.h).
+// Fixed order everywhere, so the sums are deterministic. Culled Gaussians own no rows and are not written (never
+// read downstream).
 constexpr int RED_THREADS = 256;
+#ifndef OMR_RED_SHORT
+#define OMR_RED_SHORT 32
+#endif
+constexpr uint32_t RED_SHORT = OMR_RED_SHORT;
+
+__device__ __forceinline__ void add_row(float* acc, const float* inst_grad, uint32_t row)
+{
+    const float* p = inst_grad + (size_t)row * GRAD_ROW;
+#pragma unroll
+    for (int c = 0; c < GRAD_ROW; ++c) acc[c] += p[c];
+}
 
 __global__ __launch_bounds__(RED_THREADS) void instance_reduce_kernel(int P, const uint32_t* order,
                                                                       const uint32_t* offsets, const float* inst_grad,
                                                                       float* grad_sum)
 {
-    __shared__ uint32_t s_end[RED_THREADS];  // inclusive scan value (segment end) of each rank in the block
-    __shared__ float s_scan[RED_THREADS][GRAD_ROW + 1];
-    const int t = threadIdx.x;
-    const int r0 = blockIdx.x * RED_THREADS;
-    const int nr = min(RED_THREADS, P - r0);
-    const uint32_t base = r0 == 0 ? 0u : offsets[r0 - 1];
-    if (t < nr) s_end[t] = offsets[r0 + t];
-    __syncthreads();
-    const uint32_t E1 = s_end[nr - 1];
-    const uint32_t my_lo = t == 0 ? base : (t < nr ? s_end[t - 1] : E1);
-    const uint32_t my_hi = t < nr ? s_end[t] : E1;
-    float acc[GRAD_ROW];
+    const int r = blockIdx.x * RED_THREADS + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    const bool valid = r < P;
+    const uint32_t s = (r == 0 || !valid) ? 0u : offsets[r - 1];
+    const uint32_t e = valid ? offsets[r] : s;
+    const uint32_t n = e - s;
+    if (n != 0 && n <= RED_SHORT) {
+        float acc[GRAD_ROW];
 #pragma unroll
-    for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
-    const uint32_t lane = t & 63;
-    for (uint32_t C0 = base; C0 < E1; C0 += RED_THREADS) {
-        const uint32_t e = C0 + t;
-        const bool valid = e < E1;
-        // owner: first local rank with s_end > e
-        int lo = 0, hi = nr;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (s_end[mid] > e) hi = mid;
-            else lo = mid + 1;
+        for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
+#ifndef OMR_RED_NO_UNROLL
+        // 4 rows in flight per step (predicated), then the remainder
+        uint32_t k = 0;
+        for (; k + 4 <= n; k += 4) {
+            float x[4][GRAD_ROW];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int c = 0; c < GRAD_ROW; ++c) x[i][c] = inst_grad[(size_t)(s + k + i) * GRAD_ROW + c];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int c = 0; c < GRAD_ROW; ++c) acc[c] += x[i][c];
         }
-        const int key = valid ? lo : -1 - (int)lane;  // invalid lanes never join a segment
-        float x[GRAD_ROW];
-        const float* row = inst_grad + (size_t)e * GRAD_ROW;
-#pragma unroll
-        for (int c = 0; c < GRAD_ROW; ++c) x[c] = valid ? row[c] : 0.f;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int kk = __shfl_up(key, off, 64);
-            const bool same = lane >= (uint32_t)off && kk == key;
-#pragma unroll
-            for (int c = 0; c < GRAD_ROW; ++c) {
-                const float y = __shfl_up(x[c], off, 64);
-                if (same) x[c] += y;
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < GRAD_ROW; ++c) s_scan[t][c] = x[c];
-        __syncthreads();
-        // this thread's Gaussian: rows [max(my_lo, C0), min(my_hi, C0 + 256)) -> add the segment tail of each wave
-        uint32_t a = max(my_lo, C0);
-        const uint32_t b = min(my_hi, C0 + RED_THREADS);
-        while (a < b) {
-            const uint32_t wave_end = C0 + ((a - C0) / 64 + 1) * 64;
-            const uint32_t tail = min(b, wave_end) - 1;
-#pragma unroll
-            for (int c = 0; c < GRAD_ROW; ++c) acc[c] += s_scan[tail - C0][c];
-            a = min(b, wave_end);
-        }
-        __syncthreads();
-    }
-    if (t < nr && my_hi > my_lo) {
-        float* out = grad_sum + (size_t)order[r0 + t] * GRAD_ROW;
+        for (; k < n; ++k) add_row(acc, inst_grad, s + k);
+#else
+        for (uint32_t k = 0; k < n; ++k) add_row(acc, inst_grad, s + k);
+#endif
+        float* out = grad_sum + (size_t)order[r] * GRAD_ROW;
 #pragma unroll
         for (int c = 0; c < GRAD_ROW; ++c) out[c] = acc[c];
+    }
+    uint64_t longs = __ballot(n > RED_SHORT);
+    const uint32_t slot_of_lane = transposed_slot_of_lane(lane);
+    while (longs) {
+        const int j = __builtin_ctzll(longs);
+        longs &= longs - 1;
+        const uint32_t sj = __builtin_amdgcn_readlane(s, j), ej = __builtin_amdgcn_readlane(e, j);
+        float acc[GRAD_ROW];
+#pragma unroll
+        for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
+        for (uint32_t row = sj + lane; row < ej; row += 64) add_row(acc, inst_grad, row);
+        float t8;
+        const float tv = wave_sum8_transposed(acc, acc[8], lane, &t8);
+        if (lane < GRAD_ROW) {
+            const uint32_t rj = (uint32_t)(r - (int)lane) + (uint32_t)j;
+            grad_sum[(size_t)order[rj] * GRAD_ROW + slot_of_lane] = lane < 8 ? tv : t8;
+        }
     }
 }
 
