@@ -35,7 +35,8 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x)
     return x;
 }
 
-// block-wide exclusive scan of one value per thread (256 threads); returns the block total via *total
+// block-wide exclusive scan of one value per thread (THREADS threads); returns the block total via *total
+template <int THREADS = SCAN_THREADS>
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t* s_wave, uint32_t* total)
 {
     const uint32_t lane = lane_id();
@@ -45,7 +46,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t* s
     __syncthreads();
     uint32_t wave_off = 0, tot = 0;
 #pragma unroll
-    for (int k = 0; k < SCAN_THREADS / 64; ++k) {
+    for (int k = 0; k < THREADS / 64; ++k) {
         const uint32_t v = s_wave[k];
         if ((uint32_t)k < w) wave_off += v;
         tot += v;
@@ -128,6 +129,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_downsweep_kernel(const uint
     }
 }
 
+// sorts of at most this many 4096-item blocks (the depth sort up to 2M Gaussians) let each downsweep block derive
+// its digit offsets from the raw histogram: <= 512 KiB of L2 reads per block instead of three scan launches
+constexpr uint32_t SELF_SCAN_MAX_BLOCKS = 512;
+
 // ---- radix sort ------------------------------------------------------------------------------------------
 // element count: the host's n, or min(*count, n) when the count lives on the device (binning, capi.hip)
 __device__ __forceinline__ size_t live_count(size_t n, const uint32_t* count)
@@ -135,6 +140,8 @@ __device__ __forceinline__ size_t live_count(size_t n, const uint32_t* count)
     return count ? min(n, (size_t)*count) : n;
 }
 
+// BLOCK_MAJOR: hist[block][digit] (read back by the self-scanning downsweep of small sorts); else hist[digit][block]
+template <bool BLOCK_MAJOR>
 __global__ __launch_bounds__(SORT_THREADS) void radix_upsweep_kernel(const uint32_t* keys, size_t n_cap,
                                                                      const uint32_t* count, int shift, uint32_t* hist,
                                                                      uint32_t nblocks)
@@ -150,35 +157,78 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_upsweep_kernel(const uint3
         if (i < n) atomicAdd(&s_hist[(keys[i] >> shift) & (RADIX - 1)], 1u);
     }
     __syncthreads();
-    hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = s_hist[threadIdx.x];
+    if (BLOCK_MAJOR) hist[(size_t)blockIdx.x * RADIX + threadIdx.x] = s_hist[threadIdx.x];
+    else hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = s_hist[threadIdx.x];
 }
 
-// canon != NULL: values go to the canonical point list of the binning buffer at canon (raster_common.h)
+// One block sorts its 4096-item tile by the pass's digit in LDS, then writes each digit's run to its global
+// offset (the scanned [digit][block] histogram): consecutive threads store consecutive addresses, so the scatter
+// is coalesced within runs. Wave w owns the contiguous quarter [1024 w, 1024 w + 1024) of the tile and ranks its
+// items in 16 rounds of 64 with wave-private running digit counts in LDS (match by 8 ballots; no block barrier
+// inside the rounds); block order = (wave, round, lane) = item order, so the sort is stable.
+// canon != NULL: values go to the canonical point list of the binning buffer at canon (raster_common.h).
+// SELF_SCAN (small sorts, few blocks): hist is the raw block-major histogram and each block derives its global
+// digit offsets itself (column prefix over the blocks before it + scan of the digit totals), which saves the
+// three scan launches per pass; else hist is the scanned [digit][block] histogram.
+template <bool SELF_SCAN>
 __global__ __launch_bounds__(SORT_THREADS) void radix_downsweep_kernel(const uint32_t* keys_in, const uint32_t* vals_in,
                                                                        uint32_t* keys_out, uint32_t* vals_out,
                                                                        size_t n_cap, const uint32_t* count, char* canon,
                                                                        int shift, const uint32_t* hist_scanned,
                                                                        uint32_t nblocks)
 {
+    constexpr int WAVES = SORT_THREADS / 64;
+    constexpr int PER_WAVE = SORT_TILE / WAVES;
+    constexpr int ROUNDS = PER_WAVE / 64;
+    __shared__ uint32_t s_whist[WAVES][RADIX];  // running digit counts per wave, then per-wave digit offsets
+    __shared__ uint32_t s_dstart[RADIX];        // block-local start of each digit's run
+    __shared__ uint32_t s_gbase[RADIX];         // global start of this block's run of each digit
+    __shared__ uint32_t s_wave[SORT_THREADS / 64];
+    __shared__ uint32_t s_k[SORT_TILE];
+    __shared__ uint32_t s_v[SORT_TILE];
     const size_t n = live_count(n_cap, count);
     if (canon) vals_out = reinterpret_cast<uint32_t*>(canon + canonical_list_offset(n));
-    constexpr int WAVES = SORT_THREADS / 64;
-    __shared__ uint32_t s_offset[RADIX];
-    __shared__ uint32_t s_cnt[WAVES][RADIX];
-    __shared__ uint32_t s_pre[WAVES][RADIX];
     const uint32_t tid = threadIdx.x;
-    const uint32_t w = tid >> 6;
-    s_offset[tid] = hist_scanned[(size_t)tid * nblocks + blockIdx.x];
+    const uint32_t w = tid >> 6, lane = tid & 63;
+    const size_t tile0 = (size_t)blockIdx.x * SORT_TILE;
 #pragma unroll
-    for (int k = 0; k < WAVES; ++k) s_cnt[k][tid] = 0;
+    for (int q = 0; q < WAVES; ++q) s_whist[q][tid] = 0;
+    if (SELF_SCAN) {
+        uint32_t before = 0, total = 0;
+        uint32_t b = 0;
+        for (; b + 8 <= nblocks; b += 8) {  // 8 coalesced 1-KiB row loads in flight
+            uint32_t c[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) c[q] = hist_scanned[(size_t)(b + q) * RADIX + tid];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                before += b + q < blockIdx.x ? c[q] : 0u;
+                total += c[q];
+            }
+        }
+        for (; b < nblocks; ++b) {
+            const uint32_t c = hist_scanned[(size_t)b * RADIX + tid];
+            before += b < blockIdx.x ? c : 0u;
+            total += c;
+        }
+        uint32_t all;
+        s_gbase[tid] = before + block_exclusive_scan(total, s_wave, &all);
+    } else {
+        s_gbase[tid] = hist_scanned[(size_t)tid * nblocks + blockIdx.x];
+    }
+    const size_t base = tile0 + (size_t)w * PER_WAVE + lane;
+    uint32_t k[ROUNDS], v[ROUNDS], lr[ROUNDS];
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+        const size_t i = base + 64 * r;
+        k[r] = i < n ? keys_in[i] : 0u;
+        v[r] = i < n ? vals_in[i] : 0u;
+    }
     __syncthreads();
-    const size_t base = (size_t)blockIdx.x * SORT_TILE;
-    for (int r = 0; r < SORT_ITEMS; ++r) {
-        const size_t i = base + (size_t)r * SORT_THREADS + tid;
-        const bool valid = i < n;
-        const uint32_t k = valid ? keys_in[i] : 0u;
-        const uint32_t v = valid ? vals_in[i] : 0u;
-        const uint32_t d = (k >> shift) & (RADIX - 1);
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+        const bool valid = base + 64 * r < n;
+        const uint32_t d = (k[r] >> shift) & (RADIX - 1);
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < RADIX_BITS; ++b) {
@@ -187,24 +237,43 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_downsweep_kernel(const uin
             peers &= bit ? m : ~m;
         }
         const uint32_t rank = mask_rank(peers);
-        if (valid && rank == 0) s_cnt[w][d] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        {
-            uint32_t run = s_offset[tid];
+        const uint32_t prev = valid ? s_whist[w][d] : 0u;
+        lr[r] = prev + rank;
+        // every lane of the wave has read the count (LDS ops of a wave complete in order) before the leader stores
+        __builtin_amdgcn_wave_barrier();
+        if (valid && rank == 0) s_whist[w][d] = prev + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    {   // thread = digit: per-wave exclusive offsets, then the block-wide exclusive scan of the digit totals
+        uint32_t run = 0;
 #pragma unroll
-            for (int q = 0; q < WAVES; ++q) {
-                s_pre[q][tid] = run;
-                run += s_cnt[q][tid];
-                s_cnt[q][tid] = 0;
-            }
-            s_offset[tid] = run;
+        for (int q = 0; q < WAVES; ++q) {
+            const uint32_t c = s_whist[q][tid];
+            s_whist[q][tid] = run;
+            run += c;
         }
-        __syncthreads();
-        if (valid) {
-            const uint32_t dst = s_pre[w][d] + rank;
-            keys_out[dst] = k;
-            vals_out[dst] = v;
+        uint32_t total;
+        s_dstart[tid] = block_exclusive_scan(run, s_wave, &total);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+        if (base + 64 * r < n) {
+            const uint32_t d = (k[r] >> shift) & (RADIX - 1);
+            const uint32_t lp = s_dstart[d] + s_whist[w][d] + lr[r];
+            s_k[lp] = k[r];
+            s_v[lp] = v[r];
         }
+    }
+    __syncthreads();
+    const uint32_t nvalid = (uint32_t)min((size_t)SORT_TILE, n > tile0 ? n - tile0 : (size_t)0);
+    for (uint32_t j = tid; j < nvalid; j += SORT_THREADS) {
+        const uint32_t kk = s_k[j];
+        const uint32_t d = (kk >> shift) & (RADIX - 1);
+        const uint32_t dst = s_gbase[d] + (j - s_dstart[d]);
+        keys_out[dst] = kk;
+        vals_out[dst] = s_v[j];
     }
 }
 
@@ -361,10 +430,16 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
     for (int p = first_pass; p < first_pass + passes; ++p) {
         const int shift = p * RADIX_BITS;
         const bool last = p == first_pass + passes - 1;
-        radix_upsweep_kernel<<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb);
-        launch_exclusive_scan(hist, hist, scan_partials, (size_t)RADIX * nb, s);
-        radix_downsweep_kernel<<<nb, SORT_THREADS, 0, s>>>(ki, vi, ko, vo, n, count, last ? canon : nullptr, shift,
-                                                           hist, nb);
+        if (nb <= SELF_SCAN_MAX_BLOCKS) {
+            radix_upsweep_kernel<true><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb);
+            radix_downsweep_kernel<true><<<nb, SORT_THREADS, 0, s>>>(ki, vi, ko, vo, n, count, last ? canon : nullptr,
+                                                                     shift, hist, nb);
+        } else {
+            radix_upsweep_kernel<false><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb);
+            launch_exclusive_scan(hist, hist, scan_partials, (size_t)RADIX * nb, s);
+            radix_downsweep_kernel<false><<<nb, SORT_THREADS, 0, s>>>(ki, vi, ko, vo, n, count,
+                                                                      last ? canon : nullptr, shift, hist, nb);
+        }
         std::swap(ki, ko);
         std::swap(vi, vo);
         cur ^= 1;
