@@ -199,6 +199,7 @@ size_t BinningState::carve(char* base, size_t cap, BinningState* s, int tile_pas
     const size_t nh = radix_hist_size(cap);
     b.hist = c.take<uint32_t>(nh);
     b.scan_partials = c.take<uint32_t>(scan_partials_size(nh));
+    b.block_owner = c.take<uint32_t>(emit_index_size(cap));
     b.point_keys = (tile_passes & 1) != 0 ? b.key_b : b.key_a;  // result buffer of the key ping-pong
     if (s) *s = b;
     return c.size();
@@ -329,7 +330,7 @@ int forward_impl(const ForwardIn& in)
         if (!bin_base) return fail(OMR_ERR_ALLOCATION, "binning allocation failed");
         BinningState b;
         BinningState::carve(bin_base, capacity, &b, tile_passes);
-        { StageScope st_(ST_EMIT, s); launch_emit_instances(in.P, capacity, count_dev, g, d.gx, b.key_a, b.val_a, s); }
+        { StageScope st_(ST_EMIT, s); launch_emit_instances(in.P, capacity, count_dev, g, d.gx, b.block_owner, b.key_a, b.val_a, s); }
         {
             StageScope st_(ST_TILE_SORT, s);
             radix_sort_pairs(b.key_a, b.key_b, b.val_a, b.val_b, b.hist, b.scan_partials, capacity, count_dev,

@@ -42,9 +42,11 @@ size_t radix_hist_size(size_t n);
 int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* hist,
                      uint32_t* scan_partials, size_t n, const uint32_t* count, char* canon, int first_pass, int passes,
                      hipStream_t s);
-// duplicateWithKeys; L_cap = capacity, *count (device) = num_rendered
+// duplicateWithKeys; L_cap = capacity, *count (device) = num_rendered; block_owner: emit_index_size(L_cap) words
+constexpr int EMIT_BLOCK = 256;
+size_t emit_index_size(size_t L_cap);
 void launch_emit_instances(int P, size_t L_cap, const uint32_t* count, const GeomState& g, uint32_t gx,
-                           uint32_t* tile_keys, uint32_t* gauss_vals, hipStream_t s);
+                           uint32_t* block_owner, uint32_t* tile_keys, uint32_t* gauss_vals, hipStream_t s);
 void launch_tile_ranges(size_t L_cap, const uint32_t* count, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s);
 // render schedule: within each of 8 contiguous shares of the tiles (one per XCD), tiles by descending cost
 // (cost[t] if cost != NULL, else the instance count ranges[t].y - ranges[t].x)

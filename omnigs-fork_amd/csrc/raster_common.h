@@ -118,6 +118,7 @@ struct BinningState {
     uint32_t* val_b;
     uint32_t* hist;        // radix histograms
     uint32_t* scan_partials;
+    uint32_t* block_owner;  // emit index: owner rank of every EMIT_BLOCK-th slot
     uint32_t* point_keys;  // sorted tile ids (points at key_a or key_b)
     // carve for capacity cap; point_list is set for L = cap (exact sizing: backward, debug, omr_binning_bytes)
     static size_t carve(char* base, size_t cap, BinningState* s, int tile_passes);

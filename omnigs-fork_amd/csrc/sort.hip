@@ -289,30 +289,56 @@ __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* offsets, uin
     return lo;
 }
 
+// Emission index: block_owner[B] = the depth rank owning slot B * EMIT_BLOCK (the rank whose slot range
+// [offsets[r-1], offsets[r]) contains it). One thread per rank; only ranks containing a block start write.
+__global__ __launch_bounds__(256) void emit_index_kernel(int P, const uint32_t* offsets, uint32_t* block_owner)
+{
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= P) return;
+    const uint32_t lo = r == 0 ? 0u : offsets[r - 1], hi = offsets[r];
+    for (uint32_t B = (lo + EMIT_BLOCK - 1) / EMIT_BLOCK; B * EMIT_BLOCK < hi; ++B) block_owner[B] = (uint32_t)r;
+}
+
 // duplicateWithKeys (rasterizer_impl.cu:94-140) in depth order: Gaussian order[r] owns slots
 // [offsets[r-1], offsets[r]) and its tiles are emitted row-major like the reference. One thread per INSTANCE
 // (not per Gaussian as in the reference): writes are fully coalesced and a polar Gaussian spanning hundreds
-// of tiles no longer serialises its wave. The owner of each slot is found by binary search over the scan,
-// narrowed per block to the few Gaussians that own the block's 256 slots.
-__global__ __launch_bounds__(256) void emit_kernel(int P, size_t L_cap, const uint32_t* count, const uint32_t* order,
-                                                   const uint32_t* offsets, float4* splat, uint32_t gx,
-                                                   uint32_t* tile_keys, uint32_t* gauss_vals)
+// of tiles no longer serialises its wave. The block's slots belong to ranks [block_owner[B], block_owner[B+1]];
+// their slot ends are staged in LDS and each thread finds its owner by a binary search there.
+__global__ __launch_bounds__(EMIT_BLOCK) void emit_kernel(int P, size_t L_cap, const uint32_t* count,
+                                                          const uint32_t* order, const uint32_t* offsets,
+                                                          const uint32_t* block_owner, float4* splat, uint32_t gx,
+                                                          uint32_t* tile_keys, uint32_t* gauss_vals)
 {
+    __shared__ uint32_t s_end[EMIT_BLOCK];
+    __shared__ uint32_t s_start0;
     const size_t L = live_count(L_cap, count);
-    __shared__ uint32_t s_lo, s_hi;
-    const size_t e0 = (size_t)blockIdx.x * blockDim.x;
-    const size_t e = e0 + threadIdx.x;
+    const uint32_t B = blockIdx.x;
+    const size_t e0 = (size_t)B * EMIT_BLOCK;
     if (e0 >= L) return;  // block-uniform
-    if (threadIdx.x == 0) {
-        const size_t elast = min(L, e0 + blockDim.x) - 1;
-        s_lo = upper_bound_u32(offsets, 0, (uint32_t)P, (uint32_t)e0);
-        s_hi = upper_bound_u32(offsets, s_lo, (uint32_t)P, (uint32_t)elast) + 1;
-    }
+    const size_t e = e0 + threadIdx.x;
+    const uint32_t r_lo = block_owner[B];
+    const uint32_t r_hi = e0 + EMIT_BLOCK < L ? block_owner[B + 1] + 1 : (uint32_t)P;  // exclusive
+    const uint32_t nr = r_hi - r_lo;
+    const bool staged = nr <= EMIT_BLOCK;  // block-uniform; more only with runs of empty (culled) segments
+    if (staged && threadIdx.x < nr) s_end[threadIdx.x] = offsets[r_lo + threadIdx.x];
+    if (threadIdx.x == 0) s_start0 = r_lo == 0 ? 0u : offsets[r_lo - 1];
     __syncthreads();
     if (e >= L) return;
-    const uint32_t r = upper_bound_u32(offsets, s_lo, min(s_hi, (uint32_t)P), (uint32_t)e);
+    uint32_t r, start;
+    if (staged) {
+        uint32_t lo = 0, hi = nr;  // first i with s_end[i] > e
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_end[mid] > (uint32_t)e) hi = mid;
+            else lo = mid + 1;
+        }
+        r = r_lo + lo;
+        start = lo == 0 ? s_start0 : s_end[lo - 1];
+    } else {
+        r = upper_bound_u32(offsets, r_lo, r_hi, (uint32_t)e);
+        start = r == 0 ? 0u : offsets[r - 1];
+    }
     const uint32_t gid = order[r];
-    const uint32_t start = r == 0 ? 0u : offsets[r - 1];
     const uint32_t k = (uint32_t)e - start;
     float4* rec = splat + (size_t)gid * SPLAT_F4;
     const float4 rect = rec[3];  // {x0, y0, x1, y1} from preprocess (getRect)
@@ -447,12 +473,15 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
     return cur;
 }
 
+size_t emit_index_size(size_t L_cap) { return div_up(L_cap, EMIT_BLOCK) + 1; }
+
 void launch_emit_instances(int P, size_t L_cap, const uint32_t* count, const GeomState& g, uint32_t gx,
-                           uint32_t* tile_keys, uint32_t* gauss_vals, hipStream_t s)
+                           uint32_t* block_owner, uint32_t* tile_keys, uint32_t* gauss_vals, hipStream_t s)
 {
     if (P <= 0 || L_cap == 0) return;
-    emit_kernel<<<div_up(L_cap, 256), 256, 0, s>>>(P, L_cap, count, g.order, g.offsets, g.splat, gx, tile_keys,
-                                                   gauss_vals);
+    emit_index_kernel<<<div_up(P, 256), 256, 0, s>>>(P, g.offsets, block_owner);
+    emit_kernel<<<div_up(L_cap, EMIT_BLOCK), EMIT_BLOCK, 0, s>>>(P, L_cap, count, g.order, g.offsets, block_owner,
+                                                                 g.splat, gx, tile_keys, gauss_vals);
 }
 
 void launch_tile_ranges(size_t L_cap, const uint32_t* count, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s)
