@@ -141,8 +141,22 @@ __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const
     if (clamp_bits & 1) dRGB.x = 0.f;
     if (clamp_bits & 2) dRGB.y = 0.f;
     if (clamp_bits & 4) dRGB.z = 0.f;
-    const float* sh = shs + (size_t)idx * Mr * 3;
+    const float* sh_row = shs + (size_t)idx * Mr * 3;
     float* out = dL_dsh + (size_t)idx * Mr * 3;
+    float shv[MC == 16 ? 48 : 1];
+    const float* sh = sh_row;
+    if constexpr (MC == 16) {  // the row as 16-B loads (launch_gaussian_backward checks the alignment)
+        const int nf4 = (3 * (deg + 1) * (deg + 1) + 3) >> 2;
+#pragma unroll
+        for (int q = 0; q < 12; ++q) {
+            const float4 v = q < nf4 ? reinterpret_cast<const float4*>(sh_row)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            shv[4 * q] = v.x;
+            shv[4 * q + 1] = v.y;
+            shv[4 * q + 2] = v.z;
+            shv[4 * q + 3] = v.w;
+        }
+        sh = shv;
+    }
     float coef[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) coef[k] = 0.f;
@@ -506,7 +520,8 @@ void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_
 {
     if (a.P <= 0) return;
     const dim3 grid(div_up(a.P, 256));
-    const bool m16 = a.M == 16 && (reinterpret_cast<uintptr_t>(a.dL_dsh) % 16) == 0;
+    const bool m16 = a.M == 16 && (reinterpret_cast<uintptr_t>(a.dL_dsh) % 16) == 0 &&
+                     (reinterpret_cast<uintptr_t>(a.shs) % 16) == 0;
     if (camera_type == CAM_LONLAT) {
         if (m16) gaussian_bwd_kernel<CAM_LONLAT, 16><<<grid, 256, 0, s>>>(a);
         else gaussian_bwd_kernel<CAM_LONLAT, 0><<<grid, 256, 0, s>>>(a);

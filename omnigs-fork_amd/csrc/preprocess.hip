@@ -218,7 +218,23 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
         dx = dx / len;
         dy = dy / len;
         dz = dz / len;
-        sh_to_rgb(a.D, dx, dy, dz, a.shs + (size_t)idx * a.M * 3, rgb, clamp_bits);
+        const float* row = a.shs + (size_t)idx * a.M * 3;
+        if (a.M == 16 && (reinterpret_cast<uintptr_t>(a.shs) & 15u) == 0) {
+            // the row as 16-B loads: 12 wide accesses per lane instead of 48 dword gathers 192 B apart
+            float shv[48];
+            const int nf4 = (3 * (a.D + 1) * (a.D + 1) + 3) >> 2;
+#pragma unroll
+            for (int q = 0; q < 12; ++q) {
+                const float4 v = q < nf4 ? reinterpret_cast<const float4*>(row)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+                shv[4 * q] = v.x;
+                shv[4 * q + 1] = v.y;
+                shv[4 * q + 2] = v.z;
+                shv[4 * q + 3] = v.w;
+            }
+            sh_to_rgb(a.D, dx, dy, dz, shv, rgb, clamp_bits);
+        } else {
+            sh_to_rgb(a.D, dx, dy, dz, row, rgb, clamp_bits);
+        }
     } else {
         rgb[0] = a.colors_precomp[3 * idx];
         rgb[1] = a.colors_precomp[3 * idx + 1];
