@@ -43,6 +43,10 @@ def parse():
     p.add_argument("--boundary", choices=["ctypes", "libtorch"], default="ctypes",
                    help="ctypes: Python host on the C ABI (writes grads into the flat all-reduce buffer); libtorch: "
                         "the rasterize_points.h drop-in (librasterize_points.so) through its pybind module")
+    p.add_argument("--rehearse", action="store_true",
+                   help="multi-rank rehearsal on a one-GPU box: every rank on cuda:0, gloo instead of RCCL "
+                        "(exercises the N > 1 code path; numbers are not a scaling measurement)")
+    p.add_argument("--scene", default=None, help="override the scene of this rank (e.g. E_pinhole)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     return p.parse_args()
 
@@ -64,6 +68,19 @@ def stage_bytes(stage, P, V, L, N, T, M=16, D=3):
         # writes every gradient output: 3+3+1+3+6+3*M(coeffs)+3+4 floats per Gaussian
         "gaussian_backward": 4 * P + (36 + 12 + 12 + 16 + sh + 1) * V + (92 + 12 * M) * P,
     }.get(stage, 0)
+
+
+def workload_text(cfg_name, config, world, P, W, H, camera_type, sh_degree):
+    cam = lambda w, h, t: f"{w}x{h} " + ("equirect (camera_type=3)" if t == 3 else "pinhole (camera_type=1)")
+    if config == "E" and world > 1:
+        views = (f"{cam(4096, 2048, 3)} on ranks 0-{world // 2 - 1}, {cam(1920, 1080, 1)} on ranks "
+                 f"{world // 2}-{world - 1}")
+    else:
+        views = cam(W, H, camera_type)
+    text = f"{cfg_name}: {P} Gaussians, {views}, SH degree {sh_degree}, one view per GPU"
+    if world > 1:
+        text += ", RCCL sum all-reduce of 236 B/Gaussian gradients"
+    return text
 
 
 def cpu_baseline(g, cam, dL, seconds, threads):
@@ -109,16 +126,28 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     info = par.DistInfo(rank, world, local)
+    if args.rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     if world != args.gpus and rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
 
     # config D is config C's scene rendered one view per GPU: the same Gaussians for every N (weak scaling)
     cfg_name = "D" if (world > 1 and args.config == "C") else args.config
-    g, cam, dL = scene.config_scene(args.config, view_index=rank % 8, P=args.gaussians)
+    # config E is a mixed batch (BASELINE.json): the first half of the ranks render 4096x2048 equirect views, the
+    # second half 1920x1080 pinhole views; every other config is one camera type
+    scene_name = args.config
+    if args.config == "E" and world > 1 and rank >= world // 2:
+        scene_name = "E_pinhole"
+    if args.scene:
+        scene_name = args.scene
+    g, cam, dL = scene.config_scene(scene_name, view_index=rank % 8, P=args.gaussians)
     P, W, H = g.P, cam.width, cam.height
     M = g.shs.shape[1]
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)
@@ -198,7 +227,11 @@ def main():
         elapsed = float(e.item())
 
     ms_per_step = elapsed / args.steps * 1e3
-    value = world * W * H / (elapsed / args.steps) / 1e6
+    # whole-job pixels per step: every rank's view (ranks of a mixed config render different resolutions)
+    pix = torch.tensor([float(W * H)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(pix, op=dist.ReduceOp.SUM)
+    value = float(pix.item()) / (elapsed / args.steps) / 1e6
     L, N = int(stats["L"]), W * H
     T = ((W + 15) // 16) * ((H + 15) // 16)
 
@@ -231,9 +264,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (SplitMix64 scene, SURVEY.md §8(d)); random-init Gaussians, fixed dL/dout",
-        "config": {"workload": f"{cfg_name}: {P} Gaussians, {W}x{H} equirect (camera_type=3), SH degree "
-                               f"{g.sh_degree}, one view per GPU" + (", RCCL sum all-reduce of 236 B/Gaussian "
-                                                                    "gradients" if world > 1 else ""),
+        "config": {"workload": workload_text(cfg_name, args.config, world, P, W, H, cam.camera_type, g.sh_degree),
                    "P": P, "V": V, "L": L, "N": N, "T": T, "width": W, "height": H,
                    "parallelism": f"view-parallel dp{world}", "boundary": args.boundary},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

@@ -200,6 +200,7 @@ size_t BinningState::carve(char* base, size_t cap, BinningState* s, int tile_pas
     b.hist = c.take<uint32_t>(nh);
     b.scan_partials = c.take<uint32_t>(scan_partials_size(nh));
     b.block_owner = c.take<uint32_t>(emit_index_size(cap));
+    b.row_valid = c.take<uint8_t>(cap);
     b.point_keys = (tile_passes & 1) != 0 ? b.key_b : b.key_a;  // result buffer of the key ping-pong
     if (s) *s = b;
     return c.size();
@@ -411,6 +412,8 @@ int backward_impl(const BackwardIn& in)
     rb.W = in.width; rb.H = in.height; rb.gx = d.gx; rb.gy = d.gy;
     rb.ranges = im.ranges; rb.tile_order = im.tile_order; rb.point_list = b.point_list; rb.splat = g.splat; rb.bg = in.background;
     rb.final_T = im.final_T; rb.n_contrib = im.n_contrib; rb.dL_dpix = in.dL_dpix; rb.inst_grad = b.inst_grad;
+    rb.row_valid = b.row_valid;
+    if (in.R > 0) OMR_HIP(hipMemsetAsync(b.row_valid, 0, (size_t)in.R, s));
     {
         StageScope st_(ST_RENDER_BWD, s);
         launch_tile_order(im.ranges, im.tile_cost, d.T, im.tile_order, s);  // costliest tiles first
@@ -427,7 +430,7 @@ int backward_impl(const BackwardIn& in)
     ga.clamped = g.clamped; ga.grad_sum = g.grad_sum;
     {
         StageScope st_(ST_INSTANCE_REDUCE, s);
-        launch_instance_reduce(in.P, g.order, g.offsets, b.inst_grad, g.grad_sum, s);
+        launch_instance_reduce(in.P, g.order, g.offsets, b.inst_grad, b.row_valid, g.grad_sum, s);
     }
     ga.dL_dmean2D = in.dL_dmean2D; ga.dL_dconic = in.dL_dconic; ga.dL_dopacity = in.dL_dopacity; ga.dL_dcolor = in.dL_dcolor;
     ga.dL_dmean3D = in.dL_dmean3D; ga.dL_dcov3D = in.dL_dcov3D; ga.dL_dsh = in.M > 0 ? in.dL_dsh : nullptr;

@@ -432,6 +432,7 @@ __global__ __launch_bounds__(256) void gaussian_bwd_kernel(GaussBwdArgs a)
 
 // Segmented sum of the per-instance rows. Gaussian order[r] (depth rank r) owns the contiguous emission slots
 // [offsets[r-1], offsets[r]); lane r of the grid sums the rows of rank r.
+//  * Only rows marked in row_valid are read (render_bwd.hip writes no row where no pixel took a contribution).
 //  * Short segments (<= RED_SHORT rows, ~95 % of the Gaussians, median 4 rows at config C): the lane adds its rows
 //    in order straight from global memory. The 64 lanes of a wave own consecutive ranks, hence one contiguous
 //    span of rows, so the loads stay within a few KB that L1/L2 serve after the first touch.
@@ -445,8 +446,9 @@ constexpr int RED_THREADS = 256;
 #endif
 constexpr uint32_t RED_SHORT = OMR_RED_SHORT;
 
-__device__ __forceinline__ void add_row(float* acc, const float* inst_grad, uint32_t row)
+__device__ __forceinline__ void add_row(float* acc, const float* inst_grad, const uint8_t* row_valid, uint32_t row)
 {
+    if (!row_valid[row]) return;  // no pixel of that tile took a contribution
     const float* p = inst_grad + (size_t)row * GRAD_ROW;
 #pragma unroll
     for (int c = 0; c < GRAD_ROW; ++c) acc[c] += p[c];
@@ -454,7 +456,7 @@ __device__ __forceinline__ void add_row(float* acc, const float* inst_grad, uint
 
 __global__ __launch_bounds__(RED_THREADS) void instance_reduce_kernel(int P, const uint32_t* order,
                                                                       const uint32_t* offsets, const float* inst_grad,
-                                                                      float* grad_sum)
+                                                                      const uint8_t* row_valid, float* grad_sum)
 {
     const int r = blockIdx.x * RED_THREADS + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63;
@@ -466,24 +468,23 @@ __global__ __launch_bounds__(RED_THREADS) void instance_reduce_kernel(int P, con
         float acc[GRAD_ROW];
 #pragma unroll
         for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
-#ifndef OMR_RED_NO_UNROLL
-        // 4 rows in flight per step (predicated), then the remainder
+        // 4 rows in flight per step (each read only where marked), then the remainder
         uint32_t k = 0;
         for (; k + 4 <= n; k += 4) {
+            bool ok[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ok[i] = row_valid[s + k + i] != 0;
             float x[4][GRAD_ROW];
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int c = 0; c < GRAD_ROW; ++c) x[i][c] = inst_grad[(size_t)(s + k + i) * GRAD_ROW + c];
+                for (int c = 0; c < GRAD_ROW; ++c) x[i][c] = ok[i] ? inst_grad[(size_t)(s + k + i) * GRAD_ROW + c] : 0.f;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int c = 0; c < GRAD_ROW; ++c) acc[c] += x[i][c];
         }
-        for (; k < n; ++k) add_row(acc, inst_grad, s + k);
-#else
-        for (uint32_t k = 0; k < n; ++k) add_row(acc, inst_grad, s + k);
-#endif
+        for (; k < n; ++k) add_row(acc, inst_grad, row_valid, s + k);
         float* out = grad_sum + (size_t)order[r] * GRAD_ROW;
 #pragma unroll
         for (int c = 0; c < GRAD_ROW; ++c) out[c] = acc[c];
@@ -497,7 +498,7 @@ __global__ __launch_bounds__(RED_THREADS) void instance_reduce_kernel(int P, con
         float acc[GRAD_ROW];
 #pragma unroll
         for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
-        for (uint32_t row = sj + lane; row < ej; row += 64) add_row(acc, inst_grad, row);
+        for (uint32_t row = sj + lane; row < ej; row += 64) add_row(acc, inst_grad, row_valid, row);
         float t8;
         const float tv = wave_sum8_transposed(acc, acc[8], lane, &t8);
         if (lane < GRAD_ROW) {
@@ -510,10 +511,11 @@ __global__ __launch_bounds__(RED_THREADS) void instance_reduce_kernel(int P, con
 }  // namespace
 
 void launch_instance_reduce(int P, const uint32_t* order, const uint32_t* offsets, const float* inst_grad,
-                            float* grad_sum, hipStream_t s)
+                            const uint8_t* row_valid, float* grad_sum, hipStream_t s)
 {
     if (P <= 0) return;
-    instance_reduce_kernel<<<div_up(P, RED_THREADS), RED_THREADS, 0, s>>>(P, order, offsets, inst_grad, grad_sum);
+    instance_reduce_kernel<<<div_up(P, RED_THREADS), RED_THREADS, 0, s>>>(P, order, offsets, inst_grad, row_valid,
+                                                                          grad_sum);
 }
 
 void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s)

@@ -82,6 +82,7 @@ struct RenderBwdArgs {
     const uint32_t* n_contrib;
     const float* dL_dpix;
     float* inst_grad;
+    uint8_t* row_valid;  // [L] zeroed; 1 where inst_grad holds a row
 };
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
 #ifdef OMR_STAMPS
@@ -119,6 +120,7 @@ struct GaussBwdArgs {
 void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s);
 // sums each Gaussian's instance rows (slots [offsets[r-1], offsets[r]) of depth rank r) into grad_sum[order[r]]
 void launch_instance_reduce(int P, const uint32_t* order, const uint32_t* offsets, const float* inst_grad,
+                            const uint8_t* row_valid,
                             float* grad_sum, hipStream_t s);
 
 }  // namespace omr

@@ -119,6 +119,7 @@ struct BinningState {
     uint32_t* hist;        // radix histograms
     uint32_t* scan_partials;
     uint32_t* block_owner;  // emit index: owner rank of every EMIT_BLOCK-th slot
+    uint8_t* row_valid;     // backward: 1 where inst_grad holds a row (carved for R in the backward only)
     uint32_t* point_keys;  // sorted tile ids (points at key_a or key_b)
     // carve for capacity cap; point_list is set for L = cap (exact sizing: backward, debug, omr_binning_bytes)
     static size_t carve(char* base, size_t cap, BinningState* s, int tile_passes);

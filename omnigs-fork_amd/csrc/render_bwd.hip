@@ -11,8 +11,10 @@
 // The per-Gaussian constants of the reference's expressions (conic, opacity, 0.5 W, 0.5 H, -1/2) are linear
 // factors, so they are applied once per instance to the lane's sums — not once per pixel — and the nine values
 // are then summed over the wave in registers (DPP transposed butterfly + v_permlane{16,32}_swap, wave_ops.h).
-// Lanes 0..8 store the instance's 36-B gradient row, indexed by its emission slot, with plain stores;
-// gaussian_bwd.hip sums each Gaussian's rows in a fixed order. No atomics: gradients are bitwise reproducible.
+// Lanes 0..8 store the instance's 36-B gradient row, indexed by its emission slot, with plain stores, and lane 0
+// marks the slot in row_valid (zeroed before the launch); an instance no pixel takes a contribution from writes
+// nothing — at dense configs most instances lie behind every pixel's last contributor. gaussian_bwd.hip sums each
+// Gaussian's marked rows in a fixed order. No atomics: gradients are bitwise reproducible.
 //
 // The per-pixel recurrence keeps two numbers instead of the reference's seven (T, accum_rec[3], last_alpha,
 // last_color[3]): T and s = bg . dL/dpix * T_final + sum over the contributors j behind the current instance of
@@ -21,7 +23,7 @@
 //     dL/dalpha_i = T_i (c_i - accum_rec_i) . dL/dpix - T_final / (1 - alpha_i) bg . dL/dpix
 // equals T_i c_i . dL/dpix - s / (1 - alpha_i): the same quantity, rounded differently.
 // T_i is recovered with v_rcp_f32 (T_{i+1} / (1 - alpha_i)), as the reference divides (backward.cu:782).
-// Instances at or behind every band's last contributor are skipped (their rows are zero).
+// Instances at or behind every band's last contributor are skipped.
 #include "kernels.h"
 #include "tile_wave.h"
 #include "wave_ops.h"
@@ -30,12 +32,6 @@ namespace omr {
 
 namespace {
 
-__device__ __forceinline__ void zero_row(float* inst_grad, uint32_t slot)
-{
-    float* row = inst_grad + (size_t)slot * GRAD_ROW;
-#pragma unroll
-    for (int c = 0; c < GRAD_ROW; ++c) row[c] = 0.f;
-}
 
 OMR_STAMP_DECL(g_stamps_bwd)
 
@@ -109,11 +105,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
     const uint32_t n = range.y - range.x;
     max_c = min(max_c, n);
 
-    // instances behind every pixel's last contributor: zero rows
-    for (uint32_t k = max_c + lane; k < n; k += TW_BATCH) {
-        const float4* rec = a.splat + (size_t)a.point_list[range.x + k] * SPLAT_F4;
-        zero_row(a.inst_grad, splat_slot(rec[0], rec[2], tl.tx, tl.ty));
-    }
+    // instances behind every pixel's last contributor get no row (row_valid stays 0 for them)
 
     const float half_w = 0.5f * (float)a.W, half_h = 0.5f * (float)a.H;  // ddelx_dx, ddely_dy (backward.cu:700-701)
     const uint32_t slot_of_lane = transposed_slot_of_lane(lane);
@@ -135,7 +127,6 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
 #pragma unroll
             for (int b = 0; b < TW_BANDS; ++b)
                 if (pos >= band_end[b]) m &= ~(1u << b);
-            if (m == 0) zero_row(a.inst_grad, slot);
         }
         const uint64_t useful = __ballot(m != 0);
         if (m != 0) {
@@ -199,10 +190,8 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
             }
             const uint32_t slot_j = __builtin_bit_cast(uint32_t, f.w);
             float* row = a.inst_grad + (size_t)slot_j * GRAD_ROW;
-            if (!uniform(any)) {
-                if (lane < GRAD_ROW) row[lane] = 0.f;
-                continue;
-            }
+            if (!uniform(any)) continue;  // no pixel took a contribution: no row
+            if (lane == 0) a.row_valid[slot_j] = 1;
             // per-instance factors of backward.cu:805-840 (dG/ddelx = -G (dx a + dy b), ...)
             // conic (a, b, c) back from the staged quadratic form: q = (-a/2, -b, -c/2) log2(e)
             const float ca = q.qa * (-2.0f / LOG2E), cb = q.qb * (-1.0f / LOG2E), cc = q.qc * (-2.0f / LOG2E);
