@@ -123,7 +123,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
             co = rec[1];
             c = rec[2];
             slot = splat_slot(p, c, tl.tx, tl.ty);
-            m = band_mask(make_float2(p.x, p.y), co, tl.tx, tl.ty);
+            m = band_mask<TW_BANDS>(make_float2(p.x, p.y), co, tl.tx, tl.ty, 0);
 #pragma unroll
             for (int b = 0; b < TW_BANDS; ++b)
                 if (pos >= band_end[b]) m &= ~(1u << b);

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
             pos = rec[0];
             co = rec[1];
             c = DEPTH ? make_float4(pos.z, pos.z, pos.z, 0.f) : rec[2];
-            m = (band_mask(make_float2(pos.x, pos.y), co, tl.tx, tl.ty) >> band0) & active;
+            m = band_mask<FWD_BANDS>(make_float2(pos.x, pos.y), co, tl.tx, tl.ty, band0) & active;
         }
         const uint64_t useful = __ballot(m != 0);
         if (m != 0) {
