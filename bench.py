@@ -40,6 +40,10 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-oracle sample budget")
     p.add_argument("--cpu-threads", type=int, default=None)
     p.add_argument("--bucket-mb", type=float, default=0.0, help="all-reduce bucket size (0 = one collective)")
+    p.add_argument("--exchange", choices=["compact", "flat"], default="compact",
+                   help="N > 1 gradient exchange: compact = all-reduce of the 44 B/G non-SH gradients + all-gather of "
+                        "12 B/G colour gradients and an SH rebuild (parallel.allreduce_compact_); flat = one "
+                        "all-reduce of all 236 B/G")
     p.add_argument("--boundary", choices=["ctypes", "libtorch"], default="ctypes",
                    help="ctypes: Python host on the C ABI (writes grads into the flat all-reduce buffer); libtorch: "
                         "the rasterize_points.h drop-in (librasterize_points.so) through its pybind module")
@@ -171,11 +175,18 @@ def main():
                                                ib, cam.camera_type)
         if world > 1:  # the drop-in allocates its own gradient tensors: gather them into the flat buffer
             for name, idx in (("dL_dmeans3D", 3), ("dL_dsh", 5), ("dL_dopacity", 2), ("dL_dscales", 6),
-                              ("dL_drotations", 7)):
-                grads.views[name].copy_(gr[idx])
-        par.allreduce_(grads, info, average=False, bucket_bytes=bucket)
+                              ("dL_drotations", 7), ("dL_dcolors", 1)):
+                (out if name == "dL_dcolors" else grads.views)[name].copy_(gr[idx])
+        exchange()
         stats["L"] = nr
         stats["radii"] = radii
+
+    def exchange():
+        if args.exchange == "compact":
+            par.allreduce_compact_(grads, info, out["dL_dcolors"], campos,
+                                   lambda c, d, out: R.sh_grad_from_colors(means3D, shs, g.sh_degree, c, d, out=out))
+        else:
+            par.allreduce_(grads, info, average=False, bucket_bytes=bucket)
 
     def step():
         if LT is not None:
@@ -186,7 +197,7 @@ def main():
         R.RasterizeGaussiansBackwardCUDA(bg, means3D, radii, empty, scales, rots, 1.0, empty, view, proj, cam.tanfovx,
                                          cam.tanfovy, dL_dout, shs, g.sh_degree, campos, gb, nr, bb, ib,
                                          cam.camera_type, out=out)
-        par.allreduce_(grads, info, average=False, bucket_bytes=bucket)
+        exchange()
         stats["L"] = nr
         stats["radii"] = radii
 

@@ -104,6 +104,14 @@ int omr_lonlat_backward(int P, int D, int M, int R, const float* background, int
                         float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D,
                         float* dL_dsh, float* dL_dscale, float* dL_drot, float* dpx_dt, float* dpy_dt, void* stream);
 
+/* --- view-parallel data parallelism (extension, not in the reference; omnigs-fork_amd/parallel.py) -- */
+/* dL_dsh [P,M,3] = sum over nviews views of the SH gradient the backward computes for each, rebuilt from each
+ * view's dL_dcolors ([nviews][P][3], RasterizeGaussiansBackwardCUDA's second output) and camera position
+ * (campos [nviews][3]) with the backward's own SH arithmetic. Lets view-parallel ranks exchange 12 B per
+ * Gaussian and view instead of all-reducing the 192-B SH gradient (M = 16). */
+int omr_sh_grad_from_colors(int P, int D, int M, int nviews, const float* means3D, const float* shs,
+                            const float* campos, const float* dL_dcolors, float* dL_dsh, void* stream);
+
 /* --- scratch sizes (bytes the allocation callbacks are asked for) -------------------------------- */
 size_t omr_geometry_bytes(int P);
 size_t omr_image_bytes(int width, int height);

@@ -528,6 +528,17 @@ int omr_lonlat_backward(int P, int D, int M, int R, const float* background, int
     return backward_impl(in);
 }
 
+int omr_sh_grad_from_colors(int P, int D, int M, int nviews, const float* means3D, const float* shs,
+                            const float* campos, const float* dL_dcolors, float* dL_dsh, void* stream)
+{
+    g_last_error.clear();
+    if (P < 0 || nviews < 0 || M < 0 || M > 16) return fail(OMR_ERR_INVALID_ARGUMENT, "bad P / M / nviews");
+    if (P == 0 || M == 0) return OMR_OK;
+    if (!means3D || !shs || !campos || !dL_dcolors || !dL_dsh) return fail(OMR_ERR_INVALID_ARGUMENT, "missing pointer");
+    launch_sh_grad_from_colors(P, D, M, nviews, means3D, shs, campos, dL_dcolors, dL_dsh, (hipStream_t)stream);
+    return hip_check("sh_grad_from_colors");
+}
+
 size_t omr_geometry_bytes(int P) { return GeomState::carve(nullptr, (size_t)std::max(P, 0), nullptr); }
 
 size_t omr_image_bytes(int width, int height)

@@ -14,18 +14,13 @@
 // caller needs no zero-initialised gradient tensors (the reference zero-fills ~324 B/Gaussian first,
 // rasterize_points.cu:200-208).
 #include "kernels.h"
+#include "sh_eval.h"
 #include "wave_ops.h"
 
 namespace omr {
 
 namespace {
 
-constexpr float SH_C0 = 0.28209479177387814f;  // auxiliary.h:32-49
-constexpr float SH_C1 = 0.4886025119029199f;
-constexpr float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f, -1.0925484305920792f,
-                            0.5462742152960396f};
-constexpr float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f, 0.3731763325901154f,
-                            -0.4570457994644658f, 1.445305721320277f, -0.5900435899266435f};
 constexpr float INV_PI = 0.318309886183790671537767526745028724f;
 
 struct F3 {
@@ -158,32 +153,9 @@ __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const
         sh = shv;
     }
     float coef[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) coef[k] = 0.f;
+    sh_basis(deg, x, y, z, coef);
     float gx[3] = {0.f, 0.f, 0.f}, gy[3] = {0.f, 0.f, 0.f}, gz[3] = {0.f, 0.f, 0.f};  // dRGB/dx etc per channel
-    coef[0] = SH_C0;
     const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-    if (deg > 0) {
-        coef[1] = -SH_C1 * y;
-        coef[2] = SH_C1 * z;
-        coef[3] = -SH_C1 * x;
-        if (deg > 1) {
-            coef[4] = SH_C2[0] * xy;
-            coef[5] = SH_C2[1] * yz;
-            coef[6] = SH_C2[2] * (2.f * zz - xx - yy);
-            coef[7] = SH_C2[3] * xz;
-            coef[8] = SH_C2[4] * (xx - yy);
-            if (deg > 2) {
-                coef[9] = SH_C3[0] * y * (3.f * xx - yy);
-                coef[10] = SH_C3[1] * xy * z;
-                coef[11] = SH_C3[2] * y * (4.f * zz - xx - yy);
-                coef[12] = SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
-                coef[13] = SH_C3[4] * x * (4.f * zz - xx - yy);
-                coef[14] = SH_C3[5] * z * (xx - yy);
-                coef[15] = SH_C3[6] * x * (xx - 3.f * yy);
-            }
-        }
-    }
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
         auto s = [&](int k) { return sh[3 * k + ch]; };
@@ -508,7 +480,89 @@ __global__ __launch_bounds__(RED_THREADS) void instance_reduce_kernel(int P, con
     }
 }
 
+// View-parallel data parallelism (parallel.py): the sum over n views of dL/dsh, rebuilt from each view's colour
+// gradient. Per view v, backward.cu:30-151 gives dL/dsh_k = basis_k(dir_v) * dRGB_v, dRGB_v = dL/dcolour_v masked
+// by the forward's clamp bits; the basis and the clamp bits are functions of (mean, SH row, campos_v), which every
+// rank holds. So ranks exchange dL/dcolour (12 B per Gaussian and view) and campos instead of all-reducing the
+// 192-B SH gradient, and each rebuilds the sum with the per-view backward's own arithmetic (sh_eval.h), summing the
+// views in index order. A view whose colour gradient is zero (culled there) adds nothing and is skipped.
+template <int MC>
+__global__ __launch_bounds__(256) void sh_grad_from_colors_kernel(int P, int D, int M, int nviews,
+                                                                  const float* means3D, const float* shs,
+                                                                  const float* campos, const float* dL_dcolors,
+                                                                  float* dL_dsh)
+{
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= P) return;
+    const int Mr = MC > 0 ? MC : M;
+    const int nk = min(16, min(Mr, (D + 1) * (D + 1)));
+    const float* row = shs + (size_t)idx * Mr * 3;
+    float shv[48];
+#pragma unroll
+    for (int f = 0; f < 48; ++f) shv[f] = 0.f;
+    if constexpr (MC == 16) {
+        const int nf4 = (3 * nk + 3) >> 2;
+#pragma unroll
+        for (int q = 0; q < 12; ++q) {
+            if (q < nf4) {
+                const float4 v = reinterpret_cast<const float4*>(row)[q];
+                shv[4 * q] = v.x;
+                shv[4 * q + 1] = v.y;
+                shv[4 * q + 2] = v.z;
+                shv[4 * q + 3] = v.w;
+            }
+        }
+    } else {
+        for (int f = 0; f < 3 * nk; ++f) shv[f] = row[f];
+    }
+    float acc[48];
+#pragma unroll
+    for (int f = 0; f < 48; ++f) acc[f] = 0.f;
+    const float px = means3D[3 * idx], py = means3D[3 * idx + 1], pz = means3D[3 * idx + 2];
+    for (int v = 0; v < nviews; ++v) {
+        const float* dc = dL_dcolors + ((size_t)v * P + idx) * 3;
+        float d[3] = {dc[0], dc[1], dc[2]};
+        if (d[0] == 0.f && d[1] == 0.f && d[2] == 0.f) continue;
+        float x, y, z;
+        sh_direction(px, py, pz, campos + 3 * v, x, y, z);
+        float rgb[3];
+        uint8_t clamp_bits;
+        sh_to_rgb(D, x, y, z, shv, rgb, clamp_bits);
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            if (clamp_bits & (1u << c)) d[c] = 0.f;
+        float coef[16];
+        sh_basis(D, x, y, z, coef);
+#pragma unroll
+        for (int f = 0; f < 48; ++f) acc[f] += coef[f / 3] * d[f % 3];
+    }
+    float* out = dL_dsh + (size_t)idx * Mr * 3;
+    if constexpr (MC == 16) {
+        float4* o4 = reinterpret_cast<float4*>(out);
+#pragma unroll
+        for (int q = 0; q < 12; ++q) {
+            float w[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w[e] = (4 * q + e) / 3 < nk ? acc[4 * q + e] : 0.f;
+            o4[q] = make_float4(w[0], w[1], w[2], w[3]);
+        }
+    } else {
+        for (int f = 0; f < Mr * 3; ++f) out[f] = f / 3 < nk ? acc[f < 48 ? f : 0] : 0.f;
+    }
+}
+
 }  // namespace
+
+void launch_sh_grad_from_colors(int P, int D, int M, int nviews, const float* means3D, const float* shs,
+                                const float* campos, const float* dL_dcolors, float* dL_dsh, hipStream_t s)
+{
+    if (P <= 0) return;
+    const bool m16 = M == 16 && (reinterpret_cast<uintptr_t>(shs) % 16) == 0 &&
+                     (reinterpret_cast<uintptr_t>(dL_dsh) % 16) == 0;
+    const dim3 grid(div_up(P, 256));
+    if (m16) sh_grad_from_colors_kernel<16><<<grid, 256, 0, s>>>(P, D, M, nviews, means3D, shs, campos, dL_dcolors, dL_dsh);
+    else sh_grad_from_colors_kernel<0><<<grid, 256, 0, s>>>(P, D, M, nviews, means3D, shs, campos, dL_dcolors, dL_dsh);
+}
 
 void launch_instance_reduce(int P, const uint32_t* order, const uint32_t* offsets, const float* inst_grad,
                             const uint8_t* row_valid, float* grad_sum, hipStream_t s)

@@ -118,6 +118,9 @@ struct GaussBwdArgs {
     float* dpy_dt;       // [P,3] optional
 };
 void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s);
+// view-parallel DP: dL_dsh[P,M,3] = sum over views of dL/dsh rebuilt from dL_dcolors [nviews][P][3] + campos [nviews][3]
+void launch_sh_grad_from_colors(int P, int D, int M, int nviews, const float* means3D, const float* shs,
+                                const float* campos, const float* dL_dcolors, float* dL_dsh, hipStream_t s);
 // sums each Gaussian's instance rows (slots [offsets[r-1], offsets[r]) of depth rank r) into grad_sum[order[r]]
 void launch_instance_reduce(int P, const uint32_t* order, const uint32_t* offsets, const float* inst_grad,
                             const uint8_t* row_valid,

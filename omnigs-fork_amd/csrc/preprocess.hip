@@ -12,6 +12,7 @@
 // HBM per Gaussian (D=3): reads 12 (xyz) + 12 (scale) + 16 (rot) + 4 (opacity) + 192 (SH) = 236 B,
 // writes 8 + 16 + 16 + 4 + 1 + 4 + 4 (radius) + 8 (sort key/value) = 61 B.
 #include "kernels.h"
+#include "sh_eval.h"
 
 namespace omr {
 
@@ -19,13 +20,6 @@ namespace omr {
 
 namespace {
 
-constexpr float SH_C0 = 0.28209479177387814f;  // auxiliary.h:32-49
-constexpr float SH_C1 = 0.4886025119029199f;
-constexpr float SH_C2_0 = 1.0925484305920792f, SH_C2_1 = -1.0925484305920792f, SH_C2_2 = 0.31539156525252005f,
-                SH_C2_3 = -1.0925484305920792f, SH_C2_4 = 0.5462742152960396f;
-constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH_C3_2 = -0.4570457994644658f,
-                SH_C3_3 = 0.3731763325901154f, SH_C3_4 = -0.4570457994644658f, SH_C3_5 = 1.445305721320277f,
-                SH_C3_6 = -0.5900435899266435f;
 constexpr float INV_PI = 0.318309886183790671537767526745028724f;  // M_1_PIf32
 constexpr float TWO_INV_PI = 0.636619772367581343075535053490057448f;  // M_2_PIf32
 
@@ -82,37 +76,6 @@ __device__ __forceinline__ float3 cov2d_from_J(const float* v, const float J0[3]
     c00 += 0.3f;
     c11 += 0.3f;
     return {c00, c01, c11};
-}
-
-// forward.cu:30-83, one channel at a time (glm vec3 ops are componentwise, same order)
-__device__ __forceinline__ void sh_to_rgb(int deg, float x, float y, float z, const float* sh, float out[3],
-                                          uint8_t& clamp_bits)
-{
-    clamp_bits = 0;
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-        auto s = [&](int k) { return sh[3 * k + ch]; };
-        float res = SH_C0 * s(0);
-        if (deg > 0) {
-            res = res - SH_C1 * y * s(1) + SH_C1 * z * s(2) - SH_C1 * x * s(3);
-            if (deg > 1) {
-                const float xx = x * x, yy = y * y, zz = z * z;
-                const float xy = x * y, yz = y * z, xz = x * z;
-                res = res + SH_C2_0 * xy * s(4) + SH_C2_1 * yz * s(5) + SH_C2_2 * (2.0f * zz - xx - yy) * s(6) +
-                      SH_C2_3 * xz * s(7) + SH_C2_4 * (xx - yy) * s(8);
-                if (deg > 2) {
-                    res = res + SH_C3_0 * y * (3.0f * xx - yy) * s(9) + SH_C3_1 * xy * z * s(10) +
-                          SH_C3_2 * y * (4.0f * zz - xx - yy) * s(11) +
-                          SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * s(12) +
-                          SH_C3_4 * x * (4.0f * zz - xx - yy) * s(13) + SH_C3_5 * z * (xx - yy) * s(14) +
-                          SH_C3_6 * x * (xx - 3.0f * yy) * s(15);
-                }
-            }
-        }
-        res += 0.5f;
-        if (res < 0) clamp_bits |= (uint8_t)(1u << ch);
-        out[ch] = fmaxf(res, 0.0f);
-    }
 }
 
 template <int CAM>

@@ -10,9 +10,18 @@ through exp/normalize/sigmoid is per Gaussian and linear in the incoming gradien
 sum over views and is applied once after the reduction instead of once per view.
 
 Flat buffer layout (float32, one segment per tensor, each contiguous — 59 floats = 236 B per Gaussian):
-    [ means3D 3P | sh 3MP | opacity P | scales 3P | rotations 4P ]
+    [ means3D 3P | opacity P | scales 3P | rotations 4P | sh 3MP ]
 The rasterizer backward writes straight into these views (RasterizeGaussiansBackwardCUDA(out=...)), so there
 is no pack/unpack copy before or after the collective.
+
+Two exchanges give the same summed gradients (up to the order of the float additions):
+  * allreduce_          one RCCL all-reduce of the whole 236 B/Gaussian buffer;
+  * allreduce_compact_  (default in bench.py) all-reduce of the first 44 B/Gaussian (xyz, opacity, scale,
+                        rotation) and an all-gather of each view's colour gradient (12 B/Gaussian) and camera
+                        position; every rank then rebuilds the summed SH gradient with the backward's own SH
+                        arithmetic (omr_sh_grad_from_colors). Per rank on a ring of n: 2(n-1)/n * 236 B/G vs
+                        2(n-1)/n * 44 + (n-1) * 12 B/G — at n = 8, 413 vs 161 MB for 1 M Gaussians, at n = 2 236 vs
+                        56 MB. xGMI is point-to-point (a 2-GPU job has ONE link), so bytes are the scaling cost.
 """
 from __future__ import annotations
 
@@ -21,7 +30,8 @@ from dataclasses import dataclass
 import torch
 import torch.distributed as dist
 
-SEGMENTS = ("dL_dmeans3D", "dL_dsh", "dL_dopacity", "dL_dscales", "dL_drotations")
+SEGMENTS = ("dL_dmeans3D", "dL_dopacity", "dL_dscales", "dL_drotations", "dL_dsh")
+REDUCED_FLOATS = 11  # per Gaussian ahead of the SH segment: xyz 3, opacity 1, scales 3, rotations 4
 
 
 @dataclass
@@ -40,8 +50,8 @@ class GradBuffer:
 
     def __init__(self, P: int, M: int, device, dtype=torch.float32):
         self.P, self.M = P, M
-        sizes = [3 * P, 3 * M * P, P, 3 * P, 4 * P]
-        shapes = [(P, 3), (P, M, 3), (P, 1), (P, 3), (P, 4)]
+        sizes = [3 * P, P, 3 * P, 4 * P, 3 * M * P]
+        shapes = [(P, 3), (P, 1), (P, 3), (P, 4), (P, M, 3)]
         self.flat = torch.empty(sum(sizes), dtype=dtype, device=device)
         self.views = {}
         off = 0
@@ -80,3 +90,32 @@ def allreduce_(buf: GradBuffer, info: DistInfo, average: bool = False, bucket_by
         dist.all_reduce(flat, op=dist.ReduceOp.SUM)
     if average:
         flat.div_(info.world_size)
+
+
+def allreduce_compact_(buf: GradBuffer, info: DistInfo, dL_dcolors: torch.Tensor, campos: torch.Tensor, rebuild,
+                       average: bool = False):
+    """Sum over ranks with the compact SH exchange (module docstring): all-reduce the 11 non-SH floats per
+    Gaussian, all-gather every rank's dL_dcolors [P,3] and campos [3], then
+    rebuild(campos_all [n,3], dcolors_all [n,P,3], out=dL_dsh view) writes the summed SH gradient. `rebuild` is
+    rasterizer.sh_grad_from_colors bound to the (replicated) means3D / SH / degree; tests pass a CPU model."""
+    if not info.enabled:
+        return
+    n, P = info.world_size, buf.P
+    prefix = buf.flat[:REDUCED_FLOATS * P]
+    dist.all_reduce(prefix, op=dist.ReduceOp.SUM)
+    dc = dL_dcolors.contiguous().view(P, 3)
+    cp = campos.contiguous().view(3).to(dc.dtype)
+    if dist.get_backend() == "nccl":
+        dcolors_all = torch.empty((n, P, 3), dtype=dc.dtype, device=dc.device)
+        campos_all = torch.empty((n, 3), dtype=dc.dtype, device=dc.device)
+        dist.all_gather_into_tensor(dcolors_all, dc)
+        dist.all_gather_into_tensor(campos_all, cp)
+    else:
+        parts = [torch.empty_like(dc) for _ in range(n)]
+        cps = [torch.empty_like(cp) for _ in range(n)]
+        dist.all_gather(parts, dc)
+        dist.all_gather(cps, cp)
+        dcolors_all, campos_all = torch.stack(parts), torch.stack(cps)
+    rebuild(campos_all, dcolors_all, out=buf.views["dL_dsh"])
+    if average:
+        buf.flat.div_(n)

@@ -66,6 +66,7 @@ def lib() -> C.CDLL:
         L.omr_debug_geometry.argtypes = [vp, i, vp, vp, vp, vp, vp, vp]
         L.omr_debug_wave_sum.argtypes = [vp, vp, vp]
         L.omr_profile_enable.argtypes = [i]
+        L.omr_sh_grad_from_colors.argtypes = [i, i, i, i, vp, vp, vp, vp, vp, vp]
         L.omr_profile_set_mask.argtypes = [C.c_uint32]
         L.omr_profile_read.restype = i
         L.omr_profile_read.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_uint64), i]
@@ -232,6 +233,26 @@ def RasterizeGaussiansBackwardCUDA(background, means3D, radii, colors, scales, r
         _check(rc, "RasterizeGaussiansBackwardCUDA")
     return (o["dL_dmeans2D"], o["dL_dcolors"], o["dL_dopacity"], o["dL_dmeans3D"], o["dL_dcov3D"], o["dL_dsh"],
             o["dL_dscales"], o["dL_drotations"])
+
+
+def sh_grad_from_colors(means3D, sh, degree, campos_all, dcolors_all, out=None):
+    """Extension for view-parallel DP (parallel.allreduce_compact_): the sum over n views of dL/dsh, rebuilt from
+    each view's dL_dcolors ([n,P,3], the backward's second output) and camera position ([n,3]) with the backward's
+    own SH arithmetic (omr_sh_grad_from_colors). Returns dL_dsh [P,M,3] (written into `out` if given)."""
+    m, shc = _dev_f32(means3D, "means3D"), _dev_f32(sh, "sh")
+    cp, dc = _dev_f32(campos_all, "campos_all"), _dev_f32(dcolors_all, "dcolors_all")
+    P, M = int(m.shape[0]), int(shc.shape[1])
+    n = int(cp.shape[0])
+    if tuple(dc.shape) != (n, P, 3) or tuple(cp.shape) != (n, 3):
+        raise RasterizerError("dcolors_all must be [n,P,3] and campos_all [n,3]")
+    if out is None:
+        out = torch.empty((P, M, 3), dtype=torch.float32, device=m.device)
+    elif tuple(out.shape) != (P, M, 3) or not out.is_contiguous() or out.dtype != torch.float32:
+        raise RasterizerError(f"out must be a contiguous float32 tensor of shape {(P, M, 3)}")
+    rc = lib().omr_sh_grad_from_colors(P, int(degree), M, n, _ptr(m), _ptr(shc), _ptr(cp), _ptr(dc), out.data_ptr(),
+                                       _stream(m.device))
+    _check(rc, "sh_grad_from_colors")
+    return out
 
 
 def markVisible(means3D, viewmatrix, projmatrix, camera_type=CAMERA_PINHOLE):

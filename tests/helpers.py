@@ -84,3 +84,47 @@ def grad_close(a, b, rtol=1e-3, atol_frac=1e-4):
     lim = rtol * np.abs(b) + atol_frac * scale
     bad = err > lim
     return (not bad.any()), (float(err.max()) if err.size else 0.0), int(bad.sum())
+
+
+# SH constants of cuda_rasterizer/auxiliary.h:32-49 (the test-side model of omr_sh_grad_from_colors)
+_C0, _C1 = 0.28209479177387814, 0.4886025119029199
+_C2 = (1.0925484305920792, -1.0925484305920792, 0.31539156525252005, -1.0925484305920792, 0.5462742152960396)
+_C3 = (-0.5900435899266435, 2.890611442640554, -0.4570457994644658, 0.3731763325901154, -0.4570457994644658,
+       1.445305721320277, -0.5900435899266435)
+
+
+def sh_basis_np(deg, x, y, z):
+    """SH basis values [..., 16] of forward.cu:30-83 / backward.cu:56-112 (zeros beyond (deg+1)^2), float64."""
+    c = np.zeros(x.shape + (16,))
+    c[..., 0] = _C0
+    if deg > 0:
+        c[..., 1], c[..., 2], c[..., 3] = -_C1 * y, _C1 * z, -_C1 * x
+    if deg > 1:
+        xx, yy, zz = x * x, y * y, z * z
+        c[..., 4], c[..., 5] = _C2[0] * x * y, _C2[1] * y * z
+        c[..., 6], c[..., 7], c[..., 8] = _C2[2] * (2 * zz - xx - yy), _C2[3] * x * z, _C2[4] * (xx - yy)
+    if deg > 2:
+        c[..., 9] = _C3[0] * y * (3 * xx - yy)
+        c[..., 10] = _C3[1] * x * y * z
+        c[..., 11] = _C3[2] * y * (4 * zz - xx - yy)
+        c[..., 12] = _C3[3] * z * (2 * zz - 3 * xx - 3 * yy)
+        c[..., 13] = _C3[4] * x * (4 * zz - xx - yy)
+        c[..., 14] = _C3[5] * z * (xx - yy)
+        c[..., 15] = _C3[6] * x * (xx - 3 * yy)
+    return c
+
+
+def sh_grad_from_colors_np(means3D, shs, deg, campos_all, dcolors_all):
+    """Sum over views of dL/dsh rebuilt from each view's colour gradient (model of omr_sh_grad_from_colors):
+    dL/dsh_k = basis_k(dir_v) * dRGB_v, dRGB_v zeroed where the forward clamped the colour (backward.cu:30-151)."""
+    m = np.asarray(means3D, np.float64)
+    sh = np.asarray(shs, np.float64)
+    out = np.zeros_like(sh)
+    for cp, dc in zip(np.asarray(campos_all, np.float64), np.asarray(dcolors_all, np.float64)):
+        d = m - cp
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        basis = sh_basis_np(deg, d[:, 0], d[:, 1], d[:, 2])
+        rgb = np.einsum("pk,pkc->pc", basis, sh[:, :16]) + 0.5
+        dm = np.where(rgb < 0, 0.0, dc)
+        out[:, :16] += basis[:, :, None] * dm[:, None, :]
+    return out

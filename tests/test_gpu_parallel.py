@@ -1,0 +1,48 @@
+"""The view-parallel SH-gradient rebuild (omr_sh_grad_from_colors, parallel.allreduce_compact_) on the GPU.
+
+For several views of the same Gaussians, the HIP backward gives per-view dL/dsh and dL/dcolors. Summing the
+per-view dL/dsh in view order must equal, bit for bit, the rebuild from the per-view dL/dcolors and camera
+positions (same SH arithmetic, sh_eval.h, same products, same summation order); it must also match the float64
+numpy model of tests/helpers.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import grad_close, hip_run, make_case, omr, scene, sh_grad_from_colors_np, to_np
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("cam_type,deg", [(scene.CAMERA_LONLAT, 3), (scene.CAMERA_PINHOLE, 3),
+                                          (scene.CAMERA_LONLAT, 1)])
+def test_sh_rebuild_equals_sum_of_views(cam_type, deg):
+    R = omr.rasterizer
+    views = (0, 3, 5)
+    W, H = (256, 128) if cam_type == scene.CAMERA_LONLAT else (160, 90)
+    dsh_sum, dcolors, campos = None, [], []
+    g = None
+    for v in views:
+        g, cam, dL = make_case(3000, W, H, cam_type, 91, view_index=v, sh_degree=deg, spread=2.0)
+        h = hip_run(g, cam, dL)
+        dsh = h["grads"]["dsh"]
+        dsh_sum = dsh.clone() if dsh_sum is None else dsh_sum + dsh
+        dcolors.append(h["grads"]["dcolor"])
+        campos.append(torch.from_numpy(cam.campos).cuda())
+    dev = dsh_sum.device
+    means = torch.from_numpy(g.means3D).to(dev)
+    shs = torch.from_numpy(g.shs).to(dev)
+    rebuilt = R.sh_grad_from_colors(means, shs, deg, torch.stack(campos), torch.stack(dcolors))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(to_np(rebuilt), to_np(dsh_sum))
+    model = sh_grad_from_colors_np(g.means3D, g.shs, deg, to_np(torch.stack(campos)), to_np(torch.stack(dcolors)))
+    ok, emax, nbad = grad_close(to_np(rebuilt), model)
+    assert ok, (emax, nbad)
+
+
+def test_sh_rebuild_argument_checks():
+    R = omr.rasterizer
+    m = torch.zeros((10, 3), device="cuda")
+    sh = torch.zeros((10, 16, 3), device="cuda")
+    with pytest.raises(R.RasterizerError):
+        R.sh_grad_from_colors(m, sh, 3, torch.zeros((2, 3), device="cuda"), torch.zeros((3, 10, 3), device="cuda"))

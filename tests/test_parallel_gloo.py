@@ -33,10 +33,11 @@ def _view_grads(view):
     g, cam, dL = make_case(300, 64, 32, 3, 77, view_index=view, spread=3.0)
     _, _, gr = oracle_run(g, cam, dL)
     return {"dL_dmeans3D": gr["dmean3D"], "dL_dsh": gr["dsh"], "dL_dopacity": gr["dopacity"],
-            "dL_dscales": gr["dscale"], "dL_drotations": gr["drot"]}
+            "dL_dscales": gr["dscale"], "dL_drotations": gr["drot"], "dL_dcolors": gr["dcolor"],
+            "campos": cam.campos, "means3D": g.means3D, "shs": g.shs, "deg": g.sh_degree}
 
 
-def _worker(rank, world, port, bucket, average, q):
+def _worker(rank, world, port, bucket, average, q, compact=False):
     import sys
 
     sys.path[:0] = [ROOT]
@@ -53,18 +54,31 @@ def _worker(rank, world, port, bucket, average, q):
         buf = par.GradBuffer(300, 16, torch.device("cpu"))
         for k, v in buf.views.items():
             v.copy_(torch.from_numpy(grads[k]))
-        par.allreduce_(buf, par.DistInfo(rank, world, rank), average=average, bucket_bytes=bucket)
+        info = par.DistInfo(rank, world, rank)
+        if compact:
+            sys.path[:0] = [os.path.join(ROOT, "tests")]
+            from helpers import sh_grad_from_colors_np
+
+            def rebuild(campos_all, dcolors_all, out):
+                out.copy_(torch.from_numpy(sh_grad_from_colors_np(grads["means3D"], grads["shs"], grads["deg"],
+                                                                  campos_all.numpy(), dcolors_all.numpy())))
+
+            par.allreduce_compact_(buf, info, torch.from_numpy(grads["dL_dcolors"]),
+                                   torch.from_numpy(grads["campos"]), rebuild, average=average)
+        else:
+            par.allreduce_(buf, info, average=average, bucket_bytes=bucket)
         q.put((rank, {k: v.numpy().copy() for k, v in buf.views.items()}))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bucket,average", [(0, False), (4096, False), (0, True)])
-def test_allreduce_equals_sum_of_views(bucket, average, oracle_mod):
+@pytest.mark.parametrize("bucket,average,compact", [(0, False, False), (4096, False, False), (0, True, False),
+                                                    (0, False, True), (0, True, True)])
+def test_allreduce_equals_sum_of_views(bucket, average, compact, oracle_mod):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, bucket, average, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, bucket, average, q, compact)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=240) for _ in procs)
@@ -72,12 +86,17 @@ def test_allreduce_equals_sum_of_views(bucket, average, oracle_mod):
         p.join(timeout=60)
         assert p.exitcode == 0
     g0, g1 = _view_grads(0), _view_grads(1)
-    for k in g0:
+    for k in ("dL_dmeans3D", "dL_dsh", "dL_dopacity", "dL_dscales", "dL_drotations"):
         ref = g0[k] + g1[k]
         if average:
             ref = ref / 2
+        # the compact exchange rebuilds the SH sum in float64 here (the HIP rebuild is checked bitwise on the GPU)
+        rtol, atol = (1e-5, 1e-8) if compact and k == "dL_dsh" else (1e-6, 1e-9)
         for r in (0, 1):
-            np.testing.assert_allclose(res[r][k], ref, rtol=1e-6, atol=1e-9, err_msg=f"{k} rank {r}")
+            np.testing.assert_allclose(res[r][k], ref, rtol=rtol, atol=atol, err_msg=f"{k} rank {r}")
+    if compact:  # every rank holds the identical sum
+        for k in res[0]:
+            np.testing.assert_array_equal(res[0][k], res[1][k])
 
 
 def test_gradbuffer_layout():
