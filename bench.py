@@ -74,7 +74,7 @@ def stage_bytes(stage, P, V, L, N, T, M=16, D=3):
     }.get(stage, 0)
 
 
-def workload_text(cfg_name, config, world, P, W, H, camera_type, sh_degree):
+def workload_text(cfg_name, config, world, P, W, H, camera_type, sh_degree, exchange="compact"):
     cam = lambda w, h, t: f"{w}x{h} " + ("equirect (camera_type=3)" if t == 3 else "pinhole (camera_type=1)")
     if config == "E" and world > 1:
         views = (f"{cam(4096, 2048, 3)} on ranks 0-{world // 2 - 1}, {cam(1920, 1080, 1)} on ranks "
@@ -82,7 +82,10 @@ def workload_text(cfg_name, config, world, P, W, H, camera_type, sh_degree):
     else:
         views = cam(W, H, camera_type)
     text = f"{cfg_name}: {P} Gaussians, {views}, SH degree {sh_degree}, one view per GPU"
-    if world > 1:
+    if world > 1 and exchange == "compact":
+        text += (", RCCL gradient exchange: all-reduce of 44 B/Gaussian + all-gather of 12 B/Gaussian/view colour "
+                 "gradients, SH gradient rebuilt on every rank")
+    elif world > 1:
         text += ", RCCL sum all-reduce of 236 B/Gaussian gradients"
     return text
 
@@ -275,9 +278,11 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (SplitMix64 scene, SURVEY.md §8(d)); random-init Gaussians, fixed dL/dout",
-        "config": {"workload": workload_text(cfg_name, args.config, world, P, W, H, cam.camera_type, g.sh_degree),
+        "config": {"workload": workload_text(cfg_name, args.config, world, P, W, H, cam.camera_type, g.sh_degree,
+                                               args.exchange),
                    "P": P, "V": V, "L": L, "N": N, "T": T, "width": W, "height": H,
-                   "parallelism": f"view-parallel dp{world}", "boundary": args.boundary},
+                   "parallelism": f"view-parallel dp{world}", "boundary": args.boundary,
+                   "exchange": args.exchange if world > 1 else None},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 4),
