@@ -112,6 +112,15 @@ int omr_lonlat_backward(int P, int D, int M, int R, const float* background, int
 int omr_sh_grad_from_colors(int P, int D, int M, int nviews, const float* means3D, const float* shs,
                             const float* campos, const float* dL_dcolors, float* dL_dsh, void* stream);
 
+/* --- training loss (extension; reference include/loss_utils.h:31-129, gaussian_trainer.cpp:88-90) --- */
+/* loss = (1 - lambda) * mean|img - gt| + lambda * (1 - ssim(img, gt)) over [C,H,W] float images (11x11 Gaussian
+ * window, sigma 1.5, zero padding, C1 = 0.01^2, C2 = 0.03^2), forward and backward in one pass:
+ * dL_dimg [C,H,W] = dloss/dimg, out3 (device, 3 floats) = {loss, l1, ssim}. scratch: device floats, at least
+ * omr_l1_ssim_scratch_floats(C, H, W). */
+size_t omr_l1_ssim_scratch_floats(int C, int H, int W);
+int omr_l1_ssim_loss(const float* img, const float* gt, int C, int H, int W, float lambda_dssim, float* dL_dimg,
+                     float* out3, float* scratch, void* stream);
+
 /* --- scratch sizes (bytes the allocation callbacks are asked for) -------------------------------- */
 size_t omr_geometry_bytes(int P);
 size_t omr_image_bytes(int width, int height);

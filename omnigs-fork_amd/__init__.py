@@ -7,7 +7,8 @@ Layout:
   csrc/rasterize_points.cpp  LibTorch drop-in of include/rasterize_points.h (reference symbols)
   rasterizer.py    Python mirror of the reference boundary + autograd wrapper, on the C ABI
   renderer.py      GaussianRenderer::renderLonlat / render glue (activations, settings)
-  parallel.py      view-parallel data parallelism (one view per GPU, RCCL all-reduce of Gaussian gradients)
+  parallel.py      view-parallel data parallelism (one view per GPU, RCCL exchange of Gaussian gradients)
+  losses.py        training loss (1 - lambda) L1 + lambda (1 - SSIM), fused forward+backward HIP kernel
   scene.py         deterministic synthetic scenes and camera poses
 """
 from . import scene  # noqa: F401
@@ -17,7 +18,7 @@ __all__ = ["scene", "rasterizer"]
 
 def __getattr__(name):
     # the HIP-backed modules import torch and the shared library lazily
-    if name in ("rasterizer", "renderer", "parallel"):
+    if name in ("rasterizer", "renderer", "parallel", "losses"):
         import importlib
 
         mod = importlib.import_module(f"{__name__}.{name}")

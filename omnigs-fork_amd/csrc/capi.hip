@@ -539,6 +539,21 @@ int omr_sh_grad_from_colors(int P, int D, int M, int nviews, const float* means3
     return hip_check("sh_grad_from_colors");
 }
 
+size_t omr_l1_ssim_scratch_floats(int C, int H, int W)
+{
+    return (C <= 0 || H <= 0 || W <= 0) ? 0 : l1_ssim_scratch_floats(C, H, W);
+}
+
+int omr_l1_ssim_loss(const float* img, const float* gt, int C, int H, int W, float lambda_dssim, float* dL_dimg,
+                     float* out3, float* scratch, void* stream)
+{
+    g_last_error.clear();
+    if (C <= 0 || H <= 0 || W <= 0) return fail(OMR_ERR_INVALID_ARGUMENT, "bad C / H / W");
+    if (!img || !gt || !dL_dimg || !out3 || !scratch) return fail(OMR_ERR_INVALID_ARGUMENT, "missing pointer");
+    launch_l1_ssim(img, gt, C, H, W, lambda_dssim, dL_dimg, out3, scratch, (hipStream_t)stream);
+    return hip_check("l1_ssim_loss");
+}
+
 size_t omr_geometry_bytes(int P) { return GeomState::carve(nullptr, (size_t)std::max(P, 0), nullptr); }
 
 size_t omr_image_bytes(int width, int height)

@@ -126,4 +126,13 @@ void launch_instance_reduce(int P, const uint32_t* order, const uint32_t* offset
                             const uint8_t* row_valid,
                             float* grad_sum, hipStream_t s);
 
+// ssim.hip: fused L1 + SSIM loss (loss_utils.h:31-129), forward and backward
+struct SsimWindow {
+    float w[11];
+};
+SsimWindow ssim_window();
+size_t l1_ssim_scratch_floats(int C, int H, int W);
+void launch_l1_ssim(const float* img, const float* gt, int C, int H, int W, float lambda, float* dimg, float* out3,
+                    float* scratch, hipStream_t s);
+
 }  // namespace omr

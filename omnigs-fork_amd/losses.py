@@ -1,0 +1,77 @@
+"""Training loss of OmniGS on the gfx950 library: (1 - lambda) * L1 + lambda * (1 - SSIM).
+
+Mirrors include/loss_utils.h:31-129 (l1_loss, ssim) as combined by gaussian_trainer.cpp:88-90 and
+gaussian_mapper.cpp:403-412. `l1_ssim_loss` runs the fused HIP kernel (omr_l1_ssim_loss, csrc/ssim.hip): one pass
+computes the loss and d loss / d image, and the autograd backward scales that gradient. `l1_loss` / `ssim` are the
+reference's own formulas in torch (kept for callers that want the separate terms; they are not the hot path).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+import torch.nn.functional as F
+
+from . import rasterizer as R
+
+
+def l1_loss(network_output: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
+    """loss_utils.h:31-34."""
+    return torch.abs(network_output - gt).mean()
+
+
+def _gaussian(window_size: int, sigma: float, device) -> torch.Tensor:
+    """loss_utils.h:54-67."""
+    x = torch.arange(window_size, dtype=torch.float32, device=device) - window_size // 2
+    g = torch.exp(-(x * x) / (2.0 * sigma * sigma))
+    return g / g.sum()
+
+
+def ssim(img1: torch.Tensor, img2: torch.Tensor, window_size: int = 11, size_average: bool = True) -> torch.Tensor:
+    """loss_utils.h:69-129 with torch ops ([C,H,W] images, depthwise 11x11 Gaussian window, zero padding)."""
+    channel = img1.shape[-3]
+    g = _gaussian(window_size, 1.5, img1.device).unsqueeze(1)
+    window = (g @ g.t()).to(img1.dtype).expand(channel, 1, window_size, window_size).contiguous()
+    pad = window_size // 2
+    conv = lambda x: F.conv2d(x, window, padding=pad, groups=channel)
+    mu1, mu2 = conv(img1), conv(img2)
+    mu1_sq, mu2_sq, mu1_mu2 = mu1 * mu1, mu2 * mu2, mu1 * mu2
+    sigma1_sq = conv(img1 * img1) - mu1_sq
+    sigma2_sq = conv(img2 * img2) - mu2_sq
+    sigma12 = conv(img1 * img2) - mu1_mu2
+    C1, C2 = 0.01 ** 2, 0.03 ** 2
+    ssim_map = ((2 * mu1_mu2 + C1) * (2 * sigma12 + C2)) / ((mu1_sq + mu2_sq + C1) * (sigma1_sq + sigma2_sq + C2))
+    return ssim_map.mean() if size_average else ssim_map.mean(1).mean(1).mean(1)
+
+
+class _FusedL1SSIM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, image, gt, lambda_dssim):
+        if image.device.type != "cuda" or gt.device.type != "cuda":
+            raise R.RasterizerError("l1_ssim_loss needs HIP tensors (the fused loss has no CPU path)")
+        img = image.detach().contiguous().float()
+        ref = gt.detach().contiguous().float()
+        if img.shape != ref.shape or img.dim() != 3:
+            raise R.RasterizerError("image and gt must both be [C,H,W]")
+        Cn, H, W = (int(s) for s in img.shape)
+        L = R.lib()
+        grad = torch.empty_like(img)
+        out3 = torch.empty(3, dtype=torch.float32, device=img.device)
+        scratch = torch.empty(int(L.omr_l1_ssim_scratch_floats(Cn, H, W)), dtype=torch.float32, device=img.device)
+        rc = L.omr_l1_ssim_loss(img.data_ptr(), ref.data_ptr(), Cn, H, W, float(lambda_dssim), grad.data_ptr(),
+                                out3.data_ptr(), scratch.data_ptr(), R._stream(img.device))
+        R._check(rc, "l1_ssim_loss")
+        ctx.save_for_backward(grad)
+        ctx.mark_non_differentiable(out3)
+        return out3[0], out3
+
+    @staticmethod
+    def backward(ctx, grad_loss, _grad_terms):
+        (grad,) = ctx.saved_tensors
+        return grad * grad_loss, None, None
+
+
+def l1_ssim_loss(image: torch.Tensor, gt: torch.Tensor, lambda_dssim: float):
+    """(1 - lambda) * l1_loss(image, gt) + lambda * (1 - ssim(image, gt)), fused. Returns (loss, terms) where
+    terms = tensor([loss, l1, ssim]) (no gradient; for logging like gaussian_trainer.cpp:99-110)."""
+    return _FusedL1SSIM.apply(image, gt, float(lambda_dssim))

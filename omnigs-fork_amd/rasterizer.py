@@ -67,6 +67,9 @@ def lib() -> C.CDLL:
         L.omr_debug_wave_sum.argtypes = [vp, vp, vp]
         L.omr_profile_enable.argtypes = [i]
         L.omr_sh_grad_from_colors.argtypes = [i, i, i, i, vp, vp, vp, vp, vp, vp]
+        L.omr_l1_ssim_scratch_floats.restype = sz
+        L.omr_l1_ssim_scratch_floats.argtypes = [i, i, i]
+        L.omr_l1_ssim_loss.argtypes = [vp, vp, i, i, i, f, vp, vp, vp, vp]
         L.omr_profile_set_mask.argtypes = [C.c_uint32]
         L.omr_profile_read.restype = i
         L.omr_profile_read.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_uint64), i]
