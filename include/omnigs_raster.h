@@ -121,6 +121,52 @@ size_t omr_l1_ssim_scratch_floats(int C, int H, int W);
 int omr_l1_ssim_loss(const float* img, const float* gt, int C, int H, int W, float lambda_dssim, float* dL_dimg,
                      float* out3, float* scratch, void* stream);
 
+/* --- training step after the backward (extension) ------------------------------- */
+/* Adam over the six GaussianModel parameter groups in ONE launch, replacing torch::optim::Adam::step (LibTorch
+ * 2.0.1 adam.cpp; groups, learning rates and eps 1e-15 from gaussian_model.cpp:485-518, stepped at
+ * gaussian_mapper.cpp:486). Group order k: 0 xyz [P,3], 1 features_dc [P,1,3], 2 features_rest [P,Mr,3],
+ * 3 opacity [P,1] (logit), 4 scaling [P,3] (log), 5 rotation [P,4] (raw). params / exp_avg / exp_avg_sq are
+ * updated in place and must be 16-byte aligned. step[k] is the step count AFTER this step's increment (>= 1).
+ * A group with params[k] or grads[k] NULL is skipped (adam.cpp skips parameters whose gradient is undefined).
+ * grad_kind:
+ *   OMR_ADAM_RAW_GRADS     grads[k] has params[k]'s layout (the gradients autograd would leave in .grad);
+ *   OMR_ADAM_RASTER_GRADS  grads are the rasterizer backward's outputs w.r.t. the ACTIVATED tensors the renderer
+ *                          feeds it (gaussian_renderer.cpp:167-290): grads[0] dL_dmeans3D, grads[1] = grads[2] =
+ *                          dL_dsh [P,Mr+1,3], grads[3] dL_dopacity (of sigmoid(opacity)), grads[4] dL_dscales (of
+ *                          exp(scaling)), grads[5] dL_drotations (of normalize(rotation)); the activation
+ *                          backward (cat / sigmoid / exp / normalize) is applied in registers. */
+#define OMR_ADAM_RAW_GRADS 0
+#define OMR_ADAM_RASTER_GRADS 1
+int omr_adam_step(int P, int Mr, float* const params[6], float* const exp_avg[6], float* const exp_avg_sq[6],
+                  const float* const grads[6], int grad_kind, const float lr[6], const int64_t step[6], float beta1,
+                  float beta2, float eps, void* stream);
+/* addDensificationStats (gaussian_model.cpp:839-853) + the max_radii2D update (gaussian_mapper.cpp:427-432) for
+ * visibility_filter = radii > 0: accum[i] += |viewspace_grad[i][0:2]|, denom[i] += 1, max_radii2D[i] =
+ * max(max_radii2D[i], radii[i]). viewspace_grad is dL_dmeans2D with row stride viewspace_stride (3). */
+int omr_densification_stats(int P, const int* radii, const float* viewspace_grad, int viewspace_stride,
+                            float* xyz_gradient_accum, float* denom, float* max_radii2D, void* stream);
+/* densifyAndPrune (gaussian_model.cpp:812-837 with densifyAndClone / densifyAndSplit / prunePoints :619-810) in
+ * two calls. omr_densify_plan classifies every Gaussian into `plan` (device, omr_densify_plan_bytes(P)) and
+ * synchronises the stream (the reference reads counts to the host too, :768) to return counts = {P_new, clones
+ * kept, split-selected S, splits kept}. The caller allocates the P_new-row outputs and 2*S*3 standard normal
+ * samples (batch-major: copy 1 of every selected split, then copy 2; the reference draws them with at::normal,
+ * :751) and calls omr_densify_apply, which writes the final arrays in the reference's order. exp_avg / exp_avg_sq
+ * arrays may be NULL (no optimizer state) or hold NULL entries; exist_in / exist_out (int32 exist_since_iter)
+ * may be NULL. xyz_gradient_accum, denom and max_radii2D of the result are zeros (the caller's memset). */
+size_t omr_densify_plan_bytes(int P);
+int omr_densify_plan(int P, const float* xyz_gradient_accum, const float* denom, const float* scaling,
+                     const float* opacity, float max_grad, float min_opacity, float extent, float percent_dense,
+                     int max_screen_size, int prune_by_extent, void* plan, int64_t counts[4], void* stream);
+int omr_densify_apply(int P, int Mr, const void* plan, const float* const params_in[6],
+                      const float* const exp_avg_in[6], const float* const exp_avg_sq_in[6], const int32_t* exist_in,
+                      const float* normals, float* const params_out[6], float* const exp_avg_out[6],
+                      float* const exp_avg_sq_out[6], int32_t* exist_out, void* stream);
+/* resetOpacity (gaussian_model.cpp:564-572): opacity = inverse_sigmoid(min(sigmoid(opacity), ceiling)) and the
+ * opacity group's Adam moments zeroed (either may be NULL). The reference passes
+ * ones_like(sigmoid(opacity) * 0.01) as the bound, i.e. ceiling = 1 (value unchanged up to rounding; only the
+ * moments reset); 0.01 gives the 3DGS behaviour. */
+int omr_reset_opacity(int P, float* opacity, float* exp_avg, float* exp_avg_sq, float ceiling, void* stream);
+
 /* --- scratch sizes (bytes the allocation callbacks are asked for) -------------------------------- */
 size_t omr_geometry_bytes(int P);
 size_t omr_image_bytes(int width, int height);

@@ -9,6 +9,8 @@ Layout:
   renderer.py      GaussianRenderer::renderLonlat / render glue (activations, settings)
   parallel.py      view-parallel data parallelism (one view per GPU, RCCL exchange of Gaussian gradients)
   losses.py        training loss (1 - lambda) L1 + lambda (1 - SSIM), fused forward+backward HIP kernel
+  optim.py         Adam over the six GaussianModel groups (activation backward fused), LR schedule, densification
+  trainer.py       one training iteration without autograd: render, fused loss, backward, stats, Adam
   scene.py         deterministic synthetic scenes and camera poses
 """
 from . import scene  # noqa: F401
@@ -18,7 +20,7 @@ __all__ = ["scene", "rasterizer"]
 
 def __getattr__(name):
     # the HIP-backed modules import torch and the shared library lazily
-    if name in ("rasterizer", "renderer", "parallel", "losses"):
+    if name in ("rasterizer", "renderer", "parallel", "losses", "optim", "trainer"):
         import importlib
 
         mod = importlib.import_module(f"{__name__}.{name}")

@@ -7,6 +7,7 @@
 //   render backward (per-instance gradient rows) -> fused per-Gaussian backward.
 // Everything is enqueued on the caller's stream; no allocation happens outside the three callbacks.
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -552,6 +553,119 @@ int omr_l1_ssim_loss(const float* img, const float* gt, int C, int H, int W, flo
     if (!img || !gt || !dL_dimg || !out3 || !scratch) return fail(OMR_ERR_INVALID_ARGUMENT, "missing pointer");
     launch_l1_ssim(img, gt, C, H, W, lambda_dssim, dL_dimg, out3, scratch, (hipStream_t)stream);
     return hip_check("l1_ssim_loss");
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+int omr_adam_step(int P, int Mr, float* const params[6], float* const exp_avg[6], float* const exp_avg_sq[6],
+                  const float* const grads[6], int grad_kind, const float lr[6], const int64_t step[6], float beta1,
+                  float beta2, float eps, void* stream)
+{
+    g_last_error.clear();
+    if (P < 0 || Mr < 0 || Mr > 15) return fail(OMR_ERR_INVALID_ARGUMENT, "bad P / Mr");
+    if (grad_kind != OMR_ADAM_RAW_GRADS && grad_kind != OMR_ADAM_RASTER_GRADS)
+        return fail(OMR_ERR_INVALID_ARGUMENT, "bad grad_kind");
+    if (!params || !exp_avg || !exp_avg_sq || !grads || !lr || !step) return fail(OMR_ERR_INVALID_ARGUMENT, "missing array");
+    if ((size_t)P * 3 * (size_t)Mr > 0xFFFFFFF0u) return fail(OMR_ERR_INVALID_ARGUMENT, "P too large");
+    const uint32_t width[6] = {3u, 3u, 3u * (uint32_t)Mr, 1u, 3u, 4u};
+    static const int raster_kind[6] = {ADAM_PLAIN, ADAM_SH_DC, ADAM_SH_REST, ADAM_OPACITY, ADAM_SCALING, ADAM_ROTATION};
+    AdamArgs a{};
+    a.M = Mr + 1;
+    a.beta1 = beta1, a.beta2 = beta2, a.omb1 = (float)(1.0 - (double)beta1), a.omb2 = (float)(1.0 - (double)beta2);
+    a.eps = eps;
+    for (int k = 0; k < 6; ++k) {
+        const uint32_t n = (uint32_t)P * width[k];
+        if (n == 0 || !params[k] || !grads[k]) continue;  // adam.cpp skips parameters without a gradient
+        if (!exp_avg[k] || !exp_avg_sq[k]) return fail(OMR_ERR_INVALID_ARGUMENT, "missing optimizer state");
+        const bool gplain = grad_kind == OMR_ADAM_RAW_GRADS || (k != 1 && k != 2);
+        if (!aligned16(params[k]) || !aligned16(exp_avg[k]) || !aligned16(exp_avg_sq[k]) || (gplain && !aligned16(grads[k])))
+            return fail(OMR_ERR_INVALID_ARGUMENT, "parameter / state / gradient not 16-byte aligned");
+        if (step[k] < 1) return fail(OMR_ERR_INVALID_ARGUMENT, "step must be >= 1");
+        // adam.cpp: bias corrections in double, step_size = lr / bias_correction1
+        const double bc1 = 1.0 - std::pow((double)beta1, (double)step[k]);
+        const double bc2 = 1.0 - std::pow((double)beta2, (double)step[k]);
+        AdamGroup& G = a.group[a.ngroups++];
+        G.p = params[k], G.m = exp_avg[k], G.v = exp_avg_sq[k], G.g = grads[k], G.n = n;
+        G.kind = grad_kind == OMR_ADAM_RAW_GRADS ? ADAM_PLAIN : raster_kind[k];
+        G.neg_step_size = (float)(-((double)lr[k] / bc1));
+        G.bc2_sqrt = (float)std::sqrt(bc2);
+    }
+    launch_adam(a, (hipStream_t)stream);
+    return hip_check("adam_step");
+}
+
+int omr_densification_stats(int P, const int* radii, const float* viewspace_grad, int viewspace_stride,
+                            float* xyz_gradient_accum, float* denom, float* max_radii2D, void* stream)
+{
+    g_last_error.clear();
+    if (P < 0 || viewspace_stride < 2) return fail(OMR_ERR_INVALID_ARGUMENT, "bad P / stride");
+    if (P == 0) return OMR_OK;
+    if (!radii || !viewspace_grad || !xyz_gradient_accum || !denom || !max_radii2D)
+        return fail(OMR_ERR_INVALID_ARGUMENT, "missing pointer");
+    launch_densification_stats(P, radii, viewspace_grad, viewspace_stride, xyz_gradient_accum, denom, max_radii2D,
+                               (hipStream_t)stream);
+    return hip_check("densification_stats");
+}
+
+size_t omr_densify_plan_bytes(int P) { return densify_plan_bytes(P); }
+
+int omr_densify_plan(int P, const float* xyz_gradient_accum, const float* denom, const float* scaling,
+                     const float* opacity, float max_grad, float min_opacity, float extent, float percent_dense,
+                     int max_screen_size, int prune_by_extent, void* plan, int64_t counts[4], void* stream)
+{
+    g_last_error.clear();
+    if (P < 0) return fail(OMR_ERR_INVALID_ARGUMENT, "bad P");
+    if (!plan || !counts) return fail(OMR_ERR_INVALID_ARGUMENT, "missing pointer");
+    if (P > 0 && (!xyz_gradient_accum || !denom || !scaling || !opacity))
+        return fail(OMR_ERR_INVALID_ARGUMENT, "missing pointer");
+    hipStream_t s = (hipStream_t)stream;
+    launch_densify_plan(P, xyz_gradient_accum, denom, scaling, opacity, max_grad, min_opacity, extent, percent_dense,
+                        max_screen_size, prune_by_extent, (char*)plan, s);
+    uint4 t;
+    OMR_HIP(hipMemcpyAsync(&t, densify_plan_totals(P, (const char*)plan), sizeof(t), hipMemcpyDeviceToHost, s));
+    OMR_HIP(hipStreamSynchronize(s));
+    counts[0] = (int64_t)t.x + t.y + 2 * (int64_t)t.z;  // P after densify and prune
+    counts[1] = t.y;                                     // clones kept
+    counts[2] = t.w;                                     // split-selected: rows of normals = 2 * counts[2]
+    counts[3] = t.z;                                     // splits kept (each adds two points)
+    return hip_check("densify_plan");
+}
+
+int omr_densify_apply(int P, int Mr, const void* plan, const float* const params_in[6],
+                      const float* const exp_avg_in[6], const float* const exp_avg_sq_in[6], const int32_t* exist_in,
+                      const float* normals, float* const params_out[6], float* const exp_avg_out[6],
+                      float* const exp_avg_sq_out[6], int32_t* exist_out, void* stream)
+{
+    g_last_error.clear();
+    if (P < 0 || Mr < 0 || Mr > 15) return fail(OMR_ERR_INVALID_ARGUMENT, "bad P / Mr");
+    if (P == 0) return OMR_OK;
+    if (!plan || !params_in || !params_out) return fail(OMR_ERR_INVALID_ARGUMENT, "missing pointer");
+    DensifyIO io{};
+    for (int k = 0; k < 6; ++k) {
+        if ((!params_in[k] || !params_out[k]) && !(k == 2 && Mr == 0))
+            return fail(OMR_ERR_INVALID_ARGUMENT, "missing parameter pointer");
+        io.p_in[k] = params_in[k], io.p_out[k] = params_out[k];
+        io.m_in[k] = exp_avg_in ? exp_avg_in[k] : nullptr;
+        io.v_in[k] = exp_avg_sq_in ? exp_avg_sq_in[k] : nullptr;
+        io.m_out[k] = exp_avg_out ? exp_avg_out[k] : nullptr;
+        io.v_out[k] = exp_avg_sq_out ? exp_avg_sq_out[k] : nullptr;
+    }
+    if (exist_out && !exist_in) return fail(OMR_ERR_INVALID_ARGUMENT, "exist_out without exist_in");
+    io.exist_in = exist_in, io.exist_out = exist_out;
+    io.normals = normals;
+    io.Mr = Mr;
+    launch_densify_apply(P, (const char*)plan, io, (hipStream_t)stream);
+    return hip_check("densify_apply");
+}
+
+int omr_reset_opacity(int P, float* opacity, float* exp_avg, float* exp_avg_sq, float ceiling, void* stream)
+{
+    g_last_error.clear();
+    if (P < 0) return fail(OMR_ERR_INVALID_ARGUMENT, "bad P");
+    if (P == 0) return OMR_OK;
+    if (!opacity) return fail(OMR_ERR_INVALID_ARGUMENT, "missing pointer");
+    launch_reset_opacity(P, opacity, exp_avg, exp_avg_sq, ceiling, (hipStream_t)stream);
+    return hip_check("reset_opacity");
 }
 
 size_t omr_geometry_bytes(int P) { return GeomState::carve(nullptr, (size_t)std::max(P, 0), nullptr); }

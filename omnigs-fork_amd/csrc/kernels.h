@@ -135,4 +135,52 @@ size_t l1_ssim_scratch_floats(int C, int H, int W);
 void launch_l1_ssim(const float* img, const float* gt, int C, int H, int W, float lambda, float* dimg, float* out3,
                     float* scratch, hipStream_t s);
 
+// optim.hip: Adam over the GaussianModel groups, densification stats, densifyAndPrune, resetOpacity
+constexpr int ADAM_MAX_GROUPS = 6;
+enum AdamKind : int { ADAM_PLAIN = 0, ADAM_SH_DC = 1, ADAM_SH_REST = 2, ADAM_OPACITY = 3, ADAM_SCALING = 4,
+                      ADAM_ROTATION = 5 };
+struct AdamGroup {
+    float* p;               // raw parameter (16-B aligned)
+    float* m;               // exp_avg
+    float* v;               // exp_avg_sq
+    const float* g;         // gradient: same layout as p (ADAM_PLAIN / OPACITY / SCALING / ROTATION) or dL_dsh
+    uint32_t n;             // floats in p
+    int kind;               // AdamKind
+    float neg_step_size;    // -(lr / (1 - beta1^step))
+    float bc2_sqrt;         // sqrt(1 - beta2^step)
+};
+struct AdamArgs {
+    AdamGroup group[ADAM_MAX_GROUPS];
+    uint32_t block0[ADAM_MAX_GROUPS];  // first block of each group (filled by launch_adam)
+    int ngroups;
+    int M;                             // SH coefficients per Gaussian in dL_dsh (f_dc + f_rest)
+    float beta1, beta2, omb1, omb2, eps;
+};
+void launch_adam(AdamArgs a, hipStream_t s);
+void launch_densification_stats(int P, const int* radii, const float* vgrad, int vstride, float* accum, float* denom,
+                                float* max_radii, hipStream_t s);
+struct DensifyParams {
+    float max_grad, min_opacity, extent, percent_dense;
+    int max_screen_size, prune_by_extent;
+};
+struct DensifyIO {
+    const float* p_in[6];   // xyz, f_dc, f_rest, opacity, scaling, rotation (raw)
+    const float* m_in[6];   // exp_avg per group (null: no state)
+    const float* v_in[6];
+    float* p_out[6];
+    float* m_out[6];        // null: skip
+    float* v_out[6];
+    const int32_t* exist_in;
+    int32_t* exist_out;     // null: skip
+    const float* normals;   // [2 S, 3] standard normal samples of the split copies (batch-major)
+    int Mr;                 // f_rest coefficients per Gaussian
+};
+size_t densify_plan_bytes(int P);
+void launch_densify_plan(int P, const float* accum, const float* denom, const float* scaling, const float* opacity,
+                         float max_grad, float min_opacity, float extent, float percent_dense, int max_screen_size,
+                         int prune_by_extent, char* plan, hipStream_t s);
+const uint4* densify_plan_totals(int P, const char* plan);
+void launch_densify_apply(int P, const char* plan, const DensifyIO& io, hipStream_t s);
+void launch_reset_opacity(int P, float* opacity, float* m, float* v, float ceiling, hipStream_t s);
+
 }  // namespace omr

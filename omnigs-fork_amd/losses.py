@@ -44,23 +44,31 @@ def ssim(img1: torch.Tensor, img2: torch.Tensor, window_size: int = 11, size_ave
     return ssim_map.mean() if size_average else ssim_map.mean(1).mean(1).mean(1)
 
 
+def l1_ssim_loss_and_grad(image: torch.Tensor, gt: torch.Tensor, lambda_dssim: float, grad_out=None):
+    """The fused kernel without autograd: returns (terms = tensor([loss, l1, ssim]), dloss/dimage [C,H,W])."""
+    if image.device.type != "cuda" or gt.device.type != "cuda":
+        raise R.RasterizerError("l1_ssim_loss needs HIP tensors (the fused loss has no CPU path)")
+    img = image.detach().contiguous().float()
+    ref = gt.detach().contiguous().float()
+    if img.shape != ref.shape or img.dim() != 3:
+        raise R.RasterizerError("image and gt must both be [C,H,W]")
+    Cn, H, W = (int(s) for s in img.shape)
+    L = R.lib()
+    grad = torch.empty_like(img) if grad_out is None else grad_out
+    if grad.shape != img.shape or not grad.is_contiguous() or grad.dtype != torch.float32:
+        raise R.RasterizerError("grad_out must be a contiguous float32 tensor shaped like image")
+    out3 = torch.empty(3, dtype=torch.float32, device=img.device)
+    scratch = torch.empty(int(L.omr_l1_ssim_scratch_floats(Cn, H, W)), dtype=torch.float32, device=img.device)
+    rc = L.omr_l1_ssim_loss(img.data_ptr(), ref.data_ptr(), Cn, H, W, float(lambda_dssim), grad.data_ptr(),
+                            out3.data_ptr(), scratch.data_ptr(), R._stream(img.device))
+    R._check(rc, "l1_ssim_loss")
+    return out3, grad
+
+
 class _FusedL1SSIM(torch.autograd.Function):
     @staticmethod
     def forward(ctx, image, gt, lambda_dssim):
-        if image.device.type != "cuda" or gt.device.type != "cuda":
-            raise R.RasterizerError("l1_ssim_loss needs HIP tensors (the fused loss has no CPU path)")
-        img = image.detach().contiguous().float()
-        ref = gt.detach().contiguous().float()
-        if img.shape != ref.shape or img.dim() != 3:
-            raise R.RasterizerError("image and gt must both be [C,H,W]")
-        Cn, H, W = (int(s) for s in img.shape)
-        L = R.lib()
-        grad = torch.empty_like(img)
-        out3 = torch.empty(3, dtype=torch.float32, device=img.device)
-        scratch = torch.empty(int(L.omr_l1_ssim_scratch_floats(Cn, H, W)), dtype=torch.float32, device=img.device)
-        rc = L.omr_l1_ssim_loss(img.data_ptr(), ref.data_ptr(), Cn, H, W, float(lambda_dssim), grad.data_ptr(),
-                                out3.data_ptr(), scratch.data_ptr(), R._stream(img.device))
-        R._check(rc, "l1_ssim_loss")
+        out3, grad = l1_ssim_loss_and_grad(image, gt, lambda_dssim)
         ctx.save_for_backward(grad)
         ctx.mark_non_differentiable(out3)
         return out3[0], out3

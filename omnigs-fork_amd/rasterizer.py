@@ -70,6 +70,14 @@ def lib() -> C.CDLL:
         L.omr_l1_ssim_scratch_floats.restype = sz
         L.omr_l1_ssim_scratch_floats.argtypes = [i, i, i]
         L.omr_l1_ssim_loss.argtypes = [vp, vp, i, i, i, f, vp, vp, vp, vp]
+        P6 = C.c_void_p * 6
+        L.omr_adam_step.argtypes = [i, i, P6, P6, P6, P6, i, C.c_float * 6, C.c_int64 * 6, f, f, f, vp]
+        L.omr_densification_stats.argtypes = [i, vp, vp, i, vp, vp, vp, vp]
+        L.omr_densify_plan_bytes.restype = sz
+        L.omr_densify_plan_bytes.argtypes = [i]
+        L.omr_densify_plan.argtypes = [i, vp, vp, vp, vp, f, f, f, f, i, i, vp, C.c_int64 * 4, vp]
+        L.omr_densify_apply.argtypes = [i, i, vp, P6, P6, P6, vp, vp, P6, P6, P6, vp, vp]
+        L.omr_reset_opacity.argtypes = [i, vp, vp, vp, f, vp]
         L.omr_profile_set_mask.argtypes = [C.c_uint32]
         L.omr_profile_read.restype = i
         L.omr_profile_read.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_uint64), i]

@@ -1,0 +1,68 @@
+"""One training iteration with no autograd graph (SURVEY.md §8(f) ranks 1-3 put together).
+
+GaussianMapper::trainForOneIteration (gaussian_mapper.cpp:338-488), minus the SLAM bookkeeping:
+  activations (gaussian_model.cpp:54-77) -> RasterizeGaussiansCUDA -> fused L1 + SSIM loss and dloss/dimage
+  (loss_utils.h, csrc/ssim.hip) -> RasterizeGaussiansBackwardCUDA -> max_radii2D + addDensificationStats
+  -> Adam on the rasterizer's activated-space gradients with the activation backward fused (csrc/optim.hip).
+The reference reaches the same state through torch autograd (loss.backward()) and torch::optim::Adam;
+tests/test_gpu_optim.py checks the two agree. Densification / opacity reset stay with the caller, as in the
+reference's loop (:436-452), through GaussianOptimizer.densify_and_prune / reset_opacity.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import losses
+from . import optim as O
+from . import rasterizer as R
+from .parallel import GradBuffer
+
+
+class TrainStep:
+    """Reusable buffers for train_step (the gradient buffer is sized once per P)."""
+
+    def __init__(self):
+        self.buf: Optional[GradBuffer] = None
+        self.dimg: Optional[torch.Tensor] = None
+
+
+def train_step(opt: O.GaussianOptimizer, viewpoint, image_height: int, image_width: int, gt_image: torch.Tensor,
+               bg_color: torch.Tensor, camera_type: int = R.CAMERA_LONLAT, lambda_dssim: float = 0.2,
+               densification_stats: bool = True, state: Optional[TrainStep] = None):
+    """Render `viewpoint`, take the loss against gt_image, backpropagate and step Adam. Returns
+    (terms = tensor([loss, l1, ssim]), rendered image, radii)."""
+    pc = opt.model
+    state = state or TrainStep()
+    P, Mr = opt.P, opt.Mr
+    dev = pc.xyz.device
+    with torch.no_grad():
+        means3D = pc.xyz
+        shs = torch.cat([pc.features_dc, pc.features_rest], dim=1)
+        opacity = torch.sigmoid(pc.opacity)
+        scales = torch.exp(pc.scaling)
+        rotations = torch.nn.functional.normalize(pc.rotation)
+    if camera_type == R.CAMERA_PINHOLE:  # std::tan(FoV * 0.5f) in float (gaussian_renderer.cpp:58-59)
+        tanfovx = float(np.tan(np.float32(viewpoint.FoVx) * np.float32(0.5)))
+        tanfovy = float(np.tan(np.float32(viewpoint.FoVy) * np.float32(0.5)))
+    else:
+        tanfovx = tanfovy = 0.0
+    vm, pm, cp = viewpoint.world_view_transform, viewpoint.full_proj_transform, viewpoint.camera_center
+    nr, image, radii, geom, binning, img = R.RasterizeGaussiansCUDA(
+        bg_color, means3D, None, opacity, scales, rotations, 1.0, None, vm, pm, tanfovx, tanfovy, image_height,
+        image_width, shs, pc.active_sh_degree, cp, False, camera_type)
+    if state.dimg is None or state.dimg.shape != image.shape:
+        state.dimg = torch.empty_like(image)
+    terms, dimg = losses.l1_ssim_loss_and_grad(image, gt_image, lambda_dssim, grad_out=state.dimg)
+    if state.buf is None or state.buf.P != P or state.buf.M != Mr + 1:
+        state.buf = GradBuffer(P, Mr + 1, dev)
+    out = state.buf.out_dict(dev)
+    R.RasterizeGaussiansBackwardCUDA(bg_color, means3D, radii, None, scales, rotations, 1.0, None, vm, pm, tanfovx,
+                                     tanfovy, dimg, shs, pc.active_sh_degree, cp, geom, nr, binning, img, camera_type,
+                                     out=out)
+    if densification_stats:
+        opt.add_densification_stats(out["dL_dmeans2D"], radii)
+    opt.step(raster_grads=out)
+    return terms, image, radii

@@ -1,0 +1,277 @@
+"""The training step after the backward on the GPU (csrc/optim.hip through the C ABI), against LibTorch's own Adam
+(tests/golden/optim/adam_*.npz, made by make_adam_golden.py) and the CPU oracle (oracle/optim_oracle.py).
+
+Bars: parameters 2e-6 relative (float order and expf/sqrtf ulps differ from LibTorch's CPU kernels); moments 1e-5
+relative with a floor of 1e-5 x the group's largest moment (sums of gradients of both signs cancel); everything
+densifyAndPrune copies or reorders is bit-exact; the split positions / scalings it computes are 1e-6 relative.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import omr, to_np
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import optim_oracle as OO  # noqa: E402
+
+OPT, RD = omr.optim, omr.renderer
+GOLDEN = [os.path.join(ROOT, "tests", "golden", "optim", n) for n in ("adam_deg3_P61.npz", "adam_deg1_P67.npz")]
+
+
+def _cuda(a, grad=False):
+    return torch.tensor(np.ascontiguousarray(a), dtype=torch.float32, device="cuda", requires_grad=grad)
+
+
+def _model(params, grad=False):
+    t = [_cuda(p, grad) for p in params]
+    return RD.GaussianModelParams(t[0], t[1], t[2], t[3], t[4], t[5], 3, 3)
+
+
+def _check(p, m, v, ref_p, ref_m, ref_v, what):
+    assert p.shape == ref_p.shape, what
+    if ref_p.size == 0:
+        return
+    np.testing.assert_allclose(p, ref_p, rtol=2e-6, atol=2e-7, err_msg=f"param {what}")
+    for name, x, ref in (("exp_avg", m, ref_m), ("exp_avg_sq", v, ref_v)):
+        np.testing.assert_allclose(x, ref, rtol=1e-5, atol=1e-5 * max(np.abs(ref).max(), 1e-30),
+                                   err_msg=f"{name} {what}")
+
+
+def _raster_grads(d, s):
+    return {"dL_dmeans3D": _cuda(d[f"act_grad{s}_0"]), "dL_dsh": _cuda(d[f"act_grad{s}_1"]),
+            "dL_dopacity": _cuda(d[f"act_grad{s}_2"]), "dL_dscales": _cuda(d[f"act_grad{s}_3"]),
+            "dL_drotations": _cuda(d[f"act_grad{s}_4"])}
+
+
+@pytest.mark.parametrize("path", GOLDEN)
+@pytest.mark.parametrize("mode", ["raster", "raw"])
+def test_adam_matches_libtorch_golden(path, mode):
+    """mode raster: the fused activation backward + Adam on the rasterizer's gradients; mode raw: Adam on the raw
+    gradients LibTorch's autograd produced (what .grad holds in the reference)."""
+    d = np.load(path)
+    steps = int(d["steps"])
+    model = _model([d[f"param{k}"] for k in range(6)], grad=(mode == "raw"))
+    opt = OPT.GaussianOptimizer(model, OPT.OptimizationParams())
+    for s in range(steps):
+        opt.lr = [float(x) for x in d["lrs"][s]]
+        if mode == "raster":
+            opt.step(raster_grads=_raster_grads(d, s))
+        else:
+            for k, p in enumerate(opt.params()):
+                p.grad = _cuda(d[f"raw_grad{s}_{k}"])
+            opt.step()
+            opt.zero_grad()
+    torch.cuda.synchronize()
+    assert opt.steps == [steps] * 6
+    for k, p in enumerate(opt.params()):
+        _check(to_np(p), to_np(opt.exp_avg[k]), to_np(opt.exp_avg_sq[k]), d[f"out_param{k}"], d[f"out_exp_avg{k}"],
+               d[f"out_exp_avg_sq{k}"], f"group {k}")
+
+
+def _random_params(P, Mr, seed):
+    rng = np.random.default_rng(seed)
+    f = np.float32
+    return [rng.normal(0, 1, (P, 3)).astype(f), rng.normal(0, 0.5, (P, 1, 3)).astype(f),
+            rng.normal(0, 0.2, (P, Mr, 3)).astype(f), rng.normal(0, 2, (P, 1)).astype(f),
+            rng.normal(-4, 1.5, (P, 3)).astype(f), rng.normal(0, 1, (P, 4)).astype(f)]
+
+
+@pytest.mark.parametrize("P,Mr", [(100003, 15), (4097, 3), (777, 0), (1, 8)])
+def test_adam_raster_grads_vs_oracle(P, Mr):
+    """Sizes with ragged 16-B chunks in every group (3P, 3*Mr*P not multiples of 4), SH degrees 3, 1, 0, 2."""
+    rng = np.random.default_rng(P + Mr)
+    params = _random_params(P, Mr, P)
+    model = _model(params)
+    opt = OPT.GaussianOptimizer(model, OPT.OptimizationParams(), spatial_lr_scale=2.5)
+    ref = [p.copy() for p in params]
+    ms = [np.zeros_like(p) for p in ref]
+    vs = [np.zeros_like(p) for p in ref]
+    for s in range(3):
+        opt.update_learning_rate(1000 * s)
+        g = {"dL_dmeans3D": rng.normal(0, 1e-4, (P, 3)), "dL_dsh": rng.normal(0, 1e-4, (P, Mr + 1, 3)),
+             "dL_dopacity": rng.normal(0, 1e-3, (P, 1)), "dL_dscales": rng.normal(0, 1e-3, (P, 3)),
+             "dL_drotations": rng.normal(0, 1e-4, (P, 4))}
+        g = {k: v.astype(np.float32) for k, v in g.items()}
+        g["dL_dmeans3D"][rng.random(P) < 0.5] = 0
+        opt.step(raster_grads={k: _cuda(v) for k, v in g.items()})
+        raw = OO.activation_backward(ref, g)
+        for k in range(6):
+            OO.adam_step(ref[k], ms[k], vs[k], raw[k], opt.lr[k], s + 1)
+    torch.cuda.synchronize()
+    for k, p in enumerate(opt.params()):
+        _check(to_np(p), to_np(opt.exp_avg[k]), to_np(opt.exp_avg_sq[k]), ref[k], ms[k], vs[k], f"group {k}")
+
+
+def test_adam_skips_groups_without_grad():
+    params = _random_params(1000, 15, 3)
+    model = _model(params, grad=True)
+    opt = OPT.GaussianOptimizer(model, OPT.OptimizationParams())
+    model.opacity.grad = torch.full_like(model.opacity, 1e-3)
+    opt.step()
+    torch.cuda.synchronize()
+    assert opt.steps == [0, 0, 0, 1, 0, 0]
+    for k, p in enumerate(opt.params()):
+        if k == 3:
+            assert not np.array_equal(to_np(p), params[k])
+        else:
+            np.testing.assert_array_equal(to_np(p), params[k])
+            assert not to_np(opt.exp_avg[k]).any()
+
+
+def test_adam_rejects_misaligned_and_bad_shapes():
+    params = _random_params(64, 15, 4)
+    model = _model(params)
+    opt = OPT.GaussianOptimizer(model, OPT.OptimizationParams())
+    bad = torch.zeros(64 * 3 + 1, device="cuda")[1:].view(64, 3)  # 4-byte offset
+    g = {"dL_dmeans3D": bad, "dL_dsh": torch.zeros(64, 16, 3, device="cuda"), "dL_dopacity": torch.zeros(64, 1, device="cuda"),
+         "dL_dscales": torch.zeros(64, 3, device="cuda"), "dL_drotations": torch.zeros(64, 4, device="cuda")}
+    with pytest.raises(omr.rasterizer.RasterizerError, match="aligned"):
+        opt.step(raster_grads=g)
+    g["dL_dmeans3D"] = torch.zeros(64, 3, device="cuda")
+    g["dL_dsh"] = torch.zeros(64, 4, 3, device="cuda")
+    with pytest.raises(omr.rasterizer.RasterizerError, match="dL_dsh"):
+        opt.step(raster_grads=g)
+
+
+def test_densification_stats_vs_oracle():
+    P = 50001
+    rng = np.random.default_rng(5)
+    model = _model(_random_params(P, 15, 5))
+    opt = OPT.GaussianOptimizer(model, OPT.OptimizationParams())
+    accum, denom, mr = np.zeros((P, 1), np.float32), np.zeros((P, 1), np.float32), np.zeros(P, np.float32)
+    for s in range(3):
+        radii = rng.integers(-2, 30, P).astype(np.int32)
+        vg = rng.normal(0, 1e-3, (P, 3)).astype(np.float32)
+        opt.add_densification_stats(_cuda(vg), torch.tensor(radii, device="cuda"))
+        OO.densification_stats(radii, vg, accum, denom, mr)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(to_np(opt.xyz_gradient_accum), accum, rtol=1e-6)
+    np.testing.assert_array_equal(to_np(opt.denom), denom)
+    np.testing.assert_array_equal(to_np(opt.max_radii2D), mr)
+
+
+def _densify_case(P, Mr, seed, max_grad, min_op, extent, max_screen, by_ext):
+    rng = np.random.default_rng(seed)
+    params = _random_params(P, Mr, seed)
+    model = _model(params)
+    opt = OPT.GaussianOptimizer(model, OPT.OptimizationParams())
+    ea = [rng.random(p.shape).astype(np.float32) for p in params]
+    es = [rng.random(p.shape).astype(np.float32) for p in params]
+    accum = (rng.random((P, 1)) * 4e-3).astype(np.float32)
+    denom = rng.integers(0, 5, (P, 1)).astype(np.float32)
+    accum[denom == 0] = 0
+    exist = rng.integers(0, 1000, P).astype(np.int32)
+    mr = (rng.random(P) * 40).astype(np.float32)
+    opt.exp_avg = [_cuda(a) for a in ea]
+    opt.exp_avg_sq = [_cuda(a) for a in es]
+    opt.xyz_gradient_accum, opt.denom, opt.max_radii2D = _cuda(accum), _cuda(denom), _cuda(mr)
+    opt.exist_since_iter = torch.tensor(exist, device="cuda")
+    ref = OO.ModelState(params, ea, es, exist, accum, denom, mr)
+    normals = rng.normal(size=(2 * P, 3)).astype(np.float32)
+    info = opt.densify_and_prune(max_grad, min_op, extent, max_screen, by_ext, normals=_cuda(normals))
+    S = ref.densify_and_prune(max_grad, min_op, extent, max_screen, by_ext, 0.01, normals)
+    torch.cuda.synchronize()
+    return opt, ref, info, S
+
+
+@pytest.mark.parametrize("P,Mr,max_screen,by_ext,extent", [(30001, 15, 20, True, 5.0), (5000, 3, 0, True, 5.0),
+                                                           (5000, 15, 20, False, 5.0), (4099, 0, 20, True, 0.3)])
+def test_densify_and_prune_vs_oracle(P, Mr, max_screen, by_ext, extent):
+    opt, ref, info, S = _densify_case(P, Mr, 7 + P, 2e-4, 0.005, extent, max_screen, by_ext)
+    assert info["splits_selected"] == S
+    assert info["P_new"] == ref.P == opt.P
+    assert info["clones"] > 0 and S > 0
+    np.testing.assert_array_equal(to_np(opt.exist_since_iter), ref.exist)
+    n_fixed = ref.P - 2 * info["splits_kept"]  # kept originals + clones: pure copies
+    for k, p in enumerate(opt.params()):
+        got, want = to_np(p), ref.params[k]
+        assert got.shape == want.shape, k
+        if k in (0, 4):  # split copies: positions and scalings are computed
+            np.testing.assert_array_equal(got[:n_fixed], want[:n_fixed])
+            np.testing.assert_allclose(got[n_fixed:], want[n_fixed:], rtol=1e-6, atol=1e-6)
+        else:
+            np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(to_np(opt.exp_avg[k]), ref.exp_avg[k])
+        np.testing.assert_array_equal(to_np(opt.exp_avg_sq[k]), ref.exp_avg_sq[k])
+    for t in (opt.xyz_gradient_accum, opt.denom, opt.max_radii2D):
+        assert t.shape[0] == ref.P and not t.any()
+
+
+def test_densify_nothing_selected_and_all_pruned():
+    opt, ref, info, S = _densify_case(2000, 15, 3, 1e9, 0.0, 5.0, 0, True)  # nothing to do
+    assert info == {"P_new": 2000, "clones": 0, "splits_selected": 0, "splits_kept": 0}
+    np.testing.assert_array_equal(to_np(opt.exist_since_iter), ref.exist)
+    opt, ref, info, S = _densify_case(2000, 15, 3, 2e-4, 1.1, 5.0, 0, True)  # every opacity < 1.1: all pruned
+    assert info["P_new"] == 0 == ref.P and opt.P == 0
+
+
+@pytest.mark.parametrize("ceiling", [1.0, 0.01])
+def test_reset_opacity_vs_oracle(ceiling):
+    P = 10000
+    params = _random_params(P, 15, 9)
+    model = _model(params)
+    opt = OPT.GaussianOptimizer(model, OPT.OptimizationParams())
+    opt.exp_avg[3].fill_(1.0)
+    opt.exp_avg_sq[3].fill_(1.0)
+    opt.reset_opacity(ceiling)
+    o, m, v = params[3].copy(), np.ones_like(params[3]), np.ones_like(params[3])
+    OO.reset_opacity(o, m, v, ceiling)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(to_np(model.opacity), o, rtol=1e-5, atol=1e-5)
+    assert not opt.exp_avg[3].any() and not opt.exp_avg_sq[3].any()
+
+
+def test_fused_train_step_matches_autograd_reference_composition():
+    """trainer.train_step (no autograd: fused loss, rasterizer backward, fused activation backward + Adam) reaches
+    the same parameters as the reference's composition: torch activations -> rasterizer autograd -> l1/ssim loss
+    in torch (loss_utils.h) -> loss.backward() -> Adam on .grad (raw mode)."""
+    from helpers import make_case, scene
+
+    W, H = 256, 128
+    g, cam, _ = make_case(3000, W, H, scene.CAMERA_LONLAT, 21, spread=2.0)
+    rng = np.random.default_rng(1)
+    o = np.clip(g.opacity.astype(np.float64), 1e-4, 1 - 1e-4)
+    params = [g.means3D, g.shs[:, :1], g.shs[:, 1:], np.log(o / (1 - o)), np.log(g.scales),
+              g.rotations * rng.uniform(0.5, 2.0, (g.P, 1))]
+    params = [np.ascontiguousarray(p, dtype=np.float32) for p in params]
+    gt = torch.tensor(rng.random((3, H, W)), dtype=torch.float32, device="cuda")
+    bg = torch.zeros(3, device="cuda")
+    t = lambda a: torch.tensor(np.ascontiguousarray(a, dtype=np.float32), device="cuda")  # noqa: E731
+    vp = RD.Viewpoint(t(cam.viewmatrix), t(cam.projmatrix), t(cam.campos))
+    args = OPT.OptimizationParams()
+
+    # fused
+    m1 = _model(params)
+    opt1 = OPT.GaussianOptimizer(m1, args)
+    state = omr.trainer.TrainStep()
+    # reference composition
+    m2 = _model(params, grad=True)
+    opt2 = OPT.GaussianOptimizer(m2, args)
+    for it in range(3):
+        for opt in (opt1, opt2):
+            opt.update_learning_rate(it)
+        terms, img1, radii1 = omr.trainer.train_step(opt1, vp, H, W, gt, bg, lambda_dssim=0.2, state=state)
+        img2, vsp, vis, radii2 = RD.render_lonlat(vp, H, W, m2, RD.PipelineParams(), bg)
+        loss = 0.8 * omr.losses.l1_loss(img2, gt) + 0.2 * (1.0 - omr.losses.ssim(img2, gt))
+        loss.backward()
+        opt2.add_densification_stats(vsp.grad, radii2)
+        opt2.step()
+        opt2.zero_grad()
+        torch.cuda.synchronize()
+        assert abs(float(terms[0]) - float(loss.detach())) <= 1e-5 * abs(float(loss.detach())) + 1e-7
+        assert torch.equal(radii1, radii2)
+    for k, (p1, p2) in enumerate(zip(opt1.params(), opt2.params())):
+        # the two paths take different float routes to the same gradient. Adam (eps 1e-15) normalises magnitudes, so
+        # an element whose gradient is at rounding-noise level may move by +-lr either way: compare the parameter
+        # moves and allow such elements to be rare
+        d1, d2 = to_np(p1) - params[k], to_np(p2) - params[k]
+        bad = np.abs(d1 - d2) > 2e-3 * np.abs(d2).max() + 1e-9
+        assert bad.mean() <= 1e-3, (k, int(bad.sum()), d1.size)
+    np.testing.assert_allclose(to_np(opt1.xyz_gradient_accum), to_np(opt2.xyz_gradient_accum), rtol=2e-3,
+                               atol=1e-3 * float(opt2.xyz_gradient_accum.abs().max()))
+    np.testing.assert_array_equal(to_np(opt1.denom), to_np(opt2.denom))
