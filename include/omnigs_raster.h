@@ -167,6 +167,26 @@ int omr_densify_apply(int P, int Mr, const void* plan, const float* const params
  * moments reset); 0.01 gives the 3DGS behaviour. */
 int omr_reset_opacity(int P, float* opacity, float* exp_avg, float* exp_avg_sq, float ceiling, void* stream);
 
+/* --- formats (extension) ------------------------------------------------------------ */
+/* distCUDA2 (third_party/simple-knn/spatial.cu:15-25, simple_knn.cu:185-220): mean_dists[i] = mean of the squared
+ * distances from points[i] ([P,3]) to its 3 nearest other points (exact; FLT_MAX stands in for missing neighbours
+ * when P < 4, as in the reference). scratch: device bytes, at least omr_dist2_scratch_bytes(P). */
+size_t omr_dist2_scratch_bytes(int P);
+int omr_dist2(int P, const float* points, float* mean_dists, void* scratch, void* stream);
+/* GaussianModel::loadPly / savePly (gaussian_model.cpp:860-1070) — the 62-property binary PLY. Reading takes two
+ * calls so the caller can allocate: omr_ply_open parses the header (requires x y z f_dc_0..2 f_rest_0..(3Mr-1)
+ * opacity scale_0..2 rot_0..3 in the vertex element, Mr = (max_sh_degree + 1)^2 - 1; any order, extra properties,
+ * ascii / big-endian / non-float types accepted) and returns the vertex count; omr_ply_read fills the six device
+ * parameter arrays (xyz [P,3], features_dc [P,1,3], features_rest [P,Mr,3], opacity [P,1], scaling [P,3],
+ * rotation [P,4]) and synchronises the stream; omr_ply_close frees the handle. omr_ply_save writes the file
+ * savePly writes (header as tinyply.h:664-703, zero normals, channel-major SH). Both use a temporary device buffer
+ * of P records (hipMalloc) and move it in one copy. */
+typedef struct omr_ply omr_ply;
+int omr_ply_open(const char* path, int max_sh_degree, omr_ply** out, int64_t* num_points);
+int omr_ply_read(omr_ply* ply, float* const params[6], void* stream);
+void omr_ply_close(omr_ply* ply);
+int omr_ply_save(const char* path, int P, int Mr, const float* const params[6], void* stream);
+
 /* --- scratch sizes (bytes the allocation callbacks are asked for) -------------------------------- */
 size_t omr_geometry_bytes(int P);
 size_t omr_image_bytes(int width, int height);

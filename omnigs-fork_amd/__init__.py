@@ -11,6 +11,7 @@ Layout:
   losses.py        training loss (1 - lambda) L1 + lambda (1 - SSIM), fused forward+backward HIP kernel
   optim.py         Adam over the six GaussianModel groups (activation backward fused), LR schedule, densification
   trainer.py       one training iteration without autograd: render, fused loss, backward, stats, Adam
+  formats.py       PLY load / save (HIP (de)interleave), distCUDA2 (exact 3-NN on gfx950), createFromPcd
   scene.py         deterministic synthetic scenes and camera poses
 """
 from . import scene  # noqa: F401
@@ -20,7 +21,7 @@ __all__ = ["scene", "rasterizer"]
 
 def __getattr__(name):
     # the HIP-backed modules import torch and the shared library lazily
-    if name in ("rasterizer", "renderer", "parallel", "losses", "optim", "trainer"):
+    if name in ("rasterizer", "renderer", "parallel", "losses", "optim", "trainer", "formats"):
         import importlib
 
         mod = importlib.import_module(f"{__name__}.{name}")

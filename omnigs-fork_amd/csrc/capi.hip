@@ -668,6 +668,67 @@ int omr_reset_opacity(int P, float* opacity, float* exp_avg, float* exp_avg_sq, 
     return hip_check("reset_opacity");
 }
 
+size_t omr_dist2_scratch_bytes(int P) { return P > 0 ? knn_scratch_bytes(P) : 0; }
+
+int omr_dist2(int P, const float* points, float* mean_dists, void* scratch, void* stream)
+{
+    g_last_error.clear();
+    if (P < 0) return fail(OMR_ERR_INVALID_ARGUMENT, "bad P");
+    if (P == 0) return OMR_OK;
+    if (!points || !mean_dists || !scratch) return fail(OMR_ERR_INVALID_ARGUMENT, "missing pointer");
+    launch_knn(P, points, mean_dists, (char*)scratch, (hipStream_t)stream);
+    return hip_check("dist2");
+}
+
+struct omr_ply {
+    PlyFile* f;
+};
+
+int omr_ply_open(const char* path, int max_sh_degree, omr_ply** out, int64_t* num_points)
+{
+    g_last_error.clear();
+    if (!path || !out || !num_points) return fail(OMR_ERR_INVALID_ARGUMENT, "missing pointer");
+    if (max_sh_degree < 0 || max_sh_degree > 3) return fail(OMR_ERR_INVALID_ARGUMENT, "max_sh_degree must be 0..3");
+    std::string err;
+    PlyFile* f = ply_open(path, max_sh_degree, err);
+    if (!f) return fail(OMR_ERR_INVALID_ARGUMENT, err);
+    *out = new omr_ply{f};
+    *num_points = ply_num_points(f);
+    return OMR_OK;
+}
+
+int omr_ply_read(omr_ply* ply, float* const params[6], void* stream)
+{
+    g_last_error.clear();
+    if (!ply || !params) return fail(OMR_ERR_INVALID_ARGUMENT, "missing pointer");
+    if (ply_num_points(ply->f) > 0)
+        for (int k = 0; k < 6; ++k)
+            if (!params[k] && !(k == 2 && ply_rest_coeffs(ply->f) == 0))
+                return fail(OMR_ERR_INVALID_ARGUMENT, "missing parameter pointer");
+    std::string err;
+    if (!ply_read(ply->f, params, (hipStream_t)stream, err)) return fail(OMR_ERR_INVALID_ARGUMENT, err);
+    return hip_check("ply_read");
+}
+
+void omr_ply_close(omr_ply* ply)
+{
+    if (!ply) return;
+    ply_close(ply->f);
+    delete ply;
+}
+
+int omr_ply_save(const char* path, int P, int Mr, const float* const params[6], void* stream)
+{
+    g_last_error.clear();
+    if (!path || P < 0 || Mr < 0 || Mr > 15 || !params) return fail(OMR_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (P > 0)
+        for (int k = 0; k < 6; ++k)
+            if (!params[k] && !(k == 2 && Mr == 0)) return fail(OMR_ERR_INVALID_ARGUMENT, "missing parameter pointer");
+    std::string err;
+    if (!ply_save(path, P, Mr, params, (hipStream_t)stream, err)) return fail(OMR_ERR_INVALID_ARGUMENT, err);
+    return hip_check("ply_save");
+}
+
 size_t omr_geometry_bytes(int P) { return GeomState::carve(nullptr, (size_t)std::max(P, 0), nullptr); }
 
 size_t omr_image_bytes(int width, int height)

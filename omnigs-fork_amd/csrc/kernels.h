@@ -1,6 +1,8 @@
 // kernels.h — launch-side declarations shared by the orchestration (capi.hip) and the kernel files.
 #pragma once
 
+#include <string>
+
 #include "raster_common.h"
 
 namespace omr {
@@ -182,5 +184,18 @@ void launch_densify_plan(int P, const float* accum, const float* denom, const fl
 const uint4* densify_plan_totals(int P, const char* plan);
 void launch_densify_apply(int P, const char* plan, const DensifyIO& io, hipStream_t s);
 void launch_reset_opacity(int P, float* opacity, float* m, float* v, float ceiling, hipStream_t s);
+
+// knn.hip: distCUDA2 (simple_knn.cu:185-220)
+size_t knn_scratch_bytes(int P);
+void launch_knn(int P, const float* pts, float* dists, char* scratch, hipStream_t s);
+
+// formats.hip: Gaussian PLY files (gaussian_model.cpp:860-1070)
+struct PlyFile;
+PlyFile* ply_open(const char* path, int max_sh_degree, std::string& err);
+int64_t ply_num_points(const PlyFile* f);
+int ply_rest_coeffs(const PlyFile* f);
+void ply_close(PlyFile* f);
+bool ply_read(PlyFile* f, float* const params[6], hipStream_t s, std::string& err);
+bool ply_save(const char* path, int P, int Mr, const float* const params[6], hipStream_t s, std::string& err);
 
 }  // namespace omr

@@ -240,10 +240,11 @@ class GaussianOptimizer:
         new_m = [torch.empty(s, device=dev) for s in shapes]
         new_v = [torch.empty(s, device=dev) for s in shapes]
         new_exist = torch.empty((P_new,), dtype=torch.int32, device=dev)
-        rc = L.omr_densify_apply(P, Mr, self._plan.data_ptr(), _p6(ps), _p6(self.exp_avg), _p6(self.exp_avg_sq),
-                                 self.exist_since_iter.data_ptr(), normals.data_ptr() if normals.numel() else None,
-                                 _p6(new_p), _p6(new_m), _p6(new_v), new_exist.data_ptr(), stream)
-        R._check(rc, "omr_densify_apply")
+        if P_new:  # (everything pruned: nothing to write)
+            rc = L.omr_densify_apply(P, Mr, self._plan.data_ptr(), _p6(ps), _p6(self.exp_avg), _p6(self.exp_avg_sq),
+                                     self.exist_since_iter.data_ptr(), normals.data_ptr() if normals.numel() else None,
+                                     _p6(new_p), _p6(new_m), _p6(new_v), new_exist.data_ptr(), stream)
+            R._check(rc, "omr_densify_apply")
         for old, new in zip(ps, new_p):
             new.requires_grad_(old.requires_grad)
         self._set_params(new_p)

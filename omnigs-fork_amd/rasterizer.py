@@ -78,6 +78,14 @@ def lib() -> C.CDLL:
         L.omr_densify_plan.argtypes = [i, vp, vp, vp, vp, f, f, f, f, i, i, vp, C.c_int64 * 4, vp]
         L.omr_densify_apply.argtypes = [i, i, vp, P6, P6, P6, vp, vp, P6, P6, P6, vp, vp]
         L.omr_reset_opacity.argtypes = [i, vp, vp, vp, f, vp]
+        L.omr_dist2_scratch_bytes.restype = sz
+        L.omr_dist2_scratch_bytes.argtypes = [i]
+        L.omr_dist2.argtypes = [i, vp, vp, vp, vp]
+        L.omr_ply_open.argtypes = [C.c_char_p, i, C.POINTER(vp), C.POINTER(C.c_int64)]
+        L.omr_ply_read.argtypes = [vp, P6, vp]
+        L.omr_ply_close.argtypes = [vp]
+        L.omr_ply_close.restype = None
+        L.omr_ply_save.argtypes = [C.c_char_p, i, i, P6, vp]
         L.omr_profile_set_mask.argtypes = [C.c_uint32]
         L.omr_profile_read.restype = i
         L.omr_profile_read.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_uint64), i]

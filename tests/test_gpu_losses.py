@@ -30,7 +30,7 @@ def test_fused_l1_ssim_matches_reference(C, H, W, lam, seed):
     loss.backward()
     ref_loss, ref_grad, ref_l1, ref_ssim = _reference(img, gt, lam)
     t = to_np(terms)
-    assert abs(float(loss) - ref_loss) < 1e-5, (float(loss), ref_loss)
+    assert abs(float(loss.detach()) - ref_loss) < 1e-5, (float(loss.detach()), ref_loss)
     assert abs(t[1] - ref_l1) < 1e-6 and abs(t[2] - ref_ssim) < 1e-5, (t, ref_l1, ref_ssim)
     ok, emax, nbad = grad_close(to_np(img_d.grad), ref_grad, rtol=1e-3, atol_frac=1e-4)
     assert ok, (emax, nbad)
