@@ -3,7 +3,7 @@
 //
 // File layout (what savePly writes through tinyply, tinyply.h:664-703 for the header): an ASCII header
 //   ply / format binary_little_endian 1.0 / element vertex P / property float <name> ... / end_header
-// then P interleaved records of 14 + 3 Mr float32: x y z nx ny nz f_dc_0..2 f_rest_0..(3Mr-1) opacity
+// then P interleaved records of 17 + 3 Mr float32: x y z nx ny nz f_dc_0..2 f_rest_0..(3Mr-1) opacity
 // scale_0..2 rot_0..3 (62 floats = 248 B at SH degree 3). Normals are written as zeros; f_dc / f_rest are stored
 // channel-major (features.transpose(1, 2).flatten(1)): f_rest_{c*Mr + k} = features_rest[p][k][c].
 //
@@ -75,7 +75,7 @@ struct PlyElement {
     std::vector<PlyProp> props;
 };
 
-constexpr int COLS_MAX = 14 + 45;  // requested columns at SH degree 3
+constexpr int COLS_MAX = 14 + 45;  // columns loadPly requests at SH degree 3 (no normals)
 
 }  // namespace
 
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(256) void ply_pack_kernel(int P, int Mr, const floa
 {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P) return;
-    const int nr = 3 * Mr, stride = 14 + nr;
+    const int nr = 3 * Mr, stride = 17 + nr;
     float* r = rows + (size_t)p * stride;
     for (int k = 0; k < 3; ++k) r[k] = xyz[3 * (size_t)p + k];
     for (int k = 0; k < 3; ++k) r[3 + k] = 0.f;
@@ -315,7 +315,7 @@ bool ply_read(PlyFile* f, float* const params[6], hipStream_t s, std::string& er
 
 bool ply_save(const char* path, int P, int Mr, const float* const params[6], hipStream_t s, std::string& err)
 {
-    const int stride = 14 + 3 * Mr;
+    const int stride = 17 + 3 * Mr;
     std::vector<float> rows((size_t)P * stride);
     if (P > 0) {
         float* d_rows = nullptr;

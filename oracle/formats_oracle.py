@@ -70,7 +70,7 @@ def _names(Mr):
 
 
 def ply_columns(xyz, f_dc, f_rest, opacity, scaling, rotation):
-    """[P, 14 + 3 Mr] float32 table in savePly's property order."""
+    """[P, 17 + 3 Mr] float32 table in savePly's property order."""
     P = xyz.shape[0]
     Mr = f_rest.shape[1]
     cols = [xyz.reshape(P, 3), np.zeros((P, 3), f32), f_dc.reshape(P, 1, 3).transpose(0, 2, 1).reshape(P, 3),
