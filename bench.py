@@ -51,6 +51,8 @@ def parse():
                    help="multi-rank rehearsal on a one-GPU box: every rank on cuda:0, gloo instead of RCCL "
                         "(exercises the N > 1 code path; numbers are not a scaling measurement)")
     p.add_argument("--scene", default=None, help="override the scene of this rank (e.g. E_pinhole)")
+    p.add_argument("--no-train-step", action="store_true",
+                   help="skip the extra whole-training-iteration timing (N = 1 only; not part of `value`)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     return p.parse_args()
 
@@ -295,10 +297,52 @@ def main():
             result["cpu_baseline"] = cpu_baseline(g, cam, dL, args.cpu_seconds, threads)
         except Exception as ex:  # the GPU number stands on its own; report why the baseline is missing
             result["cpu_baseline"] = {"value": None, "error": repr(ex)}
+    if world == 1 and rank == 0 and not args.no_train_step:
+        try:
+            result["train_step"] = train_step_timing(omr, g, cam, dev, steps=10, warmup=3)
+        except Exception as ex:  # informational only
+            result["train_step"] = {"error": repr(ex)}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def train_step_timing(omr, g, cam, dev, steps, warmup):
+    """Extra, informational (not `value`): one whole training iteration without autograd on the same scene and
+    view (trainer.train_step: activations -> rasterizer forward -> fused L1+SSIM loss and dloss/dimage ->
+    rasterizer backward -> densification stats -> fused activation-backward + Adam over the six groups). The
+    reference's derived anchor for its whole training step is ~23 MP/s on an RTX 3090."""
+    import numpy as np
+    import torch
+
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)  # noqa: E731
+    model = omr.renderer.GaussianModelParams.from_activated(t(g.means3D), t(g.scales), t(g.rotations),
+                                                            t(g.opacity).reshape(-1, 1), t(g.shs), g.sh_degree)
+    for name in ("xyz", "features_dc", "features_rest", "opacity", "scaling", "rotation"):
+        setattr(model, name, getattr(model, name).contiguous())
+    opt = omr.optim.GaussianOptimizer(model, omr.optim.OptimizationParams())
+    vp = omr.renderer.Viewpoint(t(cam.viewmatrix), t(cam.projmatrix), t(cam.campos))
+    gen = torch.Generator(device=dev).manual_seed(5)
+    gt = torch.rand((3, cam.height, cam.width), device=dev, generator=gen)
+    bg = torch.zeros(3, device=dev)
+    state = omr.trainer.TrainStep()
+
+    def it(k):
+        opt.update_learning_rate(k)
+        return omr.trainer.train_step(opt, vp, cam.height, cam.width, gt, bg, cam.camera_type, 0.2, state=state)
+
+    for k in range(warmup):
+        it(k)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        terms, _, _ = it(warmup + k)
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    return {"ms": round(ms, 4), "Mpixels_s": round(cam.width * cam.height / (ms * 1e-3) / 1e6, 2),
+            "iterations_s": round(1e3 / ms, 1), "loss": round(float(terms[0]), 6),
+            "includes": "fwd + fused L1/SSIM loss + bwd + densification stats + fused Adam (6 groups)"}
 
 
 if __name__ == "__main__":

@@ -11,7 +11,8 @@ OBJ=$OUT/obj_$NAME
 mkdir -p "$OBJ"
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-rdc -Wall -Wno-unused-function"
 pids=()
-for f in preprocess sort render_fwd render_bwd gaussian_bwd ssim capi; do
+SRCS=$(sed -n 's/^SRCS := //p' "$HERE/Makefile" | sed 's/\.hip//g')
+for f in $SRCS; do
     EXTRA=""
     [ "$f" = render_bwd ] && EXTRA="-ffp-contract=fast"
     /opt/rocm/bin/hipcc $FLAGS $EXTRA "$@" -c "$HERE/$f.hip" -o "$OBJ/$f.o" &

@@ -45,6 +45,6 @@ def test_fused_loss_is_deterministic():
         x = img.clone().requires_grad_(True)
         loss, _ = omr.losses.l1_ssim_loss(x, gt, 0.2)
         loss.backward()
-        runs.append((float(loss), to_np(x.grad)))
+        runs.append((float(loss.detach()), to_np(x.grad)))
     assert runs[0][0] == runs[1][0]
     np.testing.assert_array_equal(runs[0][1], runs[1][1])
