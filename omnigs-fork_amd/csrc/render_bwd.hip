@@ -35,6 +35,15 @@ namespace {
 
 OMR_STAMP_DECL(g_stamps_bwd)
 
+#ifdef OMR_BWD_COUNT
+// diagnostic: staged instances, (instance, band) evaluations, evaluations with a contributing pixel, instances
+// with any contribution, contributing (pixel, instance) pairs
+__device__ unsigned long long g_bwd_counts[5];
+#define BWD_COUNT(k, v) cnt_[k] += (v)
+#else
+#define BWD_COUNT(k, v)
+#endif
+
 #ifndef OMR_BWD_MINW
 #define OMR_BWD_MINW 1
 #endif
@@ -109,6 +118,9 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
 
     const float half_w = 0.5f * (float)a.W, half_h = 0.5f * (float)a.H;  // ddelx_dx, ddely_dy (backward.cu:700-701)
     const uint32_t slot_of_lane = transposed_slot_of_lane(lane);
+#ifdef OMR_BWD_COUNT
+    uint32_t cnt_[5] = {0, 0, 0, 0, 0};
+#endif
 
     // positions max_c-1 .. 0, 64 per batch, back to front: batch entry `lane` <-> position hi-1-lane
     for (int hi = (int)max_c; hi > 0; hi -= TW_BATCH) {
@@ -138,6 +150,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
         }
         wave_sync();  // orders this wave's LDS stores before its reads below
         const uint32_t nuse = (uint32_t)__popcll(useful);
+        BWD_COUNT(0, nuse);
         for (uint32_t j = 0; j < nuse; ++j) {
             const float4 g = s_geo[j];
             const float4 qo = s_quad[j];
@@ -167,7 +180,10 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
                 const float alpha = fminf(0.99f, qo.w * G);
                 // backward.cu:770-781: skip positions at/after the pixel's last contributor, power > 0, alpha < 1/255
                 const bool contrib = ipos < lastb && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
+                BWD_COUNT(1, 1);
                 if (!__ballot(contrib)) continue;
+                BWD_COUNT(2, 1);
+                BWD_COUNT(4, (uint32_t)__popcll(__ballot(contrib)));
                 any = true;
                 const float inv = __builtin_amdgcn_rcpf(1.0f - alpha);
                 const float Ti = T[b] * inv;
@@ -191,6 +207,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
             const uint32_t slot_j = __builtin_bit_cast(uint32_t, f.w);
             float* row = a.inst_grad + (size_t)slot_j * GRAD_ROW;
             if (!uniform(any)) continue;  // no pixel took a contribution: no row
+            BWD_COUNT(3, 1);
             if (lane == 0) a.row_valid[slot_j] = 1;
             // per-instance factors of backward.cu:805-840 (dG/ddelx = -G (dx a + dy b), ...)
             // conic (a, b, c) back from the staged quadratic form: q = (-a/2, -b, -c/2) log2(e)
@@ -212,6 +229,10 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
         wave_sync();  // the next batch overwrites the staging arrays
     }
     OMR_STAMP_END(g_stamps_bwd, tile);
+#ifdef OMR_BWD_COUNT
+    if (lane == 0)
+        for (int k = 0; k < 5; ++k) atomicAdd(&g_bwd_counts[k], (unsigned long long)cnt_[k]);
+#endif
 }
 
 }  // namespace
@@ -220,6 +241,18 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
 int omr_debug_stamps_bwd(uint64_t* dst, size_t bytes)
 {
     return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps_bwd), bytes);
+}
+#endif
+
+#ifdef OMR_BWD_COUNT
+extern "C" int omr_debug_bwd_counts(uint64_t* dst, int reset)
+{
+    int rc = (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_bwd_counts), 5 * sizeof(uint64_t));
+    if (reset) {
+        const uint64_t z[5] = {0, 0, 0, 0, 0};
+        rc |= (int)hipMemcpyToSymbol(HIP_SYMBOL(g_bwd_counts), z, sizeof(z));
+    }
+    return rc;
 }
 #endif
 
