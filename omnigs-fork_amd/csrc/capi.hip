@@ -429,7 +429,9 @@ int backward_impl(const BackwardIn& in)
     ga.focal_y = (float)in.height / (2.0f * in.tan_fovy);
     ga.focal_x = (float)in.width / (2.0f * in.tan_fovx);
     ga.clamped = g.clamped; ga.grad_sum = g.grad_sum;
-    {
+    ga.splat = g.splat; ga.tiles_touched = g.tiles_touched; ga.inst_grad = b.inst_grad; ga.row_valid = b.row_valid;
+    ga.R = (uint32_t)in.R;
+    if (!gaussian_bwd_fused_reduce()) {  // otherwise gaussian_bwd sums each Gaussian's rows itself
         StageScope st_(ST_INSTANCE_REDUCE, s);
         launch_instance_reduce(in.P, g.order, g.offsets, b.inst_grad, b.row_valid, g.grad_sum, s);
     }

@@ -213,10 +213,99 @@ __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const
     return r;
 }
 
+// Segmented sum of the per-instance rows. Gaussian order[r] (depth rank r) owns the contiguous emission slots
+// [offsets[r-1], offsets[r]); lane r of the grid sums the rows of rank r.
+//  * Only rows marked in row_valid are read (render_bwd.hip writes no row where no pixel took a contribution).
+//  * Short segments (<= RED_SHORT rows, ~95 % of the Gaussians, median 4 rows at config C): the lane adds its rows
+//    in order straight from global memory. The 64 lanes of a wave own consecutive ranks, hence one contiguous
+//    span of rows, so the loads stay within a few KB that L1/L2 serve after the first touch.
+//  * Long segments (polar Gaussians span up to every tile of the image): the whole wave takes them one at a
+//    time, 64 rows per step (one per lane, coalesced), and reduces the 9 sums over the wave (wave_ops.h).
+// Fixed order everywhere, so the sums are deterministic. Culled Gaussians own no rows and are not written (never
+// read downstream).
+constexpr int RED_THREADS = 256;
+#ifndef OMR_RED_SHORT
+#define OMR_RED_SHORT 32
+#endif
+constexpr uint32_t RED_SHORT = OMR_RED_SHORT;
+
+__device__ __forceinline__ void add_row(float* acc, const float* inst_grad, const uint8_t* row_valid, uint32_t row)
+{
+    if (!row_valid[row]) return;  // no pixel of that tile took a contribution
+    const float* p = inst_grad + (size_t)row * GRAD_ROW;
+#pragma unroll
+    for (int c = 0; c < GRAD_ROW; ++c) acc[c] += p[c];
+}
+
+#ifndef OMR_FUSED_REDUCE
+#define OMR_FUSED_REDUCE 1
+#endif
+
+// Sum of Gaussian idx's instance rows into g, with the arithmetic of instance_reduce_kernel (so the result is the
+// same to the bit): short segments lane by lane, 4 rows in flight; long ones by the whole wave, one at a time.
+// Every lane of the wave must call it (the long segments are summed cooperatively).
+__device__ __forceinline__ void own_row_sum(const GaussBwdArgs& a, int idx, float* g)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t s = 0, n = 0;
+    if (idx < a.P && a.radii[idx] > 0) {
+        n = a.tiles_touched[idx];
+        // first emission slot = the slot of the rect's first tile (x0, y0) (raster_common.h: splat_slot)
+        const float4* rec = a.splat + (size_t)idx * SPLAT_F4;
+        const float4 rect = rec[3];
+        s = splat_slot(rec[0], rec[2], __builtin_bit_cast(uint32_t, rect.x), __builtin_bit_cast(uint32_t, rect.y));
+        if (s >= a.R || n > a.R - s) n = 0;  // never true for a consistent forward; keeps reads inside the rows
+    }
+#pragma unroll
+    for (int c = 0; c < GRAD_ROW; ++c) g[c] = 0.f;
+    if (n != 0 && n <= RED_SHORT) {
+        uint32_t k = 0;
+        for (; k + 4 <= n; k += 4) {
+            bool ok[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ok[i] = a.row_valid[s + k + i] != 0;
+            float x[4][GRAD_ROW];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int c = 0; c < GRAD_ROW; ++c) x[i][c] = ok[i] ? a.inst_grad[(size_t)(s + k + i) * GRAD_ROW + c] : 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int c = 0; c < GRAD_ROW; ++c) g[c] += x[i][c];
+        }
+        for (; k < n; ++k) add_row(g, a.inst_grad, a.row_valid, s + k);
+    }
+    uint64_t longs = __ballot(n > RED_SHORT);
+    while (longs) {
+        const int j = __builtin_ctzll(longs);
+        longs &= longs - 1;
+        const uint32_t sj = __builtin_amdgcn_readlane(s, j), ej = sj + __builtin_amdgcn_readlane(n, j);
+        float acc[GRAD_ROW];
+#pragma unroll
+        for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
+        for (uint32_t row = sj + lane; row < ej; row += 64) add_row(acc, a.inst_grad, a.row_valid, row);
+        float t8;
+        const float tv = wave_sum8_transposed(acc, acc[8], lane, &t8);
+        // value c < 8 sits in lane bitrev3(c) (transposed_slot_of_lane is its own inverse)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const float v = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tv),
+                                                                                transposed_slot_of_lane(c)));
+            if ((int)lane == j) g[c] = v;
+        }
+        if ((int)lane == j) g[8] = t8;
+    }
+}
+
 template <int CAM, int MC>
 __global__ __launch_bounds__(256) void gaussian_bwd_kernel(GaussBwdArgs a)
 {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+#if OMR_FUSED_REDUCE
+    float g[GRAD_ROW];
+    own_row_sum(a, idx, g);  // before any lane leaves: long segments take the whole wave
+#endif
     if (idx >= a.P) return;
     const int Mr = MC > 0 ? MC : a.M;
     if (!(a.radii[idx] > 0)) {
@@ -243,10 +332,12 @@ __global__ __launch_bounds__(256) void gaussian_bwd_kernel(GaussBwdArgs a)
         return;
     }
 
-    // 1. this Gaussian's summed instance rows (instance_reduce_kernel)
+    // 1. this Gaussian's summed instance rows
+#if !OMR_FUSED_REDUCE
     float g[GRAD_ROW];
 #pragma unroll
     for (int c = 0; c < GRAD_ROW; ++c) g[c] = a.grad_sum[(size_t)idx * GRAD_ROW + c];
+#endif
     a.dL_dmean2D[3 * idx + 0] = g[0];
     a.dL_dmean2D[3 * idx + 1] = g[1];
     a.dL_dmean2D[3 * idx + 2] = 0.f;
@@ -402,30 +493,6 @@ __global__ __launch_bounds__(256) void gaussian_bwd_kernel(GaussBwdArgs a)
     for (int k = 0; k < 4; ++k) a.dL_drot[4 * idx + k] = dr[k];
 }
 
-// Segmented sum of the per-instance rows. Gaussian order[r] (depth rank r) owns the contiguous emission slots
-// [offsets[r-1], offsets[r]); lane r of the grid sums the rows of rank r.
-//  * Only rows marked in row_valid are read (render_bwd.hip writes no row where no pixel took a contribution).
-//  * Short segments (<= RED_SHORT rows, ~95 % of the Gaussians, median 4 rows at config C): the lane adds its rows
-//    in order straight from global memory. The 64 lanes of a wave own consecutive ranks, hence one contiguous
-//    span of rows, so the loads stay within a few KB that L1/L2 serve after the first touch.
-//  * Long segments (polar Gaussians span up to every tile of the image): the whole wave takes them one at a
-//    time, 64 rows per step (one per lane, coalesced), and reduces the 9 sums over the wave (wave_ops.h).
-// Fixed order everywhere, so the sums are deterministic. Culled Gaussians own no rows and are not written (never
-// read downstream).
-constexpr int RED_THREADS = 256;
-#ifndef OMR_RED_SHORT
-#define OMR_RED_SHORT 32
-#endif
-constexpr uint32_t RED_SHORT = OMR_RED_SHORT;
-
-__device__ __forceinline__ void add_row(float* acc, const float* inst_grad, const uint8_t* row_valid, uint32_t row)
-{
-    if (!row_valid[row]) return;  // no pixel of that tile took a contribution
-    const float* p = inst_grad + (size_t)row * GRAD_ROW;
-#pragma unroll
-    for (int c = 0; c < GRAD_ROW; ++c) acc[c] += p[c];
-}
-
 __global__ __launch_bounds__(RED_THREADS) void instance_reduce_kernel(int P, const uint32_t* order,
                                                                       const uint32_t* offsets, const float* inst_grad,
                                                                       const uint8_t* row_valid, float* grad_sum)
@@ -552,6 +619,8 @@ __global__ __launch_bounds__(256) void sh_grad_from_colors_kernel(int P, int D, 
 }
 
 }  // namespace
+
+bool gaussian_bwd_fused_reduce() { return OMR_FUSED_REDUCE != 0; }
 
 void launch_sh_grad_from_colors(int P, int D, int M, int nviews, const float* means3D, const float* shs,
                                 const float* campos, const float* dL_dcolors, float* dL_dsh, hipStream_t s)

@@ -106,7 +106,14 @@ struct GaussBwdArgs {
     const float* campos;
     float tan_fovx, tan_fovy, focal_x, focal_y;
     const uint8_t* clamped;
-    const float* grad_sum;  // [P][GRAD_ROW] per-Gaussian sums of the instance rows (instance_reduce)
+    const float* grad_sum;  // [P][GRAD_ROW] per-Gaussian sums of the instance rows (instance_reduce; unfused build)
+    // fused row sums (gaussian_bwd.hip, OMR_FUSED_REDUCE): each Gaussian's rows are the emission slots
+    // [first, first + tiles_touched) of the canonical binning layout, first = splat_slot(rect x0, y0)
+    const float4* splat;          // render records
+    const uint32_t* tiles_touched;
+    const float* inst_grad;       // [R][GRAD_ROW]
+    const uint8_t* row_valid;     // [R]
+    uint32_t R;                   // rows (num_rendered)
     float* dL_dmean2D;   // [P,3]
     float* dL_dconic;    // [P,4] optional (may be null)
     float* dL_dopacity;  // [P]
@@ -120,6 +127,8 @@ struct GaussBwdArgs {
     float* dpy_dt;       // [P,3] optional
 };
 void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s);
+// true when gaussian_bwd sums the instance rows itself (OMR_FUSED_REDUCE) and instance_reduce is not launched
+bool gaussian_bwd_fused_reduce();
 // view-parallel DP: dL_dsh[P,M,3] = sum over views of dL/dsh rebuilt from dL_dcolors [nviews][P][3] + campos [nviews][3]
 void launch_sh_grad_from_colors(int P, int D, int M, int nviews, const float* means3D, const float* shs,
                                 const float* campos, const float* dL_dcolors, float* dL_dsh, hipStream_t s);
