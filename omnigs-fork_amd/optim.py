@@ -210,11 +210,23 @@ class GaussianOptimizer:
                                              self.max_radii2D.data_ptr(), R._stream(radii.device))
         R._check(rc, "omr_densification_stats")
 
+    def sync_densification_stats(self, dist_info=None):
+        """View-parallel training: sum xyz_gradient_accum / denom and take the max of max_radii2D over the ranks
+        (SURVEY.md §8(e)), so every replica densifies identically. Call before densify_and_prune."""
+        import torch.distributed as dist
+
+        if dist_info is None or not dist_info.enabled:
+            return
+        dist.all_reduce(self.xyz_gradient_accum, op=dist.ReduceOp.SUM)
+        dist.all_reduce(self.denom, op=dist.ReduceOp.SUM)
+        dist.all_reduce(self.max_radii2D, op=dist.ReduceOp.MAX)
+
     def densify_and_prune(self, max_grad: float, min_opacity: float, extent: float, max_screen_size: int,
                           prune_by_extent: bool = True, normals: Optional[torch.Tensor] = None,
                           generator: Optional[torch.Generator] = None) -> dict:
         """densifyAndPrune (gaussian_model.cpp:812-837). The split samples are standard normals drawn with torch
-        (the reference's at::normal, :751) unless `normals` [2*S,3] is given. Returns the plan's counts."""
+        (the reference's at::normal, :751) unless `normals` [2*S,3] is given; view-parallel replicas must pass the
+        same samples (or identically seeded generators) to stay identical. Returns the plan's counts."""
         ps = self.params()
         P, Mr, dev = self.P, self.Mr, ps[0].device
         L = R.lib()

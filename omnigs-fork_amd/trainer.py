@@ -18,7 +18,7 @@ import torch
 from . import losses
 from . import optim as O
 from . import rasterizer as R
-from .parallel import GradBuffer
+from .parallel import DistInfo, GradBuffer, allreduce_compact_
 
 
 class TrainStep:
@@ -31,9 +31,16 @@ class TrainStep:
 
 def train_step(opt: O.GaussianOptimizer, viewpoint, image_height: int, image_width: int, gt_image: torch.Tensor,
                bg_color: torch.Tensor, camera_type: int = R.CAMERA_LONLAT, lambda_dssim: float = 0.2,
-               densification_stats: bool = True, state: Optional[TrainStep] = None):
+               densification_stats: bool = True, state: Optional[TrainStep] = None,
+               dist_info: Optional[DistInfo] = None):
     """Render `viewpoint`, take the loss against gt_image, backpropagate and step Adam. Returns
-    (terms = tensor([loss, l1, ssim]), rendered image, radii)."""
+    (terms = tensor([loss, l1, ssim]), rendered image, radii).
+
+    View-parallel (dist_info.world_size > 1): every rank renders its own view of the replicated
+    Gaussians; the compact exchange (parallel.allreduce_compact_) sums the rasterizer gradients over the views and
+    every rank then takes the same Adam step on the same sums, so the replicas stay identical without a parameter
+    broadcast (the kernels are deterministic). Densification statistics stay per rank until
+    GaussianOptimizer.sync_densification_stats() at a densification iteration (the sums commute)."""
     pc = opt.model
     state = state or TrainStep()
     P, Mr = opt.P, opt.Mr
@@ -64,5 +71,8 @@ def train_step(opt: O.GaussianOptimizer, viewpoint, image_height: int, image_wid
                                      out=out)
     if densification_stats:
         opt.add_densification_stats(out["dL_dmeans2D"], radii)
+    if dist_info is not None and dist_info.enabled:
+        allreduce_compact_(state.buf, dist_info, out["dL_dcolors"], cp,
+                           lambda c, d, out: R.sh_grad_from_colors(means3D, shs, pc.active_sh_degree, c, d, out=out))
     opt.step(raster_grads=out)
     return terms, image, radii
