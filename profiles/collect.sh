@@ -15,11 +15,11 @@ mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- \
-    python3 "$R/bench.py" --steps "$STEPS" --warmup 3 --no-cpu-baseline > "$OUT/bench_prof_$TAG.json" 2> "$OUT/bench_prof_$TAG.err"
+    python3 "$R/bench.py" --steps "$STEPS" --warmup 3 --no-cpu-baseline --no-train-step > "$OUT/bench_prof_$TAG.json" 2> "$OUT/bench_prof_$TAG.err"
 echo "[collect] kernel trace done"
 timeout -k 10 420 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$TAG" -o run -- \
-    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/bench_pmc_fetch_$TAG.json" 2> "$OUT/pmc_fetch_$TAG.err"
+    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-train-step > "$OUT/bench_pmc_fetch_$TAG.json" 2> "$OUT/pmc_fetch_$TAG.err"
 echo "[collect] FETCH_SIZE done"
 timeout -k 10 420 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$TAG" -o run -- \
-    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/bench_pmc_write_$TAG.json" 2> "$OUT/pmc_write_$TAG.err"
+    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-train-step > "$OUT/bench_pmc_write_$TAG.json" 2> "$OUT/pmc_write_$TAG.err"
 echo "[collect] WRITE_SIZE done"
