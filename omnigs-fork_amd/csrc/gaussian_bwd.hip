@@ -237,6 +237,9 @@ __device__ __forceinline__ void add_row(float* acc, const float* inst_grad, cons
     for (int c = 0; c < GRAD_ROW; ++c) acc[c] += p[c];
 }
 
+#ifndef OMR_GBWD_MINW
+#define OMR_GBWD_MINW 1
+#endif
 #ifndef OMR_FUSED_REDUCE
 #define OMR_FUSED_REDUCE 1
 #endif
@@ -299,7 +302,7 @@ __device__ __forceinline__ void own_row_sum(const GaussBwdArgs& a, int idx, floa
 }
 
 template <int CAM, int MC>
-__global__ __launch_bounds__(256) void gaussian_bwd_kernel(GaussBwdArgs a)
+__global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussBwdArgs a)
 {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
 #if OMR_FUSED_REDUCE

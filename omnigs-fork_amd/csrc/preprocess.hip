@@ -78,6 +78,10 @@ __device__ __forceinline__ float3 cov2d_from_J(const float* v, const float J0[3]
     return {c00, c01, c11};
 }
 
+#ifndef OMR_PRE_SH_EARLY
+#define OMR_PRE_SH_EARLY 1
+#endif
+
 template <int CAM>
 __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
 {
@@ -91,6 +95,17 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
 
     const float3 p_orig = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
     const float* v = a.viewmatrix;
+    // lonlat culls almost nothing (|t| <= 0.2 only), so the 192-B SH row is requested before the projection math
+    // and its latency overlaps it; pinhole frustum-culls most of a scene and loads rows only for survivors
+    constexpr bool kEarlySH = OMR_PRE_SH_EARLY && CAM == CAM_LONLAT;
+    const bool sh16 = a.colors_precomp == nullptr && a.M == 16 && (reinterpret_cast<uintptr_t>(a.shs) & 15u) == 0;
+    const int nf4 = (3 * (a.D + 1) * (a.D + 1) + 3) >> 2;
+    float4 shq[12];
+    if (kEarlySH && sh16) {
+        const float4* row4 = reinterpret_cast<const float4*>(a.shs + (size_t)idx * 48);
+#pragma unroll
+        for (int q = 0; q < 12; ++q) shq[q] = q < nf4 ? row4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     const float3 t = transformPoint4x3(p_orig, v);
     float2 point_image;
     float depth;
@@ -182,13 +197,13 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
         dy = dy / len;
         dz = dz / len;
         const float* row = a.shs + (size_t)idx * a.M * 3;
-        if (a.M == 16 && (reinterpret_cast<uintptr_t>(a.shs) & 15u) == 0) {
+        if (sh16) {
             // the row as 16-B loads: 12 wide accesses per lane instead of 48 dword gathers 192 B apart
             float shv[48];
-            const int nf4 = (3 * (a.D + 1) * (a.D + 1) + 3) >> 2;
 #pragma unroll
             for (int q = 0; q < 12; ++q) {
-                const float4 v = q < nf4 ? reinterpret_cast<const float4*>(row)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 v = kEarlySH ? shq[q]
+                                          : (q < nf4 ? reinterpret_cast<const float4*>(row)[q] : make_float4(0.f, 0.f, 0.f, 0.f));
                 shv[4 * q] = v.x;
                 shv[4 * q + 1] = v.y;
                 shv[4 * q + 2] = v.z;
