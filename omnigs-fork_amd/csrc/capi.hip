@@ -33,6 +33,19 @@ __global__ __launch_bounds__(64) void debug_wave_sum_kernel(const float* in, flo
     if (lane < 9) out[transposed_slot_of_lane(lane)] = lane < 8 ? tv : t8;
 }
 
+// the same through wave_sum9_rows (the render backward's default reduction)
+__global__ __launch_bounds__(64) void debug_wave_sum9_kernel(const float* in, float* out)
+{
+    const uint32_t lane = threadIdx.x;
+    float v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = in[lane * 9 + c];
+    float t8;
+    const float tv = wave_sum9_rows(v, in[lane * 9 + 8], lane, &t8);
+    if ((lane & 7) == 0) out[lane >> 3] = tv;
+    if (lane == 1) out[8] = t8;
+}
+
 thread_local std::string g_last_error;
 
 int fail(int code, const std::string& msg)
@@ -743,6 +756,13 @@ size_t omr_binning_bytes(int num_rendered, int width, int height)
 {
     const Dims d = dims(width, height);
     return BinningState::carve(nullptr, (size_t)std::max(num_rendered, 0), nullptr, tile_sort_passes(d.T));
+}
+
+int omr_debug_wave_sum9(const float* in, float* out, void* stream)
+{
+    g_last_error.clear();
+    debug_wave_sum9_kernel<<<1, 64, 0, (hipStream_t)stream>>>(in, out);
+    return hip_check("debug_wave_sum9");
 }
 
 int omr_debug_wave_sum(const float* in, float* out, void* stream)

@@ -47,6 +47,10 @@ __device__ unsigned long long g_bwd_counts[5];
 #ifndef OMR_BWD_MINW
 #define OMR_BWD_MINW 1
 #endif
+// wave reduction of the per-instance sums: wave_sum9_rows (1) or the transposed DPP butterfly (0), wave_ops.h
+#ifndef OMR_BWD_ROWS_RED
+#define OMR_BWD_ROWS_RED 1
+#endif
 // keep each pixel's dL/dpix and last contributor in LDS (read per instance and band) instead of 16 VGPRs
 #ifndef OMR_BWD_PIX_LDS
 #define OMR_BWD_PIX_LDS 0
@@ -117,7 +121,9 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
     // instances behind every pixel's last contributor get no row (row_valid stays 0 for them)
 
     const float half_w = 0.5f * (float)a.W, half_h = 0.5f * (float)a.H;  // ddelx_dx, ddely_dy (backward.cu:700-701)
+#if !OMR_BWD_ROWS_RED
     const uint32_t slot_of_lane = transposed_slot_of_lane(lane);
+#endif
 #ifdef OMR_BWD_COUNT
     uint32_t cnt_[5] = {0, 0, 0, 0, 0};
 #endif
@@ -223,8 +229,15 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
             v[6] = sc0;                                        // dL/dcolour
             v[7] = sc1;
             float t8;
+#if OMR_BWD_ROWS_RED
+            const float tv = wave_sum9_rows(v, sc2, lane, &t8);
+            // lane 8k holds value k (k < 8), every lane the 9th: lanes 0, 8, ..., 56 and 1 store the 36-B row
+            const bool lead = (lane & 7) == 0;
+            if (lead || lane == 1) row[lead ? (lane >> 3) : 8u] = lead ? tv : t8;
+#else
             const float tv = wave_sum8_transposed(v, sc2, lane, &t8);
             if (lane < GRAD_ROW) row[slot_of_lane] = lane < 8 ? tv : t8;
+#endif
         }
         wave_sync();  // the next batch overwrites the staging arrays
     }

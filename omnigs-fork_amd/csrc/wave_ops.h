@@ -16,6 +16,7 @@ constexpr int DPP_XOR1 = 0xb1;   // quad_perm [1,0,3,2]
 constexpr int DPP_XOR2 = 0x4e;   // quad_perm [2,3,0,1]
 constexpr int DPP_ROR4 = 0x124;  // row_ror:4
 constexpr int DPP_ROR8 = 0x128;  // row_ror:8
+constexpr int DPP_HALF_MIRROR = 0x141;  // row_half_mirror: lane i <-> 7 - i within each 8 lanes
 
 // Sum over the four 16-lane rows: x(lane) + x(lane^16) + x(lane^32) + x(lane^48). v_permlane16_swap swaps the
 // odd rows of its first operand with the even rows of its second; with both operands = x, vdst' + src' =
@@ -56,6 +57,43 @@ __device__ __forceinline__ float wave_sum8_transposed(const float v[8], float v8
     return cross_row_sum(c);
 }
 
+
+// Wave-sum of v[0..7] and v8 with the cross-row levels FIRST, where v_permlane32_swap / v_permlane16_swap move
+// whole halves / rows between two registers in one instruction (no per-lane select, unlike the DPP levels):
+//   level 1  permlane32_swap(v[i], v[i+4]) + add: lanes 0-31 hold v[i] summed with lane+32, lanes 32-63 v[i+4]
+//   level 2  permlane16_swap(a[i], a[i+2]) + add: row r of b[i] holds value index i + 2r, summed over 4 rows
+//   level 3  within the row (DPP row_ror:8, select by lane bit 3), then an 8-lane sum (xor1, xor2, half mirror)
+// 26 VALU (+2 s_nop) against 34 for wave_sum8_transposed. Returns, in every lane l, the wave total of value index
+// (l >> 3) & 7; *t8 = the total of v8 on every lane.
+__device__ __forceinline__ float wave_sum9_rows(const float v[8], float v8, uint32_t lane, float* t8)
+{
+    float x0 = v[0], x1 = v[1], x2 = v[2], x3 = v[3], y0 = v[4], y1 = v[5], y2 = v[6], y3 = v[7], w0 = v8, w1 = v8;
+    asm volatile("s_nop 1\n\t"
+                 "v_permlane32_swap_b32 %0, %4\n\t"
+                 "v_permlane32_swap_b32 %1, %5\n\t"
+                 "v_permlane32_swap_b32 %2, %6\n\t"
+                 "v_permlane32_swap_b32 %3, %7\n\t"
+                 "v_permlane32_swap_b32 %8, %9"
+                 : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(y0), "+v"(y1), "+v"(y2), "+v"(y3), "+v"(w0), "+v"(w1));
+    float a0 = x0 + y0, a1 = x1 + y1, a2 = x2 + y2, a3 = x3 + y3, u0 = w0 + w1, u1 = u0;
+    asm volatile("s_nop 1\n\t"
+                 "v_permlane16_swap_b32 %0, %2\n\t"
+                 "v_permlane16_swap_b32 %1, %3\n\t"
+                 "v_permlane16_swap_b32 %4, %5"
+                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(u0), "+v"(u1));
+    const float b0 = a0 + a2, b1 = a1 + a3;  // row r: index 2r (b0) and 2r + 1 (b1), 4 rows summed
+    float u = u0 + u1;
+    const bool hi = lane & 8;
+    float c = add_dpp<DPP_ROR8>(hi ? b1 : b0, hi ? b0 : b1);
+    c = add_dpp<DPP_XOR1>(c, c);
+    c = add_dpp<DPP_XOR2>(c, c);
+    c = add_dpp<DPP_HALF_MIRROR>(c, c);
+    u = add_dpp<DPP_ROR8>(u, u);
+    u = add_dpp<DPP_XOR1>(u, u);
+    u = add_dpp<DPP_XOR2>(u, u);
+    *t8 = add_dpp<DPP_HALF_MIRROR>(u, u);
+    return c;
+}
 
 // lane l < 8 holds value index bitrev3(l) after wave_sum8_transposed; lane 8 is used for the 9th value
 __device__ __forceinline__ uint32_t transposed_slot_of_lane(uint32_t lane)

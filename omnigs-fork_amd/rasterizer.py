@@ -65,6 +65,7 @@ def lib() -> C.CDLL:
         L.omr_debug_image_state.argtypes = [vp, i, i, vp, vp, vp]
         L.omr_debug_geometry.argtypes = [vp, i, vp, vp, vp, vp, vp, vp]
         L.omr_debug_wave_sum.argtypes = [vp, vp, vp]
+        L.omr_debug_wave_sum9.argtypes = [vp, vp, vp]
         L.omr_profile_enable.argtypes = [i]
         L.omr_sh_grad_from_colors.argtypes = [i, i, i, i, vp, vp, vp, vp, vp, vp]
         L.omr_l1_ssim_scratch_floats.restype = sz
@@ -439,10 +440,12 @@ def profile_read() -> dict:
     return {lib().omr_profile_stage_name(i).decode(): (float(tot[i]), int(cnt[i])) for i in range(n)}
 
 
-def debug_wave_sum(x: torch.Tensor) -> torch.Tensor:
-    """Column sums of a [64, 9] float32 device tensor through the render backward's wave reduction."""
+def debug_wave_sum(x: torch.Tensor, rows: bool = False) -> torch.Tensor:
+    """Column sums of a [64, 9] float32 device tensor through a wave reduction of wave_ops.h: the transposed DPP
+    butterfly (rows=False) or the cross-row-first wave_sum9_rows (rows=True, the render backward's)."""
     x = _dev_f32(x, "x")
     assert tuple(x.shape) == (64, 9)
     out = torch.empty(9, dtype=torch.float32, device=x.device)
-    _check(lib().omr_debug_wave_sum(x.data_ptr(), out.data_ptr(), _stream(x.device)), "debug_wave_sum")
+    fn = lib().omr_debug_wave_sum9 if rows else lib().omr_debug_wave_sum
+    _check(fn(x.data_ptr(), out.data_ptr(), _stream(x.device)), "debug_wave_sum")
     return out

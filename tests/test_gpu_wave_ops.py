@@ -6,24 +6,26 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("rows", [False, True])
 @pytest.mark.parametrize("seed", [0, 1, 2])
-def test_wave_sum_matches_column_sums(seed, omr):
+def test_wave_sum_matches_column_sums(seed, rows, omr):
     import torch
 
     rng = np.random.default_rng(seed)
     x = rng.standard_normal((64, 9)).astype(np.float32)
     if seed == 2:  # sparse: most lanes zero, as when few pixels of a wave contribute
         x[rng.uniform(size=x.shape) < 0.85] = 0.0
-    got = omr.rasterizer.debug_wave_sum(torch.from_numpy(x).cuda()).cpu().numpy()
+    got = omr.rasterizer.debug_wave_sum(torch.from_numpy(x).cuda(), rows=rows).cpu().numpy()
     ref = x.astype(np.float64).sum(axis=0)
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
 
 
-def test_wave_sum_lane_identity(omr):
+@pytest.mark.parametrize("rows", [False, True])
+def test_wave_sum_lane_identity(rows, omr):
     import torch
 
     # value c of lane l = (c + 1) * 1000 + l: distinguishes every (lane, column) contribution exactly in f32
     x = np.array([[(c + 1) * 1000 + l for c in range(9)] for l in range(64)], dtype=np.float32)
-    got = omr.rasterizer.debug_wave_sum(torch.from_numpy(x).cuda()).cpu().numpy()
+    got = omr.rasterizer.debug_wave_sum(torch.from_numpy(x).cuda(), rows=rows).cpu().numpy()
     ref = x.astype(np.float64).sum(axis=0)
     np.testing.assert_array_equal(got, ref)
