@@ -16,6 +16,7 @@
 #include "kernels.h"
 #include "sh_eval.h"
 #include "wave_ops.h"
+#include "wave_rows.h"
 
 namespace omr {
 
@@ -124,10 +125,14 @@ __device__ __forceinline__ void cov3d_forward(float sx, float sy, float sz, floa
     c[5] = sig(2, 2);
 }
 
-// backward.cu:30-151; writes dL_dsh for all M coefficients (zeros beyond (deg+1)^2), returns dL/dmean part
+// backward.cu:30-151; writes dL_dsh for all M coefficients (zeros beyond (deg+1)^2), returns dL/dmean part.
+// MC == 16: the SH row is read as 12 float4 from row4 and the dL_dsh row written as 12 float4 to out4 (both the
+// lane's row of the wave's LDS staging image, or both global rows; the row is read before it is overwritten);
+// otherwise both are read/written in global memory at idx.
 template <int MC>
 __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const float* campos, const float* shs,
-                                          uint8_t clamp_bits, F3 dRGB, float* dL_dsh)
+                                          const float4* row4, uint8_t clamp_bits, F3 dRGB, float* dL_dsh,
+                                          float4* out4)
 {
     const int Mr = MC > 0 ? MC : M;
     const float dox = pos.x - campos[0], doy = pos.y - campos[1], doz = pos.z - campos[2];
@@ -137,20 +142,17 @@ __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const
     if (clamp_bits & 2) dRGB.y = 0.f;
     if (clamp_bits & 4) dRGB.z = 0.f;
     const float* sh_row = shs + (size_t)idx * Mr * 3;
-    float* out = dL_dsh + (size_t)idx * Mr * 3;
     float shv[MC == 16 ? 48 : 1];
-    const float* sh = sh_row;
-    if constexpr (MC == 16) {  // the row as 16-B loads (launch_gaussian_backward checks the alignment)
+    if constexpr (MC == 16) {
         const int nf4 = (3 * (deg + 1) * (deg + 1) + 3) >> 2;
 #pragma unroll
         for (int q = 0; q < 12; ++q) {
-            const float4 v = q < nf4 ? reinterpret_cast<const float4*>(sh_row)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 v = q < nf4 ? row4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
             shv[4 * q] = v.x;
             shv[4 * q + 1] = v.y;
             shv[4 * q + 2] = v.z;
             shv[4 * q + 3] = v.w;
         }
-        sh = shv;
     }
     float coef[16];
     sh_basis(deg, x, y, z, coef);
@@ -158,7 +160,7 @@ __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const
     const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
-        auto s = [&](int k) { return sh[3 * k + ch]; };
+        auto s = [&](int k) { return MC == 16 ? shv[3 * k + ch] : sh_row[3 * k + ch]; };
         if (deg > 0) {
             gx[ch] = -SH_C1 * s(3);
             gy[ch] = -SH_C1 * s(1);
@@ -183,8 +185,7 @@ __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const
     }
     const float d[3] = {dRGB.x, dRGB.y, dRGB.z};
     if constexpr (MC == 16) {
-        // 16 coefficients x 3 channels = 48 floats = 12 float4 stores (row is 16-B aligned for M = 16)
-        float4* o4 = reinterpret_cast<float4*>(out);
+        // 16 coefficients x 3 channels = 48 floats = 12 float4
 #pragma unroll
         for (int q = 0; q < 12; ++q) {
             float v[4];
@@ -193,9 +194,10 @@ __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const
                 const int f = 4 * q + e;
                 v[e] = (f / 3) < (deg + 1) * (deg + 1) ? coef[f / 3] * d[f % 3] : 0.f;
             }
-            o4[q] = make_float4(v[0], v[1], v[2], v[3]);
+            out4[q] = make_float4(v[0], v[1], v[2], v[3]);
         }
     } else {
+        float* out = dL_dsh + (size_t)idx * Mr * 3;
         const int nk = (deg + 1) * (deg + 1);
         for (int k = 0; k < Mr; ++k)
 #pragma unroll
@@ -301,43 +303,18 @@ __device__ __forceinline__ void own_row_sum(const GaussBwdArgs& a, int idx, floa
     }
 }
 
-template <int CAM, int MC>
-__global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussBwdArgs a)
-{
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-#if OMR_FUSED_REDUCE
-    float g[GRAD_ROW];
-    own_row_sum(a, idx, g);  // before any lane leaves: long segments take the whole wave
+#ifndef OMR_GBWD_STAGE
+#define OMR_GBWD_STAGE 1
 #endif
-    if (idx >= a.P) return;
-    const int Mr = MC > 0 ? MC : a.M;
-    if (!(a.radii[idx] > 0)) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            a.dL_dmean2D[3 * idx + c] = 0.f;
-            a.dL_dcolor[3 * idx + c] = 0.f;
-            a.dL_dmean3D[3 * idx + c] = 0.f;
-            a.dL_dscale[3 * idx + c] = 0.f;
-        }
-        a.dL_dopacity[idx] = 0.f;
-#pragma unroll
-        for (int c = 0; c < 6; ++c) a.dL_dcov3D[6 * idx + c] = 0.f;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) a.dL_drot[4 * idx + c] = 0.f;
-        if (a.dL_dconic)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) a.dL_dconic[4 * idx + c] = 0.f;
-        if (a.dL_dsh)
-            for (int c = 0; c < Mr * 3; ++c) a.dL_dsh[(size_t)idx * Mr * 3 + c] = 0.f;
-        if (a.dpx_dt)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) a.dpx_dt[3 * idx + c] = a.dpy_dt[3 * idx + c] = 0.f;
-        return;
-    }
 
+// Everything after the row sums for one visible Gaussian idx (radii > 0). dsh4: where the MC == 16 dL_dsh row goes.
+template <int CAM, int MC>
+__device__ __forceinline__ void gaussian_bwd_point(const GaussBwdArgs& a, int idx, float (&g)[GRAD_ROW],
+                                                   const float4* sh4, float4* dsh4)
+{
+    const int Mr = MC > 0 ? MC : a.M;
     // 1. this Gaussian's summed instance rows
 #if !OMR_FUSED_REDUCE
-    float g[GRAD_ROW];
 #pragma unroll
     for (int c = 0; c < GRAD_ROW; ++c) g[c] = a.grad_sum[(size_t)idx * GRAD_ROW + c];
 #endif
@@ -360,7 +337,10 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
     const float* v = a.viewmatrix;
     float c3[6];
     float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (a.scales) q = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
+    if (a.scales) {
+        if ((reinterpret_cast<uintptr_t>(a.rotations) & 15u) == 0) q = reinterpret_cast<const float4*>(a.rotations)[idx];
+        else q = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
+    }
     if (a.cov3D_precomp) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) c3[k] = a.cov3D_precomp[6 * idx + k];
@@ -476,12 +456,18 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
 
     // 3. SH backward
     if (a.shs) {
-        const F3 dm = sh_backward<MC>(idx, a.D, a.M, mean, a.campos, a.shs, a.clamped[idx], F3{g[6], g[7], g[8]}, a.dL_dsh);
+        const F3 dm = sh_backward<MC>(idx, a.D, a.M, mean, a.campos, a.shs, sh4, a.clamped[idx], F3{g[6], g[7], g[8]},
+                                      a.dL_dsh, dsh4);
         dmean.x += dm.x;
         dmean.y += dm.y;
         dmean.z += dm.z;
     } else if (a.dL_dsh) {
-        for (int c = 0; c < Mr * 3; ++c) a.dL_dsh[(size_t)idx * Mr * 3 + c] = 0.f;
+        if constexpr (MC == 16) {
+#pragma unroll
+            for (int q = 0; q < 12; ++q) dsh4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+            for (int c = 0; c < Mr * 3; ++c) a.dL_dsh[(size_t)idx * Mr * 3 + c] = 0.f;
+        }
     }
     a.dL_dmean3D[3 * idx + 0] = dmean.x;
     a.dL_dmean3D[3 * idx + 1] = dmean.y;
@@ -494,6 +480,84 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
     for (int k = 0; k < 3; ++k) a.dL_dscale[3 * idx + k] = ds[k];
 #pragma unroll
     for (int k = 0; k < 4; ++k) a.dL_drot[4 * idx + k] = dr[k];
+}
+
+// backward.cu:805-840 targets etc. of a culled Gaussian (radii == 0): every output zero (the caller allocates the
+// gradient tensors without zero-filling them)
+template <int MC>
+__device__ __forceinline__ void gaussian_bwd_culled(const GaussBwdArgs& a, int idx, float4* dsh4)
+{
+    const int Mr = MC > 0 ? MC : a.M;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        a.dL_dmean2D[3 * idx + c] = 0.f;
+        a.dL_dcolor[3 * idx + c] = 0.f;
+        a.dL_dmean3D[3 * idx + c] = 0.f;
+        a.dL_dscale[3 * idx + c] = 0.f;
+    }
+    a.dL_dopacity[idx] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) a.dL_dcov3D[6 * idx + c] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a.dL_drot[4 * idx + c] = 0.f;
+    if (a.dL_dconic)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a.dL_dconic[4 * idx + c] = 0.f;
+    if (a.dL_dsh) {
+        if constexpr (MC == 16) {
+#pragma unroll
+            for (int q = 0; q < 12; ++q) dsh4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+            for (int c = 0; c < Mr * 3; ++c) a.dL_dsh[(size_t)idx * Mr * 3 + c] = 0.f;
+        }
+    }
+    if (a.dpx_dt)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) a.dpx_dt[3 * idx + c] = a.dpy_dt[3 * idx + c] = 0.f;
+}
+
+// One wave per 64 consecutive Gaussians. For MC == 16 (launch_gaussian_backward checks the 16-B alignment) the
+// wave reads its 64 SH rows and writes its 64 dL_dsh rows as contiguous 12-KiB spans through LDS (wave_rows.h):
+// each lane reads its SH row from the image where it needs it and overwrites the same row with its dL_dsh row
+// (only that lane touches it), so one image serves both directions. SH rows of culled Gaussians are not read;
+// their dL_dsh rows are written as zeros.
+template <int CAM, int MC>
+__global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussBwdArgs a)
+{
+    constexpr int SH_F4 = 12;
+    constexpr bool STAGED = MC == 16 && OMR_GBWD_STAGE;
+    __shared__ float4 s_stage[4][STAGED ? stage_f4<SH_F4>() : 1];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const int wave_first = (int)(blockIdx.x * 256u + wv * 64u);
+    if (wave_first >= a.P) return;  // wave-uniform
+    const int idx = wave_first + (int)lane;
+    float g[GRAD_ROW];
+#if OMR_FUSED_REDUCE
+    own_row_sum(a, idx, g);  // before any lane leaves: long segments take the whole wave
+#endif
+    const bool valid = idx < a.P;
+    const bool vis = valid && a.radii[idx] > 0;
+    float4* stage = s_stage[wv];
+    // MC == 16 only (the MC == 0 path reads and writes the rows itself)
+    float4* dsh4 = STAGED ? stage + lane * stage_stride<SH_F4>() : reinterpret_cast<float4*>(a.dL_dsh) + (size_t)idx * SH_F4;
+    const float4* sh4 = STAGED ? stage + lane * stage_stride<SH_F4>() : reinterpret_cast<const float4*>(a.shs) + (size_t)idx * SH_F4;
+    if constexpr (STAGED) {
+        if (a.shs) {
+            const int nf4 = (3 * (a.D + 1) * (a.D + 1) + 3) >> 2;
+            wave_rows_load<SH_F4>(reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4, __ballot(vis), nf4,
+                                  stage, lane);
+            wave_sync();
+        }
+    }
+    if (vis) gaussian_bwd_point<CAM, MC>(a, idx, g, sh4, dsh4);
+    else if (valid) gaussian_bwd_culled<MC>(a, idx, dsh4);
+    if constexpr (STAGED) {
+        if (a.dL_dsh) {
+            wave_sync();
+            wave_rows_store<SH_F4>(reinterpret_cast<float4*>(a.dL_dsh) + (size_t)wave_first * SH_F4, __ballot(valid),
+                                   stage, lane);
+        }
+    }
 }
 
 __global__ __launch_bounds__(RED_THREADS) void instance_reduce_kernel(int P, const uint32_t* order,

@@ -13,6 +13,7 @@
 // writes 8 + 16 + 16 + 4 + 1 + 4 + 4 (radius) + 8 (sort key/value) = 61 B.
 #include "kernels.h"
 #include "sh_eval.h"
+#include "wave_rows.h"
 
 namespace omr {
 
@@ -78,34 +79,27 @@ __device__ __forceinline__ float3 cov2d_from_J(const float* v, const float J0[3]
     return {c00, c01, c11};
 }
 
-#ifndef OMR_PRE_SH_EARLY
-#define OMR_PRE_SH_EARLY 1
+#ifndef OMR_PRE_STAGE
+#define OMR_PRE_STAGE 1
 #endif
 
-template <int CAM>
-__global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
-{
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= a.P) return;
-    GeomState& g = a.g;
-    a.radii[idx] = 0;
-    g.tiles_touched[idx] = 0;
-    g.key_a[idx] = 0xFFFFFFFFu;  // culled Gaussians sort last and emit nothing
-    g.val_a[idx] = (uint32_t)idx;
+// What one Gaussian's preprocess produces (forward.cu:693-702); rec = the 64-B render record (raster_common.h)
+struct PreOut {
+    float4 rec[SPLAT_F4];
+    int rad;
+    uint32_t area;
+    uint8_t clamp_bits;
+    float depth;
+};
 
-    const float3 p_orig = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
+// One Gaussian, forward.cu:593-703 (lonlat) / :231-340 (pinhole). Returns false for a culled Gaussian (the caller
+// then writes radius 0, no tiles, the culled sort key). shv: the Gaussian's SH row in registers when sh16, else
+// the row is read from a.shs.
+template <int CAM>
+__device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, int idx, float3 p_orig, bool sh16,
+                                                 const float (&shv)[48], PreOut& o)
+{
     const float* v = a.viewmatrix;
-    // lonlat culls almost nothing (|t| <= 0.2 only), so the 192-B SH row is requested before the projection math
-    // and its latency overlaps it; pinhole frustum-culls most of a scene and loads rows only for survivors
-    constexpr bool kEarlySH = OMR_PRE_SH_EARLY && CAM == CAM_LONLAT;
-    const bool sh16 = a.colors_precomp == nullptr && a.M == 16 && (reinterpret_cast<uintptr_t>(a.shs) & 15u) == 0;
-    const int nf4 = (3 * (a.D + 1) * (a.D + 1) + 3) >> 2;
-    float4 shq[12];
-    if (kEarlySH && sh16) {
-        const float4* row4 = reinterpret_cast<const float4*>(a.shs + (size_t)idx * 48);
-#pragma unroll
-        for (int q = 0; q < 12; ++q) shq[q] = q < nf4 ? row4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
     const float3 t = transformPoint4x3(p_orig, v);
     float2 point_image;
     float depth;
@@ -114,7 +108,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     if constexpr (CAM == CAM_LONLAT) {
         // too_close (auxiliary.h:198-220)
         const float rr = t.x * t.x + t.y * t.y + t.z * t.z;
-        if (rr <= 0.04f) return;
+        if (rr <= 0.04f) return false;
         const float r = sqrtf(rr);
         // point3ToLonlatScreen (auxiliary.h:236-248)
         const float inv_r = 1.0f / (r + 0.0000001f);
@@ -141,7 +135,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
         // in_frustum (auxiliary.h:166-196)
         if (t.z <= 0.2f) {
             if (a.prefiltered) atomicOr(a.error_flag, 1);
-            return;
+            return false;
         }
         const float4 p_hom = transformPoint4x4(p_orig, a.projmatrix);
         const float p_w = 1.0f / (p_hom.w + 0.0000001f);
@@ -167,14 +161,16 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
 #pragma unroll
         for (int k = 0; k < 6; ++k) c3[k] = a.cov3D_precomp[6 * idx + k];
     } else {
-        const float4 q = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
+        float4 q;
+        if ((reinterpret_cast<uintptr_t>(a.rotations) & 15u) == 0) q = reinterpret_cast<const float4*>(a.rotations)[idx];
+        else q = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
         cov3d_from_scale_rot(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2], a.scale_modifier, q, c3);
     }
     const float3 cov = cov2d_from_J(v, J0, J1, c3);
 
     // conic and radius (forward.cu:660-674)
     const float det = (cov.x * cov.z - cov.y * cov.y);
-    if (det == 0.0f) return;
+    if (det == 0.0f) return false;
     const float det_inv = 1.f / det;
     const float3 conic = {cov.z * det_inv, -cov.y * det_inv, cov.x * det_inv};
     const float mid = 0.5f * (cov.x + cov.z);
@@ -185,7 +181,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     uint32_t x0, y0, x1, y1;
     getRect(point_image, rad, a.gx, a.gy, x0, y0, x1, y1);
     const uint32_t area = (y1 - y0) * (x1 - x0);
-    if (area == 0) return;
+    if (area == 0) return false;
 
     float rgb[3];
     uint8_t clamp_bits = 0;
@@ -196,38 +192,96 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
         dx = dx / len;
         dy = dy / len;
         dz = dz / len;
-        const float* row = a.shs + (size_t)idx * a.M * 3;
-        if (sh16) {
-            // the row as 16-B loads: 12 wide accesses per lane instead of 48 dword gathers 192 B apart
-            float shv[48];
-#pragma unroll
-            for (int q = 0; q < 12; ++q) {
-                const float4 v = kEarlySH ? shq[q]
-                                          : (q < nf4 ? reinterpret_cast<const float4*>(row)[q] : make_float4(0.f, 0.f, 0.f, 0.f));
-                shv[4 * q] = v.x;
-                shv[4 * q + 1] = v.y;
-                shv[4 * q + 2] = v.z;
-                shv[4 * q + 3] = v.w;
-            }
-            sh_to_rgb(a.D, dx, dy, dz, shv, rgb, clamp_bits);
-        } else {
-            sh_to_rgb(a.D, dx, dy, dz, row, rgb, clamp_bits);
-        }
+        if (sh16) sh_to_rgb(a.D, dx, dy, dz, shv, rgb, clamp_bits);
+        else sh_to_rgb(a.D, dx, dy, dz, a.shs + (size_t)idx * a.M * 3, rgb, clamp_bits);
     } else {
         rgb[0] = a.colors_precomp[3 * idx];
         rgb[1] = a.colors_precomp[3 * idx + 1];
         rgb[2] = a.colors_precomp[3 * idx + 2];
     }
-    float4* rec = g.splat + (size_t)idx * SPLAT_F4;
-    rec[0] = {point_image.x, point_image.y, depth, 0.0f};  // .w (slot base) is written by emit
-    rec[1] = {conic.x, conic.y, conic.z, a.opacities[idx]};
-    rec[2] = {rgb[0], rgb[1], rgb[2], __builtin_bit_cast(float, x1 - x0)};
-    rec[3] = {__builtin_bit_cast(float, x0), __builtin_bit_cast(float, y0), __builtin_bit_cast(float, x1),
-              __builtin_bit_cast(float, y1)};
-    g.clamped[idx] = clamp_bits;
-    a.radii[idx] = rad;
-    g.tiles_touched[idx] = area;
-    g.key_a[idx] = __float_as_uint(depth);
+    o.rec[0] = {point_image.x, point_image.y, depth, 0.0f};  // .w (slot base) is written by emit
+    o.rec[1] = {conic.x, conic.y, conic.z, a.opacities[idx]};
+    o.rec[2] = {rgb[0], rgb[1], rgb[2], __builtin_bit_cast(float, x1 - x0)};
+    o.rec[3] = {__builtin_bit_cast(float, x0), __builtin_bit_cast(float, y0), __builtin_bit_cast(float, x1),
+                __builtin_bit_cast(float, y1)};
+    o.rad = rad;
+    o.area = area;
+    o.clamp_bits = clamp_bits;
+    o.depth = depth;
+    return true;
+}
+
+// One wave per 64 consecutive Gaussians. With OMR_PRE_STAGE the wave reads its 64 SH rows (12 KiB) and writes its
+// 64 render records (4 KiB) as contiguous spans through LDS (wave_rows.h). The SH rows are requested before the
+// projection math so their latency overlaps it; pinhole views, which frustum-cull most of a scene, request only
+// the rows of points in front of the camera.
+template <int CAM>
+__global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
+{
+    constexpr int SH_F4 = 12;  // 16 coefficients x 3 channels
+    __shared__ float4 s_stage[4][stage_f4<SH_F4>()];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const int wave_first = (int)(blockIdx.x * 256u + wv * 64u);
+    if (wave_first >= a.P) return;  // wave-uniform
+    const int idx = wave_first + (int)lane;
+    const bool valid = idx < a.P;
+    float4* stage = s_stage[wv];
+    GeomState& g = a.g;
+
+    const float3 p_orig = valid ? make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2])
+                                : make_float3(0.f, 0.f, 0.f);
+    const bool sh16 = a.colors_precomp == nullptr && a.M == 16 && (reinterpret_cast<uintptr_t>(a.shs) & 15u) == 0;
+    const int nf4 = (3 * (a.D + 1) * (a.D + 1) + 3) >> 2;
+    float shv[48];
+    if (sh16) {
+        float4 shq[SH_F4];
+        if (OMR_PRE_STAGE) {
+            const bool want = CAM == CAM_LONLAT ? valid : valid && transformPoint4x3(p_orig, a.viewmatrix).z > 0.2f;
+            const uint64_t rows = __ballot(want);
+            wave_rows_load<SH_F4>(reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4, rows, nf4,
+                                  stage, lane);
+            wave_sync();
+#pragma unroll
+            for (int q = 0; q < SH_F4; ++q)
+                shq[q] = q < nf4 ? stage[lane * stage_stride<SH_F4>() + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            wave_sync();  // the image is reused for the records below
+        } else {
+            const float4* row4 = reinterpret_cast<const float4*>(a.shs + (size_t)idx * 48);
+#pragma unroll
+            for (int q = 0; q < SH_F4; ++q) shq[q] = valid && q < nf4 ? row4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int q = 0; q < SH_F4; ++q) {
+            shv[4 * q] = shq[q].x;
+            shv[4 * q + 1] = shq[q].y;
+            shv[4 * q + 2] = shq[q].z;
+            shv[4 * q + 3] = shq[q].w;
+        }
+    }
+
+    PreOut o;
+    const bool vis = valid && preprocess_point<CAM>(a, idx, p_orig, sh16, shv, o);
+    if (valid) {
+        a.radii[idx] = vis ? o.rad : 0;
+        g.tiles_touched[idx] = vis ? o.area : 0u;
+        g.key_a[idx] = vis ? __float_as_uint(o.depth) : 0xFFFFFFFFu;  // culled Gaussians sort last, emit nothing
+        g.val_a[idx] = (uint32_t)idx;
+        if (vis) g.clamped[idx] = o.clamp_bits;
+    }
+    // the render record of a visible Gaussian (culled records are never read)
+    if (OMR_PRE_STAGE) {
+        const uint64_t rows = __ballot(vis);
+        if (vis) {
+#pragma unroll
+            for (int j = 0; j < SPLAT_F4; ++j) stage[lane * stage_stride<SPLAT_F4>() + j] = o.rec[j];
+        }
+        wave_sync();
+        wave_rows_store<SPLAT_F4>(g.splat + (size_t)wave_first * SPLAT_F4, rows, stage, lane);
+    } else if (vis) {
+        float4* rec = g.splat + (size_t)idx * SPLAT_F4;
+#pragma unroll
+        for (int j = 0; j < SPLAT_F4; ++j) rec[j] = o.rec[j];
+    }
 }
 
 __global__ void mark_frustum_kernel(int P, const float* means3D, const float* viewmatrix, bool* present)
