@@ -63,14 +63,16 @@ def stage_bytes(stage, P, V, L, N, T, M=16, D=3):
     return {
         "preprocess": 28 * P + (40 + sh + 45) * V,
         "depth_sort": 4 * 2 * 8 * P,               # 4 passes x (key+value read + write)
-        "scan": 8 * P,
+        "scan": 16 * P,                            # tiles_touched read in depth and index order; two scans written
         "emit": 8 * P + 12 * V + 8 * L,
         "tile_sort": 2 * 2 * 8 * L,                # 2 passes x (tile id + index, read + write)
         "tile_ranges": 4 * L + 16 * T,
         "render_forward": 40 * L + 20 * N + 8 * T,
         "render_backward": 40 * L + 20 * N + 8 * T + 88 * V,
-        "instance_reduce": 8 * P + 36 * L + 36 * V,
-        # reads radii 4P + (grad sums 36, xyz 12, scale 12, rot 16, SH, clamped 1) per visible Gaussian;
+        # tiles_touched + row_first + row_valid bytes + one 36-B sum row written per Gaussian; the marked 36-B
+        # instance rows it reads depend on the scene and are not counted
+        "row_sums": 8 * P + L + 36 * P,
+        # reads radii 4P + (row sums 36, xyz 12, scale 12, rot 16, SH, clamped 1) per visible Gaussian;
         # writes every gradient output: 3+3+1+3+6+3*M(coeffs)+3+4 floats per Gaussian
         "gaussian_backward": 4 * P + (36 + 12 + 12 + 16 + sh + 1) * V + (92 + 12 * M) * P,
     }.get(stage, 0)

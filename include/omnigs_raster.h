@@ -194,7 +194,7 @@ size_t omr_binning_bytes(int num_rendered, int width, int height);
 
 /* --- stage timing (HIP events recorded on the launch stream; for bench.py / tools) --------------- */
 /* stages: 0 preprocess, 1 depth_sort, 2 scan, 3 emit, 4 tile_sort, 5 tile_ranges, 6 render_forward,
- *         7 render_backward, 8 gaussian_backward, 9 instance_reduce                                */
+ *         7 render_backward, 8 gaussian_backward, 9 row_sums                                       */
 #define OMR_NUM_STAGES 10
 void omr_profile_enable(int on);
 /* restrict recording to the stages whose bit (1 << stage) is set (default: all); each recorded stage costs a

@@ -69,9 +69,9 @@ int hip_check(const char* where)
 
 // ---- stage profiler: hipEvent pairs on the launch stream, resolved lazily by omr_profile_read -------------
 enum Stage { ST_PREPROCESS, ST_DEPTH_SORT, ST_SCAN, ST_EMIT, ST_TILE_SORT, ST_RANGES, ST_RENDER_FWD, ST_RENDER_BWD,
-             ST_GAUSS_BWD, ST_INSTANCE_REDUCE, ST_COUNT };
+             ST_GAUSS_BWD, ST_ROW_SUMS, ST_COUNT };
 const char* kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "scan", "emit", "tile_sort", "tile_ranges",
-                                     "render_forward", "render_backward", "gaussian_backward", "instance_reduce"};
+                                     "render_forward", "render_backward", "gaussian_backward", "row_sums"};
 
 struct Profiler {
     bool on = false;
@@ -169,11 +169,12 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s)
     g.val_b = c.take<uint32_t>(P);
     const size_t nh = radix_hist_size(P);
     g.hist = c.take<uint32_t>(nh);
-    g.scan_partials = c.take<uint32_t>(std::max(scan_partials_size(P), scan_partials_size(nh)));
+    g.scan_partials = c.take<uint32_t>(std::max(scan2_partials_size(P), scan_partials_size(nh)));
     g.offsets = c.take<uint32_t>(P);
     g.counters = c.take<uint32_t>(4);
+    g.row_first = c.take<uint32_t>(P);
+    g.row_sums = c.take<float>(P * GRAD_ROW);
     g.internal_radii = c.take<int>(P);
-    g.grad_sum = c.take<float>(P * GRAD_ROW);
     g.order = g.val_a;  // the depth sort runs DEPTH_SORT_PASSES (even) passes, so its result lands in val_a
     if (s) *s = g;
     return c.size();
@@ -307,7 +308,7 @@ int forward_impl(const ForwardIn& in)
     // depth order of the Gaussians (stable: ties keep index order)
     int which; { StageScope st_(ST_DEPTH_SORT, s); which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr, nullptr, 0, 4, s); }
     g.order = which ? g.val_b : g.val_a;
-    { StageScope st_(ST_SCAN, s); launch_inclusive_scan(g.tiles_touched, g.order, g.offsets, g.scan_partials, P, s); }
+    { StageScope st_(ST_SCAN, s); launch_forward_scans(g.tiles_touched, g.order, g.offsets, g.row_first, g.scan_partials, P, s); }
 
     // num_rendered = offsets[P-1] (+ the prefiltered error flag) to pinned host memory, without waiting for it:
     // the binning buffer is sized from a capacity hint and everything after the scan reads the count on the device,
@@ -425,6 +426,7 @@ int backward_impl(const BackwardIn& in)
     RenderBwdArgs rb;
     rb.W = in.width; rb.H = in.height; rb.gx = d.gx; rb.gy = d.gy;
     rb.ranges = im.ranges; rb.tile_order = im.tile_order; rb.point_list = b.point_list; rb.splat = g.splat; rb.bg = in.background;
+    rb.row_first = g.row_first;
     rb.final_T = im.final_T; rb.n_contrib = im.n_contrib; rb.dL_dpix = in.dL_dpix; rb.inst_grad = b.inst_grad;
     rb.row_valid = b.row_valid;
     if (in.R > 0) OMR_HIP(hipMemsetAsync(b.row_valid, 0, (size_t)in.R, s));
@@ -441,13 +443,9 @@ int backward_impl(const BackwardIn& in)
     ga.projmatrix = in.projmatrix; ga.campos = in.campos; ga.tan_fovx = in.tan_fovx; ga.tan_fovy = in.tan_fovy;
     ga.focal_y = (float)in.height / (2.0f * in.tan_fovy);
     ga.focal_x = (float)in.width / (2.0f * in.tan_fovx);
-    ga.clamped = g.clamped; ga.grad_sum = g.grad_sum;
-    ga.splat = g.splat; ga.tiles_touched = g.tiles_touched; ga.inst_grad = b.inst_grad; ga.row_valid = b.row_valid;
-    ga.R = (uint32_t)in.R;
-    if (!gaussian_bwd_fused_reduce()) {  // otherwise gaussian_bwd sums each Gaussian's rows itself
-        StageScope st_(ST_INSTANCE_REDUCE, s);
-        launch_instance_reduce(in.P, g.order, g.offsets, b.inst_grad, b.row_valid, g.grad_sum, s);
-    }
+    ga.clamped = g.clamped;
+    ga.row_sums = g.row_sums;
+    { StageScope st_(ST_ROW_SUMS, s); launch_row_sums(in.P, g.row_first, g.tiles_touched, b.inst_grad, b.row_valid, (uint32_t)in.R, g.row_sums, s); }
     ga.dL_dmean2D = in.dL_dmean2D; ga.dL_dconic = in.dL_dconic; ga.dL_dopacity = in.dL_dopacity; ga.dL_dcolor = in.dL_dcolor;
     ga.dL_dmean3D = in.dL_dmean3D; ga.dL_dcov3D = in.dL_dcov3D; ga.dL_dsh = in.M > 0 ? in.dL_dsh : nullptr;
     ga.dL_dscale = in.dL_dscale; ga.dL_drot = in.dL_drot; ga.dpx_dt = in.dpx_dt; ga.dpy_dt = in.dpy_dt;

@@ -215,93 +215,126 @@ __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const
     return r;
 }
 
-// Segmented sum of the per-instance rows. Gaussian order[r] (depth rank r) owns the contiguous emission slots
-// [offsets[r-1], offsets[r]); lane r of the grid sums the rows of rank r.
-//  * Only rows marked in row_valid are read (render_bwd.hip writes no row where no pixel took a contribution).
-//  * Short segments (<= RED_SHORT rows, ~95 % of the Gaussians, median 4 rows at config C): the lane adds its rows
-//    in order straight from global memory. The 64 lanes of a wave own consecutive ranks, hence one contiguous
-//    span of rows, so the loads stay within a few KB that L1/L2 serve after the first touch.
-//  * Long segments (polar Gaussians span up to every tile of the image): the whole wave takes them one at a
-//    time, 64 rows per step (one per lane, coalesced), and reduces the 9 sums over the wave (wave_ops.h).
-// Fixed order everywhere, so the sums are deterministic. Culled Gaussians own no rows and are not written (never
-// read downstream).
-constexpr int RED_THREADS = 256;
-#ifndef OMR_RED_SHORT
-#define OMR_RED_SHORT 32
+// ---- per-Gaussian sums of the instance rows (the reference's atomicAdd targets, backward.cu:805-840) ---------
+// Gaussian i owns the contiguous rows [row_first[i], row_first[i] + tiles_touched[i]) of inst_grad: the backward
+// numbers the rows in Gaussian INDEX order (launch_forward_scans), so the 64 Gaussians of a wave own one contiguous
+// span of rows (507 rows on average at config C, 24 % of them marked valid by render_bwd).
+// The wave streams its span through LDS in chunks of RS_ROWS rows: every lane loads 4 rows of the chunk, rows
+// q*64 + lane (coalesced), marked ones only, then
+//  * a Gaussian with at most RS_LONG rows adds its rows of the chunk itself, in row order, from LDS;
+//  * a longer one (polar Gaussians reach every tile of the image) is summed by the whole wave: each lane adds the
+//    chunk rows it holds, then one wave reduction (wave_ops.h) per (long Gaussian, chunk), in chunk order.
+// Two HBM round trips per chunk (row_valid bytes, then the rows) for the whole wave, instead of two per 4 rows
+// of its slowest lane. The order of every sum is fixed: the result is deterministic.
+constexpr int RS_ROWS = 256;
+#ifndef OMR_RS_LONG
+#define OMR_RS_LONG 32
 #endif
-constexpr uint32_t RED_SHORT = OMR_RED_SHORT;
+constexpr uint32_t RS_LONG = OMR_RS_LONG;
 
-__device__ __forceinline__ void add_row(float* acc, const float* inst_grad, const uint8_t* row_valid, uint32_t row)
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
 {
-    if (!row_valid[row]) return;  // no pixel of that tile took a contribution
-    const float* p = inst_grad + (size_t)row * GRAD_ROW;
 #pragma unroll
-    for (int c = 0; c < GRAD_ROW; ++c) acc[c] += p[c];
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return v;
+}
+
+__global__ __launch_bounds__(256) void row_sum_kernel(int P, const uint32_t* __restrict__ row_first,
+                                                      const uint32_t* __restrict__ tiles_touched,
+                                                      const float* __restrict__ inst_grad,
+                                                      const uint8_t* __restrict__ row_valid, uint32_t R,
+                                                      float* __restrict__ row_sums)
+{
+    __shared__ float s_rows_all[4][RS_ROWS * GRAD_ROW];  // row-major, 9 floats per row (odd stride: no conflicts)
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const int g0 = (int)(blockIdx.x * 256u + wv * 64u);
+    if (g0 >= P) return;  // wave-uniform
+    float* s_rows = s_rows_all[wv];
+    const int idx = g0 + (int)lane;
+    uint32_t n = 0, s = 0;
+    if (idx < P) {
+        n = tiles_touched[idx];
+        s = row_first[idx];
+        if (n != 0 && (s >= R || n > R - s)) n = 0;  // never true for a consistent forward; keeps reads inside R rows
+    }
+    const uint32_t e = s + n;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(wave_min_u32(n ? s : 0xFFFFFFFFu));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(wave_max_u32(n ? e : 0u));
+    const bool is_long = n > RS_LONG;
+    float acc[GRAD_ROW];
+#pragma unroll
+    for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
+
+    for (uint32_t c0 = lo; c0 < hi; c0 += RS_ROWS) {  // lo > hi when the wave owns no rows
+        // stage the chunk: row c0 + q*64 + lane at s_rows[(q*64 + lane) * 9], zeros where not marked / past hi
+        bool ok[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t r = c0 + (uint32_t)q * 64u + lane;
+            ok[q] = r < hi && row_valid[r] != 0;
+        }
+        float x[4][GRAD_ROW];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float* p = inst_grad + (size_t)(c0 + (uint32_t)q * 64u + lane) * GRAD_ROW;
+#pragma unroll
+            for (int c = 0; c < GRAD_ROW; ++c) x[q][c] = 0.f;
+            if (ok[q]) {
+#pragma unroll
+                for (int c = 0; c < GRAD_ROW; ++c) x[q][c] = p[c];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int c = 0; c < GRAD_ROW; ++c) s_rows[(q * 64 + lane) * GRAD_ROW + c] = x[q][c];
+        wave_sync();
+        const uint32_t c1 = c0 + RS_ROWS;
+        // short segments: the owner adds its rows of this chunk in order
+        if (n != 0 && !is_long && s < c1 && e > c0) {
+            const uint32_t j1 = min(e, c1) - c0;
+            for (uint32_t j = max(s, c0) - c0; j < j1; ++j)
+#pragma unroll
+                for (int c = 0; c < GRAD_ROW; ++c) acc[c] += s_rows[j * GRAD_ROW + c];
+        }
+        // long segments overlapping this chunk: the whole wave, one Gaussian at a time
+        uint64_t longs = __ballot(is_long && s < c1 && e > c0);
+        while (longs) {
+            const int jl = __builtin_ctzll(longs);
+            longs &= longs - 1;
+            const uint32_t sj = max(__builtin_amdgcn_readlane(s, jl), c0) - c0;
+            const uint32_t ej = min(__builtin_amdgcn_readlane(e, jl), c1) - c0;
+            float v[GRAD_ROW];
+#pragma unroll
+            for (int c = 0; c < GRAD_ROW; ++c) v[c] = 0.f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t pos = (uint32_t)q * 64u + lane;
+                if (pos >= sj && pos < ej)
+#pragma unroll
+                    for (int c = 0; c < GRAD_ROW; ++c) v[c] += x[q][c];
+            }
+            float t8;
+            const float tv = wave_sum9_rows(v, v[8], lane, &t8);  // lane l: total of value (l >> 3) & 7
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const float tc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tv), 8 * c));
+                if ((int)lane == jl) acc[c] += tc;
+            }
+            if ((int)lane == jl) acc[8] += t8;
+        }
+        wave_sync();  // the next chunk overwrites the staging rows
+    }
+    if (idx < P) {
+        float* out = row_sums + (size_t)idx * GRAD_ROW;
+#pragma unroll
+        for (int c = 0; c < GRAD_ROW; ++c) out[c] = acc[c];
+    }
 }
 
 #ifndef OMR_GBWD_MINW
 #define OMR_GBWD_MINW 1
 #endif
-#ifndef OMR_FUSED_REDUCE
-#define OMR_FUSED_REDUCE 1
-#endif
-
-// Sum of Gaussian idx's instance rows into g, with the arithmetic of instance_reduce_kernel (so the result is the
-// same to the bit): short segments lane by lane, 4 rows in flight; long ones by the whole wave, one at a time.
-// Every lane of the wave must call it (the long segments are summed cooperatively).
-__device__ __forceinline__ void own_row_sum(const GaussBwdArgs& a, int idx, float* g)
-{
-    const uint32_t lane = threadIdx.x & 63;
-    uint32_t s = 0, n = 0;
-    if (idx < a.P && a.radii[idx] > 0) {
-        n = a.tiles_touched[idx];
-        // first emission slot = the slot of the rect's first tile (x0, y0) (raster_common.h: splat_slot)
-        const float4* rec = a.splat + (size_t)idx * SPLAT_F4;
-        const float4 rect = rec[3];
-        s = splat_slot(rec[0], rec[2], __builtin_bit_cast(uint32_t, rect.x), __builtin_bit_cast(uint32_t, rect.y));
-        if (s >= a.R || n > a.R - s) n = 0;  // never true for a consistent forward; keeps reads inside the rows
-    }
-#pragma unroll
-    for (int c = 0; c < GRAD_ROW; ++c) g[c] = 0.f;
-    if (n != 0 && n <= RED_SHORT) {
-        uint32_t k = 0;
-        for (; k + 4 <= n; k += 4) {
-            bool ok[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) ok[i] = a.row_valid[s + k + i] != 0;
-            float x[4][GRAD_ROW];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int c = 0; c < GRAD_ROW; ++c) x[i][c] = ok[i] ? a.inst_grad[(size_t)(s + k + i) * GRAD_ROW + c] : 0.f;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int c = 0; c < GRAD_ROW; ++c) g[c] += x[i][c];
-        }
-        for (; k < n; ++k) add_row(g, a.inst_grad, a.row_valid, s + k);
-    }
-    uint64_t longs = __ballot(n > RED_SHORT);
-    while (longs) {
-        const int j = __builtin_ctzll(longs);
-        longs &= longs - 1;
-        const uint32_t sj = __builtin_amdgcn_readlane(s, j), ej = sj + __builtin_amdgcn_readlane(n, j);
-        float acc[GRAD_ROW];
-#pragma unroll
-        for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
-        for (uint32_t row = sj + lane; row < ej; row += 64) add_row(acc, a.inst_grad, a.row_valid, row);
-        float t8;
-        const float tv = wave_sum8_transposed(acc, acc[8], lane, &t8);
-        // value c < 8 sits in lane bitrev3(c) (transposed_slot_of_lane is its own inverse)
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const float v = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tv),
-                                                                                transposed_slot_of_lane(c)));
-            if ((int)lane == j) g[c] = v;
-        }
-        if ((int)lane == j) g[8] = t8;
-    }
-}
 
 #ifndef OMR_GBWD_STAGE
 #define OMR_GBWD_STAGE 1
@@ -314,10 +347,6 @@ __device__ __forceinline__ void gaussian_bwd_point(const GaussBwdArgs& a, int id
 {
     const int Mr = MC > 0 ? MC : a.M;
     // 1. this Gaussian's summed instance rows
-#if !OMR_FUSED_REDUCE
-#pragma unroll
-    for (int c = 0; c < GRAD_ROW; ++c) g[c] = a.grad_sum[(size_t)idx * GRAD_ROW + c];
-#endif
     a.dL_dmean2D[3 * idx + 0] = g[0];
     a.dL_dmean2D[3 * idx + 1] = g[1];
     a.dL_dmean2D[3 * idx + 2] = 0.f;
@@ -532,9 +561,10 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
     if (wave_first >= a.P) return;  // wave-uniform
     const int idx = wave_first + (int)lane;
     float g[GRAD_ROW];
-#if OMR_FUSED_REDUCE
-    own_row_sum(a, idx, g);  // before any lane leaves: long segments take the whole wave
-#endif
+    if (idx < a.P) {
+#pragma unroll
+        for (int c = 0; c < GRAD_ROW; ++c) g[c] = a.row_sums[(size_t)idx * GRAD_ROW + c];
+    }
     const bool valid = idx < a.P;
     const bool vis = valid && a.radii[idx] > 0;
     float4* stage = s_stage[wv];
@@ -556,60 +586,6 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
             wave_sync();
             wave_rows_store<SH_F4>(reinterpret_cast<float4*>(a.dL_dsh) + (size_t)wave_first * SH_F4, __ballot(valid),
                                    stage, lane);
-        }
-    }
-}
-
-__global__ __launch_bounds__(RED_THREADS) void instance_reduce_kernel(int P, const uint32_t* order,
-                                                                      const uint32_t* offsets, const float* inst_grad,
-                                                                      const uint8_t* row_valid, float* grad_sum)
-{
-    const int r = blockIdx.x * RED_THREADS + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63;
-    const bool valid = r < P;
-    const uint32_t s = (r == 0 || !valid) ? 0u : offsets[r - 1];
-    const uint32_t e = valid ? offsets[r] : s;
-    const uint32_t n = e - s;
-    if (n != 0 && n <= RED_SHORT) {
-        float acc[GRAD_ROW];
-#pragma unroll
-        for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
-        // 4 rows in flight per step (each read only where marked), then the remainder
-        uint32_t k = 0;
-        for (; k + 4 <= n; k += 4) {
-            bool ok[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) ok[i] = row_valid[s + k + i] != 0;
-            float x[4][GRAD_ROW];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int c = 0; c < GRAD_ROW; ++c) x[i][c] = ok[i] ? inst_grad[(size_t)(s + k + i) * GRAD_ROW + c] : 0.f;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int c = 0; c < GRAD_ROW; ++c) acc[c] += x[i][c];
-        }
-        for (; k < n; ++k) add_row(acc, inst_grad, row_valid, s + k);
-        float* out = grad_sum + (size_t)order[r] * GRAD_ROW;
-#pragma unroll
-        for (int c = 0; c < GRAD_ROW; ++c) out[c] = acc[c];
-    }
-    uint64_t longs = __ballot(n > RED_SHORT);
-    const uint32_t slot_of_lane = transposed_slot_of_lane(lane);
-    while (longs) {
-        const int j = __builtin_ctzll(longs);
-        longs &= longs - 1;
-        const uint32_t sj = __builtin_amdgcn_readlane(s, j), ej = __builtin_amdgcn_readlane(e, j);
-        float acc[GRAD_ROW];
-#pragma unroll
-        for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
-        for (uint32_t row = sj + lane; row < ej; row += 64) add_row(acc, inst_grad, row_valid, row);
-        float t8;
-        const float tv = wave_sum8_transposed(acc, acc[8], lane, &t8);
-        if (lane < GRAD_ROW) {
-            const uint32_t rj = (uint32_t)(r - (int)lane) + (uint32_t)j;
-            grad_sum[(size_t)order[rj] * GRAD_ROW + slot_of_lane] = lane < 8 ? tv : t8;
         }
     }
 }
@@ -687,8 +663,6 @@ __global__ __launch_bounds__(256) void sh_grad_from_colors_kernel(int P, int D, 
 
 }  // namespace
 
-bool gaussian_bwd_fused_reduce() { return OMR_FUSED_REDUCE != 0; }
-
 void launch_sh_grad_from_colors(int P, int D, int M, int nviews, const float* means3D, const float* shs,
                                 const float* campos, const float* dL_dcolors, float* dL_dsh, hipStream_t s)
 {
@@ -700,12 +674,11 @@ void launch_sh_grad_from_colors(int P, int D, int M, int nviews, const float* me
     else sh_grad_from_colors_kernel<0><<<grid, 256, 0, s>>>(P, D, M, nviews, means3D, shs, campos, dL_dcolors, dL_dsh);
 }
 
-void launch_instance_reduce(int P, const uint32_t* order, const uint32_t* offsets, const float* inst_grad,
-                            const uint8_t* row_valid, float* grad_sum, hipStream_t s)
+void launch_row_sums(int P, const uint32_t* row_first, const uint32_t* tiles_touched, const float* inst_grad,
+                     const uint8_t* row_valid, uint32_t R, float* row_sums, hipStream_t s)
 {
     if (P <= 0) return;
-    instance_reduce_kernel<<<div_up(P, RED_THREADS), RED_THREADS, 0, s>>>(P, order, offsets, inst_grad, row_valid,
-                                                                          grad_sum);
+    row_sum_kernel<<<div_up(P, 256), 256, 0, s>>>(P, row_first, tiles_touched, inst_grad, row_valid, R, row_sums);
 }
 
 void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s)

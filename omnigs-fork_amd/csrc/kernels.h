@@ -34,10 +34,14 @@ void launch_mark_visible(int camera_type, int P, const float* means3D, const flo
                          bool* present, hipStream_t s);
 
 // sort.hip
-// inclusive scan of in[gather ? gather[i] : i] into out (u32, n items); partials needs scan_partials_size(n)
+// scan block-sum scratch for n items (words)
 size_t scan_partials_size(size_t n);
-void launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, uint32_t* partials, size_t n, hipStream_t s);
 size_t radix_hist_size(size_t n);
+// the forward's scans of tiles_touched (sort.hip): offsets = inclusive scan in depth order (gather by order),
+// row_first = exclusive scan in index order (gradient row numbering); partials: scan2_partials_size(n) words
+size_t scan2_partials_size(size_t n);
+void launch_forward_scans(const uint32_t* tiles_touched, const uint32_t* order, uint32_t* offsets, uint32_t* row_first,
+                          uint32_t* partials, size_t n, hipStream_t s);
 // stable LSD radix sort of (key, value) over bits [0, 8*passes); returns which buffer holds the result (0: a, 1: b).
 // n = capacity; count (device, may be NULL) = live element count <= n. canon != NULL: the last pass writes the
 // values to the canonical point list of the binning buffer at canon (raster_common.h) instead of val_a / val_b.
@@ -79,6 +83,7 @@ struct RenderBwdArgs {
     const uint32_t* tile_order;  // [T] schedule (launch_tile_order)
     const uint32_t* point_list;
     const float4* splat;  // [P][SPLAT_F4] render records
+    const uint32_t* row_first;  // [P] first gradient row of each Gaussian (index-order scan, launch_forward_scans)
     const float* bg;
     const float* final_T;
     const uint32_t* n_contrib;
@@ -106,14 +111,7 @@ struct GaussBwdArgs {
     const float* campos;
     float tan_fovx, tan_fovy, focal_x, focal_y;
     const uint8_t* clamped;
-    const float* grad_sum;  // [P][GRAD_ROW] per-Gaussian sums of the instance rows (instance_reduce; unfused build)
-    // fused row sums (gaussian_bwd.hip, OMR_FUSED_REDUCE): each Gaussian's rows are the emission slots
-    // [first, first + tiles_touched) of the canonical binning layout, first = splat_slot(rect x0, y0)
-    const float4* splat;          // render records
-    const uint32_t* tiles_touched;
-    const float* inst_grad;       // [R][GRAD_ROW]
-    const uint8_t* row_valid;     // [R]
-    uint32_t R;                   // rows (num_rendered)
+    const float* row_sums;  // [P][GRAD_ROW] each Gaussian's instance rows summed (launch_row_sums)
     float* dL_dmean2D;   // [P,3]
     float* dL_dconic;    // [P,4] optional (may be null)
     float* dL_dopacity;  // [P]
@@ -127,15 +125,13 @@ struct GaussBwdArgs {
     float* dpy_dt;       // [P,3] optional
 };
 void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s);
-// true when gaussian_bwd sums the instance rows itself (OMR_FUSED_REDUCE) and instance_reduce is not launched
-bool gaussian_bwd_fused_reduce();
+// Per-Gaussian sums of the render backward's instance rows: Gaussian i owns rows [row_first[i], row_first[i] +
+// tiles_touched[i]) of inst_grad (index-order numbering, launch_forward_scans); only rows marked in row_valid are read.
+void launch_row_sums(int P, const uint32_t* row_first, const uint32_t* tiles_touched, const float* inst_grad,
+                     const uint8_t* row_valid, uint32_t R, float* row_sums, hipStream_t s);
 // view-parallel DP: dL_dsh[P,M,3] = sum over views of dL/dsh rebuilt from dL_dcolors [nviews][P][3] + campos [nviews][3]
 void launch_sh_grad_from_colors(int P, int D, int M, int nviews, const float* means3D, const float* shs,
                                 const float* campos, const float* dL_dcolors, float* dL_dsh, hipStream_t s);
-// sums each Gaussian's instance rows (slots [offsets[r-1], offsets[r]) of depth rank r) into grad_sum[order[r]]
-void launch_instance_reduce(int P, const uint32_t* order, const uint32_t* offsets, const float* inst_grad,
-                            const uint8_t* row_valid,
-                            float* grad_sum, hipStream_t s);
 
 // ssim.hip: fused L1 + SSIM loss (loss_utils.h:31-129), forward and backward
 struct SsimWindow {

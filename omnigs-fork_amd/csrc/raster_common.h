@@ -58,16 +58,11 @@ struct Carver {
 // indices. Keeping everything an instance needs in ONE 64-B aligned record makes that one random 64-B line
 // instead of five (means2D, conic_opacity, rgb, radii, emit offset in separate arrays: measured 2.8 GB of
 // traffic per render backward at config C against 0.45 GB of algorithmic bytes).
-//   [0] pos   = {x, y, depth, slot_base}   means2D (forward.cu:699), depth (:697 / :334); slot_base (u32 bits,
-//                                          written by emit) = first emission slot - (y0 * w + x0), mod 2^32
+//   [0] pos   = {x, y, depth, -}           means2D (forward.cu:699), depth (:697 / :334)
 //   [1] conic = {a, b, c, opacity}         conic_opacity (forward.cu:701)
 //   [2] rgb   = {r, g, b, w}               colour (SH or colors_precomp); w = rect width in tiles (u32 bits)
 //   [3] rect  = {x0, y0, x1, y1}           getRect (u32 bits), read by emit
 constexpr int SPLAT_F4 = 4;
-__host__ __device__ inline uint32_t splat_slot(float4 pos, float4 rgb, uint32_t tx, uint32_t ty)
-{
-    return __builtin_bit_cast(uint32_t, pos.w) + ty * __builtin_bit_cast(uint32_t, rgb.w) + tx;
-}
 
 // ---- geometry state: P Gaussians --------------------------------------------------------------------------
 struct GeomState {
@@ -83,8 +78,9 @@ struct GeomState {
     uint32_t* offsets;        // inclusive scan of tiles_touched in depth order
     uint32_t* counters;       // [0] = num_rendered
     uint32_t* order;          // depth order (points at val_a or val_b after the sort)
+    uint32_t* row_first;      // first gradient row of each Gaussian (index-order exclusive scan, launch_forward_scans)
+    float* row_sums;          // backward: [P][GRAD_ROW] each Gaussian's instance rows summed (launch_row_sums)
     int* internal_radii;      // used when the caller passes radii == NULL (rasterizer_impl.cu:284-287)
-    float* grad_sum;          // [P][GRAD_ROW] backward: per-Gaussian sums of its instance rows
 
     static size_t carve(char* base, size_t P, GeomState* s);
 };
@@ -103,14 +99,14 @@ struct ImageState {
 // The forward sizes this buffer BEFORE it knows L (capacity `cap` >= L from a hint, see capi.hip) so that it never
 // waits for the host; the backward only learns R = L. So the two arrays the backward reads sit at offsets that
 // depend on L alone: inst_grad at 0 and the sorted point list right after R rows of it (canonical_list_offset).
-// In the forward, the region [0, align(cap * 36) + align(cap * 4)) is reserved for them; the final tile-sort pass
+// In the forward, the region [0, align(cap * 4 * GRAD_ROW) + align(cap * 4)) is reserved for them; the final tile-sort pass
 // writes the point list to base + canonical_list_offset(L) with L read on the device.
 __host__ __device__ inline size_t canonical_list_offset(size_t L)
 {
     return (L * GRAD_ROW * sizeof(float) + ALIGN - 1) & ~(ALIGN - 1);
 }
 struct BinningState {
-    float* inst_grad;      // [L][GRAD_ROW] backward scratch, indexed by emission slot (offset 0)
+    float* inst_grad;      // [L][GRAD_ROW] backward scratch, indexed by gradient row slot (offset 0)
     uint32_t* point_list;  // sorted Gaussian indices at base + canonical_list_offset(L) (host-known only when L is)
     uint32_t* key_a;       // tile id ping-pong
     uint32_t* key_b;

@@ -11,8 +11,8 @@
 // The per-Gaussian constants of the reference's expressions (conic, opacity, 0.5 W, 0.5 H, -1/2) are linear
 // factors, so they are applied once per instance to the lane's sums — not once per pixel — and the nine values
 // are then summed over the wave in registers (DPP transposed butterfly + v_permlane{16,32}_swap, wave_ops.h).
-// Lanes 0..8 store the instance's 36-B gradient row, indexed by its emission slot, with plain stores, and lane 0
-// marks the slot in row_valid (zeroed before the launch); an instance no pixel takes a contribution from writes
+// Lanes 0..8 store the instance's 36-B gradient row, indexed by its row slot (Gaussian-index-major: row_first), with
+// plain stores, and lane 0 marks the slot in row_valid (zeroed before the launch); an instance no pixel takes a contribution from writes
 // nothing — at dense configs most instances lie behind every pixel's last contributor. gaussian_bwd.hip sums each
 // Gaussian's marked rows in a fixed order. No atomics: gradients are bitwise reproducible.
 //
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
     OMR_STAMP_BEGIN
     __shared__ float4 s_geo_all[TW_WAVES][TW_BATCH];   // x, y, position in range (u32 bits), band mask (u32 bits)
     __shared__ float4 s_quad_all[TW_WAVES][TW_BATCH];  // qa, qb, qc, opacity
-    __shared__ float4 s_rgb_all[TW_WAVES][TW_BATCH];   // colour, emission slot (u32 bits)
+    __shared__ float4 s_rgb_all[TW_WAVES][TW_BATCH];   // colour, gradient row slot (u32 bits)
 #if OMR_BWD_PIX_LDS
     __shared__ float4 s_pix_all[TW_WAVES][TW_BANDS][64];  // dL/dpix rgb, last contributor (u32 bits)
 #endif
@@ -136,11 +136,16 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
         uint32_t pos = 0, slot = 0;
         if ((int)lane < cnt) {
             pos = (uint32_t)(hi - 1 - (int)lane);
-            const float4* rec = a.splat + (size_t)a.point_list[range.x + pos] * SPLAT_F4;  // one 64-B line
+            const uint32_t gid = a.point_list[range.x + pos];
+            const float4* rec = a.splat + (size_t)gid * SPLAT_F4;  // one 64-B line
+            const uint32_t first = a.row_first[gid];
             p = rec[0];
             co = rec[1];
             c = rec[2];
-            slot = splat_slot(p, c, tl.tx, tl.ty);
+            const float4 rect = rec[3];
+            // gradient row of (Gaussian, tile): its rows follow its rect row-major (duplicateWithKeys order)
+            slot = first + (tl.ty - __builtin_bit_cast(uint32_t, rect.y)) * __builtin_bit_cast(uint32_t, c.w) +
+                   (tl.tx - __builtin_bit_cast(uint32_t, rect.x));
             m = band_mask<TW_BANDS>(make_float2(p.x, p.y), co, tl.tx, tl.ty, 0);
 #pragma unroll
             for (int b = 0; b < TW_BANDS; ++b)

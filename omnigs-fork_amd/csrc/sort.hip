@@ -129,6 +129,101 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_downsweep_kernel(const uint
     }
 }
 
+// ---- the forward's two scans of tiles_touched, in one pass over the counts ----------------------------------
+// offsets   = inclusive scan in depth order (gather by `order`): the emission slots, num_rendered = offsets[P-1];
+// row_first = exclusive scan in Gaussian INDEX order: the first gradient row of each Gaussian. The backward numbers
+//             its per-instance gradient rows this way (render_bwd.hip), so the 64 Gaussians of a wave own one
+//             contiguous span of rows when their sums are taken (gaussian_bwd.hip: row_sum_kernel).
+// Both sequences have the same block structure, so one reduce / partials / downsweep launch triple does both;
+// partials holds the two block-sum arrays back to back (2 * nb words).
+__global__ __launch_bounds__(SCAN_THREADS) void scan2_reduce_kernel(const uint32_t* in, const uint32_t* order, size_t n,
+                                                                    uint32_t* partials, uint32_t nb)
+{
+    __shared__ uint32_t s_wave[SCAN_THREADS / 64];
+    const size_t base = (size_t)blockIdx.x * SCAN_TILE;
+    uint32_t sum_d = 0, sum_i = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const size_t i = base + (size_t)k * SCAN_THREADS + threadIdx.x;
+        if (i < n) {
+            sum_d += in[order[i]];
+            sum_i += in[i];
+        }
+    }
+    uint32_t total_d, total_i;
+    block_exclusive_scan(sum_d, s_wave, &total_d);
+    block_exclusive_scan(sum_i, s_wave, &total_i);
+    if (threadIdx.x == 0) {
+        partials[blockIdx.x] = total_d;
+        partials[nb + blockIdx.x] = total_i;
+    }
+}
+
+// block 0 scans the depth-order block sums, block 1 the index-order ones
+__global__ __launch_bounds__(SCAN_THREADS) void scan2_partials_kernel(uint32_t* partials, uint32_t nb)
+{
+    __shared__ uint32_t s_wave[SCAN_THREADS / 64];
+    uint32_t* part = partials + (size_t)blockIdx.x * nb;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nb; base += SCAN_THREADS) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t x = i < nb ? part[i] : 0u;
+        uint32_t total;
+        const uint32_t ex = block_exclusive_scan(x, s_wave, &total);
+        if (i < nb) part[i] = carry + ex;
+        carry += total;
+    }
+}
+
+// the thread owning items [16t, 16t+16) of the block's tile scans LDS copies of both sequences
+__global__ __launch_bounds__(SCAN_THREADS) void scan2_downsweep_kernel(const uint32_t* in, const uint32_t* order, size_t n,
+                                                                       const uint32_t* partials, uint32_t nb,
+                                                                       uint32_t* offsets, uint32_t* row_first)
+{
+    __shared__ uint32_t s_d[SCAN_TILE + SCAN_TILE / 32];  // +1 pad per 32 to break the 16-stride conflicts
+    __shared__ uint32_t s_i[SCAN_TILE + SCAN_TILE / 32];
+    __shared__ uint32_t s_wave[SCAN_THREADS / 64];
+    const size_t base = (size_t)blockIdx.x * SCAN_TILE;
+    auto pad = [](uint32_t i) { return i + (i >> 5); };
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint32_t li = k * SCAN_THREADS + threadIdx.x;
+        const size_t i = base + li;
+        s_d[pad(li)] = i < n ? in[order[i]] : 0u;
+        s_i[pad(li)] = i < n ? in[i] : 0u;
+    }
+    __syncthreads();
+    uint32_t vd[SCAN_ITEMS], vi[SCAN_ITEMS];
+    uint32_t sum_d = 0, sum_i = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        vd[k] = s_d[pad(threadIdx.x * SCAN_ITEMS + k)];
+        vi[k] = s_i[pad(threadIdx.x * SCAN_ITEMS + k)];
+        sum_d += vd[k];
+        sum_i += vi[k];
+    }
+    uint32_t total;
+    uint32_t run_d = partials[blockIdx.x] + block_exclusive_scan(sum_d, s_wave, &total);
+    uint32_t run_i = partials[nb + blockIdx.x] + block_exclusive_scan(sum_i, s_wave, &total);
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        run_d += vd[k];  // inclusive
+        s_d[pad(threadIdx.x * SCAN_ITEMS + k)] = run_d;
+        s_i[pad(threadIdx.x * SCAN_ITEMS + k)] = run_i;  // exclusive
+        run_i += vi[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint32_t li = k * SCAN_THREADS + threadIdx.x;
+        const size_t i = base + li;
+        if (i < n) {
+            offsets[i] = s_d[pad(li)];
+            row_first[i] = s_i[pad(li)];
+        }
+    }
+}
+
 // sorts of at most this many 4096-item blocks (the depth sort up to 2M Gaussians) let each downsweep block derive
 // its digit offsets from the raw histogram: <= 512 KiB of L2 reads per block instead of three scan launches
 constexpr uint32_t SELF_SCAN_MAX_BLOCKS = 512;
@@ -306,7 +401,7 @@ __global__ __launch_bounds__(256) void emit_index_kernel(int P, const uint32_t* 
 // their slot ends are staged in LDS and each thread finds its owner by a binary search there.
 __global__ __launch_bounds__(EMIT_BLOCK) void emit_kernel(int P, size_t L_cap, const uint32_t* count,
                                                           const uint32_t* order, const uint32_t* offsets,
-                                                          const uint32_t* block_owner, float4* splat, uint32_t gx,
+                                                          const uint32_t* block_owner, const float4* splat, uint32_t gx,
                                                           uint32_t* tile_keys, uint32_t* gauss_vals)
 {
     __shared__ uint32_t s_end[EMIT_BLOCK];
@@ -340,12 +435,9 @@ __global__ __launch_bounds__(EMIT_BLOCK) void emit_kernel(int P, size_t L_cap, c
     }
     const uint32_t gid = order[r];
     const uint32_t k = (uint32_t)e - start;
-    float4* rec = splat + (size_t)gid * SPLAT_F4;
-    const float4 rect = rec[3];  // {x0, y0, x1, y1} from preprocess (getRect)
+    const float4 rect = splat[(size_t)gid * SPLAT_F4 + 3];  // {x0, y0, x1, y1} from preprocess (getRect)
     const uint32_t x0 = __builtin_bit_cast(uint32_t, rect.x), y0 = __builtin_bit_cast(uint32_t, rect.y);
     const uint32_t w = __builtin_bit_cast(uint32_t, rect.z) - x0;
-    // slot of tile (tx, ty) = start + (ty - y0) * w + (tx - x0) = slot_base + ty * w + tx  (mod 2^32)
-    if (k == 0) rec[0].w = __builtin_bit_cast(float, start - (y0 * w + x0));
     const uint32_t ky = k / w;
     tile_keys[e] = (y0 + ky) * gx + (x0 + (k - ky * w));
     gauss_vals[e] = gid;
@@ -424,16 +516,6 @@ void launch_tile_order(const uint2* ranges, const uint32_t* cost, uint32_t T, ui
 
 size_t scan_partials_size(size_t n) { return div_up(n, SCAN_TILE) + 1; }
 
-void launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, uint32_t* partials, size_t n,
-                           hipStream_t s)
-{
-    if (n == 0) return;
-    const uint32_t nb = div_up(n, SCAN_TILE);
-    scan_reduce_kernel<<<nb, SCAN_THREADS, 0, s>>>(in, gather, n, partials);
-    scan_partials_kernel<<<1, SCAN_THREADS, 0, s>>>(partials, nb);
-    scan_downsweep_kernel<false><<<nb, SCAN_THREADS, 0, s>>>(in, gather, n, partials, out);
-}
-
 static void launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t* partials, size_t n, hipStream_t s)
 {
     if (n == 0) return;
@@ -441,6 +523,18 @@ static void launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t* p
     scan_reduce_kernel<<<nb, SCAN_THREADS, 0, s>>>(in, nullptr, n, partials);
     scan_partials_kernel<<<1, SCAN_THREADS, 0, s>>>(partials, nb);
     scan_downsweep_kernel<true><<<nb, SCAN_THREADS, 0, s>>>(in, nullptr, n, partials, out);
+}
+
+size_t scan2_partials_size(size_t n) { return 2 * scan_partials_size(n); }
+
+void launch_forward_scans(const uint32_t* tiles_touched, const uint32_t* order, uint32_t* offsets, uint32_t* row_first,
+                          uint32_t* partials, size_t n, hipStream_t s)
+{
+    if (n == 0) return;
+    const uint32_t nb = div_up(n, SCAN_TILE);
+    scan2_reduce_kernel<<<nb, SCAN_THREADS, 0, s>>>(tiles_touched, order, n, partials, nb);
+    scan2_partials_kernel<<<2, SCAN_THREADS, 0, s>>>(partials, nb);
+    scan2_downsweep_kernel<<<nb, SCAN_THREADS, 0, s>>>(tiles_touched, order, n, partials, nb, offsets, row_first);
 }
 
 size_t radix_hist_size(size_t n) { return (size_t)RADIX * div_up(n, SORT_TILE); }

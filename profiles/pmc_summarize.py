@@ -27,7 +27,7 @@ STAGES = {
     "tile_ranges_kernel": "tile_ranges",
     "render_fwd_kernel": "render_forward",
     "render_bwd_kernel": "render_backward",
-    "instance_reduce_kernel": "instance_reduce",
+    "row_sum_kernel": "row_sums",
     "gaussian_bwd_kernel": "gaussian_backward",
 }
 

@@ -38,7 +38,7 @@ def test_abi_version_and_sizes(omr):
     lib = omr.rasterizer.lib()
     assert lib.omr_abi_version() == 1
     g0, g1 = lib.omr_geometry_bytes(1000), lib.omr_geometry_bytes(2000)
-    assert g1 > g0 > 1000 * 100  # SoA state of ~100+ B per Gaussian
+    assert g1 > g0 > 1000 * 93  # 64-B render record + clamped, tiles_touched, sort keys/values, offsets, radii
     assert lib.omr_image_bytes(64, 32) >= 64 * 32 * 8 + 8 * 8
     b0, b1 = lib.omr_binning_bytes(0, 64, 32), lib.omr_binning_bytes(1000, 64, 32)
     assert b1 - b0 >= 1000 * (16 + 36)  # keys/values ping-pong + one gradient row per instance
