@@ -174,6 +174,7 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s)
     g.counters = c.take<uint32_t>(4);
     g.row_first = c.take<uint32_t>(P);
     g.row_sums = c.take<float>(P * GRAD_ROW);
+    g.huge_list = c.take<uint32_t>(P);
     g.internal_radii = c.take<int>(P);
     g.order = g.val_a;  // the depth sort runs DEPTH_SORT_PASSES (even) passes, so its result lands in val_a
     if (s) *s = g;
@@ -308,7 +309,7 @@ int forward_impl(const ForwardIn& in)
     // depth order of the Gaussians (stable: ties keep index order)
     int which; { StageScope st_(ST_DEPTH_SORT, s); which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr, nullptr, 0, 4, s); }
     g.order = which ? g.val_b : g.val_a;
-    { StageScope st_(ST_SCAN, s); launch_forward_scans(g.tiles_touched, g.order, g.offsets, g.row_first, g.scan_partials, P, s); }
+    { StageScope st_(ST_SCAN, s); launch_forward_scans(g.tiles_touched, g.order, g.offsets, g.row_first, g.huge_list, g.counters + 2, g.scan_partials, P, s); }
 
     // num_rendered = offsets[P-1] (+ the prefiltered error flag) to pinned host memory, without waiting for it:
     // the binning buffer is sized from a capacity hint and everything after the scan reads the count on the device,
@@ -445,7 +446,7 @@ int backward_impl(const BackwardIn& in)
     ga.focal_x = (float)in.width / (2.0f * in.tan_fovx);
     ga.clamped = g.clamped;
     ga.row_sums = g.row_sums;
-    { StageScope st_(ST_ROW_SUMS, s); launch_row_sums(in.P, g.row_first, g.tiles_touched, b.inst_grad, b.row_valid, (uint32_t)in.R, g.row_sums, s); }
+    { StageScope st_(ST_ROW_SUMS, s); launch_row_sums(in.P, g.row_first, g.tiles_touched, g.huge_list, g.counters + 2, b.inst_grad, b.row_valid, (uint32_t)in.R, g.row_sums, s); }
     ga.dL_dmean2D = in.dL_dmean2D; ga.dL_dconic = in.dL_dconic; ga.dL_dopacity = in.dL_dopacity; ga.dL_dcolor = in.dL_dcolor;
     ga.dL_dmean3D = in.dL_dmean3D; ga.dL_dcov3D = in.dL_dcov3D; ga.dL_dsh = in.M > 0 ? in.dL_dsh : nullptr;
     ga.dL_dscale = in.dL_dscale; ga.dL_drot = in.dL_drot; ga.dpx_dt = in.dpx_dt; ga.dpy_dt = in.dpy_dt;

@@ -222,15 +222,20 @@ __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const
 // The wave streams its span through LDS in chunks of RS_ROWS rows: every lane loads 4 rows of the chunk, rows
 // q*64 + lane (coalesced), marked ones only, then
 //  * a Gaussian with at most RS_LONG rows adds its rows of the chunk itself, in row order, from LDS;
-//  * a longer one (polar Gaussians reach every tile of the image) is summed by the whole wave: each lane adds the
-//    chunk rows it holds, then one wave reduction (wave_ops.h) per (long Gaussian, chunk), in chunk order.
-// Two HBM round trips per chunk (row_valid bytes, then the rows) for the whole wave, instead of two per 4 rows
-// of its slowest lane. The order of every sum is fixed: the result is deterministic.
+//  * a longer one is summed by the whole wave: each lane adds the chunk rows it holds, then one wave reduction
+//    (wave_ops.h) per (long Gaussian, chunk), in chunk order.
+// The row_valid bytes of the next chunk are requested with the rows of the current one: one HBM round trip per
+// chunk for the whole wave. Gaussians with more than ROW_SUM_HUGE rows (polar Gaussians reach every tile of the
+// image; 0.1 % of them at config C, 13 % of the rows) would make their wave the kernel's tail: the wave skips them
+// (and the chunks only they own), and RS_HUGE_BLOCKS extra workgroups at the start of the grid take them from the
+// forward's huge_list, 256 threads per Gaussian. The order of every sum is fixed: the result is deterministic.
 constexpr int RS_ROWS = 256;
 #ifndef OMR_RS_LONG
 #define OMR_RS_LONG 32
 #endif
 constexpr uint32_t RS_LONG = OMR_RS_LONG;
+constexpr uint32_t RS_HUGE_BLOCKS = 512;
+constexpr int RS_HUGE_STEP = 8;  // rows in flight per thread of a huge-Gaussian workgroup
 
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
 {
@@ -239,23 +244,83 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
     return v;
 }
 
-__global__ __launch_bounds__(256) void row_sum_kernel(int P, const uint32_t* __restrict__ row_first,
-                                                      const uint32_t* __restrict__ tiles_touched,
-                                                      const float* __restrict__ inst_grad,
-                                                      const uint8_t* __restrict__ row_valid, uint32_t R,
-                                                      float* __restrict__ row_sums)
+__device__ __forceinline__ void add_marked_row(float* acc, const float* __restrict__ inst_grad, uint32_t row, bool ok)
+{
+    if (ok) {
+        const float* p = inst_grad + (size_t)row * GRAD_ROW;
+#pragma unroll
+        for (int c = 0; c < GRAD_ROW; ++c) acc[c] += p[c];
+    }
+}
+
+struct RowSumArgs {
+    int P;
+    uint32_t R;
+    uint32_t main_blocks;
+    const uint32_t* row_first;
+    const uint32_t* tiles_touched;
+    const uint32_t* huge_list;
+    const uint32_t* huge_count;
+    const float* inst_grad;
+    const uint8_t* row_valid;
+    float* row_sums;
+};
+
+// one workgroup per huge Gaussian (the first RS_HUGE_BLOCKS blocks of the grid): thread t adds rows t, t + 256, ... (RS_HUGE_STEP in flight), then
+// the four waves' sums are combined in a fixed order
+__device__ __forceinline__ void huge_row_sums(const RowSumArgs& a, uint32_t hb, float* s_red)
+{
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t count = *a.huge_count;
+    for (uint32_t t = hb; t < count; t += RS_HUGE_BLOCKS) {
+        const uint32_t idx = a.huge_list[t];
+        const uint32_t s = a.row_first[idx];
+        uint32_t n = a.tiles_touched[idx];
+        if (s >= a.R || n > a.R - s) n = 0;  // never true for a consistent forward
+        float acc[GRAD_ROW];
+#pragma unroll
+        for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
+        for (uint32_t k0 = 0; k0 < n; k0 += 256u * RS_HUGE_STEP) {
+            bool ok[RS_HUGE_STEP];
+#pragma unroll
+            for (int q = 0; q < RS_HUGE_STEP; ++q) {
+                const uint32_t k = k0 + (uint32_t)q * 256u + tid;
+                ok[q] = k < n && a.row_valid[s + k] != 0;
+            }
+#pragma unroll
+            for (int q = 0; q < RS_HUGE_STEP; ++q) add_marked_row(acc, a.inst_grad, s + k0 + (uint32_t)q * 256u + tid, ok[q]);
+        }
+        float t8;
+        const float tv = wave_sum9_rows(acc, acc[8], lane, &t8);  // lane l: total of value (l >> 3) & 7
+        if ((lane & 7) == 0) s_red[wv * GRAD_ROW + (lane >> 3)] = tv;
+        if (lane == 1) s_red[wv * GRAD_ROW + 8] = t8;
+        __syncthreads();
+        if (tid < GRAD_ROW)
+            a.row_sums[(size_t)idx * GRAD_ROW + tid] =
+                ((s_red[tid] + s_red[GRAD_ROW + tid]) + s_red[2 * GRAD_ROW + tid]) + s_red[3 * GRAD_ROW + tid];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
 {
     __shared__ float s_rows_all[4][RS_ROWS * GRAD_ROW];  // row-major, 9 floats per row (odd stride: no conflicts)
+    if (blockIdx.x < RS_HUGE_BLOCKS) {  // dispatched first: the huge Gaussians overlap the rest of the grid
+        huge_row_sums(a, blockIdx.x, &s_rows_all[0][0]);
+        return;
+    }
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const int g0 = (int)(blockIdx.x * 256u + wv * 64u);
-    if (g0 >= P) return;  // wave-uniform
+    const int g0 = (int)((blockIdx.x - RS_HUGE_BLOCKS) * 256u + wv * 64u);
+    if (g0 >= a.P) return;  // wave-uniform
     float* s_rows = s_rows_all[wv];
     const int idx = g0 + (int)lane;
     uint32_t n = 0, s = 0;
-    if (idx < P) {
-        n = tiles_touched[idx];
-        s = row_first[idx];
-        if (n != 0 && (s >= R || n > R - s)) n = 0;  // never true for a consistent forward; keeps reads inside R rows
+    bool huge = false;
+    if (idx < a.P) {
+        n = a.tiles_touched[idx];
+        s = a.row_first[idx];
+        huge = n > ROW_SUM_HUGE;  // summed by the workgroups at the end of the grid
+        if (huge || (n != 0 && (s >= a.R || n > a.R - s))) n = 0;  // the latter: never for a consistent forward
     }
     const uint32_t e = s + n;
     const uint32_t lo = __builtin_amdgcn_readfirstlane(wave_min_u32(n ? s : 0xFFFFFFFFu));
@@ -265,31 +330,44 @@ __global__ __launch_bounds__(256) void row_sum_kernel(int P, const uint32_t* __r
 #pragma unroll
     for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
 
+    // row_valid bytes of the first chunk; each iteration requests the next chunk's with its rows
+    uint32_t flag[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t r = lo + (uint32_t)q * 64u + lane;
+        flag[q] = lo < hi && r < hi ? a.row_valid[r] : 0u;
+    }
     for (uint32_t c0 = lo; c0 < hi; c0 += RS_ROWS) {  // lo > hi when the wave owns no rows
-        // stage the chunk: row c0 + q*64 + lane at s_rows[(q*64 + lane) * 9], zeros where not marked / past hi
+        const uint32_t c1 = c0 + RS_ROWS;
         bool ok[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t r = c0 + (uint32_t)q * 64u + lane;
-            ok[q] = r < hi && row_valid[r] != 0;
+        for (int q = 0; q < 4; ++q) ok[q] = flag[q] != 0;
+        // chunks inside a skipped huge Gaussian's rows: nothing to stage
+        if (!__ballot(n != 0 && s < c1 && e > c0)) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t r = c1 + (uint32_t)q * 64u + lane;
+                flag[q] = r < hi ? a.row_valid[r] : 0u;
+            }
+            continue;
         }
         float x[4][GRAD_ROW];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const float* p = inst_grad + (size_t)(c0 + (uint32_t)q * 64u + lane) * GRAD_ROW;
 #pragma unroll
             for (int c = 0; c < GRAD_ROW; ++c) x[q][c] = 0.f;
-            if (ok[q]) {
+            add_marked_row(x[q], a.inst_grad, c0 + (uint32_t)q * 64u + lane, ok[q]);
+        }
 #pragma unroll
-                for (int c = 0; c < GRAD_ROW; ++c) x[q][c] = p[c];
-            }
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t r = c1 + (uint32_t)q * 64u + lane;
+            flag[q] = r < hi ? a.row_valid[r] : 0u;
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
             for (int c = 0; c < GRAD_ROW; ++c) s_rows[(q * 64 + lane) * GRAD_ROW + c] = x[q][c];
         wave_sync();
-        const uint32_t c1 = c0 + RS_ROWS;
         // short segments: the owner adds its rows of this chunk in order
         if (n != 0 && !is_long && s < c1 && e > c0) {
             const uint32_t j1 = min(e, c1) - c0;
@@ -325,8 +403,8 @@ __global__ __launch_bounds__(256) void row_sum_kernel(int P, const uint32_t* __r
         }
         wave_sync();  // the next chunk overwrites the staging rows
     }
-    if (idx < P) {
-        float* out = row_sums + (size_t)idx * GRAD_ROW;
+    if (idx < a.P && !huge) {
+        float* out = a.row_sums + (size_t)idx * GRAD_ROW;
 #pragma unroll
         for (int c = 0; c < GRAD_ROW; ++c) out[c] = acc[c];
     }
@@ -674,11 +752,23 @@ void launch_sh_grad_from_colors(int P, int D, int M, int nviews, const float* me
     else sh_grad_from_colors_kernel<0><<<grid, 256, 0, s>>>(P, D, M, nviews, means3D, shs, campos, dL_dcolors, dL_dsh);
 }
 
-void launch_row_sums(int P, const uint32_t* row_first, const uint32_t* tiles_touched, const float* inst_grad,
-                     const uint8_t* row_valid, uint32_t R, float* row_sums, hipStream_t s)
+void launch_row_sums(int P, const uint32_t* row_first, const uint32_t* tiles_touched, const uint32_t* huge_list,
+                     const uint32_t* huge_count, const float* inst_grad, const uint8_t* row_valid, uint32_t R,
+                     float* row_sums, hipStream_t s)
 {
     if (P <= 0) return;
-    row_sum_kernel<<<div_up(P, 256), 256, 0, s>>>(P, row_first, tiles_touched, inst_grad, row_valid, R, row_sums);
+    RowSumArgs a;
+    a.P = P;
+    a.R = R;
+    a.main_blocks = div_up(P, 256);  // after the RS_HUGE_BLOCKS huge-Gaussian workgroups
+    a.row_first = row_first;
+    a.tiles_touched = tiles_touched;
+    a.huge_list = huge_list;
+    a.huge_count = huge_count;
+    a.inst_grad = inst_grad;
+    a.row_valid = row_valid;
+    a.row_sums = row_sums;
+    row_sum_kernel<<<a.main_blocks + RS_HUGE_BLOCKS, 256, 0, s>>>(a);
 }
 
 void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s)

@@ -38,10 +38,11 @@ void launch_mark_visible(int camera_type, int P, const float* means3D, const flo
 size_t scan_partials_size(size_t n);
 size_t radix_hist_size(size_t n);
 // the forward's scans of tiles_touched (sort.hip): offsets = inclusive scan in depth order (gather by order),
-// row_first = exclusive scan in index order (gradient row numbering); partials: scan2_partials_size(n) words
+// row_first = exclusive scan in index order (gradient row numbering); huge_list / *huge_count (zeroed by the
+// caller) = the Gaussians with more than ROW_SUM_HUGE tiles; partials: scan2_partials_size(n) words
 size_t scan2_partials_size(size_t n);
 void launch_forward_scans(const uint32_t* tiles_touched, const uint32_t* order, uint32_t* offsets, uint32_t* row_first,
-                          uint32_t* partials, size_t n, hipStream_t s);
+                          uint32_t* huge_list, uint32_t* huge_count, uint32_t* partials, size_t n, hipStream_t s);
 // stable LSD radix sort of (key, value) over bits [0, 8*passes); returns which buffer holds the result (0: a, 1: b).
 // n = capacity; count (device, may be NULL) = live element count <= n. canon != NULL: the last pass writes the
 // values to the canonical point list of the binning buffer at canon (raster_common.h) instead of val_a / val_b.
@@ -127,8 +128,10 @@ struct GaussBwdArgs {
 void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s);
 // Per-Gaussian sums of the render backward's instance rows: Gaussian i owns rows [row_first[i], row_first[i] +
 // tiles_touched[i]) of inst_grad (index-order numbering, launch_forward_scans); only rows marked in row_valid are read.
-void launch_row_sums(int P, const uint32_t* row_first, const uint32_t* tiles_touched, const float* inst_grad,
-                     const uint8_t* row_valid, uint32_t R, float* row_sums, hipStream_t s);
+// Gaussians in huge_list (*huge_count of them) are summed by whole workgroups.
+void launch_row_sums(int P, const uint32_t* row_first, const uint32_t* tiles_touched, const uint32_t* huge_list,
+                     const uint32_t* huge_count, const float* inst_grad, const uint8_t* row_valid, uint32_t R,
+                     float* row_sums, hipStream_t s);
 // view-parallel DP: dL_dsh[P,M,3] = sum over views of dL/dsh rebuilt from dL_dcolors [nviews][P][3] + campos [nviews][3]
 void launch_sh_grad_from_colors(int P, int D, int M, int nviews, const float* means3D, const float* shs,
                                 const float* campos, const float* dL_dcolors, float* dL_dsh, hipStream_t s);

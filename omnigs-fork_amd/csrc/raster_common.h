@@ -34,6 +34,9 @@ constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
 // per-instance gradient row written by the render backward (render_bwd.hip) and reduced per Gaussian
 // (gaussian_bwd.hip): dmean2D.x, dmean2D.y, dconic.x, dconic.y, dconic.w, dopacity, dcolor.rgb
 constexpr int GRAD_ROW = 9;
+// a Gaussian touching more tiles than this gets a whole workgroup for its row sums (gaussian_bwd.hip); the
+// forward's scan lists these Gaussians (sort.hip: scan2_downsweep_kernel)
+constexpr uint32_t ROW_SUM_HUGE = 256;
 
 constexpr size_t ALIGN = 256;
 inline size_t align_up(size_t x) { return (x + ALIGN - 1) & ~(ALIGN - 1); }
@@ -80,6 +83,7 @@ struct GeomState {
     uint32_t* order;          // depth order (points at val_a or val_b after the sort)
     uint32_t* row_first;      // first gradient row of each Gaussian (index-order exclusive scan, launch_forward_scans)
     float* row_sums;          // backward: [P][GRAD_ROW] each Gaussian's instance rows summed (launch_row_sums)
+    uint32_t* huge_list;      // Gaussians with more than ROW_SUM_HUGE tiles, any order; count in counters[2]
     int* internal_radii;      // used when the caller passes radii == NULL (rasterizer_impl.cu:284-287)
 
     static size_t carve(char* base, size_t P, GeomState* s);

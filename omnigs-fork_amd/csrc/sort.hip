@@ -135,7 +135,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_downsweep_kernel(const uint
 //             its per-instance gradient rows this way (render_bwd.hip), so the 64 Gaussians of a wave own one
 //             contiguous span of rows when their sums are taken (gaussian_bwd.hip: row_sum_kernel).
 // Both sequences have the same block structure, so one reduce / partials / downsweep launch triple does both;
-// partials holds the two block-sum arrays back to back (2 * nb words).
+// partials holds the two block-sum arrays back to back (2 * nb words). The downsweep also lists the Gaussians with
+// more than ROW_SUM_HUGE tiles (huge_list, in no particular order), whose row sums take a whole workgroup.
 __global__ __launch_bounds__(SCAN_THREADS) void scan2_reduce_kernel(const uint32_t* in, const uint32_t* order, size_t n,
                                                                     uint32_t* partials, uint32_t nb)
 {
@@ -178,7 +179,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_partials_kernel(uint32_t* 
 // the thread owning items [16t, 16t+16) of the block's tile scans LDS copies of both sequences
 __global__ __launch_bounds__(SCAN_THREADS) void scan2_downsweep_kernel(const uint32_t* in, const uint32_t* order, size_t n,
                                                                        const uint32_t* partials, uint32_t nb,
-                                                                       uint32_t* offsets, uint32_t* row_first)
+                                                                       uint32_t* offsets, uint32_t* row_first,
+                                                                       uint32_t* huge_list, uint32_t* huge_count)
 {
     __shared__ uint32_t s_d[SCAN_TILE + SCAN_TILE / 32];  // +1 pad per 32 to break the 16-stride conflicts
     __shared__ uint32_t s_i[SCAN_TILE + SCAN_TILE / 32];
@@ -212,6 +214,18 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_downsweep_kernel(const uin
         s_i[pad(threadIdx.x * SCAN_ITEMS + k)] = run_i;  // exclusive
         run_i += vi[k];
     }
+    // the block's huge Gaussians get consecutive list slots: LDS ranks, one global reservation per block
+    __shared__ uint32_t s_huge, s_huge_base;
+    if (threadIdx.x == 0) s_huge = 0;
+    __syncthreads();
+    uint32_t hrank[SCAN_ITEMS];
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const size_t i = base + k * SCAN_THREADS + threadIdx.x;
+        hrank[k] = i < n && in[i] > ROW_SUM_HUGE ? atomicAdd(&s_huge, 1u) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_huge_base = s_huge ? atomicAdd(huge_count, s_huge) : 0u;
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; ++k) {
@@ -220,6 +234,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_downsweep_kernel(const uin
         if (i < n) {
             offsets[i] = s_d[pad(li)];
             row_first[i] = s_i[pad(li)];
+            if (hrank[k] != 0xFFFFFFFFu) huge_list[s_huge_base + hrank[k]] = (uint32_t)i;
         }
     }
 }
@@ -528,13 +543,14 @@ static void launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t* p
 size_t scan2_partials_size(size_t n) { return 2 * scan_partials_size(n); }
 
 void launch_forward_scans(const uint32_t* tiles_touched, const uint32_t* order, uint32_t* offsets, uint32_t* row_first,
-                          uint32_t* partials, size_t n, hipStream_t s)
+                          uint32_t* huge_list, uint32_t* huge_count, uint32_t* partials, size_t n, hipStream_t s)
 {
     if (n == 0) return;
     const uint32_t nb = div_up(n, SCAN_TILE);
     scan2_reduce_kernel<<<nb, SCAN_THREADS, 0, s>>>(tiles_touched, order, n, partials, nb);
     scan2_partials_kernel<<<2, SCAN_THREADS, 0, s>>>(partials, nb);
-    scan2_downsweep_kernel<<<nb, SCAN_THREADS, 0, s>>>(tiles_touched, order, n, partials, nb, offsets, row_first);
+    scan2_downsweep_kernel<<<nb, SCAN_THREADS, 0, s>>>(tiles_touched, order, n, partials, nb, offsets, row_first,
+                                                        huge_list, huge_count);
 }
 
 size_t radix_hist_size(size_t n) { return (size_t)RADIX * div_up(n, SORT_TILE); }

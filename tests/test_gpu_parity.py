@@ -75,6 +75,23 @@ def test_parity(case):
     _compare(g, cam, dL)
 
 
+def test_long_and_huge_row_segments():
+    """Gaussians spanning > 32 tiles (wave-cooperative row sums) and > ROW_SUM_HUGE = 256 tiles (whole-workgroup
+    row sums, gaussian_bwd.hip) next to ordinary ones, several huge ones in one wave of 64."""
+    g, cam, dL = make_case(3000, 512, 256, LON, 31, view_index=2, spread=1.0)
+    rng = np.random.default_rng(31)
+    big = rng.choice(g.P, 40, replace=False)
+    big[:6] = np.arange(100, 106)  # adjacent indices: one wave owns several huge segments
+    g.scales = g.scales.copy()
+    g.scales[big] *= rng.uniform(5.0, 40.0, size=(40, 1)).astype(np.float32)
+    g.means3D = g.means3D.copy()
+    g.means3D[big[:10]] = np.array([0.3, 2.5, 0.2], np.float32) * rng.uniform(0.8, 1.2, (10, 1)).astype(np.float32)
+    o, _, _ = oracle_run(g, cam)
+    tt = o.get("tiles_touched")
+    assert (tt > 256).sum() >= 5 and ((tt > 32) & (tt <= 256)).sum() >= 5, np.sort(tt)[-20:]
+    _compare(g, cam, dL)
+
+
 def test_white_background():
     g, cam, dL = make_case(1000, 128, 64, LON, 21, spread=3.0)
     _compare(g, cam, dL, bg=(1.0, 1.0, 1.0))
