@@ -168,7 +168,7 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s)
     g.val_a = c.take<uint32_t>(P);
     g.val_b = c.take<uint32_t>(P);
     const size_t nh = radix_hist_size(P);
-    g.hist = c.take<uint32_t>(nh);
+    g.hist = c.take<uint32_t>(radix_scratch_words(P, DEPTH_SORT_PASSES));
     g.scan_partials = c.take<uint32_t>(std::max(scan2_partials_size(P), scan_partials_size(nh)));
     g.offsets = c.take<uint32_t>(P);
     g.counters = c.take<uint32_t>(4);
@@ -213,7 +213,7 @@ size_t BinningState::carve(char* base, size_t cap, BinningState* s, int tile_pas
     b.val_a = c.take<uint32_t>(cap);
     b.val_b = c.take<uint32_t>(cap);
     const size_t nh = radix_hist_size(cap);
-    b.hist = c.take<uint32_t>(nh);
+    b.hist = c.take<uint32_t>(radix_scratch_words(cap, tile_passes));
     b.scan_partials = c.take<uint32_t>(scan_partials_size(nh));
     b.block_owner = c.take<uint32_t>(emit_index_size(cap));
     b.row_valid = c.take<uint8_t>(cap);
@@ -307,7 +307,7 @@ int forward_impl(const ForwardIn& in)
     { StageScope st_(ST_PREPROCESS, s); launch_preprocess(in.camera_type, pa, s); }
 
     // depth order of the Gaussians (stable: ties keep index order)
-    int which; { StageScope st_(ST_DEPTH_SORT, s); which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr, nullptr, 0, 4, s); }
+    int which; { StageScope st_(ST_DEPTH_SORT, s); which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr, nullptr, 0, DEPTH_SORT_PASSES, s); }
     g.order = which ? g.val_b : g.val_a;
     { StageScope st_(ST_SCAN, s); launch_forward_scans(g.tiles_touched, g.order, g.offsets, g.row_first, g.huge_list, g.counters + 2, g.scan_partials, P, s); }
 

@@ -26,6 +26,7 @@ constexpr int SORT_ITEMS = 16;  // items per thread per block tile
 constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;
 constexpr int RADIX_BITS = 8;
 constexpr int RADIX = 1 << RADIX_BITS;
+constexpr int DEPTH_SORT_PASSES = 4;  // the depth sort's 32-bit keys (float bits of the depth)
 // scan geometry
 constexpr int SCAN_THREADS = 256;
 constexpr int SCAN_ITEMS = 16;

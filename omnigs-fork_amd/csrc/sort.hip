@@ -14,8 +14,11 @@
 // Stability of both sorts makes the result bit-identical to the reference permutation.
 //
 // MI355X notes: 256-thread blocks own 4096-key tiles; digits are ranked inside a wave by 8 ballots
-// (wave64 match-any), across the 4 waves of a block through LDS, and across blocks through a scanned
-// [digit][block] histogram — no atomics on the data path, so the sort is deterministic.
+// (wave64 match-any), across the 4 waves of a block through LDS, and across blocks either through a scanned
+// [digit][block] histogram (upsweep / scan / downsweep launches per pass) or, for sorts of at most OS_MAX_BLOCKS
+// tiles, through a decoupled look-back inside one launch per pass (onesweep_kernel). Either way every key's
+// destination follows from counts alone, so the permutation is deterministic.
+#include <algorithm>
 #include <utility>
 
 #include "kernels.h"
@@ -387,6 +390,193 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_downsweep_kernel(const uin
     }
 }
 
+// ---- single-pass ("onesweep") LSD passes with decoupled look-back ------------------------------------------
+// One launch per 8-bit pass instead of upsweep + (scan) + downsweep: the digit histograms of ALL passes come from
+// one read of the keys up front (onesweep_hist_kernel), and each pass block finds the global start of its digit runs
+// by looking back over the blocks before it. Block v publishes, per digit, its own count (AGG) as soon as it has
+// ranked its tile, then the inclusive prefix (PRE) once it knows its exclusive one; a block looking back adds AGG
+// counts until it meets a PRE. Tiles are handed out by an atomic ticket, so every block a block waits on has already
+// started, and no block waits on a later one: the look-back always finishes (each wait is also bounded, see below).
+// The ranking inside a block is radix_downsweep_kernel's; the result is the same stable permutation.
+constexpr uint32_t LB_AGG = 1u << 30, LB_PRE = 2u << 30, LB_COUNT = LB_AGG - 1u;
+constexpr uint32_t LB_SPIN_MAX = 1u << 20;  // polls of one status word before a block gives up (sets the error word)
+#ifndef OMR_LB_WINDOW
+#define OMR_LB_WINDOW 8
+#endif
+constexpr int LB_WINDOW = OMR_LB_WINDOW;  // predecessors read per look-back round trip
+
+// scratch words for a sort of n items over `passes` passes: status [passes][blocks][RADIX], digit totals
+// [passes][RADIX], tickets [passes], error word
+constexpr int OS_TILE = SORT_TILE;                   // keys per onesweep block (smaller tiles measured slower)
+constexpr uint32_t OS_HIST_BLOCKS = 128;             // histogram blocks: each digit total takes <= 128 global adds
+// Onesweep only for sorts of at most this many tiles (the depth sort up to 2 M Gaussians: 0.100 vs 0.122 ms at
+// 1 M). Past that the look-back chains and the same-address ticket / histogram adds cost more than the launches
+// they save (the 7.9 M-instance tile sort: 0.185 vs 0.142 ms), and the upsweep / scan / downsweep passes run.
+constexpr uint32_t OS_MAX_BLOCKS = 512;
+
+__host__ __device__ inline size_t onesweep_words(size_t n, int passes)
+{
+    const size_t nb = (n + OS_TILE - 1) / OS_TILE;
+    return (size_t)passes * (nb * RADIX + RADIX + 1) + 1;
+}
+
+// digit totals of every pass (ghist, zeroed by the caller; OS_HIST_BLOCKS blocks, grid-stride, so every total
+// takes at most OS_HIST_BLOCKS same-address global adds) and the zeroed status words of every pass
+__global__ __launch_bounds__(SORT_THREADS) void onesweep_hist_kernel(const uint32_t* keys, size_t n_cap,
+                                                                     const uint32_t* count, int first_pass, int passes,
+                                                                     uint32_t* status, size_t status_words,
+                                                                     uint32_t* ghist)
+{
+    __shared__ uint32_t s_h[4][RADIX];
+    const size_t n = live_count(n_cap, count);
+    const uint32_t tid = threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * SORT_THREADS;
+    for (size_t i = (size_t)blockIdx.x * SORT_THREADS + tid; i < status_words; i += stride) status[i] = 0;
+    for (int p = 0; p < passes; ++p) s_h[p][tid] = 0;
+    __syncthreads();
+    for (size_t i = (size_t)blockIdx.x * SORT_THREADS + tid; i < n; i += stride) {
+        const uint32_t key = keys[i];
+        for (int p = 0; p < passes; ++p) atomicAdd(&s_h[p][(key >> ((first_pass + p) * RADIX_BITS)) & (RADIX - 1)], 1u);
+    }
+    __syncthreads();
+    for (int p = 0; p < passes; ++p)
+        if (s_h[p][tid]) atomicAdd(&ghist[p * RADIX + tid], s_h[p][tid]);
+}
+
+__device__ __forceinline__ void lb_store(uint32_t* p, uint32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t lb_load(const uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one pass: status = this pass's [blocks][RADIX] words (zeroed), ghist = its digit totals, ticket = its tile counter
+__global__ __launch_bounds__(SORT_THREADS) void onesweep_kernel(const uint32_t* keys_in, const uint32_t* vals_in,
+                                                                uint32_t* keys_out, uint32_t* vals_out, size_t n_cap,
+                                                                const uint32_t* count, char* canon, int shift,
+                                                                uint32_t* status, const uint32_t* ghist,
+                                                                uint32_t* ticket, uint32_t* err)
+{
+    constexpr int WAVES = SORT_THREADS / 64;
+    constexpr int PER_WAVE = OS_TILE / WAVES;
+    constexpr int ROUNDS = PER_WAVE / 64;
+    __shared__ uint32_t s_whist[WAVES][RADIX];  // running digit counts per wave, then per-wave digit offsets
+    __shared__ uint32_t s_dstart[RADIX];        // block-local start of each digit's run
+    __shared__ uint32_t s_gbase[RADIX];         // global start of this block's run of each digit
+    __shared__ uint32_t s_wave[SORT_THREADS / 64];
+    __shared__ uint32_t s_k[OS_TILE];
+    __shared__ uint32_t s_v[OS_TILE];
+    __shared__ uint32_t s_vb;
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) s_vb = atomicAdd(ticket, 1u);
+    const size_t n = live_count(n_cap, count);
+    if (canon) vals_out = reinterpret_cast<uint32_t*>(canon + canonical_list_offset(n));
+    const uint32_t w = tid >> 6, lane = tid & 63;
+#pragma unroll
+    for (int q = 0; q < WAVES; ++q) s_whist[q][tid] = 0;
+    __syncthreads();
+    const uint32_t vb = s_vb;
+    const size_t tile0 = (size_t)vb * OS_TILE;
+    if (tile0 >= n) return;  // block-uniform; no block looks back at a tile past the live count
+    uint32_t total_unused;
+    const uint32_t gstart = block_exclusive_scan(ghist[tid], s_wave, &total_unused);  // thread = digit
+    const size_t base = tile0 + (size_t)w * PER_WAVE + lane;
+    uint32_t k[ROUNDS], v[ROUNDS], lr[ROUNDS];
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+        const size_t i = base + 64 * r;
+        k[r] = i < n ? keys_in[i] : 0u;
+        v[r] = i < n ? vals_in[i] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+        const bool valid = base + 64 * r < n;
+        const uint32_t d = (k[r] >> shift) & (RADIX - 1);
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < RADIX_BITS; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t rank = mask_rank(peers);
+        const uint32_t prev = valid ? s_whist[w][d] : 0u;
+        lr[r] = prev + rank;
+        __builtin_amdgcn_wave_barrier();
+        if (valid && rank == 0) s_whist[w][d] = prev + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    {   // thread = digit: per-wave exclusive offsets, block-local digit starts, then the look-back
+        uint32_t run = 0;
+#pragma unroll
+        for (int q = 0; q < WAVES; ++q) {
+            const uint32_t c = s_whist[q][tid];
+            s_whist[q][tid] = run;
+            run += c;
+        }
+        uint32_t total;
+        s_dstart[tid] = block_exclusive_scan(run, s_wave, &total);
+        uint32_t* mine = status + (size_t)vb * RADIX + tid;
+        uint32_t excl = 0;
+        if (vb == 0) {
+            lb_store(mine, LB_PRE | run);
+        } else {
+            lb_store(mine, LB_AGG | run);
+            // look back LB_WINDOW blocks per round trip: blocks j-1, j-2, ... (nearest first) until a PRE word;
+            // an unpublished word ends the window and is polled again
+            uint32_t j = vb, spins = 0;
+            while (true) {
+                uint32_t st[LB_WINDOW];
+#pragma unroll
+                for (int q = 0; q < LB_WINDOW; ++q)
+                    st[q] = j > (uint32_t)q ? lb_load(status + (size_t)(j - 1 - q) * RADIX + tid) : LB_PRE;
+                uint32_t used = 0;
+                bool done = false;
+#pragma unroll
+                for (int q = 0; q < LB_WINDOW; ++q) {
+                    if (done || used != (uint32_t)q || (st[q] & ~LB_COUNT) == 0) continue;
+                    excl += st[q] & LB_COUNT;
+                    ++used;
+                    done = (st[q] & LB_PRE) != 0;  // block 0 always publishes PRE: j never passes it
+                }
+                if (done) break;
+                j -= used;
+                if (used == 0) {
+                    if (++spins > LB_SPIN_MAX) {
+                        atomicOr(err, 1u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            lb_store(mine, LB_PRE | (excl + run));
+        }
+        s_gbase[tid] = gstart + excl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+        if (base + 64 * r < n) {
+            const uint32_t d = (k[r] >> shift) & (RADIX - 1);
+            const uint32_t lp = s_dstart[d] + s_whist[w][d] + lr[r];
+            s_k[lp] = k[r];
+            s_v[lp] = v[r];
+        }
+    }
+    __syncthreads();
+    const uint32_t nvalid = (uint32_t)min((size_t)OS_TILE, n - tile0);
+    for (uint32_t j = tid; j < nvalid; j += SORT_THREADS) {
+        const uint32_t kk = s_k[j];
+        const uint32_t d = (kk >> shift) & (RADIX - 1);
+        const uint32_t dst = s_gbase[d] + (j - s_dstart[d]);
+        keys_out[dst] = kk;
+        vals_out[dst] = s_v[j];
+    }
+}
+
 // ---- instances -------------------------------------------------------------------------------------------
 // first index r in [lo, hi) with offsets[r] > e (offsets = inclusive scan, non-decreasing)
 __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* offsets, uint32_t lo, uint32_t hi, uint32_t e)
@@ -555,14 +745,46 @@ void launch_forward_scans(const uint32_t* tiles_touched, const uint32_t* order, 
 
 size_t radix_hist_size(size_t n) { return (size_t)RADIX * div_up(n, SORT_TILE); }
 
+#ifndef OMR_ONESWEEP
+#define OMR_ONESWEEP 1
+#endif
+
+static bool use_onesweep(size_t n) { return OMR_ONESWEEP && div_up(n, OS_TILE) <= OS_MAX_BLOCKS; }
+
+size_t radix_scratch_words(size_t n, int passes)
+{
+    return use_onesweep(n) ? std::max(onesweep_words(n, passes), radix_hist_size(n)) : radix_hist_size(n);
+}
+
 int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* hist,
                      uint32_t* scan_partials, size_t n, const uint32_t* count, char* canon, int first_pass, int passes,
                      hipStream_t s)
 {
     if (n == 0 || passes <= 0) return 0;
-    const uint32_t nb = div_up(n, SORT_TILE);
     uint32_t *ki = key_a, *ko = key_b, *vi = val_a, *vo = val_b;
     int cur = 0;
+    if (use_onesweep(n)) {
+        const uint32_t nb = div_up(n, OS_TILE);
+        // scratch: status [passes][nb][RADIX] | ghist [passes][RADIX] | tickets [passes] | error word
+        uint32_t* status = hist;
+        uint32_t* ghist = hist + (size_t)passes * nb * RADIX;
+        uint32_t* tickets = ghist + (size_t)passes * RADIX;
+        uint32_t* err = tickets + passes;
+        (void)hipMemsetAsync(ghist, 0, ((size_t)passes * (RADIX + 1) + 1) * sizeof(uint32_t), s);
+        onesweep_hist_kernel<<<std::min(div_up(n, SORT_THREADS), OS_HIST_BLOCKS), SORT_THREADS, 0, s>>>(
+            ki, n, count, first_pass, passes, status, (size_t)passes * nb * RADIX, ghist);
+        for (int p = 0; p < passes; ++p) {
+            const bool last = p == passes - 1;
+            onesweep_kernel<<<nb, SORT_THREADS, 0, s>>>(ki, vi, ko, vo, n, count, last ? canon : nullptr,
+                                                        (first_pass + p) * RADIX_BITS, status + (size_t)p * nb * RADIX,
+                                                        ghist + (size_t)p * RADIX, tickets + p, err);
+            std::swap(ki, ko);
+            std::swap(vi, vo);
+            cur ^= 1;
+        }
+        return cur;
+    }
+    const uint32_t nb = div_up(n, SORT_TILE);
     for (int p = first_pass; p < first_pass + passes; ++p) {
         const int shift = p * RADIX_BITS;
         const bool last = p == first_pass + passes - 1;
