@@ -207,7 +207,9 @@ size_t BinningState::carve(char* base, size_t cap, BinningState* s, int tile_pas
     BinningState b;
     b.inst_grad = c.take<float>(cap * GRAD_ROW);
     c.take<uint32_t>(cap);  // room for the canonical point list when L < cap (raster_common.h)
+    c.take<uint8_t>(cap);   // room for row_valid behind it
     b.point_list = base ? reinterpret_cast<uint32_t*>(base + canonical_list_offset(cap)) : nullptr;
+    b.row_valid = base ? reinterpret_cast<uint8_t*>(base + row_valid_offset(cap)) : nullptr;
     b.key_a = c.take<uint32_t>(cap);
     b.key_b = c.take<uint32_t>(cap);
     b.val_a = c.take<uint32_t>(cap);
@@ -216,7 +218,6 @@ size_t BinningState::carve(char* base, size_t cap, BinningState* s, int tile_pas
     b.hist = c.take<uint32_t>(radix_scratch_words(cap, tile_passes));
     b.scan_partials = c.take<uint32_t>(scan_partials_size(nh));
     b.block_owner = c.take<uint32_t>(emit_index_size(cap));
-    b.row_valid = c.take<uint8_t>(cap);
     b.point_keys = (tile_passes & 1) != 0 ? b.key_b : b.key_a;  // result buffer of the key ping-pong
     if (s) *s = b;
     return c.size();
@@ -291,8 +292,13 @@ int forward_impl(const ForwardIn& in)
     ImageState::carve(img_base, d.N, d.T, &im);
     int* radii = in.radii ? in.radii : geom_internal_radii(geom_base, P);
 
-    OMR_HIP(hipMemsetAsync(g.counters, 0, 4 * sizeof(uint32_t), s));
+    // counters[1] is the prefiltered-cull flag, set by preprocess itself: cleared first, and only when it can be set
+    if (in.prefiltered) OMR_HIP(hipMemsetAsync(g.counters + 1, 0, sizeof(uint32_t), s));
     PreprocessArgs pa;
+    pa.zero[0] = {g.counters + 2, 2};                                  // huge-list count (scan), spare
+    pa.zero[1] = {reinterpret_cast<uint32_t*>(im.ranges), 2 * (size_t)d.T};  // tile_ranges writes boundaries only
+    pa.zero[2] = {im.tile_cost, (size_t)d.T};                          // render_forward adds into it
+    pa.zero[3] = radix_zero_span(g.hist, P, DEPTH_SORT_PASSES);        // the depth sort's digit totals / tickets
     pa.P = in.P; pa.D = in.D; pa.M = in.M; pa.W = in.width; pa.H = in.height; pa.gx = d.gx; pa.gy = d.gy;
     pa.means3D = in.means3D; pa.scales = in.scales; pa.scale_modifier = in.scale_modifier; pa.rotations = in.rotations;
     pa.opacities = in.opacities; pa.shs = in.shs; pa.cov3D_precomp = in.cov3D_precomp; pa.colors_precomp = in.colors_precomp;
@@ -307,7 +313,7 @@ int forward_impl(const ForwardIn& in)
     { StageScope st_(ST_PREPROCESS, s); launch_preprocess(in.camera_type, pa, s); }
 
     // depth order of the Gaussians (stable: ties keep index order)
-    int which; { StageScope st_(ST_DEPTH_SORT, s); which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr, nullptr, 0, DEPTH_SORT_PASSES, s); }
+    int which; { StageScope st_(ST_DEPTH_SORT, s); which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr, nullptr, 0, DEPTH_SORT_PASSES, s, true); }
     g.order = which ? g.val_b : g.val_a;
     { StageScope st_(ST_SCAN, s); launch_forward_scans(g.tiles_touched, g.order, g.offsets, g.row_first, g.huge_list, g.counters + 2, g.scan_partials, P, s); }
 
@@ -321,7 +327,8 @@ int forward_impl(const ForwardIn& in)
     if (!host || !ev_count) return fail(OMR_ERR_HIP, "pinned host memory / event allocation failed");
     const uint32_t* count_dev = g.offsets + (P - 1);
     OMR_HIP(hipMemcpyAsync(host, count_dev, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    OMR_HIP(hipMemcpyAsync(host + 1, g.counters + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    host[1] = 0;
+    if (in.prefiltered) OMR_HIP(hipMemcpyAsync(host + 1, g.counters + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     OMR_HIP(hipEventRecord(ev_count, s));
 
     const int tile_passes = tile_sort_passes(d.T);
@@ -341,28 +348,29 @@ int forward_impl(const ForwardIn& in)
         if (int e = wait_count()) return e;
     size_t cap = known ? L : hint;
 
+    bool rerun = false;  // a second back half must clear what the first one wrote (preprocess zeroed it once)
     auto back_half = [&](size_t capacity) -> int {
         char* bin_base = static_cast<char*>(
             in.binning_alloc(in.binning_ctx, BinningState::carve(nullptr, capacity, nullptr, tile_passes)));
         if (!bin_base) return fail(OMR_ERR_ALLOCATION, "binning allocation failed");
         BinningState b;
         BinningState::carve(bin_base, capacity, &b, tile_passes);
-        { StageScope st_(ST_EMIT, s); launch_emit_instances(in.P, capacity, count_dev, g, d.gx, b.block_owner, b.key_a, b.val_a, s); }
+        { StageScope st_(ST_EMIT, s); launch_emit_instances(in.P, capacity, count_dev, g, d.gx, b.block_owner, b.key_a, b.val_a, bin_base, s); }
         {
             StageScope st_(ST_TILE_SORT, s);
             radix_sort_pairs(b.key_a, b.key_b, b.val_a, b.val_b, b.hist, b.scan_partials, capacity, count_dev,
                              bin_base, 0, tile_passes, s);
         }
-        OMR_HIP(hipMemsetAsync(im.ranges, 0, d.T * sizeof(uint2), s));
+        if (rerun) OMR_HIP(hipMemsetAsync(im.ranges, 0, d.T * sizeof(uint2), s));
         {
             StageScope st_(ST_RANGES, s);
             launch_tile_ranges(capacity, count_dev, b.point_keys, im.ranges, s);
             launch_tile_order(im.ranges, nullptr, d.T, im.tile_order, s);
         }
-        OMR_HIP(hipMemsetAsync(im.tile_cost, 0, d.T * sizeof(uint32_t), s));
+        if (rerun) OMR_HIP(hipMemsetAsync(im.tile_cost, 0, d.T * sizeof(uint32_t), s));
         RenderFwdArgs ra;
         ra.W = in.width; ra.H = in.height; ra.gx = d.gx; ra.gy = d.gy;
-        ra.ranges = im.ranges; ra.tile_order = im.tile_order; ra.binning = bin_base; ra.count = count_dev;
+        ra.ranges = im.ranges; ra.tile_order = im.tile_order; ra.binning = bin_base; ra.count = count_dev; ra.capacity = capacity;
         ra.splat = g.splat;
         ra.bg = in.background; ra.tile_cost = im.tile_cost; ra.final_T = im.final_T; ra.n_contrib = im.n_contrib;
         ra.out_color = in.out_color;
@@ -375,6 +383,7 @@ int forward_impl(const ForwardIn& in)
         if (int e = wait_count()) return e;
     if (L > cap) {  // the hint was too small: redo the back half at the exact size (outputs are overwritten)
         cap = L;
+        rerun = true;
         if (int e = back_half(cap)) return e;
     }
     hint = L + L / 8 + 4096;
@@ -430,7 +439,7 @@ int backward_impl(const BackwardIn& in)
     rb.row_first = g.row_first;
     rb.final_T = im.final_T; rb.n_contrib = im.n_contrib; rb.dL_dpix = in.dL_dpix; rb.inst_grad = b.inst_grad;
     rb.row_valid = b.row_valid;
-    if (in.R > 0) OMR_HIP(hipMemsetAsync(b.row_valid, 0, (size_t)in.R, s));
+    // b.row_valid [R] was zeroed by the forward's emit (row_valid_offset)
     {
         StageScope st_(ST_RENDER_BWD, s);
         launch_tile_order(im.ranges, im.tile_cost, d.T, im.tile_order, s);  // costliest tiles first

@@ -7,7 +7,15 @@
 
 namespace omr {
 
+// a run of u32 words the preprocess kernel zeroes before anything reads them (replaces memset launches)
+struct ZeroSpan {
+    uint32_t* p = nullptr;
+    size_t n = 0;
+};
+constexpr int PRE_ZERO_SPANS = 4;
+
 struct PreprocessArgs {
+    ZeroSpan zero[PRE_ZERO_SPANS];
     int P, D, M;
     int W, H;
     uint32_t gx, gy;
@@ -48,14 +56,19 @@ void launch_forward_scans(const uint32_t* tiles_touched, const uint32_t* order, 
 // stable LSD radix sort of (key, value) over bits [0, 8*passes); returns which buffer holds the result (0: a, 1: b).
 // n = capacity; count (device, may be NULL) = live element count <= n. canon != NULL: the last pass writes the
 // values to the canonical point list of the binning buffer at canon (raster_common.h) instead of val_a / val_b.
+// scratch_zeroed: the caller has zeroed radix_zero_span(hist, n, passes) (else the sort clears it itself)
 int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* hist,
                      uint32_t* scan_partials, size_t n, const uint32_t* count, char* canon, int first_pass, int passes,
-                     hipStream_t s);
+                     hipStream_t s, bool scratch_zeroed = false);
+// the words of `hist` a sort of n items over `passes` passes needs zeroed before it starts (possibly none)
+ZeroSpan radix_zero_span(uint32_t* hist, size_t n, int passes);
 // duplicateWithKeys; L_cap = capacity, *count (device) = num_rendered; block_owner: emit_index_size(L_cap) words
 constexpr int EMIT_BLOCK = 256;
 size_t emit_index_size(size_t L_cap);
+// also zeroes the backward's row_valid bytes at binning + row_valid_offset(L)
 void launch_emit_instances(int P, size_t L_cap, const uint32_t* count, const GeomState& g, uint32_t gx,
-                           uint32_t* block_owner, uint32_t* tile_keys, uint32_t* gauss_vals, hipStream_t s);
+                           uint32_t* block_owner, uint32_t* tile_keys, uint32_t* gauss_vals, char* binning,
+                           hipStream_t s);
 void launch_tile_ranges(size_t L_cap, const uint32_t* count, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s);
 // render schedule: within each of 8 contiguous shares of the tiles (one per XCD), tiles by descending cost
 // (cost[t] if cost != NULL, else the instance count ranges[t].y - ranges[t].x)
@@ -69,6 +82,7 @@ struct RenderFwdArgs {
     const uint32_t* tile_order;  // [T] schedule (launch_tile_order)
     const char* binning;         // binning buffer: the point list is at binning + canonical_list_offset(*count)
     const uint32_t* count;       // num_rendered (device)
+    size_t capacity;             // instances the binning buffer was sized for (count > capacity: render nothing)
     const float4* splat;  // [P][SPLAT_F4] render records
     const float* bg;
     uint32_t* tile_cost;  // [T] zeroed; receives the (instance, band) pairs each tile evaluated (backward schedule)

@@ -221,6 +221,12 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     constexpr int SH_F4 = 12;  // 16 coefficients x 3 channels
     __shared__ float4 s_stage[4][stage_f4<SH_F4>()];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    {   // scratch words later kernels expect zeroed (counters, tile ranges / costs, sort scratch): no memset launches
+        const size_t gtid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+#pragma unroll
+        for (int z = 0; z < PRE_ZERO_SPANS; ++z)
+            for (size_t i = gtid; i < a.zero[z].n; i += nth) a.zero[z].p[i] = 0u;
+    }
     const int wave_first = (int)(blockIdx.x * 256u + wv * 64u);
     if (wave_first >= a.P) return;  // wave-uniform
     const int idx = wave_first + (int)lane;

@@ -103,12 +103,18 @@ struct ImageState {
 // ---- binning state: L instances ----------------------------------------------------------------------------
 // The forward sizes this buffer BEFORE it knows L (capacity `cap` >= L from a hint, see capi.hip) so that it never
 // waits for the host; the backward only learns R = L. So the two arrays the backward reads sit at offsets that
-// depend on L alone: inst_grad at 0 and the sorted point list right after R rows of it (canonical_list_offset).
-// In the forward, the region [0, align(cap * 4 * GRAD_ROW) + align(cap * 4)) is reserved for them; the final tile-sort pass
-// writes the point list to base + canonical_list_offset(L) with L read on the device.
+// depend on L alone: inst_grad at 0, the sorted point list right after R rows of it (canonical_list_offset), then
+// row_valid (row_valid_offset). In the forward, the region [0, align(36 cap) + align(4 cap) + cap) is reserved for
+// them; the final tile-sort pass writes the point list to base + canonical_list_offset(L) and emit zeroes row_valid
+// at base + row_valid_offset(L), with L read on the device.
 __host__ __device__ inline size_t canonical_list_offset(size_t L)
 {
     return (L * GRAD_ROW * sizeof(float) + ALIGN - 1) & ~(ALIGN - 1);
+}
+// the backward's row_valid bytes [L], right after the point list; emit zeroes them during the forward
+__host__ __device__ inline size_t row_valid_offset(size_t L)
+{
+    return canonical_list_offset(L) + ((L * sizeof(uint32_t) + ALIGN - 1) & ~(ALIGN - 1));
 }
 struct BinningState {
     float* inst_grad;      // [L][GRAD_ROW] backward scratch, indexed by gradient row slot (offset 0)
@@ -120,7 +126,7 @@ struct BinningState {
     uint32_t* hist;        // radix histograms
     uint32_t* scan_partials;
     uint32_t* block_owner;  // emit index: owner rank of every EMIT_BLOCK-th slot
-    uint8_t* row_valid;     // backward: 1 where inst_grad holds a row (carved for R in the backward only)
+    uint8_t* row_valid;     // backward: 1 where inst_grad holds a row (at row_valid_offset(L); zeroed by emit)
     uint32_t* point_keys;  // sorted tile ids (points at key_a or key_b)
     // carve for capacity cap; point_list is set for L = cap (exact sizing: backward, debug, omr_binning_bytes)
     static size_t carve(char* base, size_t cap, BinningState* s, int tile_passes);

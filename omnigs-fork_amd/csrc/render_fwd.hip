@@ -79,8 +79,10 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
         if (__ballot(inside)) active |= 1u << b;
     }
 
-    const uint32_t* point_list = reinterpret_cast<const uint32_t*>(a.binning + canonical_list_offset(*a.count));
-    const uint2 range = a.ranges[tile];
+    // a count past the capacity: the binning kernels did nothing (sort.hip: live_count) and the ranges stay empty
+    const size_t L = *a.count <= a.capacity ? *a.count : 0u;
+    const uint32_t* point_list = reinterpret_cast<const uint32_t*>(a.binning + canonical_list_offset(L));
+    const uint2 range = L ? a.ranges[tile] : make_uint2(0u, 0u);
     const uint32_t n = range.y - range.x;
     for (uint32_t start = 0; start < n && active; start += TW_BATCH) {
         const uint32_t k = start + lane;

@@ -247,10 +247,12 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_downsweep_kernel(const uin
 constexpr uint32_t SELF_SCAN_MAX_BLOCKS = 512;
 
 // ---- radix sort ------------------------------------------------------------------------------------------
-// element count: the host's n, or min(*count, n) when the count lives on the device (binning, capi.hip)
+// element count: the host's n, or *count when the count lives on the device (binning, capi.hip). A device count
+// above the capacity n means the forward sized the binning buffer from a hint that was too small: every binning
+// kernel then does nothing (count 0) and the host re-runs the back half at the exact size (capi.hip).
 __device__ __forceinline__ size_t live_count(size_t n, const uint32_t* count)
 {
-    return count ? min(n, (size_t)*count) : n;
+    return count ? ((size_t)*count <= n ? (size_t)*count : 0) : n;
 }
 
 // BLOCK_MAJOR: hist[block][digit] (read back by the self-scanning downsweep of small sorts); else hist[digit][block]
@@ -591,10 +593,11 @@ __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* offsets, uin
 
 // Emission index: block_owner[B] = the depth rank owning slot B * EMIT_BLOCK (the rank whose slot range
 // [offsets[r-1], offsets[r]) contains it). One thread per rank; only ranks containing a block start write.
-__global__ __launch_bounds__(256) void emit_index_kernel(int P, const uint32_t* offsets, uint32_t* block_owner)
+__global__ __launch_bounds__(256) void emit_index_kernel(int P, size_t L_cap, const uint32_t* count,
+                                                         const uint32_t* offsets, uint32_t* block_owner)
 {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= P) return;
+    if (r >= P || live_count(L_cap, count) == 0) return;  // block_owner holds L_cap / EMIT_BLOCK + 1 words
     const uint32_t lo = r == 0 ? 0u : offsets[r - 1], hi = offsets[r];
     for (uint32_t B = (lo + EMIT_BLOCK - 1) / EMIT_BLOCK; B * EMIT_BLOCK < hi; ++B) block_owner[B] = (uint32_t)r;
 }
@@ -607,7 +610,7 @@ __global__ __launch_bounds__(256) void emit_index_kernel(int P, const uint32_t* 
 __global__ __launch_bounds__(EMIT_BLOCK) void emit_kernel(int P, size_t L_cap, const uint32_t* count,
                                                           const uint32_t* order, const uint32_t* offsets,
                                                           const uint32_t* block_owner, const float4* splat, uint32_t gx,
-                                                          uint32_t* tile_keys, uint32_t* gauss_vals)
+                                                          uint32_t* tile_keys, uint32_t* gauss_vals, char* binning)
 {
     __shared__ uint32_t s_end[EMIT_BLOCK];
     __shared__ uint32_t s_start0;
@@ -646,6 +649,7 @@ __global__ __launch_bounds__(EMIT_BLOCK) void emit_kernel(int P, size_t L_cap, c
     const uint32_t ky = k / w;
     tile_keys[e] = (y0 + ky) * gx + (x0 + (k - ky * w));
     gauss_vals[e] = gid;
+    reinterpret_cast<uint8_t*>(binning + row_valid_offset(L))[e] = 0;  // the backward's row map (render_bwd.hip)
 }
 
 // identifyTileRanges (rasterizer_impl.cu:145-167)
@@ -756,9 +760,19 @@ size_t radix_scratch_words(size_t n, int passes)
     return use_onesweep(n) ? std::max(onesweep_words(n, passes), radix_hist_size(n)) : radix_hist_size(n);
 }
 
+ZeroSpan radix_zero_span(uint32_t* hist, size_t n, int passes)
+{
+    ZeroSpan z;
+    if (n == 0 || passes <= 0 || !use_onesweep(n)) return z;
+    // digit totals [passes][RADIX] | tickets [passes] | error word, after the status words
+    z.p = hist + (size_t)passes * div_up(n, OS_TILE) * RADIX;
+    z.n = (size_t)passes * (RADIX + 1) + 1;
+    return z;
+}
+
 int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* hist,
                      uint32_t* scan_partials, size_t n, const uint32_t* count, char* canon, int first_pass, int passes,
-                     hipStream_t s)
+                     hipStream_t s, bool scratch_zeroed)
 {
     if (n == 0 || passes <= 0) return 0;
     uint32_t *ki = key_a, *ko = key_b, *vi = val_a, *vo = val_b;
@@ -770,7 +784,7 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
         uint32_t* ghist = hist + (size_t)passes * nb * RADIX;
         uint32_t* tickets = ghist + (size_t)passes * RADIX;
         uint32_t* err = tickets + passes;
-        (void)hipMemsetAsync(ghist, 0, ((size_t)passes * (RADIX + 1) + 1) * sizeof(uint32_t), s);
+        if (!scratch_zeroed) (void)hipMemsetAsync(ghist, 0, ((size_t)passes * (RADIX + 1) + 1) * sizeof(uint32_t), s);
         onesweep_hist_kernel<<<std::min(div_up(n, SORT_THREADS), OS_HIST_BLOCKS), SORT_THREADS, 0, s>>>(
             ki, n, count, first_pass, passes, status, (size_t)passes * nb * RADIX, ghist);
         for (int p = 0; p < passes; ++p) {
@@ -808,12 +822,13 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
 size_t emit_index_size(size_t L_cap) { return div_up(L_cap, EMIT_BLOCK) + 1; }
 
 void launch_emit_instances(int P, size_t L_cap, const uint32_t* count, const GeomState& g, uint32_t gx,
-                           uint32_t* block_owner, uint32_t* tile_keys, uint32_t* gauss_vals, hipStream_t s)
+                           uint32_t* block_owner, uint32_t* tile_keys, uint32_t* gauss_vals, char* binning,
+                           hipStream_t s)
 {
     if (P <= 0 || L_cap == 0) return;
-    emit_index_kernel<<<div_up(P, 256), 256, 0, s>>>(P, g.offsets, block_owner);
+    emit_index_kernel<<<div_up(P, 256), 256, 0, s>>>(P, L_cap, count, g.offsets, block_owner);
     emit_kernel<<<div_up(L_cap, EMIT_BLOCK), EMIT_BLOCK, 0, s>>>(P, L_cap, count, g.order, g.offsets, block_owner,
-                                                                 g.splat, gx, tile_keys, gauss_vals);
+                                                                 g.splat, gx, tile_keys, gauss_vals, binning);
 }
 
 void launch_tile_ranges(size_t L_cap, const uint32_t* count, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s)

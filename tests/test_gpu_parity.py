@@ -92,6 +92,19 @@ def test_long_and_huge_row_segments():
     _compare(g, cam, dL)
 
 
+def test_capacity_hint_too_small_reruns_back_half():
+    """The binning buffer is sized from the last L of the view shape (capi.hip: capacity_hint); a scene with far
+    more instances at the same shape re-runs emit / tile sort / render at the exact size, which must clear what the
+    first pass wrote (tile ranges, tile costs) and give the same result as a fresh call."""
+    g0, cam0, _ = make_case(50, 144, 80, LON, 41, spread=1.0)
+    _, L0, _ = oracle_run(g0, cam0)
+    hip_run(g0, cam0, None)  # learns L0 for 144x80 lonlat
+    g, cam, dL = make_case(3000, 144, 80, LON, 42, view_index=3, spread=3.0)
+    _, L, _ = oracle_run(g, cam)
+    assert L > L0 + L0 // 8 + 4096, (L, L0)  # past the capacity hint: the back half runs twice
+    _compare(g, cam, dL)
+
+
 def test_white_background():
     g, cam, dL = make_case(1000, 128, 64, LON, 21, spread=3.0)
     _compare(g, cam, dL, bg=(1.0, 1.0, 1.0))
