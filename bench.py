@@ -191,7 +191,9 @@ def main():
     def exchange():
         if args.exchange == "compact":
             par.allreduce_compact_(grads, info, out["dL_dcolors"], campos,
-                                   lambda c, d, out: R.sh_grad_from_colors(means3D, shs, g.sh_degree, c, d, out=out))
+                                   lambda c, d, out: R.sh_grad_from_colors(means3D, shs, g.sh_degree, c, d, out=out),
+                                   rebuild_packed=lambda pk, out: R.sh_grad_from_colors_packed(means3D, shs,
+                                                                                              g.sh_degree, pk, out=out))
         else:
             par.allreduce_(grads, info, average=False, bucket_bytes=bucket)
 

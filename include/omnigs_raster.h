@@ -111,6 +111,10 @@ int omr_lonlat_backward(int P, int D, int M, int R, const float* background, int
  * Gaussian and view instead of all-reducing the 192-B SH gradient (M = 16). */
 int omr_sh_grad_from_colors(int P, int D, int M, int nviews, const float* means3D, const float* shs,
                             const float* campos, const float* dL_dcolors, float* dL_dsh, void* stream);
+/* The same with both inputs in one array packed[nviews][P + 1][3]: rows 0..P-1 of view v are its dL_dcolors, row P
+ * its camera position, so ranks exchange one all-gather of P + 1 rows instead of two collectives. */
+int omr_sh_grad_from_colors_packed(int P, int D, int M, int nviews, const float* means3D, const float* shs,
+                                   const float* packed, float* dL_dsh, void* stream);
 
 /* --- training loss (extension; reference include/loss_utils.h:31-129, gaussian_trainer.cpp:88-90) --- */
 /* loss = (1 - lambda) * mean|img - gt| + lambda * (1 - ssim(img, gt)) over [C,H,W] float images (11x11 Gaussian

@@ -559,8 +559,22 @@ int omr_sh_grad_from_colors(int P, int D, int M, int nviews, const float* means3
     if (P < 0 || nviews < 0 || M < 0 || M > 16) return fail(OMR_ERR_INVALID_ARGUMENT, "bad P / M / nviews");
     if (P == 0 || M == 0) return OMR_OK;
     if (!means3D || !shs || !campos || !dL_dcolors || !dL_dsh) return fail(OMR_ERR_INVALID_ARGUMENT, "missing pointer");
-    launch_sh_grad_from_colors(P, D, M, nviews, means3D, shs, campos, dL_dcolors, dL_dsh, (hipStream_t)stream);
+    launch_sh_grad_from_colors(P, D, M, nviews, means3D, shs, campos, 3, dL_dcolors, (size_t)P * 3, dL_dsh,
+                               (hipStream_t)stream);
     return hip_check("sh_grad_from_colors");
+}
+
+int omr_sh_grad_from_colors_packed(int P, int D, int M, int nviews, const float* means3D, const float* shs,
+                                   const float* packed, float* dL_dsh, void* stream)
+{
+    g_last_error.clear();
+    if (P < 0 || nviews < 0 || M < 0 || M > 16) return fail(OMR_ERR_INVALID_ARGUMENT, "bad P / M / nviews");
+    if (P == 0 || M == 0) return OMR_OK;
+    if (!means3D || !shs || !packed || !dL_dsh) return fail(OMR_ERR_INVALID_ARGUMENT, "missing pointer");
+    const size_t stride = ((size_t)P + 1) * 3;  // [nviews][P + 1][3]: P colour-gradient rows, then campos
+    launch_sh_grad_from_colors(P, D, M, nviews, means3D, shs, packed + (size_t)P * 3, stride, packed, stride, dL_dsh,
+                               (hipStream_t)stream);
+    return hip_check("sh_grad_from_colors_packed");
 }
 
 size_t omr_l1_ssim_scratch_floats(int C, int H, int W)

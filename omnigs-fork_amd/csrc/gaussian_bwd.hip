@@ -677,7 +677,8 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
 template <int MC>
 __global__ __launch_bounds__(256) void sh_grad_from_colors_kernel(int P, int D, int M, int nviews,
                                                                   const float* means3D, const float* shs,
-                                                                  const float* campos, const float* dL_dcolors,
+                                                                  const float* campos, size_t cp_stride,
+                                                                  const float* dL_dcolors, size_t dc_stride,
                                                                   float* dL_dsh)
 {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -708,11 +709,11 @@ __global__ __launch_bounds__(256) void sh_grad_from_colors_kernel(int P, int D, 
     for (int f = 0; f < 48; ++f) acc[f] = 0.f;
     const float px = means3D[3 * idx], py = means3D[3 * idx + 1], pz = means3D[3 * idx + 2];
     for (int v = 0; v < nviews; ++v) {
-        const float* dc = dL_dcolors + ((size_t)v * P + idx) * 3;
+        const float* dc = dL_dcolors + (size_t)v * dc_stride + (size_t)idx * 3;
         float d[3] = {dc[0], dc[1], dc[2]};
         if (d[0] == 0.f && d[1] == 0.f && d[2] == 0.f) continue;
         float x, y, z;
-        sh_direction(px, py, pz, campos + 3 * v, x, y, z);
+        sh_direction(px, py, pz, campos + (size_t)v * cp_stride, x, y, z);
         float rgb[3];
         uint8_t clamp_bits;
         sh_to_rgb(D, x, y, z, shv, rgb, clamp_bits);
@@ -742,14 +743,19 @@ __global__ __launch_bounds__(256) void sh_grad_from_colors_kernel(int P, int D, 
 }  // namespace
 
 void launch_sh_grad_from_colors(int P, int D, int M, int nviews, const float* means3D, const float* shs,
-                                const float* campos, const float* dL_dcolors, float* dL_dsh, hipStream_t s)
+                                const float* campos, size_t cp_stride, const float* dL_dcolors, size_t dc_stride,
+                                float* dL_dsh, hipStream_t s)
 {
     if (P <= 0) return;
     const bool m16 = M == 16 && (reinterpret_cast<uintptr_t>(shs) % 16) == 0 &&
                      (reinterpret_cast<uintptr_t>(dL_dsh) % 16) == 0;
     const dim3 grid(div_up(P, 256));
-    if (m16) sh_grad_from_colors_kernel<16><<<grid, 256, 0, s>>>(P, D, M, nviews, means3D, shs, campos, dL_dcolors, dL_dsh);
-    else sh_grad_from_colors_kernel<0><<<grid, 256, 0, s>>>(P, D, M, nviews, means3D, shs, campos, dL_dcolors, dL_dsh);
+    if (m16)
+        sh_grad_from_colors_kernel<16><<<grid, 256, 0, s>>>(P, D, M, nviews, means3D, shs, campos, cp_stride, dL_dcolors,
+                                                            dc_stride, dL_dsh);
+    else
+        sh_grad_from_colors_kernel<0><<<grid, 256, 0, s>>>(P, D, M, nviews, means3D, shs, campos, cp_stride, dL_dcolors,
+                                                           dc_stride, dL_dsh);
 }
 
 void launch_row_sums(int P, const uint32_t* row_first, const uint32_t* tiles_touched, const uint32_t* huge_list,

@@ -149,8 +149,10 @@ void launch_row_sums(int P, const uint32_t* row_first, const uint32_t* tiles_tou
                      const uint32_t* huge_count, const float* inst_grad, const uint8_t* row_valid, uint32_t R,
                      float* row_sums, hipStream_t s);
 // view-parallel DP: dL_dsh[P,M,3] = sum over views of dL/dsh rebuilt from dL_dcolors [nviews][P][3] + campos [nviews][3]
+// view v's colour gradient at dL_dcolors + v * dc_stride, its camera position at campos + v * cp_stride (floats)
 void launch_sh_grad_from_colors(int P, int D, int M, int nviews, const float* means3D, const float* shs,
-                                const float* campos, const float* dL_dcolors, float* dL_dsh, hipStream_t s);
+                                const float* campos, size_t cp_stride, const float* dL_dcolors, size_t dc_stride,
+                                float* dL_dsh, hipStream_t s);
 
 // ssim.hip: fused L1 + SSIM loss (loss_utils.h:31-129), forward and backward
 struct SsimWindow {

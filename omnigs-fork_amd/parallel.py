@@ -17,8 +17,8 @@ is no pack/unpack copy before or after the collective.
 Two exchanges give the same summed gradients (up to the order of the float additions):
   * allreduce_          one RCCL all-reduce of the whole 236 B/Gaussian buffer;
   * allreduce_compact_  (default in bench.py) all-reduce of the first 44 B/Gaussian (xyz, opacity, scale,
-                        rotation) and an all-gather of each view's colour gradient (12 B/Gaussian) and camera
-                        position; every rank then rebuilds the summed SH gradient with the backward's own SH
+                        rotation) and ONE all-gather of each view's colour gradient (12 B/Gaussian) with its camera
+                        position appended as an extra row; every rank then rebuilds the summed SH gradient with the backward's own SH
                         arithmetic (omr_sh_grad_from_colors). Per rank on a ring of n: 2(n-1)/n * 236 B/G vs
                         2(n-1)/n * 44 + (n-1) * 12 B/G — at n = 8, 413 vs 161 MB for 1 M Gaussians, at n = 2 236 vs
                         56 MB. xGMI is point-to-point (a 2-GPU job has ONE link), so bytes are the scaling cost.
@@ -59,12 +59,16 @@ class GradBuffer:
             self.views[name] = self.flat[off:off + n].view(shp)
             off += n
         self.extra = {}  # scratch outputs that are not reduced (dL_dmeans2D, dL_dcolors, dL_dcov3D)
+        # dL_dcolors lives in the first P rows of a [P + 1, 3] tensor whose last row takes the camera position, so the
+        # compact exchange gathers both with one collective (allreduce_compact_)
+        self.colors_ext = None
 
     def out_dict(self, device):
         P = self.P
         if not self.extra:
+            self.colors_ext = torch.empty((P + 1, 3), dtype=self.flat.dtype, device=device)
             self.extra = dict(dL_dmeans2D=torch.empty((P, 3), device=device),
-                              dL_dcolors=torch.empty((P, 3), device=device),
+                              dL_dcolors=self.colors_ext[:P],
                               dL_dcov3D=torch.empty((P, 6), device=device))
         d = dict(self.views)
         d.update(self.extra)
@@ -93,29 +97,32 @@ def allreduce_(buf: GradBuffer, info: DistInfo, average: bool = False, bucket_by
 
 
 def allreduce_compact_(buf: GradBuffer, info: DistInfo, dL_dcolors: torch.Tensor, campos: torch.Tensor, rebuild,
-                       average: bool = False):
+                       average: bool = False, rebuild_packed=None):
     """Sum over ranks with the compact SH exchange (module docstring): all-reduce the 11 non-SH floats per
-    Gaussian, all-gather every rank's dL_dcolors [P,3] and campos [3], then
-    rebuild(campos_all [n,3], dcolors_all [n,P,3], out=dL_dsh view) writes the summed SH gradient. `rebuild` is
-    rasterizer.sh_grad_from_colors bound to the (replicated) means3D / SH / degree; tests pass a CPU model."""
+    Gaussian, all-gather every rank's dL_dcolors [P,3] with its campos [3] appended as row P (one collective), then
+    rebuild the summed SH gradient into the dL_dsh view, either as
+    rebuild_packed(packed_all [n,P+1,3], out=...) (rasterizer.sh_grad_from_colors_packed bound to the replicated
+    means3D / SH / degree) or rebuild(campos_all [n,3], dcolors_all [n,P,3], out=...) (tests pass a CPU model)."""
     if not info.enabled:
         return
     n, P = info.world_size, buf.P
     prefix = buf.flat[:REDUCED_FLOATS * P]
     dist.all_reduce(prefix, op=dist.ReduceOp.SUM)
-    dc = dL_dcolors.contiguous().view(P, 3)
-    cp = campos.contiguous().view(3).to(dc.dtype)
+    ext = buf.colors_ext
+    if ext is None or dL_dcolors.data_ptr() != ext.data_ptr():  # colours not written into the packed tensor
+        ext = torch.empty((P + 1, 3), dtype=dL_dcolors.dtype, device=dL_dcolors.device)
+        ext[:P].copy_(dL_dcolors.reshape(P, 3))
+    ext[P].copy_(campos.reshape(3).to(ext.dtype))
     if dist.get_backend() == "nccl":
-        dcolors_all = torch.empty((n, P, 3), dtype=dc.dtype, device=dc.device)
-        campos_all = torch.empty((n, 3), dtype=dc.dtype, device=dc.device)
-        dist.all_gather_into_tensor(dcolors_all, dc)
-        dist.all_gather_into_tensor(campos_all, cp)
+        packed_all = torch.empty((n, P + 1, 3), dtype=ext.dtype, device=ext.device)
+        dist.all_gather_into_tensor(packed_all, ext)
     else:
-        parts = [torch.empty_like(dc) for _ in range(n)]
-        cps = [torch.empty_like(cp) for _ in range(n)]
-        dist.all_gather(parts, dc)
-        dist.all_gather(cps, cp)
-        dcolors_all, campos_all = torch.stack(parts), torch.stack(cps)
-    rebuild(campos_all, dcolors_all, out=buf.views["dL_dsh"])
+        parts = [torch.empty_like(ext) for _ in range(n)]
+        dist.all_gather(parts, ext)
+        packed_all = torch.stack(parts)
+    if rebuild_packed is not None:
+        rebuild_packed(packed_all, out=buf.views["dL_dsh"])
+    else:
+        rebuild(packed_all[:, P].contiguous(), packed_all[:, :P].contiguous(), out=buf.views["dL_dsh"])
     if average:
         buf.flat.div_(n)

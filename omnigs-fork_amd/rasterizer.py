@@ -68,6 +68,8 @@ def lib() -> C.CDLL:
         L.omr_debug_wave_sum9.argtypes = [vp, vp, vp]
         L.omr_profile_enable.argtypes = [i]
         L.omr_sh_grad_from_colors.argtypes = [i, i, i, i, vp, vp, vp, vp, vp, vp]
+        L.omr_sh_grad_from_colors_packed.restype = i
+        L.omr_sh_grad_from_colors_packed.argtypes = [i, i, i, i, vp, vp, vp, vp, vp]
         L.omr_l1_ssim_scratch_floats.restype = sz
         L.omr_l1_ssim_scratch_floats.argtypes = [i, i, i]
         L.omr_l1_ssim_loss.argtypes = [vp, vp, i, i, i, f, vp, vp, vp, vp]
@@ -272,6 +274,24 @@ def sh_grad_from_colors(means3D, sh, degree, campos_all, dcolors_all, out=None):
     rc = lib().omr_sh_grad_from_colors(P, int(degree), M, n, _ptr(m), _ptr(shc), _ptr(cp), _ptr(dc), out.data_ptr(),
                                        _stream(m.device))
     _check(rc, "sh_grad_from_colors")
+    return out
+
+
+def sh_grad_from_colors_packed(means3D, sh, degree, packed, out=None):
+    """sh_grad_from_colors with both inputs in one [n, P+1, 3] tensor: rows 0..P-1 of view v are its dL_dcolors, row
+    P its camera position (what parallel.allreduce_compact_ gathers with one collective)."""
+    m, shc, pk = _dev_f32(means3D, "means3D"), _dev_f32(sh, "sh"), _dev_f32(packed, "packed")
+    P, M = int(m.shape[0]), int(shc.shape[1])
+    if pk.dim() != 3 or tuple(pk.shape[1:]) != (P + 1, 3):
+        raise RasterizerError("packed must be [n, P+1, 3]")
+    n = int(pk.shape[0])
+    if out is None:
+        out = torch.empty((P, M, 3), dtype=torch.float32, device=m.device)
+    elif tuple(out.shape) != (P, M, 3) or not out.is_contiguous() or out.dtype != torch.float32:
+        raise RasterizerError(f"out must be a contiguous float32 tensor of shape {(P, M, 3)}")
+    rc = lib().omr_sh_grad_from_colors_packed(P, int(degree), M, n, _ptr(m), _ptr(shc), _ptr(pk), out.data_ptr(),
+                                              _stream(m.device))
+    _check(rc, "sh_grad_from_colors_packed")
     return out
 
 

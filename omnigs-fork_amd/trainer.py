@@ -73,6 +73,8 @@ def train_step(opt: O.GaussianOptimizer, viewpoint, image_height: int, image_wid
         opt.add_densification_stats(out["dL_dmeans2D"], radii)
     if dist_info is not None and dist_info.enabled:
         allreduce_compact_(state.buf, dist_info, out["dL_dcolors"], cp,
-                           lambda c, d, out: R.sh_grad_from_colors(means3D, shs, pc.active_sh_degree, c, d, out=out))
+                           lambda c, d, out: R.sh_grad_from_colors(means3D, shs, pc.active_sh_degree, c, d, out=out),
+                           rebuild_packed=lambda pk, out: R.sh_grad_from_colors_packed(means3D, shs,
+                                                                                      pc.active_sh_degree, pk, out=out))
     opt.step(raster_grads=out)
     return terms, image, radii

@@ -35,7 +35,10 @@ def test_sh_rebuild_equals_sum_of_views(cam_type, deg):
     rebuilt = R.sh_grad_from_colors(means, shs, deg, torch.stack(campos), torch.stack(dcolors))
     torch.cuda.synchronize()
     np.testing.assert_array_equal(to_np(rebuilt), to_np(dsh_sum))
-    model = sh_grad_from_colors_np(g.means3D, g.shs, deg, to_np(torch.stack(campos)), to_np(torch.stack(dcolors)))
+    # the packed layout parallel.allreduce_compact_ gathers: [n, P+1, 3], campos as row P of each view
+    packed = torch.cat([torch.stack(dcolors), torch.stack(campos)[:, None, :]], dim=1).contiguous()
+    np.testing.assert_array_equal(to_np(R.sh_grad_from_colors_packed(means, shs, deg, packed)), to_np(dsh_sum))
+    model =sh_grad_from_colors_np(g.means3D, g.shs, deg, to_np(torch.stack(campos)), to_np(torch.stack(dcolors)))
     ok, emax, nbad = grad_close(to_np(rebuilt), model)
     assert ok, (emax, nbad)
 
