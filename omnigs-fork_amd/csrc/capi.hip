@@ -167,9 +167,8 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s)
     g.key_b = c.take<uint32_t>(P);
     g.val_a = c.take<uint32_t>(P);
     g.val_b = c.take<uint32_t>(P);
-    const size_t nh = radix_hist_size(P);
     g.hist = c.take<uint32_t>(radix_scratch_words(P, DEPTH_SORT_PASSES));
-    g.scan_partials = c.take<uint32_t>(std::max(scan2_partials_size(P), scan_partials_size(nh)));
+    g.scan_partials = c.take<uint32_t>(std::max(scan2_partials_size(P), radix_partials_words(P)));
     g.offsets = c.take<uint32_t>(P);
     g.counters = c.take<uint32_t>(4);
     g.row_first = c.take<uint32_t>(P);
@@ -214,9 +213,8 @@ size_t BinningState::carve(char* base, size_t cap, BinningState* s, int tile_pas
     b.key_b = c.take<uint32_t>(cap);
     b.val_a = c.take<uint32_t>(cap);
     b.val_b = c.take<uint32_t>(cap);
-    const size_t nh = radix_hist_size(cap);
     b.hist = c.take<uint32_t>(radix_scratch_words(cap, tile_passes));
-    b.scan_partials = c.take<uint32_t>(scan_partials_size(nh));
+    b.scan_partials = c.take<uint32_t>(radix_partials_words(cap));  // look-back words of the histogram scan
     b.block_owner = c.take<uint32_t>(emit_index_size(cap));
     b.point_keys = (tile_passes & 1) != 0 ? b.key_b : b.key_a;  // result buffer of the key ping-pong
     if (s) *s = b;

@@ -45,8 +45,9 @@ void launch_mark_visible(int camera_type, int P, const float* means3D, const flo
 // scan block-sum scratch for n items (words)
 size_t scan_partials_size(size_t n);
 size_t radix_hist_size(size_t n);
-// words of the `hist` scratch radix_sort_pairs needs for n items over `passes` passes
+// words of the `hist` and `scan_partials` scratch radix_sort_pairs needs for n items over `passes` passes
 size_t radix_scratch_words(size_t n, int passes);
+size_t radix_partials_words(size_t n);
 // the forward's scans of tiles_touched (sort.hip): offsets = inclusive scan in depth order (gather by order),
 // row_first = exclusive scan in index order (gradient row numbering); huge_list / *huge_count (zeroed by the
 // caller) = the Gaussians with more than ROW_SUM_HUGE tiles; partials: scan2_partials_size(n) words

@@ -220,8 +220,8 @@ size_t knn_scratch_bytes(int P)
     const size_t nbox = div_up(n, KNN_BOX), nsuper = div_up(nbox, KNN_SUPER);
     Carver c(nullptr);
     c.take<uint32_t>(n), c.take<uint32_t>(n), c.take<uint32_t>(n), c.take<uint32_t>(n);
-    c.take<uint32_t>(radix_hist_size(n));
-    c.take<uint32_t>(std::max(scan_partials_size(n), scan_partials_size(radix_hist_size(n))));
+    c.take<uint32_t>(radix_scratch_words(n, 4));
+    c.take<uint32_t>(radix_partials_words(n));
     c.take<float4>(n);
     c.take<Bounds>(nbox), c.take<Bounds>(nsuper), c.take<Bounds>(BOUNDS_BLOCKS);
     return c.size();
@@ -235,8 +235,8 @@ void launch_knn(int P, const float* pts, float* dists, char* scratch, hipStream_
     Carver c(scratch);
     uint32_t *ka = c.take<uint32_t>(n), *kb = c.take<uint32_t>(n), *va = c.take<uint32_t>(n),
              *vb = c.take<uint32_t>(n);
-    uint32_t* hist = c.take<uint32_t>(radix_hist_size(n));
-    uint32_t* partials = c.take<uint32_t>(std::max(scan_partials_size(n), scan_partials_size(radix_hist_size(n))));
+    uint32_t* hist = c.take<uint32_t>(radix_scratch_words(n, 4));
+    uint32_t* partials = c.take<uint32_t>(radix_partials_words(n));
     float4* spts = c.take<float4>(n);
     Bounds* boxes = c.take<Bounds>(nbox);
     Bounds* supers = c.take<Bounds>(nsuper);

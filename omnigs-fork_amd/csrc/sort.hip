@@ -59,79 +59,6 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t* s
     return wave_off + inc - x;
 }
 
-// ---- scan ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(SCAN_THREADS) void scan_reduce_kernel(const uint32_t* in, const uint32_t* gather, size_t n,
-                                                                   uint32_t* partials)
-{
-    __shared__ uint32_t s_wave[SCAN_THREADS / 64];
-    const size_t base = (size_t)blockIdx.x * SCAN_TILE;
-    uint32_t sum = 0;
-#pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        const size_t i = base + (size_t)k * SCAN_THREADS + threadIdx.x;
-        if (i < n) sum += in[gather ? gather[i] : i];
-    }
-    uint32_t total;
-    block_exclusive_scan(sum, s_wave, &total);
-    if (threadIdx.x == 0) partials[blockIdx.x] = total;
-}
-
-// exclusive scan of partials[0..nb) in place by one block
-__global__ __launch_bounds__(SCAN_THREADS) void scan_partials_kernel(uint32_t* partials, uint32_t nb)
-{
-    __shared__ uint32_t s_wave[SCAN_THREADS / 64];
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < nb; base += SCAN_THREADS) {
-        const uint32_t i = base + threadIdx.x;
-        const uint32_t x = i < nb ? partials[i] : 0u;
-        uint32_t total;
-        const uint32_t ex = block_exclusive_scan(x, s_wave, &total);
-        if (i < nb) partials[i] = carry + ex;
-        carry += total;
-    }
-}
-
-// each block scans its 4096-item tile; the thread owning items [16t, 16t+16) of the tile works on LDS copies
-template <bool EXCLUSIVE>
-__global__ __launch_bounds__(SCAN_THREADS) void scan_downsweep_kernel(const uint32_t* in, const uint32_t* gather, size_t n,
-                                                                      const uint32_t* partials, uint32_t* out)
-{
-    __shared__ uint32_t s_data[SCAN_TILE + SCAN_TILE / 32];  // +1 pad per 32 to break the 16-stride conflicts
-    __shared__ uint32_t s_wave[SCAN_THREADS / 64];
-    const size_t base = (size_t)blockIdx.x * SCAN_TILE;
-    auto pad = [](uint32_t i) { return i + (i >> 5); };
-#pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        const uint32_t li = k * SCAN_THREADS + threadIdx.x;
-        const size_t i = base + li;
-        s_data[pad(li)] = i < n ? in[gather ? gather[i] : i] : 0u;
-    }
-    __syncthreads();
-    uint32_t v[SCAN_ITEMS];
-    uint32_t sum = 0;
-#pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        v[k] = s_data[pad(threadIdx.x * SCAN_ITEMS + k)];
-        sum += v[k];
-    }
-    uint32_t total;
-    uint32_t run = partials[blockIdx.x] + block_exclusive_scan(sum, s_wave, &total);
-#pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        const uint32_t x = v[k];
-        if (!EXCLUSIVE) run += x;
-        s_data[pad(threadIdx.x * SCAN_ITEMS + k)] = run;
-        if (EXCLUSIVE) run += x;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        const uint32_t li = k * SCAN_THREADS + threadIdx.x;
-        const size_t i = base + li;
-        if (i < n) out[i] = s_data[pad(li)];
-    }
-}
-
 // ---- the forward's two scans of tiles_touched, in one pass over the counts ----------------------------------
 // offsets   = inclusive scan in depth order (gather by `order`): the emission slots, num_rendered = offsets[P-1];
 // row_first = exclusive scan in Gaussian INDEX order: the first gradient row of each Gaussian. The backward numbers
@@ -242,6 +169,101 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_downsweep_kernel(const uin
     }
 }
 
+// Exclusive scan of a u32 array in ONE launch (decoupled look-back), for the [digit][block] histograms of the large
+// sorts (the 3-launch reduce / partials / downsweep scan before). Tiles of SCAN_TILE items are handed out by a
+// ticket; a tile publishes its total (AGG), looks back over its predecessors with one wave, 64 tiles per round
+// trip, until it meets an inclusive prefix (PRE), then publishes its own. 64-bit status words: flag in bits 62-63.
+// status / ticket: zeroed by the kernel launched before (radix_upsweep_kernel).
+constexpr uint64_t SLB_AGG = 1ull << 62, SLB_PRE = 2ull << 62, SLB_VAL = SLB_AGG - 1;
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src)
+{
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o, 64);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o, 64);
+        v += ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void scan_lookback_kernel(const uint32_t* in, uint32_t* out, size_t n,
+                                                                     uint64_t* status, uint32_t* ticket, uint32_t* err)
+{
+    __shared__ uint32_t s_data[SCAN_TILE + SCAN_TILE / 32];
+    __shared__ uint32_t s_wave[SCAN_THREADS / 64];
+    __shared__ uint32_t s_vb;
+    __shared__ uint64_t s_excl;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    if (tid == 0) s_vb = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t vb = s_vb;
+    const size_t base = (size_t)vb * SCAN_TILE;
+    auto pad = [](uint32_t i) { return i + (i >> 5); };
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint32_t li = k * SCAN_THREADS + tid;
+        const size_t i = base + li;
+        s_data[pad(li)] = i < n ? in[i] : 0u;
+    }
+    __syncthreads();
+    uint32_t v[SCAN_ITEMS];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        v[k] = s_data[pad(tid * SCAN_ITEMS + k)];
+        sum += v[k];
+    }
+    uint32_t total;
+    const uint32_t run0 = block_exclusive_scan(sum, s_wave, &total);
+    if (tid < 64) {  // wave 0: publish, look back, publish the inclusive prefix
+        uint64_t excl = 0;
+        if (vb == 0) {
+            if (tid == 0) __hip_atomic_store(&status[0], SLB_PRE | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (tid == 0) __hip_atomic_store(&status[vb], SLB_AGG | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t j = vb, spins = 0;  // next predecessor to read is j - 1 - lane
+            while (true) {
+                const uint64_t st = j > lane ? __hip_atomic_load(&status[j - 1 - lane], __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT)
+                                             : SLB_PRE;  // never reached: tile 0 publishes PRE
+                const uint64_t stop = __ballot((st & ~SLB_VAL) != SLB_AGG);  // PRE or not yet published
+                const uint32_t k = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
+                excl += wave_sum_u64(lane < k || (lane == k && (st & SLB_PRE)) ? (st & SLB_VAL) : 0ull);
+                if (k < 64u && (shfl_u64(st, (int)k) & SLB_PRE)) break;
+                if (k == 0 && ++spins > (1u << 20)) {  // bounded: a tile that never publishes sets the error word
+                    if (lane == 0) atomicOr(err, 1u);
+                    break;
+                }
+                if (k == 0) __builtin_amdgcn_s_sleep(1);
+                j -= k;
+            }
+            if (tid == 0)
+                __hip_atomic_store(&status[vb], SLB_PRE | (excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (tid == 0) s_excl = excl;
+    }
+    __syncthreads();
+    uint32_t run = (uint32_t)s_excl + run0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        s_data[pad(tid * SCAN_ITEMS + k)] = run;
+        run += v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint32_t li = k * SCAN_THREADS + tid;
+        const size_t i = base + li;
+        if (i < n) out[i] = s_data[pad(li)];
+    }
+}
+
 // sorts of at most this many 4096-item blocks (the depth sort up to 2M Gaussians) let each downsweep block derive
 // its digit offsets from the raw histogram: <= 512 KiB of L2 reads per block instead of three scan launches
 constexpr uint32_t SELF_SCAN_MAX_BLOCKS = 512;
@@ -259,8 +281,12 @@ __device__ __forceinline__ size_t live_count(size_t n, const uint32_t* count)
 template <bool BLOCK_MAJOR>
 __global__ __launch_bounds__(SORT_THREADS) void radix_upsweep_kernel(const uint32_t* keys, size_t n_cap,
                                                                      const uint32_t* count, int shift, uint32_t* hist,
-                                                                     uint32_t nblocks)
+                                                                     uint32_t nblocks, uint32_t* zero, uint32_t nzero)
 {
+    {   // the look-back words of the histogram scan that follows (scan_lookback_kernel)
+        const uint32_t z = blockIdx.x * SORT_THREADS + threadIdx.x;
+        if (z < nzero) zero[z] = 0u;
+    }
     const size_t n = live_count(n_cap, count);
     __shared__ uint32_t s_hist[RADIX];
     s_hist[threadIdx.x] = 0;
@@ -725,14 +751,7 @@ void launch_tile_order(const uint2* ranges, const uint32_t* cost, uint32_t T, ui
 
 size_t scan_partials_size(size_t n) { return div_up(n, SCAN_TILE) + 1; }
 
-static void launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t* partials, size_t n, hipStream_t s)
-{
-    if (n == 0) return;
-    const uint32_t nb = div_up(n, SCAN_TILE);
-    scan_reduce_kernel<<<nb, SCAN_THREADS, 0, s>>>(in, nullptr, n, partials);
-    scan_partials_kernel<<<1, SCAN_THREADS, 0, s>>>(partials, nb);
-    scan_downsweep_kernel<true><<<nb, SCAN_THREADS, 0, s>>>(in, nullptr, n, partials, out);
-}
+size_t radix_partials_words(size_t n) { return 2 * scan_partials_size(radix_hist_size(n)) + 2; }
 
 size_t scan2_partials_size(size_t n) { return 2 * scan_partials_size(n); }
 
@@ -803,12 +822,18 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
         const int shift = p * RADIX_BITS;
         const bool last = p == first_pass + passes - 1;
         if (nb <= SELF_SCAN_MAX_BLOCKS) {
-            radix_upsweep_kernel<true><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb);
+            radix_upsweep_kernel<true><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb, nullptr, 0);
             radix_downsweep_kernel<true><<<nb, SORT_THREADS, 0, s>>>(ki, vi, ko, vo, n, count, last ? canon : nullptr,
                                                                      shift, hist, nb);
         } else {
-            radix_upsweep_kernel<false><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb);
-            launch_exclusive_scan(hist, hist, scan_partials, (size_t)RADIX * nb, s);
+            // scan_partials: look-back status [nbs] (64-bit) | ticket | error word, zeroed by the upsweep
+            const uint32_t nbs = div_up((size_t)RADIX * nb, SCAN_TILE);
+            uint64_t* lb = reinterpret_cast<uint64_t*>(scan_partials);
+            uint32_t* lb_ticket = scan_partials + 2 * (size_t)nbs;
+            radix_upsweep_kernel<false><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb, scan_partials,
+                                                                    2 * nbs + 2);
+            scan_lookback_kernel<<<nbs, SCAN_THREADS, 0, s>>>(hist, hist, (size_t)RADIX * nb, lb, lb_ticket,
+                                                             lb_ticket + 1);
             radix_downsweep_kernel<false><<<nb, SORT_THREADS, 0, s>>>(ki, vi, ko, vo, n, count,
                                                                       last ? canon : nullptr, shift, hist, nb);
         }

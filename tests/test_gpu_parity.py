@@ -8,6 +8,8 @@ Bars (written here, checked per case):
     so a pixel whose alpha sits within an ulp of 1/255 or whose T lands within an ulp of 1e-4 may differ by one);
   * gradients: per element |gpu - oracle| <= 1e-3 |oracle| + 1e-4 max|oracle| (helpers.grad_close).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -103,6 +105,21 @@ def test_capacity_hint_too_small_reruns_back_half():
     _, L, _ = oracle_run(g, cam)
     assert L > L0 + L0 // 8 + 4096, (L, L0)  # past the capacity hint: the back half runs twice
     _compare(g, cam, dL)
+
+
+def test_config_C_forward_large_sort_paths():
+    """The bench workload itself (1 M Gaussians, 2048x1024 equirect, L = 7.9 M): the tile sort takes the large-sort
+    path (upsweep / look-back histogram scan / downsweep) that the small parity cases never reach, the row sums
+    Forward checked bit-exact (radii, instance list, ranges) and the image within 1e-4 (the backward at this size is
+    covered by the golden and smaller parity cases; the oracle backward would take minutes)."""
+    import oracle as O
+
+    O.set_threads(min(16, os.cpu_count() or 1))
+    g, cam, dL = scene.config_scene("C")
+    try:
+        _compare(g, cam, None)
+    finally:
+        O.set_threads(1)
 
 
 def test_white_background():
