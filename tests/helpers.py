@@ -70,6 +70,39 @@ def hip_run(g, cam, dL=None, bg=(0.0, 0.0, 0.0), colors_precomp=None, cov3D_prec
     return out
 
 
+def blend_threshold_flip(o, width, P, x, y, rel=1e-5):
+    """True when pixel (x, y)'s float64 re-blend of its tile list (oracle geometry, which the parity tests check
+    bit-exact) has a decision within `rel` of a threshold: alpha at 1/255 (skip, forward.cu:436-437) or T(1-alpha)
+    at 1e-4 (saturation, :440-444). There the GPU's v_exp and the oracle's expf may decide differently by one ulp,
+    and the pixel then differs by one Gaussian's contribution (up to |c|/255 T)."""
+    pl = o.get("point_list")
+    rg = o.get("ranges").reshape(-1, 2)
+    gx = (width + 15) // 16
+    t = (y // 16) * gx + x // 16
+    ids = pl[rg[t, 0]:rg[t, 1]]
+    m2 = o.get("means2D").reshape(P, 2)[ids].astype(np.float64)
+    co = o.get("conic_opacity").reshape(P, 4)[ids].astype(np.float64)
+    dx, dy = m2[:, 0] - x, m2[:, 1] - y
+    power = -0.5 * (co[:, 0] * dx * dx + co[:, 2] * dy * dy) - co[:, 1] * dx * dy
+    alpha = np.minimum(0.99, co[:, 3] * np.exp(power))
+    T = 1.0
+    for k in range(len(ids)):
+        if power[k] > 0:
+            continue
+        a = alpha[k]
+        if abs(a - 1 / 255) < rel / 255:
+            return True
+        if a < 1 / 255:
+            continue
+        tt = T * (1 - a)
+        if abs(tt - 1e-4) < rel * 1e-4:
+            return True
+        if tt < 1e-4:
+            break
+        T = tt
+    return False
+
+
 def to_np(x):
     return x.detach().cpu().numpy()
 

@@ -6,6 +6,9 @@ Bars (written here, checked per case):
   * forward colour: |gpu - oracle| <= 1e-4 absolute (north_star); final_T <= 1e-4 absolute;
     n_contrib equal on >= 99.99 % of pixels (exp() is the hardware v_exp on the GPU, glibc expf in the oracle,
     so a pixel whose alpha sits within an ulp of 1/255 or whose T lands within an ulp of 1e-4 may differ by one);
+    a pixel over 1e-4 is accepted only when a float64 re-blend of its tile list finds such a threshold decision
+    (helpers.blend_threshold_flip) and at most 1 in 1e5 pixels (at least 1) is one: config C (2 M pixels) has
+    one, |err| 3.6e-4 from a Gaussian with alpha = 1/255 (1 + 3e-6);
   * gradients: per element |gpu - oracle| <= 1e-3 |oracle| + 1e-4 max|oracle| (helpers.grad_close).
 """
 import os
@@ -13,7 +16,7 @@ import os
 import numpy as np
 import pytest
 
-from helpers import grad_close, hip_run, make_case, oracle_run, scene, to_np
+from helpers import blend_threshold_flip, grad_close, hip_run, make_case, oracle_run, scene, to_np
 
 pytestmark = pytest.mark.gpu
 
@@ -54,8 +57,11 @@ def _compare(g, cam, dL, **kw):
     np.testing.assert_array_equal(st["ranges"].astype(np.uint32).reshape(-1), o.get("ranges"))
     # forward image
     img_o = o.get("out_color").reshape(3, cam.height, cam.width)
-    err = np.abs(to_np(h["color"]) - img_o).max()
-    assert err <= 1e-4, f"out_color max abs err {err}"
+    err = np.abs(to_np(h["color"]) - img_o).max(0)
+    over = np.argwhere(err > 1e-4)
+    assert len(over) <= max(1, 1e-5 * err.size), f"out_color: {len(over)} pixels over 1e-4 (max {err.max()})"
+    for y, x in over:  # allowed only where a blend decision sits at a threshold (bar in the module docstring)
+        assert blend_threshold_flip(o, cam.width, P, int(x), int(y)), f"pixel ({x},{y}) err {err[y, x]} unexplained"
     np.testing.assert_allclose(st["final_T"], o.get("final_T"), rtol=0, atol=1e-4)
     same = (st["n_contrib"].astype(np.uint32) == o.get("n_contrib")).mean()
     assert same >= 0.9999, f"n_contrib agreement {same}"
