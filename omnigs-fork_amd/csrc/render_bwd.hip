@@ -8,6 +8,8 @@
 // render_fwd.hip. For each instance the wave accumulates, per lane and over the bands the instance reaches,
 // nine moments of the pixel weights u = G * dL/dalpha and the colour weights alpha * T:
 //     S_u, S_u dx, S_u dy, S_u dx^2, S_u dx dy, S_u dy^2, S_aT dpix_{r,g,b}
+// (a lane's four pixels share one column, so only S_u, S_u dy, S_u dy^2 are summed per band; the x-moments are
+// their dx-multiples)
 // The per-Gaussian constants of the reference's expressions (conic, opacity, 0.5 W, 0.5 H, -1/2) are linear
 // factors, so they are applied once per instance to the lane's sums — not once per pixel — and the nine values
 // are then summed over the wave in registers (DPP transposed butterfly + v_permlane{16,32}_swap, wave_ops.h).
@@ -170,8 +172,11 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
             const uint32_t ipos = __builtin_bit_cast(uint32_t, g.z);
             const Quad q = {qo.x, qo.y, qo.z};
             const float dx = g.x - pxf;
+            const ColQuad kq = column_quad(q, dx);
             const float dy0 = g.y - (float)tl.py0;
-            float su = 0.f, sux = 0.f, suy = 0.f, suxx = 0.f, suxy = 0.f, suyy = 0.f;
+            // dx is the same for all four of the lane's pixels (one column), so the x-moments are dx-multiples of
+            // the band sums: S_u dx = dx S_u, S_u dx^2 = dx^2 S_u, S_u dx dy = dx S_u dy (applied after the bands)
+            float su = 0.f, suy = 0.f, suyy = 0.f;
             float sc0 = 0.f, sc1 = 0.f, sc2 = 0.f;
             bool any = false;
 #pragma unroll
@@ -186,7 +191,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
                 const uint32_t lastb = last[b];
 #endif
                 const float dy = dy0 - (float)(4 * b);
-                const float p2 = falloff_p2(q, dx, dy);
+                const float p2 = falloff_p2(kq, dy);
                 const float G = __builtin_amdgcn_exp2f(p2);
                 const float alpha = fminf(0.99f, qo.w * G);
                 // backward.cu:770-781: skip positions at/after the pixel's last contributor, power > 0, alpha < 1/255
@@ -204,12 +209,9 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
                 s[b] = __builtin_fmaf(cdot, wc, s[b]);
                 T[b] = contrib ? Ti : T[b];
                 const float u = G * dL_dalpha;  // = dL/dopacity contribution; dL/dG * G = opacity * u
-                const float ux = u * dx, uy = u * dy;
+                const float uy = u * dy;
                 su += u;
-                sux += ux;
                 suy += uy;
-                suxx = __builtin_fmaf(ux, dx, suxx);
-                suxy = __builtin_fmaf(ux, dy, suxy);
                 suyy = __builtin_fmaf(uy, dy, suyy);
                 sc0 = __builtin_fmaf(wc, dp0b, sc0);
                 sc1 = __builtin_fmaf(wc, dp1b, sc1);
@@ -224,6 +226,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
             // conic (a, b, c) back from the staged quadratic form: q = (-a/2, -b, -c/2) log2(e)
             const float ca = q.qa * (-2.0f / LOG2E), cb = q.qb * (-1.0f / LOG2E), cc = q.qc * (-2.0f / LOG2E);
             const float o = qo.w;
+            const float sux = su * dx, suxx = sux * dx, suxy = suy * dx;
             float v[8];
             v[0] = -o * half_w * (ca * sux + cb * suy);  // dL/dmean2D.x
             v[1] = -o * half_h * (cc * suy + cb * sux);  // dL/dmean2D.y

@@ -122,13 +122,14 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
             const uint32_t contributor = __builtin_bit_cast(uint32_t, g.z) + 1u;
             const Quad q = {qo.x, qo.y, qo.z};
             const float dx = g.x - pxf;
+            const ColQuad kq = column_quad(q, dx);
             const float dy0 = g.y - (float)tl.py(band0);
             bool sat_any = false;
 #pragma unroll
             for (int b = 0; b < FWD_BANDS; ++b) {
                 if (!(mb & (1u << b))) continue;  // scalar branch
                 const float dy = dy0 - (float)(4 * b);
-                const float p2 = falloff_p2(q, dx, dy);
+                const float p2 = falloff_p2(kq, dy);
                 const float alpha = fminf(0.99f, qo.w * __builtin_amdgcn_exp2f(p2));
                 bool ok = !done[b] && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
                 const float test_T = T[b] * (1.0f - alpha);

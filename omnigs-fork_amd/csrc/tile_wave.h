@@ -17,8 +17,8 @@ constexpr float LOG2E = 1.4426950408889634f;
 
 // Gaussian falloff in base 2: p2 = log2(e) * power, power = -1/2 (a dx^2 + c dy^2) - b dx dy
 // (forward.cu:434 / backward.cu:774). The staging lane folds -1/2 and log2(e) into q = {qa, qb, qc} once per
-// instance, so each (pixel, instance) pair costs four VALU ops before v_exp_f32. Forward and backward evaluate
-// exactly this expression, so they take identical contribute / skip decisions.
+// instance, so each (pixel, instance) pair costs three VALU ops (dy, two FMAs) before v_exp_f32. Forward and backward
+// evaluate exactly this expression, so they take identical contribute / skip decisions.
 struct Quad {
     float qa, qb, qc;
 };
@@ -26,9 +26,18 @@ __device__ __forceinline__ Quad quad_of_conic(float4 co)
 {
     return {-0.5f * LOG2E * co.x, -LOG2E * co.y, -0.5f * LOG2E * co.z};
 }
-__device__ __forceinline__ float falloff_p2(const Quad& q, float dx, float dy)
+// A lane's pixels share one column (dx), so p2 is taken as a quadratic in dy whose dx-terms are formed once per
+// instance: p2 = A + dy (B + qc dy), A = qa dx^2, B = qb dx — two FMAs per pixel after the per-instance setup.
+struct ColQuad {
+    float A, B, C;
+};
+__device__ __forceinline__ ColQuad column_quad(const Quad& q, float dx)
 {
-    return __builtin_fmaf(dx, __builtin_fmaf(q.qa, dx, q.qb * dy), q.qc * dy * dy);
+    return {q.qa * dx * dx, q.qb * dx, q.qc};
+}
+__device__ __forceinline__ float falloff_p2(const ColQuad& k, float dy)
+{
+    return __builtin_fmaf(dy, __builtin_fmaf(k.C, dy, k.B), k.A);
 }
 
 // one lane's view of a tile: pixel coordinates of its band pixels; band b of the tile = rows 4b..4b+3
