@@ -64,6 +64,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
     __shared__ float4 s_geo_all[TW_WAVES][TW_BATCH];   // x, y, position in range (u32 bits), band mask (u32 bits)
     __shared__ float4 s_quad_all[TW_WAVES][TW_BATCH];  // qa, qb, qc, opacity
     __shared__ float4 s_rgb_all[TW_WAVES][TW_BATCH];   // colour, gradient row slot (u32 bits)
+    __shared__ float s_floor_all[TW_WAVES][TW_BATCH];  // p2_floor(opacity)
 #if OMR_BWD_PIX_LDS
     __shared__ float4 s_pix_all[TW_WAVES][TW_BANDS][64];  // dL/dpix rgb, last contributor (u32 bits)
 #endif
@@ -79,6 +80,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
     float4* s_geo = s_geo_all[wv];
     float4* s_quad = s_quad_all[wv];
     float4* s_rgb = s_rgb_all[wv];
+    float* s_floor = s_floor_all[wv];
     const TileLane tl(tile, a.gx);
     const uint32_t lane = tl.lane;
     const float pxf = (float)tl.px;
@@ -160,6 +162,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
             s_geo[r] = make_float4(p.x, p.y, __builtin_bit_cast(float, pos), __builtin_bit_cast(float, m));
             s_quad[r] = make_float4(q.qa, q.qb, q.qc, co.w);
             s_rgb[r] = make_float4(c.x, c.y, c.z, __builtin_bit_cast(float, slot));
+            s_floor[r] = p2_floor(co.w);
         }
         wave_sync();  // orders this wave's LDS stores before its reads below
         const uint32_t nuse = (uint32_t)__popcll(useful);
@@ -168,6 +171,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
             const float4 g = s_geo[j];
             const float4 qo = s_quad[j];
             const float4 f = s_rgb[j];
+            const float pfloor = s_floor[j];
             const uint32_t mb = uniform(__builtin_bit_cast(uint32_t, g.w));
             const uint32_t ipos = __builtin_bit_cast(uint32_t, g.z);
             const Quad q = {qo.x, qo.y, qo.z};
@@ -192,22 +196,23 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
 #endif
                 const float dy = dy0 - (float)(4 * b);
                 const float p2 = falloff_p2(kq, dy);
-                const float G = __builtin_amdgcn_exp2f(p2);
-                const float alpha = fminf(0.99f, qo.w * G);
                 // backward.cu:770-781: skip positions at/after the pixel's last contributor, power > 0, alpha < 1/255
-                const bool contrib = ipos < lastb && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
+                const bool contrib = ipos < lastb && p2 <= 0.0f && p2 >= pfloor;
                 BWD_COUNT(1, 1);
                 if (!__ballot(contrib)) continue;
                 BWD_COUNT(2, 1);
                 BWD_COUNT(4, (uint32_t)__popcll(__ballot(contrib)));
                 any = true;
+                // a lane that does not contribute gets G = alpha = 0: inv = 1, T and s unchanged, u = wc = 0
+                const float G = __builtin_amdgcn_exp2f(contrib ? p2 : -__builtin_inff());
+                const float alpha = fminf(0.99f, qo.w * G);
                 const float inv = __builtin_amdgcn_rcpf(1.0f - alpha);
                 const float Ti = T[b] * inv;
                 const float cdot = __builtin_fmaf(f.x, dp0b, __builtin_fmaf(f.y, dp1b, f.z * dp2b));
-                const float dL_dalpha = contrib ? __builtin_fmaf(Ti, cdot, -s[b] * inv) : 0.0f;
-                const float wc = contrib ? alpha * Ti : 0.0f;  // dchannel/dcolour (backward.cu:800)
+                const float dL_dalpha = __builtin_fmaf(Ti, cdot, -s[b] * inv);
+                const float wc = alpha * Ti;  // dchannel/dcolour (backward.cu:800)
                 s[b] = __builtin_fmaf(cdot, wc, s[b]);
-                T[b] = contrib ? Ti : T[b];
+                T[b] = Ti;
                 const float u = G * dL_dalpha;  // = dL/dopacity contribution; dL/dG * G = opacity * u
                 const float uy = u * dy;
                 su += u;

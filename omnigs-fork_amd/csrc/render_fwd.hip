@@ -46,6 +46,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
     __shared__ float4 s_geo_all[TW_WAVES][TW_BATCH];  // x, y, position in range (u32 bits), band mask (u32 bits)
     __shared__ float4 s_quad_all[TW_WAVES][TW_BATCH]; // qa, qb, qc, opacity
     __shared__ float4 s_rgb_all[TW_WAVES][TW_BATCH];  // feature (colour, or depth for DEPTH)
+    __shared__ float s_floor_all[TW_WAVES][TW_BATCH];  // p2_floor(opacity)
 
     OMR_STAMP_BEGIN
     const uint32_t wv = threadIdx.x >> 6;
@@ -54,6 +55,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
     float4* s_geo = s_geo_all[wv];
     float4* s_quad = s_quad_all[wv];
     float4* s_rgb = s_rgb_all[wv];
+    float* s_floor = s_floor_all[wv];
 #ifdef OMR_NO_TILE_ORDER
     const uint32_t tile = unit / FWD_GROUPS;
 #else
@@ -103,6 +105,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
             s_geo[r] = make_float4(pos.x, pos.y, __builtin_bit_cast(float, k), __builtin_bit_cast(float, m));
             s_quad[r] = make_float4(q.qa, q.qb, q.qc, co.w);
             s_rgb[r] = c;
+            s_floor[r] = p2_floor(co.w);
         }
         wave_sync();  // orders this wave's LDS stores before its reads below
         const uint32_t cnt = (uint32_t)__popcll(useful);
@@ -117,6 +120,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
             qo = s_quad[j];
             f = s_rgb[j];
 #endif
+            const float pfloor = s_floor[j];
             const uint32_t mb = uniform(__builtin_bit_cast(uint32_t, g.w)) & active;
             work += (uint32_t)__builtin_popcount(mb);
             const uint32_t contributor = __builtin_bit_cast(uint32_t, g.z) + 1u;
@@ -130,18 +134,21 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
                 if (!(mb & (1u << b))) continue;  // scalar branch
                 const float dy = dy0 - (float)(4 * b);
                 const float p2 = falloff_p2(kq, dy);
-                const float alpha = fminf(0.99f, qo.w * __builtin_amdgcn_exp2f(p2));
-                bool ok = !done[b] && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
+                bool ok = !done[b] && p2 <= 0.0f && p2 >= pfloor;  // alpha >= 1/255 (tile_wave.h: p2_floor)
+                // a lane that is not ok gets alpha = 0: test_T = T, wgt = 0
+                const float alpha = fminf(0.99f, qo.w * __builtin_amdgcn_exp2f(ok ? p2 : -__builtin_inff()));
                 const float test_T = T[b] * (1.0f - alpha);
-                const bool sat = ok && test_T < 0.0001f;
+                // T >= 1e-4 always holds (T only takes values that passed this test), and a lane that is not ok has
+                // test_T = T: so sat implies ok
+                const bool sat = test_T < 0.0001f;
                 done[b] = done[b] || sat;
                 sat_any = sat_any || sat;
                 ok = ok && !sat;
-                const float wgt = ok ? alpha * T[b] : 0.0f;
+                const float wgt = sat ? 0.0f : alpha * T[b];
                 C0[b] = __builtin_fmaf(f.x, wgt, C0[b]);
                 C1[b] = __builtin_fmaf(f.y, wgt, C1[b]);
                 C2[b] = __builtin_fmaf(f.z, wgt, C2[b]);
-                T[b] = ok ? test_T : T[b];
+                T[b] = sat ? T[b] : test_T;
                 last[b] = ok ? contributor : last[b];
             }
             if (__ballot(sat_any)) {  // some pixel saturated: drop bands with no live pixel left

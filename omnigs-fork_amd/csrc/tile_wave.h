@@ -40,6 +40,13 @@ __device__ __forceinline__ float falloff_p2(const ColQuad& k, float dy)
     return __builtin_fmaf(dy, __builtin_fmaf(k.C, dy, k.B), k.A);
 }
 
+// The reference's skip test alpha = min(0.99, o 2^p2) < 1/255 (forward.cu:436-437, backward.cu:778-779) as a
+// bound on p2 formed once per instance: o 2^p2 >= 1/255  <=>  p2 >= -log2(255 o). Both render kernels test
+// p2 <= 0 && p2 >= p2_floor BEFORE v_exp_f32 and feed v_exp -inf for a pixel that does not contribute, so G, alpha
+// and every product built from them are exactly 0 there without per-result selects. v_log_f32 is within an ulp,
+// so the boundary moves by < 1e-6 relative in alpha (the same class as v_exp_f32 vs expf).
+__device__ __forceinline__ float p2_floor(float opacity) { return -__builtin_amdgcn_logf(255.0f * opacity); }
+
 // one lane's view of a tile: pixel coordinates of its band pixels; band b of the tile = rows 4b..4b+3
 struct TileLane {
     uint32_t tx, ty, lane;
