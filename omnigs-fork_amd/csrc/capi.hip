@@ -168,7 +168,8 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s)
     g.val_a = c.take<uint32_t>(P);
     g.val_b = c.take<uint32_t>(P);
     g.hist = c.take<uint32_t>(radix_scratch_words(P, DEPTH_SORT_PASSES));
-    g.scan_partials = c.take<uint32_t>(std::max(scan2_partials_size(P), radix_partials_words(P)));
+    g.scan_partials = c.take<uint32_t>(radix_partials_words(P));
+    g.scan2_status = c.take<uint32_t>(scan2_status_words(P));
     g.offsets = c.take<uint32_t>(P);
     g.counters = c.take<uint32_t>(4);
     g.row_first = c.take<uint32_t>(P);
@@ -297,6 +298,7 @@ int forward_impl(const ForwardIn& in)
     pa.zero[1] = {reinterpret_cast<uint32_t*>(im.ranges), 2 * (size_t)d.T};  // tile_ranges writes boundaries only
     pa.zero[2] = {im.tile_cost, (size_t)d.T};                          // render_forward adds into it
     pa.zero[3] = radix_zero_span(g.hist, P, DEPTH_SORT_PASSES);        // the depth sort's digit totals / tickets
+    pa.zero[4] = {g.scan2_status, scan2_status_words(P)};             // the forward scans' look-back words
     pa.P = in.P; pa.D = in.D; pa.M = in.M; pa.W = in.width; pa.H = in.height; pa.gx = d.gx; pa.gy = d.gy;
     pa.means3D = in.means3D; pa.scales = in.scales; pa.scale_modifier = in.scale_modifier; pa.rotations = in.rotations;
     pa.opacities = in.opacities; pa.shs = in.shs; pa.cov3D_precomp = in.cov3D_precomp; pa.colors_precomp = in.colors_precomp;
@@ -313,7 +315,7 @@ int forward_impl(const ForwardIn& in)
     // depth order of the Gaussians (stable: ties keep index order)
     int which; { StageScope st_(ST_DEPTH_SORT, s); which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr, nullptr, 0, DEPTH_SORT_PASSES, s, true); }
     g.order = which ? g.val_b : g.val_a;
-    { StageScope st_(ST_SCAN, s); launch_forward_scans(g.tiles_touched, g.order, g.offsets, g.row_first, g.huge_list, g.counters + 2, g.scan_partials, P, s); }
+    { StageScope st_(ST_SCAN, s); launch_forward_scans(g.tiles_touched, g.order, g.offsets, g.row_first, g.huge_list, g.counters + 2, g.scan2_status, P, s); }
 
     // num_rendered = offsets[P-1] (+ the prefiltered error flag) to pinned host memory, without waiting for it:
     // the binning buffer is sized from a capacity hint and everything after the scan reads the count on the device,

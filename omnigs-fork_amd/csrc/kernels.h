@@ -12,7 +12,7 @@ struct ZeroSpan {
     uint32_t* p = nullptr;
     size_t n = 0;
 };
-constexpr int PRE_ZERO_SPANS = 4;
+constexpr int PRE_ZERO_SPANS = 5;
 
 struct PreprocessArgs {
     ZeroSpan zero[PRE_ZERO_SPANS];
@@ -50,10 +50,11 @@ size_t radix_scratch_words(size_t n, int passes);
 size_t radix_partials_words(size_t n);
 // the forward's scans of tiles_touched (sort.hip): offsets = inclusive scan in depth order (gather by order),
 // row_first = exclusive scan in index order (gradient row numbering); huge_list / *huge_count (zeroed by the
-// caller) = the Gaussians with more than ROW_SUM_HUGE tiles; partials: scan2_partials_size(n) words
-size_t scan2_partials_size(size_t n);
+// caller) = the Gaussians with more than ROW_SUM_HUGE tiles; status: scan2_status_words(n) words, zeroed before
+// the launch (one look-back kernel)
+size_t scan2_status_words(size_t n);
 void launch_forward_scans(const uint32_t* tiles_touched, const uint32_t* order, uint32_t* offsets, uint32_t* row_first,
-                          uint32_t* huge_list, uint32_t* huge_count, uint32_t* partials, size_t n, hipStream_t s);
+                          uint32_t* huge_list, uint32_t* huge_count, uint32_t* status, size_t n, hipStream_t s);
 // stable LSD radix sort of (key, value) over bits [0, 8*passes); returns which buffer holds the result (0: a, 1: b).
 // n = capacity; count (device, may be NULL) = live element count <= n. canon != NULL: the last pass writes the
 // values to the canonical point list of the binning buffer at canon (raster_common.h) instead of val_a / val_b.

@@ -79,6 +79,7 @@ struct GeomState {
     uint32_t* val_b;
     uint32_t* hist;           // radix histograms [RADIX][blocks]
     uint32_t* scan_partials;  // scan block sums
+    uint32_t* scan2_status;   // look-back words of the forward scans (launch_forward_scans), zeroed by preprocess
     uint32_t* offsets;        // inclusive scan of tiles_touched in depth order
     uint32_t* counters;       // [0] = num_rendered
     uint32_t* order;          // depth order (points at val_a or val_b after the sort)

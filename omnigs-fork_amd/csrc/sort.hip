@@ -59,121 +59,10 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t* s
     return wave_off + inc - x;
 }
 
-// ---- the forward's two scans of tiles_touched, in one pass over the counts ----------------------------------
-// offsets   = inclusive scan in depth order (gather by `order`): the emission slots, num_rendered = offsets[P-1];
-// row_first = exclusive scan in Gaussian INDEX order: the first gradient row of each Gaussian. The backward numbers
-//             its per-instance gradient rows this way (render_bwd.hip), so the 64 Gaussians of a wave own one
-//             contiguous span of rows when their sums are taken (gaussian_bwd.hip: row_sum_kernel).
-// Both sequences have the same block structure, so one reduce / partials / downsweep launch triple does both;
-// partials holds the two block-sum arrays back to back (2 * nb words). The downsweep also lists the Gaussians with
-// more than ROW_SUM_HUGE tiles (huge_list, in no particular order), whose row sums take a whole workgroup.
-__global__ __launch_bounds__(SCAN_THREADS) void scan2_reduce_kernel(const uint32_t* in, const uint32_t* order, size_t n,
-                                                                    uint32_t* partials, uint32_t nb)
-{
-    __shared__ uint32_t s_wave[SCAN_THREADS / 64];
-    const size_t base = (size_t)blockIdx.x * SCAN_TILE;
-    uint32_t sum_d = 0, sum_i = 0;
-#pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        const size_t i = base + (size_t)k * SCAN_THREADS + threadIdx.x;
-        if (i < n) {
-            sum_d += in[order[i]];
-            sum_i += in[i];
-        }
-    }
-    uint32_t total_d, total_i;
-    block_exclusive_scan(sum_d, s_wave, &total_d);
-    block_exclusive_scan(sum_i, s_wave, &total_i);
-    if (threadIdx.x == 0) {
-        partials[blockIdx.x] = total_d;
-        partials[nb + blockIdx.x] = total_i;
-    }
-}
-
-// block 0 scans the depth-order block sums, block 1 the index-order ones
-__global__ __launch_bounds__(SCAN_THREADS) void scan2_partials_kernel(uint32_t* partials, uint32_t nb)
-{
-    __shared__ uint32_t s_wave[SCAN_THREADS / 64];
-    uint32_t* part = partials + (size_t)blockIdx.x * nb;
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < nb; base += SCAN_THREADS) {
-        const uint32_t i = base + threadIdx.x;
-        const uint32_t x = i < nb ? part[i] : 0u;
-        uint32_t total;
-        const uint32_t ex = block_exclusive_scan(x, s_wave, &total);
-        if (i < nb) part[i] = carry + ex;
-        carry += total;
-    }
-}
-
-// the thread owning items [16t, 16t+16) of the block's tile scans LDS copies of both sequences
-__global__ __launch_bounds__(SCAN_THREADS) void scan2_downsweep_kernel(const uint32_t* in, const uint32_t* order, size_t n,
-                                                                       const uint32_t* partials, uint32_t nb,
-                                                                       uint32_t* offsets, uint32_t* row_first,
-                                                                       uint32_t* huge_list, uint32_t* huge_count)
-{
-    __shared__ uint32_t s_d[SCAN_TILE + SCAN_TILE / 32];  // +1 pad per 32 to break the 16-stride conflicts
-    __shared__ uint32_t s_i[SCAN_TILE + SCAN_TILE / 32];
-    __shared__ uint32_t s_wave[SCAN_THREADS / 64];
-    const size_t base = (size_t)blockIdx.x * SCAN_TILE;
-    auto pad = [](uint32_t i) { return i + (i >> 5); };
-#pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        const uint32_t li = k * SCAN_THREADS + threadIdx.x;
-        const size_t i = base + li;
-        s_d[pad(li)] = i < n ? in[order[i]] : 0u;
-        s_i[pad(li)] = i < n ? in[i] : 0u;
-    }
-    __syncthreads();
-    uint32_t vd[SCAN_ITEMS], vi[SCAN_ITEMS];
-    uint32_t sum_d = 0, sum_i = 0;
-#pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        vd[k] = s_d[pad(threadIdx.x * SCAN_ITEMS + k)];
-        vi[k] = s_i[pad(threadIdx.x * SCAN_ITEMS + k)];
-        sum_d += vd[k];
-        sum_i += vi[k];
-    }
-    uint32_t total;
-    uint32_t run_d = partials[blockIdx.x] + block_exclusive_scan(sum_d, s_wave, &total);
-    uint32_t run_i = partials[nb + blockIdx.x] + block_exclusive_scan(sum_i, s_wave, &total);
-#pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        run_d += vd[k];  // inclusive
-        s_d[pad(threadIdx.x * SCAN_ITEMS + k)] = run_d;
-        s_i[pad(threadIdx.x * SCAN_ITEMS + k)] = run_i;  // exclusive
-        run_i += vi[k];
-    }
-    // the block's huge Gaussians get consecutive list slots: LDS ranks, one global reservation per block
-    __shared__ uint32_t s_huge, s_huge_base;
-    if (threadIdx.x == 0) s_huge = 0;
-    __syncthreads();
-    uint32_t hrank[SCAN_ITEMS];
-#pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        const size_t i = base + k * SCAN_THREADS + threadIdx.x;
-        hrank[k] = i < n && in[i] > ROW_SUM_HUGE ? atomicAdd(&s_huge, 1u) : 0xFFFFFFFFu;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) s_huge_base = s_huge ? atomicAdd(huge_count, s_huge) : 0u;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        const uint32_t li = k * SCAN_THREADS + threadIdx.x;
-        const size_t i = base + li;
-        if (i < n) {
-            offsets[i] = s_d[pad(li)];
-            row_first[i] = s_i[pad(li)];
-            if (hrank[k] != 0xFFFFFFFFu) huge_list[s_huge_base + hrank[k]] = (uint32_t)i;
-        }
-    }
-}
-
-// Exclusive scan of a u32 array in ONE launch (decoupled look-back), for the [digit][block] histograms of the large
-// sorts (the 3-launch reduce / partials / downsweep scan before). Tiles of SCAN_TILE items are handed out by a
-// ticket; a tile publishes its total (AGG), looks back over its predecessors with one wave, 64 tiles per round
-// trip, until it meets an inclusive prefix (PRE), then publishes its own. 64-bit status words: flag in bits 62-63.
-// status / ticket: zeroed by the kernel launched before (radix_upsweep_kernel).
+// ---- decoupled look-back (single-launch scans) -------------------------------------------------------------
+// Tiles are handed out by a ticket; a tile publishes its total (AGG), looks back over its predecessors with one
+// wave, 64 tiles per round trip, until it meets an inclusive prefix (PRE), then publishes its own. 64-bit status
+// words, flag in bits 62-63, zeroed before the launch.
 constexpr uint64_t SLB_AGG = 1ull << 62, SLB_PRE = 2ull << 62, SLB_VAL = SLB_AGG - 1;
 
 __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src)
@@ -192,6 +81,124 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
     return v;
 }
 
+// Called by all 64 lanes of one wave of tile vb: publishes `total`, returns the exclusive prefix of the tile (on every
+// lane) and publishes the inclusive one. A predecessor that never publishes ends the wait after 2^20 polls with the
+// error word set (no hang).
+__device__ uint64_t wave_lookback(uint64_t* status, uint32_t vb, uint32_t total, uint32_t lane, uint32_t* err)
+{
+    if (vb == 0) {
+        if (lane == 0) __hip_atomic_store(&status[0], SLB_PRE | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    if (lane == 0) __hip_atomic_store(&status[vb], SLB_AGG | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t excl = 0;
+    uint32_t j = vb, spins = 0;  // next predecessor to read is j - 1 - lane
+    while (true) {
+        const uint64_t st = j > lane ? __hip_atomic_load(&status[j - 1 - lane], __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)
+                                     : SLB_PRE;  // never reached: tile 0 publishes PRE
+        const uint64_t stop = __ballot((st & ~SLB_VAL) != SLB_AGG);  // PRE or not yet published
+        const uint32_t k = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
+        excl += wave_sum_u64(lane < k || (lane == k && (st & SLB_PRE)) ? (st & SLB_VAL) : 0ull);
+        if (k < 64u && (shfl_u64(st, (int)k) & SLB_PRE)) break;
+        if (k == 0 && ++spins > (1u << 20)) {
+            if (lane == 0) atomicOr(err, 1u);
+            break;
+        }
+        if (k == 0) __builtin_amdgcn_s_sleep(1);
+        j -= k;
+    }
+    if (lane == 0) __hip_atomic_store(&status[vb], SLB_PRE | (excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
+// ---- the forward's two scans of tiles_touched, in one launch ---------------------------------------------------
+// offsets   = inclusive scan in depth order (gather by `order`): the emission slots, num_rendered = offsets[P-1];
+// row_first = exclusive scan in Gaussian INDEX order: the first gradient row of each Gaussian. The backward numbers
+//             its per-instance gradient rows this way (render_bwd.hip), so the 64 Gaussians of a wave own one
+//             contiguous span of rows when their sums are taken (gaussian_bwd.hip: row_sum_kernel).
+// Both sequences have the same tile structure: each 4096-item tile scans both in LDS, and its wave 0 / wave 1 find
+// the two exclusive prefixes by decoupled look-back at the same time (status_d / status_i, ticket, error word:
+// scan2_status_words(n), zeroed by preprocess). The kernel also lists the Gaussians with more than ROW_SUM_HUGE
+// tiles (huge_list, in no particular order), whose row sums take a whole workgroup.
+__global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint32_t* in, const uint32_t* order, size_t n,
+                                                                      uint64_t* status_d, uint64_t* status_i,
+                                                                      uint32_t* ticket, uint32_t* err,
+                                                                      uint32_t* offsets, uint32_t* row_first,
+                                                                      uint32_t* huge_list, uint32_t* huge_count)
+{
+    __shared__ uint32_t s_d[SCAN_TILE + SCAN_TILE / 32];  // +1 pad per 32 to break the 16-stride conflicts
+    __shared__ uint32_t s_i[SCAN_TILE + SCAN_TILE / 32];
+    __shared__ uint32_t s_wave[SCAN_THREADS / 64];
+    __shared__ uint32_t s_vb, s_huge, s_huge_base;
+    __shared__ uint32_t s_excl[2];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    if (tid == 0) {
+        s_vb = atomicAdd(ticket, 1u);
+        s_huge = 0;
+    }
+    __syncthreads();
+    const uint32_t vb = s_vb;
+    const size_t base = (size_t)vb * SCAN_TILE;
+    auto pad = [](uint32_t i) { return i + (i >> 5); };
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint32_t li = k * SCAN_THREADS + tid;
+        const size_t i = base + li;
+        s_d[pad(li)] = i < n ? in[order[i]] : 0u;
+        s_i[pad(li)] = i < n ? in[i] : 0u;
+    }
+    __syncthreads();
+    uint32_t vd[SCAN_ITEMS], vi[SCAN_ITEMS];
+    uint32_t sum_d = 0, sum_i = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        vd[k] = s_d[pad(tid * SCAN_ITEMS + k)];
+        vi[k] = s_i[pad(tid * SCAN_ITEMS + k)];
+        sum_d += vd[k];
+        sum_i += vi[k];
+    }
+    uint32_t total_d, total_i;
+    uint32_t run_d = block_exclusive_scan(sum_d, s_wave, &total_d);
+    uint32_t run_i = block_exclusive_scan(sum_i, s_wave, &total_i);
+    if (tid < 128) {  // wave 0: depth order, wave 1: index order
+        const bool dep = tid < 64;
+        const uint64_t excl = wave_lookback(dep ? status_d : status_i, vb, dep ? total_d : total_i, lane, err);
+        if (lane == 0) s_excl[dep ? 0 : 1] = (uint32_t)excl;
+    }
+    // the tile's huge Gaussians get consecutive list slots: LDS ranks, one global reservation per tile
+    uint32_t hrank[SCAN_ITEMS];
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint32_t li = k * SCAN_THREADS + tid;
+        hrank[k] = base + li < n && s_i[pad(li)] > ROW_SUM_HUGE ? atomicAdd(&s_huge, 1u) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    if (tid == 0) s_huge_base = s_huge ? atomicAdd(huge_count, s_huge) : 0u;
+    run_d += s_excl[0];
+    run_i += s_excl[1];
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        run_d += vd[k];  // inclusive
+        s_d[pad(tid * SCAN_ITEMS + k)] = run_d;
+        s_i[pad(tid * SCAN_ITEMS + k)] = run_i;  // exclusive
+        run_i += vi[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint32_t li = k * SCAN_THREADS + tid;
+        const size_t i = base + li;
+        if (i < n) {
+            offsets[i] = s_d[pad(li)];
+            row_first[i] = s_i[pad(li)];
+            if (hrank[k] != 0xFFFFFFFFu) huge_list[s_huge_base + hrank[k]] = (uint32_t)i;
+        }
+    }
+}
+
+// Exclusive scan of a u32 array in ONE launch, for the [digit][block] histograms of the large sorts (the 3-launch
+// reduce / partials / downsweep scan before); status / ticket zeroed by radix_upsweep_kernel.
 __global__ __launch_bounds__(SCAN_THREADS) void scan_lookback_kernel(const uint32_t* in, uint32_t* out, size_t n,
                                                                      uint64_t* status, uint32_t* ticket, uint32_t* err)
 {
@@ -222,30 +229,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_lookback_kernel(const uint3
     uint32_t total;
     const uint32_t run0 = block_exclusive_scan(sum, s_wave, &total);
     if (tid < 64) {  // wave 0: publish, look back, publish the inclusive prefix
-        uint64_t excl = 0;
-        if (vb == 0) {
-            if (tid == 0) __hip_atomic_store(&status[0], SLB_PRE | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (tid == 0) __hip_atomic_store(&status[vb], SLB_AGG | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t j = vb, spins = 0;  // next predecessor to read is j - 1 - lane
-            while (true) {
-                const uint64_t st = j > lane ? __hip_atomic_load(&status[j - 1 - lane], __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_AGENT)
-                                             : SLB_PRE;  // never reached: tile 0 publishes PRE
-                const uint64_t stop = __ballot((st & ~SLB_VAL) != SLB_AGG);  // PRE or not yet published
-                const uint32_t k = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
-                excl += wave_sum_u64(lane < k || (lane == k && (st & SLB_PRE)) ? (st & SLB_VAL) : 0ull);
-                if (k < 64u && (shfl_u64(st, (int)k) & SLB_PRE)) break;
-                if (k == 0 && ++spins > (1u << 20)) {  // bounded: a tile that never publishes sets the error word
-                    if (lane == 0) atomicOr(err, 1u);
-                    break;
-                }
-                if (k == 0) __builtin_amdgcn_s_sleep(1);
-                j -= k;
-            }
-            if (tid == 0)
-                __hip_atomic_store(&status[vb], SLB_PRE | (excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        const uint64_t excl = wave_lookback(status, vb, total, lane, err);
         if (tid == 0) s_excl = excl;
     }
     __syncthreads();
@@ -753,17 +737,17 @@ size_t scan_partials_size(size_t n) { return div_up(n, SCAN_TILE) + 1; }
 
 size_t radix_partials_words(size_t n) { return 2 * scan_partials_size(radix_hist_size(n)) + 2; }
 
-size_t scan2_partials_size(size_t n) { return 2 * scan_partials_size(n); }
+size_t scan2_status_words(size_t n) { return 4 * div_up(n, SCAN_TILE) + 2; }
 
 void launch_forward_scans(const uint32_t* tiles_touched, const uint32_t* order, uint32_t* offsets, uint32_t* row_first,
-                          uint32_t* huge_list, uint32_t* huge_count, uint32_t* partials, size_t n, hipStream_t s)
+                          uint32_t* huge_list, uint32_t* huge_count, uint32_t* status, size_t n, hipStream_t s)
 {
     if (n == 0) return;
     const uint32_t nb = div_up(n, SCAN_TILE);
-    scan2_reduce_kernel<<<nb, SCAN_THREADS, 0, s>>>(tiles_touched, order, n, partials, nb);
-    scan2_partials_kernel<<<2, SCAN_THREADS, 0, s>>>(partials, nb);
-    scan2_downsweep_kernel<<<nb, SCAN_THREADS, 0, s>>>(tiles_touched, order, n, partials, nb, offsets, row_first,
-                                                        huge_list, huge_count);
+    uint64_t* st = reinterpret_cast<uint64_t*>(status);  // [2][nb] 64-bit | ticket | error word
+    uint32_t* ticket = status + 4 * (size_t)nb;
+    scan2_lookback_kernel<<<nb, SCAN_THREADS, 0, s>>>(tiles_touched, order, n, st, st + nb, ticket, ticket + 1, offsets,
+                                                      row_first, huge_list, huge_count);
 }
 
 size_t radix_hist_size(size_t n) { return (size_t)RADIX * div_up(n, SORT_TILE); }
