@@ -12,7 +12,7 @@
 // their dx-multiples)
 // The per-Gaussian constants of the reference's expressions (conic, opacity, 0.5 W, 0.5 H, -1/2) are linear
 // factors, so they are applied once per instance to the lane's sums — not once per pixel — and the nine values
-// are then summed over the wave in registers (DPP transposed butterfly + v_permlane{16,32}_swap, wave_ops.h).
+// are then summed over the wave: eight transposed through LDS, the ninth by v_permlane{16,32}_swap + DPP (wave_ops.h).
 // Lanes 0..8 store the instance's 36-B gradient row, indexed by its row slot (Gaussian-index-major: row_first), with
 // plain stores, and lane 0 marks the slot in row_valid (zeroed before the launch); an instance no pixel takes a contribution from writes
 // nothing — at dense configs most instances lie behind every pixel's last contributor. gaussian_bwd.hip sums each
@@ -49,9 +49,10 @@ __device__ unsigned long long g_bwd_counts[5];
 #ifndef OMR_BWD_MINW
 #define OMR_BWD_MINW 1
 #endif
-// wave reduction of the per-instance sums: wave_sum9_rows (1) or the transposed DPP butterfly (0), wave_ops.h
+// wave reduction of the per-instance sums: wave_sum9_rows (1), wave_sum9_lds (2) or the transposed DPP butterfly (0),
+// wave_ops.h
 #ifndef OMR_BWD_ROWS_RED
-#define OMR_BWD_ROWS_RED 1
+#define OMR_BWD_ROWS_RED 2
 #endif
 // keep each pixel's dL/dpix and last contributor in LDS (read per instance and band) instead of 16 VGPRs
 #ifndef OMR_BWD_PIX_LDS
@@ -64,6 +65,9 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
     __shared__ float4 s_geo_all[TW_WAVES][TW_BATCH];   // x, y, position in range (u32 bits), band mask (u32 bits)
     __shared__ float4 s_quad_all[TW_WAVES][TW_BATCH];  // qa, qb, qc, opacity
     __shared__ float4 s_rgb_all[TW_WAVES][TW_BATCH];   // colour, gradient row slot (u32 bits)
+#if OMR_BWD_ROWS_RED == 2
+    __shared__ __attribute__((aligned(16))) float s_red_all[TW_WAVES][8 * WS_LDS_STRIDE];  // wave_sum9_lds rows
+#endif
     __shared__ float s_floor_all[TW_WAVES][TW_BATCH];  // p2_floor(opacity)
 #if OMR_BWD_PIX_LDS
     __shared__ float4 s_pix_all[TW_WAVES][TW_BANDS][64];  // dL/dpix rgb, last contributor (u32 bits)
@@ -243,7 +247,11 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
             v[7] = sc1;
             float t8;
 #if OMR_BWD_ROWS_RED
+#if OMR_BWD_ROWS_RED == 2
+            const float tv = wave_sum9_lds(v, sc2, lane, s_red_all[wv], &t8);
+#else
             const float tv = wave_sum9_rows(v, sc2, lane, &t8);
+#endif
             // lane 8k holds value k (k < 8), every lane the 9th: lanes 0, 8, ..., 56 and 1 store the 36-B row
             const bool lead = (lane & 7) == 0;
             if (lead || lane == 1) row[lead ? (lane >> 3) : 8u] = lead ? tv : t8;

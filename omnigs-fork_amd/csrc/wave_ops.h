@@ -95,6 +95,38 @@ __device__ __forceinline__ float wave_sum9_rows(const float v[8], float v8, uint
     return c;
 }
 
+// Wave-sum of v[0..7] through LDS, v8 through permlane/DPP. s_red: this wave's float[8 * WS_LDS_STRIDE]. Each lane
+// writes its eight values to the eight rows; lane l then adds the 8 entries (l & 7) * 8 .. + 7 of row l >> 3 (two
+// 16-B reads) and the 8 lanes of a row group combine by DPP: 7 adds + 3 DPP + 8 for v8 = 18 VALU (26 for
+// wave_sum9_rows), the transposition done by the LDS pipe. Same result layout as wave_sum9_rows: lane l holds the
+// total of value (l >> 3) & 7, *t8 = the total of v8 on every lane. The caller orders the LDS accesses (wave_sync).
+constexpr int WS_LDS_STRIDE = 68;  // floats per row: 16-B aligned rows, row starts on different banks
+__device__ __forceinline__ float wave_sum9_lds(const float v[8], float v8, uint32_t lane, float* s_red, float* t8)
+{
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s_red[k * WS_LDS_STRIDE + lane] = v[k];
+    float u0 = v8, u1 = v8;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(u0), "+v"(u1));
+    float u = u0 + u1;
+    u0 = u;
+    u1 = u;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(u0), "+v"(u1));
+    u = u0 + u1;
+    u = add_dpp<DPP_ROR8>(u, u);
+    u = add_dpp<DPP_XOR1>(u, u);
+    u = add_dpp<DPP_XOR2>(u, u);
+    *t8 = add_dpp<DPP_HALF_MIRROR>(u, u);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const float4* seg = reinterpret_cast<const float4*>(s_red + (lane >> 3) * WS_LDS_STRIDE + (lane & 7) * 8);
+    const float4 a = seg[0], b = seg[1];
+    float c = ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
+    c = add_dpp<DPP_XOR1>(c, c);
+    c = add_dpp<DPP_XOR2>(c, c);
+    return add_dpp<DPP_HALF_MIRROR>(c, c);
+}
+
 // lane l < 8 holds value index bitrev3(l) after wave_sum8_transposed; lane 8 is used for the 9th value
 __device__ __forceinline__ uint32_t transposed_slot_of_lane(uint32_t lane)
 {
