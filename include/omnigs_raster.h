@@ -219,7 +219,8 @@ int omr_debug_image_state(char* image_buffer, int width, int height, float* fina
 /* per-Gaussian pixel centre [P,2], conic+opacity [P,4], rgb [P,3], depth [P], tiles_touched [P] */
 /* one wave64 through the render backward's gradient reduction: in [64][9] -> out [9] (column sums) */
 int omr_debug_wave_sum(const float* in, float* out, void* stream);
-int omr_debug_wave_sum9(const float* in, float* out, void* stream); /* wave_sum9_rows (render backward) */
+int omr_debug_wave_sum9(const float* in, float* out, void* stream); /* wave_sum9_rows */
+int omr_debug_wave_sum9_lds(const float* in, float* out, void* stream); /* wave_sum9_lds (render backward) */
 int omr_debug_geometry(char* geom_buffer, int P, float* means2D, float* conic_opacity, float* rgb, float* depths,
                        uint32_t* tiles_touched, void* stream);
 

@@ -33,7 +33,7 @@ __global__ __launch_bounds__(64) void debug_wave_sum_kernel(const float* in, flo
     if (lane < 9) out[transposed_slot_of_lane(lane)] = lane < 8 ? tv : t8;
 }
 
-// the same through wave_sum9_rows (the render backward's default reduction)
+// the same through wave_sum9_rows (the render backward's reduction before wave_sum9_lds)
 __global__ __launch_bounds__(64) void debug_wave_sum9_kernel(const float* in, float* out)
 {
     const uint32_t lane = threadIdx.x;
@@ -42,6 +42,20 @@ __global__ __launch_bounds__(64) void debug_wave_sum9_kernel(const float* in, fl
     for (int c = 0; c < 8; ++c) v[c] = in[lane * 9 + c];
     float t8;
     const float tv = wave_sum9_rows(v, in[lane * 9 + 8], lane, &t8);
+    if ((lane & 7) == 0) out[lane >> 3] = tv;
+    if (lane == 1) out[8] = t8;
+}
+
+// the same through wave_sum9_lds (the render backward's default reduction, OMR_BWD_ROWS_RED 2)
+__global__ __launch_bounds__(64) void debug_wave_sum9_lds_kernel(const float* in, float* out)
+{
+    __shared__ __attribute__((aligned(16))) float s_red[8 * WS_LDS_STRIDE];
+    const uint32_t lane = threadIdx.x;
+    float v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = in[lane * 9 + c];
+    float t8;
+    const float tv = wave_sum9_lds(v, in[lane * 9 + 8], lane, s_red, &t8);
     if ((lane & 7) == 0) out[lane >> 3] = tv;
     if (lane == 1) out[8] = t8;
 }
@@ -785,6 +799,13 @@ int omr_debug_wave_sum9(const float* in, float* out, void* stream)
     g_last_error.clear();
     debug_wave_sum9_kernel<<<1, 64, 0, (hipStream_t)stream>>>(in, out);
     return hip_check("debug_wave_sum9");
+}
+
+int omr_debug_wave_sum9_lds(const float* in, float* out, void* stream)
+{
+    g_last_error.clear();
+    debug_wave_sum9_lds_kernel<<<1, 64, 0, (hipStream_t)stream>>>(in, out);
+    return hip_check("debug_wave_sum9_lds");
 }
 
 int omr_debug_wave_sum(const float* in, float* out, void* stream)

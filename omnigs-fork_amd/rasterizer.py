@@ -66,6 +66,7 @@ def lib() -> C.CDLL:
         L.omr_debug_geometry.argtypes = [vp, i, vp, vp, vp, vp, vp, vp]
         L.omr_debug_wave_sum.argtypes = [vp, vp, vp]
         L.omr_debug_wave_sum9.argtypes = [vp, vp, vp]
+        L.omr_debug_wave_sum9_lds.argtypes = [vp, vp, vp]
         L.omr_profile_enable.argtypes = [i]
         L.omr_sh_grad_from_colors.argtypes = [i, i, i, i, vp, vp, vp, vp, vp, vp]
         L.omr_sh_grad_from_colors_packed.restype = i
@@ -460,12 +461,13 @@ def profile_read() -> dict:
     return {lib().omr_profile_stage_name(i).decode(): (float(tot[i]), int(cnt[i])) for i in range(n)}
 
 
-def debug_wave_sum(x: torch.Tensor, rows: bool = False) -> torch.Tensor:
+def debug_wave_sum(x: torch.Tensor, rows: bool = False, lds: bool = False) -> torch.Tensor:
     """Column sums of a [64, 9] float32 device tensor through a wave reduction of wave_ops.h: the transposed DPP
-    butterfly (rows=False) or the cross-row-first wave_sum9_rows (rows=True, the render backward's)."""
+    butterfly (default), the cross-row-first wave_sum9_rows (rows=True) or wave_sum9_lds (lds=True, the render
+    backward's)."""
     x = _dev_f32(x, "x")
     assert tuple(x.shape) == (64, 9)
     out = torch.empty(9, dtype=torch.float32, device=x.device)
-    fn = lib().omr_debug_wave_sum9 if rows else lib().omr_debug_wave_sum
+    fn = lib().omr_debug_wave_sum9_lds if lds else (lib().omr_debug_wave_sum9 if rows else lib().omr_debug_wave_sum)
     _check(fn(x.data_ptr(), out.data_ptr(), _stream(x.device)), "debug_wave_sum")
     return out

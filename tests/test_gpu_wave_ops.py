@@ -1,31 +1,35 @@
-"""GPU unit test of the wave64 gradient reduction used by the render backward (DPP transposed butterfly +
-v_permlane16/32_swap). Column sums of a [64, 9] block must match a float64 reference to f32 rounding."""
+"""GPU unit test of the wave64 gradient reductions of wave_ops.h (DPP transposed butterfly, cross-row-first
+v_permlane16/32_swap, and the LDS-transposed one the render backward uses). Column sums of a [64, 9] block must
+match a float64 reference to f32 rounding."""
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("rows", [False, True])
+MODES = [dict(), dict(rows=True), dict(lds=True)]
+
+
+@pytest.mark.parametrize("mode", MODES, ids=["transposed", "rows", "lds"])
 @pytest.mark.parametrize("seed", [0, 1, 2])
-def test_wave_sum_matches_column_sums(seed, rows, omr):
+def test_wave_sum_matches_column_sums(seed, mode, omr):
     import torch
 
     rng = np.random.default_rng(seed)
     x = rng.standard_normal((64, 9)).astype(np.float32)
     if seed == 2:  # sparse: most lanes zero, as when few pixels of a wave contribute
         x[rng.uniform(size=x.shape) < 0.85] = 0.0
-    got = omr.rasterizer.debug_wave_sum(torch.from_numpy(x).cuda(), rows=rows).cpu().numpy()
+    got = omr.rasterizer.debug_wave_sum(torch.from_numpy(x).cuda(), **mode).cpu().numpy()
     ref = x.astype(np.float64).sum(axis=0)
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("rows", [False, True])
-def test_wave_sum_lane_identity(rows, omr):
+@pytest.mark.parametrize("mode", MODES, ids=["transposed", "rows", "lds"])
+def test_wave_sum_lane_identity(mode, omr):
     import torch
 
     # value c of lane l = (c + 1) * 1000 + l: distinguishes every (lane, column) contribution exactly in f32
     x = np.array([[(c + 1) * 1000 + l for c in range(9)] for l in range(64)], dtype=np.float32)
-    got = omr.rasterizer.debug_wave_sum(torch.from_numpy(x).cuda(), rows=rows).cpu().numpy()
+    got = omr.rasterizer.debug_wave_sum(torch.from_numpy(x).cuda(), **mode).cpu().numpy()
     ref = x.astype(np.float64).sum(axis=0)
     np.testing.assert_array_equal(got, ref)
