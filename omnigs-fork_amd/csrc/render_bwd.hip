@@ -94,7 +94,8 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
 #if OMR_BWD_PIX_LDS
     float4* s_pix = &s_pix_all[wv][0][0];
 #else
-    float dp0[TW_BANDS], dp1[TW_BANDS], dp2[TW_BANDS];
+    f2v dp01[TW_BANDS];  // dL/dpix r, g: one register pair, the packed FMA's operand
+    float dp2[TW_BANDS];
     uint32_t last[TW_BANDS];
 #endif
     uint32_t band_end[TW_BANDS];  // wave-uniform: max last contributor of the band
@@ -113,8 +114,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
         s_pix[b * 64 + lane] = make_float4(d0, d1, d2, __builtin_bit_cast(float, lc));
 #else
         last[b] = lc;
-        dp0[b] = d0;
-        dp1[b] = d1;
+        dp01[b] = f2v{d0, d1};
         dp2[b] = d2;
 #endif
         T[b] = Tf;
@@ -184,8 +184,9 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
             const float dy0 = g.y - (float)tl.py0;
             // dx is the same for all four of the lane's pixels (one column), so the x-moments are dx-multiples of
             // the band sums: S_u dx = dx S_u, S_u dx^2 = dx^2 S_u, S_u dx dy = dx S_u dy (applied after the bands)
-            float su = 0.f, suy = 0.f, suyy = 0.f;
-            float sc0 = 0.f, sc1 = 0.f, sc2 = 0.f;
+            f2v s_uy = {0.f, 0.f};  // S_u, S_u dy
+            f2v sc01 = {0.f, 0.f};  // S_aT dpix_r, S_aT dpix_g
+            float suyy = 0.f, sc2 = 0.f;
             bool any = false;
 #pragma unroll
             for (int b = 0; b < TW_BANDS; ++b) {
@@ -195,7 +196,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
                 const float dp0b = pxd.x, dp1b = pxd.y, dp2b = pxd.z;
                 const uint32_t lastb = __builtin_bit_cast(uint32_t, pxd.w);
 #else
-                const float dp0b = dp0[b], dp1b = dp1[b], dp2b = dp2[b];
+                const float dp0b = dp01[b].x, dp1b = dp01[b].y, dp2b = dp2[b];
                 const uint32_t lastb = last[b];
 #endif
                 const float dy = dy0 - (float)(4 * b);
@@ -211,19 +212,17 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
                 const float G = __builtin_amdgcn_exp2f(contrib ? p2 : -__builtin_inff());
                 const float alpha = fminf(0.99f, qo.w * G);
                 const float inv = __builtin_amdgcn_rcpf(1.0f - alpha);
-                const float Ti = T[b] * inv;
+                T[b] *= inv;
+                const float Ti = T[b];
                 const float cdot = __builtin_fmaf(f.x, dp0b, __builtin_fmaf(f.y, dp1b, f.z * dp2b));
                 const float dL_dalpha = __builtin_fmaf(Ti, cdot, -s[b] * inv);
                 const float wc = alpha * Ti;  // dchannel/dcolour (backward.cu:800)
                 s[b] = __builtin_fmaf(cdot, wc, s[b]);
-                T[b] = Ti;
                 const float u = G * dL_dalpha;  // = dL/dopacity contribution; dL/dG * G = opacity * u
                 const float uy = u * dy;
-                su += u;
-                suy += uy;
+                s_uy += f2v{u, uy};
                 suyy = __builtin_fmaf(uy, dy, suyy);
-                sc0 = __builtin_fmaf(wc, dp0b, sc0);
-                sc1 = __builtin_fmaf(wc, dp1b, sc1);
+                sc01 = __builtin_elementwise_fma(f2v{wc, wc}, dp01[b], sc01);
                 sc2 = __builtin_fmaf(wc, dp2b, sc2);
             }
             const uint32_t slot_j = __builtin_bit_cast(uint32_t, f.w);
@@ -235,6 +234,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
             // conic (a, b, c) back from the staged quadratic form: q = (-a/2, -b, -c/2) log2(e)
             const float ca = q.qa * (-2.0f / LOG2E), cb = q.qb * (-1.0f / LOG2E), cc = q.qc * (-2.0f / LOG2E);
             const float o = qo.w;
+            const float su = s_uy.x, suy = s_uy.y;
             const float sux = su * dx, suxx = sux * dx, suxy = suy * dx;
             float v[8];
             v[0] = -o * half_w * (ca * sux + cb * suy);  // dL/dmean2D.x
@@ -243,8 +243,8 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
             v[3] = -0.5f * o * suxy;                           // dL/dconic.y (the reference's half-weight slot)
             v[4] = -0.5f * o * suyy;                           // dL/dconic.w
             v[5] = su;                                         // dL/dopacity
-            v[6] = sc0;                                        // dL/dcolour
-            v[7] = sc1;
+            v[6] = sc01.x;                                     // dL/dcolour
+            v[7] = sc01.y;
             float t8;
 #if OMR_BWD_ROWS_RED
 #if OMR_BWD_ROWS_RED == 2
