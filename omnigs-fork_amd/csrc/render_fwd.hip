@@ -66,7 +66,8 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
     const uint32_t lane = tl.lane;
     const float pxf = (float)tl.px;
 
-    bool done[FWD_BANDS];
+    // T carries the pixel's "done" state in its sign: a saturated (or out-of-image) pixel holds -T, so the per-band
+    // test is one compare and no bool array lives in VGPRs; |T| is the transmittance
     float T[FWD_BANDS], C0[FWD_BANDS], C1[FWD_BANDS], C2[FWD_BANDS];
     uint32_t last[FWD_BANDS];
     uint32_t active = 0;  // local bands with at least one unsaturated in-image pixel (wave-uniform)
@@ -74,8 +75,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
 #pragma unroll
     for (int b = 0; b < FWD_BANDS; ++b) {
         const bool inside = tl.px < (uint32_t)a.W && tl.py(band0 + b) < (uint32_t)a.H;
-        done[b] = !inside;
-        T[b] = 1.0f;
+        T[b] = inside ? 1.0f : -1.0f;
         C0[b] = C1[b] = C2[b] = 0.f;
         last[b] = 0;
         if (__ballot(inside)) active |= 1u << b;
@@ -128,33 +128,35 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
             const float dx = g.x - pxf;
             const ColQuad kq = column_quad(q, dx);
             const float dy0 = g.y - (float)tl.py(band0);
-            bool sat_any = false;
+            uint64_t sat_any = 0;  // lanes that saturated at this instance (a wave mask: SALU only)
 #pragma unroll
             for (int b = 0; b < FWD_BANDS; ++b) {
                 if (!(mb & (1u << b))) continue;  // scalar branch
                 const float dy = dy0 - (float)(4 * b);
                 const float p2 = falloff_p2(kq, dy);
-                bool ok = !done[b] && p2 <= 0.0f && p2 >= pfloor;  // alpha >= 1/255 (tile_wave.h: p2_floor)
+                const bool live = T[b] > 0.0f;
+                bool ok = live && p2 <= 0.0f && p2 >= pfloor;  // alpha >= 1/255 (tile_wave.h: p2_floor)
                 // a lane that is not ok gets alpha = 0: test_T = T, wgt = 0
                 const float alpha = fminf(0.99f, qo.w * __builtin_amdgcn_exp2f(ok ? p2 : -__builtin_inff()));
                 const float test_T = T[b] * (1.0f - alpha);
-                // T >= 1e-4 always holds (T only takes values that passed this test), and a lane that is not ok has
-                // test_T = T: so sat implies ok
+                // a live T is >= 1e-4 (T only takes values that passed this test) and a lane that is not ok has
+                // test_T = T, so `sat` holds for newly saturated and already done (negative) pixels alike
                 const bool sat = test_T < 0.0001f;
-                done[b] = done[b] || sat;
-                sat_any = sat_any || sat;
+                // newly saturated = live && sat (a live lane that is not ok keeps test_T = T >= 1e-4); two ballots of
+                // plain compares stay in SGPRs, a ballot of their conjunction goes through a VGPR
+                sat_any |= __ballot(live) & __ballot(sat);
                 ok = ok && !sat;
                 const float wgt = sat ? 0.0f : alpha * T[b];
                 C0[b] = __builtin_fmaf(f.x, wgt, C0[b]);
                 C1[b] = __builtin_fmaf(f.y, wgt, C1[b]);
                 C2[b] = __builtin_fmaf(f.z, wgt, C2[b]);
-                T[b] = sat ? T[b] : test_T;
+                T[b] = sat ? -fabsf(T[b]) : test_T;  // done: keeps the last live T, negated
                 last[b] = ok ? contributor : last[b];
             }
-            if (__ballot(sat_any)) {  // some pixel saturated: drop bands with no live pixel left
+            if (sat_any) {  // some pixel saturated: drop bands with no live pixel left
 #pragma unroll
                 for (int b = 0; b < FWD_BANDS; ++b)
-                    if (!__ballot(!done[b])) active &= ~(1u << b);
+                    if (!__ballot(T[b] > 0.0f)) active &= ~(1u << b);
                 if (!active) break;
             }
 #if OMR_FWD_PREFETCH
@@ -172,11 +174,12 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
         const uint32_t py = tl.py(band0 + b);
         if (tl.px < (uint32_t)a.W && py < (uint32_t)a.H) {
             const uint32_t pix = a.W * py + tl.px;
-            a.final_T[pix] = T[b];
+            const float Tf = fabsf(T[b]);
+            a.final_T[pix] = Tf;
             a.n_contrib[pix] = last[b];
-            a.out_color[pix] = C0[b] + T[b] * a.bg[0];
-            a.out_color[plane + pix] = C1[b] + T[b] * a.bg[1];
-            a.out_color[2 * plane + pix] = C2[b] + T[b] * a.bg[2];
+            a.out_color[pix] = C0[b] + Tf * a.bg[0];
+            a.out_color[plane + pix] = C1[b] + Tf * a.bg[1];
+            a.out_color[2 * plane + pix] = C2[b] + Tf * a.bg[2];
         }
     }
     if (lane == 0 && work) atomicAdd(&a.tile_cost[tile], work);
