@@ -128,7 +128,8 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
 
     // instances behind every pixel's last contributor get no row (row_valid stays 0 for them)
 
-    const float half_w = 0.5f * (float)a.W, half_h = 0.5f * (float)a.H;  // ddelx_dx, ddely_dy (backward.cu:700-701)
+    // ddelx_dx, ddely_dy (backward.cu:700-701) = W/2, H/2, with the 2 / log2(e) of the staged conic folded in
+    const float kx = (float)a.W / LOG2E, ky = (float)a.H / LOG2E;
 #if !OMR_BWD_ROWS_RED
     const uint32_t slot_of_lane = transposed_slot_of_lane(lane);
 #endif
@@ -187,7 +188,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
             f2v s_uy = {0.f, 0.f};  // S_u, S_u dy
             f2v sc01 = {0.f, 0.f};  // S_aT dpix_r, S_aT dpix_g
             float suyy = 0.f, sc2 = 0.f;
-            bool any = false;
+            uint32_t any = 0;  // bands with a contributing pixel (set in wave-uniform branches: an SGPR)
 #pragma unroll
             for (int b = 0; b < TW_BANDS; ++b) {
                 if (!(mb & (1u << b))) continue;  // scalar branch
@@ -207,7 +208,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
                 if (!__ballot(contrib)) continue;
                 BWD_COUNT(2, 1);
                 BWD_COUNT(4, (uint32_t)__popcll(__ballot(contrib)));
-                any = true;
+                any |= 1u << b;
                 // a lane that does not contribute gets G = alpha = 0: inv = 1, T and s unchanged, u = wc = 0
                 const float G = __builtin_amdgcn_exp2f(contrib ? p2 : -__builtin_inff());
                 const float alpha = fminf(0.99f, qo.w * G);
@@ -227,21 +228,22 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
             }
             const uint32_t slot_j = __builtin_bit_cast(uint32_t, f.w);
             float* row = a.inst_grad + (size_t)slot_j * GRAD_ROW;
-            if (!uniform(any)) continue;  // no pixel took a contribution: no row
+            if (!any) continue;  // no pixel took a contribution: no row
             BWD_COUNT(3, 1);
             if (lane == 0) a.row_valid[slot_j] = 1;
-            // per-instance factors of backward.cu:805-840 (dG/ddelx = -G (dx a + dy b), ...)
-            // conic (a, b, c) back from the staged quadratic form: q = (-a/2, -b, -c/2) log2(e)
-            const float ca = q.qa * (-2.0f / LOG2E), cb = q.qb * (-1.0f / LOG2E), cc = q.qc * (-2.0f / LOG2E);
+            // per-instance factors of backward.cu:805-840 (dG/ddelx = -G (dx a + dy b), ...). With the staged
+            // quadratic form q = (-a/2, -b, -c/2) log2(e):  -(a sux + b suy) = (2 / log2 e) (qa sux + qb/2 suy),
+            // so dL/dmean2D.x = o W/2 (2 / log2 e) (qa sux + qb/2 suy), likewise y with (qc, qb/2) and H/2
             const float o = qo.w;
             const float su = s_uy.x, suy = s_uy.y;
             const float sux = su * dx, suxx = sux * dx, suxy = suy * dx;
+            const float hb = 0.5f * q.qb, mo = -0.5f * o;
             float v[8];
-            v[0] = -o * half_w * (ca * sux + cb * suy);  // dL/dmean2D.x
-            v[1] = -o * half_h * (cc * suy + cb * sux);  // dL/dmean2D.y
-            v[2] = -0.5f * o * suxx;                           // dL/dconic.x
-            v[3] = -0.5f * o * suxy;                           // dL/dconic.y (the reference's half-weight slot)
-            v[4] = -0.5f * o * suyy;                           // dL/dconic.w
+            v[0] = (o * kx) * __builtin_fmaf(q.qa, sux, hb * suy);  // dL/dmean2D.x
+            v[1] = (o * ky) * __builtin_fmaf(q.qc, suy, hb * sux);  // dL/dmean2D.y
+            v[2] = mo * suxx;                                        // dL/dconic.x
+            v[3] = mo * suxy;                                        // dL/dconic.y (the reference's half-weight slot)
+            v[4] = mo * suyy;                                        // dL/dconic.w
             v[5] = su;                                         // dL/dopacity
             v[6] = sc01.x;                                     // dL/dcolour
             v[7] = sc01.y;
