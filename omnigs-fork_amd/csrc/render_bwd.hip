@@ -54,10 +54,6 @@ __device__ unsigned long long g_bwd_counts[5];
 #ifndef OMR_BWD_ROWS_RED
 #define OMR_BWD_ROWS_RED 2
 #endif
-// keep each pixel's dL/dpix and last contributor in LDS (read per instance and band) instead of 16 VGPRs
-#ifndef OMR_BWD_PIX_LDS
-#define OMR_BWD_PIX_LDS 0
-#endif
 
 __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel(RenderBwdArgs a)
 {
@@ -69,9 +65,6 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
     __shared__ __attribute__((aligned(16))) float s_red_all[TW_WAVES][8 * WS_LDS_STRIDE];  // wave_sum9_lds rows
 #endif
     __shared__ float s_floor_all[TW_WAVES][TW_BATCH];  // p2_floor(opacity)
-#if OMR_BWD_PIX_LDS
-    __shared__ float4 s_pix_all[TW_WAVES][TW_BANDS][64];  // dL/dpix rgb, last contributor (u32 bits)
-#endif
 
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t rank = xcd_remap(blockIdx.x, gridDim.x) * TW_WAVES + wv;
@@ -91,13 +84,9 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
     const size_t plane = (size_t)a.H * a.W;
 
     float T[TW_BANDS], s[TW_BANDS];
-#if OMR_BWD_PIX_LDS
-    float4* s_pix = &s_pix_all[wv][0][0];
-#else
     f2v dp01[TW_BANDS];  // dL/dpix r, g: one register pair, the packed FMA's operand
     float dp2[TW_BANDS];
     uint32_t last[TW_BANDS];
-#endif
     uint32_t band_end[TW_BANDS];  // wave-uniform: max last contributor of the band
     uint32_t max_c = 0;
 #pragma unroll
@@ -110,13 +99,9 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
         const float d0 = inside ? a.dL_dpix[pix] : 0.f;
         const float d1 = inside ? a.dL_dpix[plane + pix] : 0.f;
         const float d2 = inside ? a.dL_dpix[2 * plane + pix] : 0.f;
-#if OMR_BWD_PIX_LDS
-        s_pix[b * 64 + lane] = make_float4(d0, d1, d2, __builtin_bit_cast(float, lc));
-#else
         last[b] = lc;
         dp01[b] = f2v{d0, d1};
         dp2[b] = d2;
-#endif
         T[b] = Tf;
         s[b] = Tf * (a.bg[0] * d0 + a.bg[1] * d1 + a.bg[2] * d2);
         band_end[b] = uniform(wave_max_u32(lc));
@@ -192,14 +177,8 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
 #pragma unroll
             for (int b = 0; b < TW_BANDS; ++b) {
                 if (!(mb & (1u << b))) continue;  // scalar branch
-#if OMR_BWD_PIX_LDS
-                const float4 pxd = s_pix[b * 64 + lane];
-                const float dp0b = pxd.x, dp1b = pxd.y, dp2b = pxd.z;
-                const uint32_t lastb = __builtin_bit_cast(uint32_t, pxd.w);
-#else
                 const float dp0b = dp01[b].x, dp1b = dp01[b].y, dp2b = dp2[b];
                 const uint32_t lastb = last[b];
-#endif
                 const float dy = dy0 - (float)(4 * b);
                 const float p2 = falloff_p2(kq, dy);
                 // backward.cu:770-781: skip positions at/after the pixel's last contributor, power > 0, alpha < 1/255
