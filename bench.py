@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, Chip-level parameters)
+VALU_PEAK_TFLOPS = 157.3  # MI355X f32 vector peak with v_pk_fma_f32 (MI355X_MICROARCH.md, MFMA/VALU peak table)
 DOMINANT = "render_backward"  # the kernel the roofline reports (largest stage at every config)
 
 
@@ -187,6 +188,7 @@ def main():
         exchange()
         stats["L"] = nr
         stats["radii"] = radii
+        stats["img"] = ib
 
     def exchange():
         if args.exchange == "compact":
@@ -209,6 +211,7 @@ def main():
         exchange()
         stats["L"] = nr
         stats["radii"] = radii
+        stats["img"] = ib
 
     for _ in range(args.warmup):
         step()
@@ -271,6 +274,15 @@ def main():
     except (OSError, ValueError):
         pass
     algo_total = sum(stage_bytes(s, P, V, L, N, T, M, g.sh_degree) for s in stage_avg)
+    # VALU secondary: pixel-instance evaluations = the forward's (instance, 16x4 band) pairs x 64,
+    # at nominal 20 flop (forward) / 60 flop (backward) each, against the f32 vector peak; the backward evaluates at
+    # most the forward's pairs (it stops at each band's last contributor), so its figure is an upper bound
+    evals = int(R.debug_tile_cost(W, H, stats["img"]).sum().item()) * 64
+    valu = {"peak_tflops": VALU_PEAK_TFLOPS, "pixel_evals": evals}
+    for k, fl in (("render_forward", 20), ("render_backward", 60)):
+        ms_k = stage_avg.get(k, 0.0)
+        tf = evals * fl / (ms_k * 1e-3) / 1e12 if ms_k > 0 else 0.0
+        valu[k] = {"flop_per_eval": fl, "tflops": round(tf, 2), "frac": round(tf / VALU_PEAK_TFLOPS, 4)}
     result = {
         "metric": "Mpixels/s fwd+bwd, 1M Gaussians @ 2048x1024 equirect; 1/2/4/8 GPU",
         "value": round(value, 3),
@@ -294,6 +306,7 @@ def main():
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 4),
                      "step_algorithmic_GBps": round(algo_total / (ms_per_step * 1e-3) / 1e9, 2)},
         "stages_ms": {k: round(v, 4) for k, v in stage_avg.items()},
+        "valu_secondary": valu,
     }
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)

@@ -216,6 +216,8 @@ int omr_debug_point_list(char* binning_buffer, int R, int width, int height, uin
 int omr_debug_ranges(char* image_buffer, int width, int height, uint32_t* dst, void* stream);
 /* per-pixel final transmittance [N] f32 and contributor count [N] u32 */
 int omr_debug_image_state(char* image_buffer, int width, int height, float* final_T, uint32_t* n_contrib, void* stream);
+/* the forward's per-tile count of (instance, 16x4 band) evaluations [T] (the backward's schedule key) */
+int omr_debug_tile_cost(char* image_buffer, int width, int height, uint32_t* dst, void* stream);
 /* per-Gaussian pixel centre [P,2], conic+opacity [P,4], rgb [P,3], depth [P], tiles_touched [P] */
 /* one wave64 through the render backward's gradient reduction: in [64][9] -> out [9] (column sums) */
 int omr_debug_wave_sum(const float* in, float* out, void* stream);

@@ -887,6 +887,16 @@ int omr_debug_image_state(char* image_buffer, int width, int height, float* fina
     return OMR_OK;
 }
 
+int omr_debug_tile_cost(char* image_buffer, int width, int height, uint32_t* dst, void* stream)
+{
+    g_last_error.clear();
+    const Dims d = dims(width, height);
+    ImageState im;
+    ImageState::carve(image_buffer, d.N, d.T, &im);
+    OMR_HIP(hipMemcpyAsync(dst, im.tile_cost, d.T * sizeof(uint32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return OMR_OK;
+}
+
 int omr_debug_geometry(char* geom_buffer, int P, float* means2D, float* conic_opacity, float* rgb, float* depths,
                        uint32_t* tiles_touched, void* stream)
 {

@@ -63,6 +63,7 @@ def lib() -> C.CDLL:
         L.omr_debug_point_list.argtypes = [vp, i, i, i, vp, vp]
         L.omr_debug_ranges.argtypes = [vp, i, i, vp, vp]
         L.omr_debug_image_state.argtypes = [vp, i, i, vp, vp, vp]
+        L.omr_debug_tile_cost.argtypes = [vp, i, i, vp, vp]
         L.omr_debug_geometry.argtypes = [vp, i, vp, vp, vp, vp, vp, vp]
         L.omr_debug_wave_sum.argtypes = [vp, vp, vp]
         L.omr_debug_wave_sum9.argtypes = [vp, vp, vp]
@@ -430,6 +431,15 @@ def debug_state(P, R, width, height, geomBuffer, binningBuffer, imgBuffer):
         _check(L.omr_debug_ranges(imgBuffer.data_ptr(), width, height, out["ranges"].data_ptr(), st), "debug_ranges")
         _check(L.omr_debug_image_state(imgBuffer.data_ptr(), width, height, out["final_T"].data_ptr(),
                                        out["n_contrib"].data_ptr(), st), "debug_image_state")
+    return out
+
+
+def debug_tile_cost(width, height, imgBuffer) -> torch.Tensor:
+    """The forward's per-tile count of (instance, 16x4 band) evaluations, int32 [T] (render_fwd.hip: `work`)."""
+    T = ((width + 15) // 16) * ((height + 15) // 16)
+    out = torch.empty((T,), dtype=torch.int32, device=imgBuffer.device)
+    _check(lib().omr_debug_tile_cost(imgBuffer.data_ptr(), width, height, out.data_ptr(), _stream(imgBuffer.device)),
+           "debug_tile_cost")
     return out
 
 

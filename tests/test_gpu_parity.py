@@ -16,7 +16,7 @@ import os
 import numpy as np
 import pytest
 
-from helpers import blend_threshold_flip, grad_close, hip_run, make_case, oracle_run, scene, to_np
+from helpers import blend_threshold_flip, grad_close, hip_run, make_case, omr, oracle_run, scene, to_np
 
 pytestmark = pytest.mark.gpu
 
@@ -201,3 +201,18 @@ def test_mark_visible():
     borderline = np.abs(z - 0.2) < 1e-5
     assert (pres[~borderline] == expect[~borderline]).all()
     assert to_np(omr.rasterizer.markVisible(m, vm, pm, LON)).all()
+
+
+def test_tile_cost_bounds():
+    """The forward's per-tile (instance, band) evaluation counts (the backward's schedule key, bench.py's VALU
+    secondary): zero on empty tiles, at most 4 bands per instance of the tile's range, non-zero where instances
+    reach the tile's pixels."""
+    g, cam, _ = make_case(10000, 512, 256, LON, scene.BASE_SEED + 0, view_index=0)
+    h = hip_run(g, cam, None)
+    cost = to_np(omr.rasterizer.debug_tile_cost(cam.width, cam.height, h["img"])).astype(np.int64)
+    rg = to_np(h["state"]["ranges"]).astype(np.int64)
+    n = rg[:, 1] - rg[:, 0]
+    assert cost.shape == n.shape
+    assert (cost >= 0).all() and (cost[n == 0] == 0).all()
+    assert (cost <= 4 * n).all()
+    assert cost.sum() > 0
