@@ -199,7 +199,9 @@ __device__ __forceinline__ uint32_t band_mask(float2 xy, float4 co, uint32_t tx,
     const float t = 2.0f * __logf(255.0f * co.w) * 1.002f + 0.02f;
     const float x0 = (float)(tx * BLOCK_X);
     const float lo = xy.x - (x0 + (float)(BLOCK_X - 1)), hi = xy.x - x0;  // dx over the tile's columns
-    const float k = -b / a;
+    // completed square: q = a (dx - k dy)^2 + (det / a) dy^2 with k = -b / a (no cancellation between large terms)
+    const float ra = __builtin_amdgcn_rcpf(a);
+    const float k = -b * ra, dd = (a * c - b * b) * ra;
     const float dy0 = xy.y - (float)(ty * BLOCK_Y + 4 * band0);
     uint32_t m = 0;
 #pragma unroll
@@ -208,8 +210,9 @@ __device__ __forceinline__ uint32_t band_mask(float2 xy, float4 co, uint32_t tx,
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const float dy = dy0 - (float)(4 * bb + r);
-            const float dx = fminf(hi, fmaxf(lo, k * dy));
-            const float q = dx * (a * dx + 2.0f * b * dy) + c * dy * dy;
+            const float kdy = k * dy;
+            const float e = __builtin_amdgcn_fmed3f(kdy, lo, hi) - kdy;  // the strip's column nearest the row minimum
+            const float q = __builtin_fmaf(a * e, e, dd * dy * dy);
             hit = hit || q <= t;
         }
         if (hit) m |= 1u << bb;
