@@ -1,4 +1,4 @@
-// wave_ops.h — wave64 cross-lane reductions for gfx950 (DPP + v_permlane{16,32}_swap).
+// wave_ops.h — wave64 cross-lane reductions for gfx950 (DPP, v_permlane{16,32}_swap, LDS transposition).
 #pragma once
 
 #include <hip/hip_runtime.h>
