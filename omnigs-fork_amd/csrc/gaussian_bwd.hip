@@ -218,8 +218,9 @@ __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const
 // ---- per-Gaussian sums of the instance rows (the reference's atomicAdd targets, backward.cu:805-840) ---------
 // Gaussian i owns the contiguous rows [row_first[i], row_first[i] + tiles_touched[i]) of inst_grad: the backward
 // numbers the rows in Gaussian INDEX order (launch_forward_scans), so the 64 Gaussians of a wave own one contiguous
-// span of rows (507 rows on average at config C, 24 % of them marked valid by render_bwd).
-// The wave streams its span through LDS in chunks of RS_ROWS rows: every lane loads 4 rows of the chunk, rows
+// span of rows (507 rows on average at config C, 24 % of them marked valid by render_bwd). Chunks of 128 rows (half
+// the LDS of 256-row chunks, more waves per CU): 0.070 ms vs 0.073 (256) and 0.091 (64) at config C.
+// The wave streams its span through LDS in chunks of RS_ROWS rows: every lane loads RS_Q rows of the chunk, rows
 // q*64 + lane (coalesced), marked ones only, then
 //  * a Gaussian with at most RS_LONG rows adds its rows of the chunk itself, in row order, from LDS;
 //  * a longer one is summed by the whole wave: each lane adds the chunk rows it holds, then one wave reduction
@@ -229,7 +230,11 @@ __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const
 // image; 0.1 % of them at config C, 13 % of the rows) would make their wave the kernel's tail: the wave skips them
 // (and the chunks only they own), and RS_HUGE_BLOCKS extra workgroups at the start of the grid take them from the
 // forward's huge_list, 256 threads per Gaussian. The order of every sum is fixed: the result is deterministic.
-constexpr int RS_ROWS = 256;
+#ifndef OMR_RS_ROWS
+#define OMR_RS_ROWS 128
+#endif
+constexpr int RS_ROWS = OMR_RS_ROWS;  // rows per staged chunk (a multiple of 64)
+constexpr int RS_Q = RS_ROWS / 64;    // rows per lane per chunk
 #ifndef OMR_RS_LONG
 #define OMR_RS_LONG 32
 #endif
@@ -331,40 +336,40 @@ __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
     for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
 
     // row_valid bytes of the first chunk; each iteration requests the next chunk's with its rows
-    uint32_t flag[4];
+    uint32_t flag[RS_Q];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < RS_Q; ++q) {
         const uint32_t r = lo + (uint32_t)q * 64u + lane;
         flag[q] = lo < hi && r < hi ? a.row_valid[r] : 0u;
     }
     for (uint32_t c0 = lo; c0 < hi; c0 += RS_ROWS) {  // lo > hi when the wave owns no rows
         const uint32_t c1 = c0 + RS_ROWS;
-        bool ok[4];
+        bool ok[RS_Q];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) ok[q] = flag[q] != 0;
+        for (int q = 0; q < RS_Q; ++q) ok[q] = flag[q] != 0;
         // chunks inside a skipped huge Gaussian's rows: nothing to stage
         if (!__ballot(n != 0 && s < c1 && e > c0)) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < RS_Q; ++q) {
                 const uint32_t r = c1 + (uint32_t)q * 64u + lane;
                 flag[q] = r < hi ? a.row_valid[r] : 0u;
             }
             continue;
         }
-        float x[4][GRAD_ROW];
+        float x[RS_Q][GRAD_ROW];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < RS_Q; ++q) {
 #pragma unroll
             for (int c = 0; c < GRAD_ROW; ++c) x[q][c] = 0.f;
             add_marked_row(x[q], a.inst_grad, c0 + (uint32_t)q * 64u + lane, ok[q]);
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < RS_Q; ++q) {
             const uint32_t r = c1 + (uint32_t)q * 64u + lane;
             flag[q] = r < hi ? a.row_valid[r] : 0u;
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < RS_Q; ++q)
 #pragma unroll
             for (int c = 0; c < GRAD_ROW; ++c) s_rows[(q * 64 + lane) * GRAD_ROW + c] = x[q][c];
         wave_sync();
@@ -386,7 +391,7 @@ __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
 #pragma unroll
             for (int c = 0; c < GRAD_ROW; ++c) v[c] = 0.f;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < RS_Q; ++q) {
                 const uint32_t pos = (uint32_t)q * 64u + lane;
                 if (pos >= sj && pos < ej)
 #pragma unroll
