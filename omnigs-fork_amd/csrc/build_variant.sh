@@ -15,6 +15,7 @@ SRCS=$(sed -n 's/^SRCS := //p' "$HERE/Makefile" | sed 's/\.hip//g')
 for f in $SRCS; do
     EXTRA=""
     [ "$f" = render_bwd ] && EXTRA="-ffp-contract=fast -fno-slp-vectorize"
+    [ "$f" = render_fwd ] && EXTRA="-fno-slp-vectorize"
     /opt/rocm/bin/hipcc $FLAGS $EXTRA "$@" -c "$HERE/$f.hip" -o "$OBJ/$f.o" &
     pids+=($!)
 done
