@@ -10,8 +10,12 @@ Inputs are synthetic (SplitMix64) and resident in HBM before t
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
         bench.py --gpus N --steps K --warmup W
 
-Rank 0 prints ONE JSON line (the driver's contract), with `roofline` for the dominant kernel (HIP events on the
-launch stream over the timed region) and, at N = 1, `cpu_baseline` (the CPU oracle on a bounded sample).
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment launches the N ranks itself (a child
+torch.distributed.run, before anything touches the GPU) and exits with its status.
+
+Rank 0 prints ONE JSON line (the driver's contract), with `roofline` for the dominant kernel (the stage with the
+largest measured time; HIP events on the launch stream over the timed region) and, at N = 1, `cpu_baseline` (the CPU
+oracle on a bounded sample: medians of >= 10 runs, all cores and one thread).
 """
 from __future__ import annotations
 
@@ -27,7 +31,6 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, Chip-level parameters)
 VALU_PEAK_TFLOPS = 157.3  # MI355X f32 vector peak with v_pk_fma_f32 (MI355X_MICROARCH.md, MFMA/VALU peak table)
-DOMINANT = "render_backward"  # the kernel the roofline reports (largest stage at every config)
 
 
 def parse():
@@ -38,7 +41,8 @@ def parse():
     p.add_argument("--config", default="C", help="scene config of omnigs-fork_amd/scene.py (default C)")
     p.add_argument("--gaussians", type=int, default=None, help="override P (testing only)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-oracle sample budget")
+    p.add_argument("--cpu-seconds", type=float, default=45.0,
+                   help="CPU-oracle time budget per leg (runs stop early past it, after at least 3)")
     p.add_argument("--cpu-threads", type=int, default=None)
     p.add_argument("--bucket-mb", type=float, default=0.0, help="all-reduce bucket size (0 = one collective)")
     p.add_argument("--exchange", choices=["compact", "flat"], default="compact",
@@ -55,7 +59,64 @@ def parse():
     p.add_argument("--no-train-step", action="store_true",
                    help="skip the extra whole-training-iteration timing (N = 1 only; not part of `value`)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    p.add_argument("--ambiguity-json", default=os.path.join(ROOT, "profiles", "ambiguity.json"),
+                   help="boundary-ambiguous Gaussian counts per config (oracle/ambiguity.py), reported as "
+                        "config.ambiguous")
+    p.add_argument("--cpu-runs", type=int, default=10, help="CPU-oracle runs per baseline leg (median reported)")
+    p.add_argument("--cpu-single-config", default="B",
+                   help="config of the one-thread CPU leg (one thread at config C takes ~30 s per run)")
+    p.add_argument("--dist-check", action="store_true",
+                   help="no GPU: only the N-rank launch and rendezvous (gloo), checking the world size; for tests")
     return p.parse_args()
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` run directly (no WORLD_SIZE): start N ranks under torch.distributed.run as a child process
+    (nothing here has touched the GPU) and return its exit status."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    print(f"[bench] launching {n} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dist_check(args) -> int:
+    """--dist-check: the multi-rank path without a GPU (gloo): world size, ranks, per-rank timing gather."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+    if world != args.gpus:
+        print(f"[bench] world size {world} != --gpus {args.gpus}", file=sys.stderr)
+        return 3
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    per_rank = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(per_rank, t)
+    else:
+        per_rank = [t]
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks_seen": world, "per_rank": [float(x.item()) for x in per_rank]}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
 
 
 def stage_bytes(stage, P, V, L, N, T, M=16, D=3):
@@ -95,16 +156,25 @@ def workload_text(cfg_name, config, world, P, W, H, camera_type, sh_degree, exch
     return text
 
 
-def cpu_baseline(g, cam, dL, seconds, threads):
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _oracle_leg(O, g, cam, dL, threads, runs, seconds):
+    """Median seconds of `runs` oracle fwd+bwd passes (stopping early once `seconds` is spent, after >= 3 runs)."""
     import numpy as np
 
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O  # test infrastructure: the CPU restatement, timed as the baseline only
-
-    O.build()
     O.set_threads(threads)
-    it, t_total = 0, 0.0
-    while t_total < seconds or it == 0:
+    times = []
+    t_start = time.perf_counter()
+    while len(times) < runs:
         t0 = time.perf_counter()
         o = O.Oracle(False)
         o.forward(background=np.zeros(3), means3D=g.means3D, opacity=g.opacity, scales=g.scales,
@@ -112,19 +182,45 @@ def cpu_baseline(g, cam, dL, seconds, threads):
                   campos=cam.campos, width=cam.width, height=cam.height, sh_degree=g.sh_degree,
                   camera_type=cam.camera_type)
         o.backward(dL, nthreads=threads)
-        t_total += time.perf_counter() - t0
-        it += 1
+        times.append(time.perf_counter() - t0)
         del o
-        if it >= 3:
+        if len(times) >= 3 and time.perf_counter() - t_start > seconds:
             break
-    mpix = cam.width * cam.height * it / t_total / 1e6
-    return {"value": round(mpix, 4), "unit": "Mpixels/s", "cores": threads, "kind": "port",
-            "sample": f"{it} x fwd+bwd of one {cam.width}x{cam.height} view, P={g.P} (same scene as the GPU run), "
-                      f"{t_total:.1f} s, OpenMP over Gaussians/tiles, oracle/ restatement (no CPU reference exists)"}
+    return float(np.median(times)), times
+
+
+def cpu_baseline(omr, g, cam, dL, seconds, threads, runs, single_config):
+    """The CPU oracle (oracle/, a port: the reference has no CPU path, rasterize_points.cu:87 hard-codes kCUDA) timed
+    on this host: all-core leg on the bench workload itself, one-thread leg on a smaller config (bounded sample)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # test infrastructure: the CPU restatement, timed as the baseline only
+
+    O.build()
+    med, times = _oracle_leg(O, g, cam, dL, threads, runs, seconds)
+    N = cam.width * cam.height
+    out = {"value": round(N / med / 1e6, 4), "unit": "Mpixels/s", "cores": threads, "kind": "port",
+           "cpu_model": cpu_model(),
+           "sample": f"median of {len(times)} fwd+bwd of the bench view ({cam.width}x{cam.height}, P={g.P}, same "
+                     f"scene as the GPU run) on {threads} OpenMP threads: {med:.2f} s (min {min(times):.2f}, max "
+                     f"{max(times):.2f}); oracle/ restatement, no CPU reference exists"}
+    if single_config:
+        g1, cam1, dL1 = omr.scene.config_scene(single_config)
+        med1, t1 = _oracle_leg(O, g1, cam1, dL1, 1, runs, seconds)
+        out["single_thread"] = {
+            "value": round(cam1.width * cam1.height / med1 / 1e6, 4), "unit": "Mpixels/s", "cores": 1,
+            "sample": f"median of {len(t1)} fwd+bwd of config {single_config} ({cam1.width}x{cam1.height}, "
+                      f"P={g1.P}) on one thread: {med1:.2f} s"}
+    O.set_threads(1)
+    return out
 
 
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return launch_ranks(args.gpus)
+    if args.dist_check:
+        return dist_check(args)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -147,8 +243,15 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
-    if world != args.gpus and rank == 0:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        seen = dist.get_world_size()
+        if seen != args.gpus:
+            print(f"[bench] error: --gpus {args.gpus} but the process group has {seen} ranks", file=sys.stderr)
+            return 3
+    elif args.gpus != 1:
+        print(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 3
+    if os.environ.get("OMR_LIB_PATH") and rank == 0:
+        print(f"[bench] warning: OMR_LIB_PATH selects {os.environ['OMR_LIB_PATH']}", file=sys.stderr)
 
     # config D is config C's scene rendered one view per GPU: the same Gaussians for every N (weak scaling)
     cfg_name = "D" if (world > 1 and args.config == "C") else args.config
@@ -171,6 +274,9 @@ def main():
     out = grads.out_dict(dev)
     bucket = int(args.bucket_mb * 1024 * 1024)
     stats = {}
+    stream = torch.cuda.current_stream(dev)
+    compute_events = []  # per step: (start, end of this rank's forward + backward), before the exchange
+    record = {"on": False}
 
     LT = R.libtorch_boundary() if args.boundary == "libtorch" else None
 
@@ -185,10 +291,7 @@ def main():
             for name, idx in (("dL_dmeans3D", 3), ("dL_dsh", 5), ("dL_dopacity", 2), ("dL_dscales", 6),
                               ("dL_drotations", 7), ("dL_dcolors", 1)):
                 (out if name == "dL_dcolors" else grads.views)[name].copy_(gr[idx])
-        exchange()
-        stats["L"] = nr
-        stats["radii"] = radii
-        stats["img"] = ib
+        return nr, radii, ib
 
     def exchange():
         if args.exchange == "compact":
@@ -200,14 +303,21 @@ def main():
             par.allreduce_(grads, info, average=False, bucket_bytes=bucket)
 
     def step():
+        if record["on"]:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(stream)
         if LT is not None:
-            return step_libtorch()
-        nr, color, radii, gb, bb, ib = R.RasterizeGaussiansCUDA(
-            bg, means3D, empty, opacity, scales, rots, 1.0, empty, view, proj, cam.tanfovx, cam.tanfovy, H, W, shs,
-            g.sh_degree, campos, False, cam.camera_type, False)
-        R.RasterizeGaussiansBackwardCUDA(bg, means3D, radii, empty, scales, rots, 1.0, empty, view, proj, cam.tanfovx,
-                                         cam.tanfovy, dL_dout, shs, g.sh_degree, campos, gb, nr, bb, ib,
-                                         cam.camera_type, out=out)
+            nr, radii, ib = step_libtorch()
+        else:
+            nr, color, radii, gb, bb, ib = R.RasterizeGaussiansCUDA(
+                bg, means3D, empty, opacity, scales, rots, 1.0, empty, view, proj, cam.tanfovx, cam.tanfovy, H, W,
+                shs, g.sh_degree, campos, False, cam.camera_type, False)
+            R.RasterizeGaussiansBackwardCUDA(bg, means3D, radii, empty, scales, rots, 1.0, empty, view, proj,
+                                             cam.tanfovx, cam.tanfovy, dL_dout, shs, g.sh_degree, campos, gb, nr, bb,
+                                             ib, cam.camera_type, out=out)
+        if record["on"]:
+            ev[1].record(stream)
+            compute_events.append(ev)
         exchange()
         stats["L"] = nr
         stats["radii"] = radii
@@ -220,11 +330,29 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    # timed region: HIP events around the dominant kernel only (the roofline's live launch duration); events at
-    # every stage boundary would add a few us of GPU idle each, so the full per-stage breakdown comes from a
-    # separate pass after the timed one
+    # per-stage pass (untimed): HIP events at every stage boundary, which cost a few us of GPU idle each; it picks
+    # the dominant stage (the largest: render_backward at A-D, the tile sort at E equirect, gaussian_backward at E
+    # pinhole). The timed pass then records events around that kernel only (the roofline's live launch duration)
+    # and, at N > 1, two per step around this rank's forward + backward (per-rank compute time).
     R.profile_reset()
-    R.profile_enable(True, stages=[DOMINANT])
+    R.profile_enable(True)
+    for _ in range(min(args.steps, 10)):
+        step()
+    torch.cuda.synchronize(dev)
+    R.profile_enable(False)
+    prof = R.profile_read()
+    stage_avg = {k: (ms / c if c else 0.0) for k, (ms, c) in prof.items()}
+    ranked = sorted((k for k in stage_avg if stage_avg[k] > 0), key=lambda k: -stage_avg[k])
+    dom = ranked[0]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    R.profile_reset()
+    R.profile_enable(True, stages=[dom])
+    R.runtime_stats_reset()
+    torch.cuda.reset_peak_memory_stats(dev)
+    mem0 = torch.cuda.memory_stats(dev)
+    record["on"] = world > 1
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -233,21 +361,27 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    record["on"] = False
+    mem1 = torch.cuda.memory_stats(dev)
+    host_stats = R.runtime_stats()
     R.profile_enable(False)
     live = R.profile_read()
-    R.profile_reset()
-    R.profile_enable(True)
-    for _ in range(min(args.steps, 10)):
-        step()
-    torch.cuda.synchronize(dev)
-    R.profile_enable(False)
-    prof = R.profile_read()
+    if compute_events:
+        compute_ms = sum(a.elapsed_time(b) for a, b in compute_events) / len(compute_events)
+    else:  # N = 1: the whole step is this rank's forward + backward
+        compute_ms = elapsed / args.steps * 1e3
     if V is None:
         V = int((stats["radii"] > 0).sum().item())
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+        cm = torch.tensor([compute_ms], dtype=torch.float64, device=dev)
+        per_rank = [torch.zeros_like(cm) for _ in range(world)]
+        dist.all_gather(per_rank, cm)
+        per_rank_ms = [round(float(x.item()), 4) for x in per_rank]
+    else:
+        per_rank_ms = [round(compute_ms, 4)]
 
     ms_per_step = elapsed / args.steps * 1e3
     # whole-job pixels per step: every rank's view (ranks of a mixed config render different resolutions)
@@ -258,21 +392,28 @@ def main():
     L, N = int(stats["L"]), W * H
     T = ((W + 15) // 16) * ((H + 15) // 16)
 
-    # dominant kernel from the live stage timings (HIP events on the launch stream)
-    stage_avg = {k: (ms / c if c else 0.0) for k, (ms, c) in prof.items()}
-    dom = DOMINANT
-    dom_bytes = stage_bytes(dom, P, V, L, N, T, M, g.sh_degree)
-    ms, cnt = live.get(dom, (0.0, 0))
-    dom_ms = ms / cnt if cnt else stage_avg[dom]
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-    traffic = None
+    # dominant kernel: the largest stage of the per-stage pass; its launch duration from the timed pass (HIP events
+    # on the launch stream around that kernel alone)
+    pmc = {}
     try:
         with open(args.traffic_json) as f:
-            pmc = json.load(f)
-        if pmc.get("config") == cfg_name and pmc.get("P") == P and dom in pmc.get("kernels", {}):
-            traffic = pmc["kernels"][dom].get("hbm_bytes_per_launch")
+            pj = json.load(f)
+        if pj.get("config") == cfg_name and pj.get("P") == P:
+            pmc = pj.get("kernels", {})
     except (OSError, ValueError):
         pass
+
+    def stage_entry(k, live_ok=True):
+        b = stage_bytes(k, P, V, L, N, T, M, g.sh_degree)
+        ms_l, cnt_l = live.get(k, (0.0, 0))
+        ms_k = ms_l / cnt_l if (cnt_l and live_ok) else stage_avg[k]
+        ach = b / (ms_k * 1e-3) / 1e9 if ms_k > 0 else 0.0
+        tr = pmc.get(k, {}).get("hbm_bytes_per_launch")
+        return {"stage": k, "avg_launch_ms": round(ms_k, 4), "algorithmic_bytes_per_launch": b,
+                "achieved_GBps": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": tr,
+                "traffic_over_algorithmic": round(tr / b, 3) if (tr and b) else None}
+
+    d = stage_entry(dom)
     algo_total = sum(stage_bytes(s, P, V, L, N, T, M, g.sh_degree) for s in stage_avg)
     # VALU secondary: pixel-instance evaluations = the forward's (instance, 16x4 band) pairs x 64,
     # at nominal 20 flop (forward) / 60 flop (backward) each, against the f32 vector peak; the backward evaluates at
@@ -283,6 +424,13 @@ def main():
         ms_k = stage_avg.get(k, 0.0)
         tf = evals * fl / (ms_k * 1e-3) / 1e12 if ms_k > 0 else 0.0
         valu[k] = {"flop_per_eval": fl, "tflops": round(tf, 2), "frac": round(tf / VALU_PEAK_TFLOPS, 4)}
+    ambiguous = None
+    try:
+        with open(args.ambiguity_json) as f:
+            ambiguous = json.load(f).get("configs", {}).get(scene_name if world == 1 else cfg_name)
+    except (OSError, ValueError):
+        pass
+    delta = lambda k: int(mem1.get(k, 0) - mem0.get(k, 0))
     result = {
         "metric": "Mpixels/s fwd+bwd, 1M Gaussians @ 2048x1024 equirect; 1/2/4/8 GPU",
         "value": round(value, 3),
@@ -300,18 +448,30 @@ def main():
                                                args.exchange),
                    "P": P, "V": V, "L": L, "N": N, "T": T, "width": W, "height": H,
                    "parallelism": f"view-parallel dp{world}", "boundary": args.boundary,
-                   "exchange": args.exchange if world > 1 else None},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 4),
-                     "step_algorithmic_GBps": round(algo_total / (ms_per_step * 1e-3) / 1e9, 2)},
+                   "exchange": args.exchange if world > 1 else None, "ambiguous": ambiguous},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": d["achieved_GBps"], "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": d["frac"], "traffic": d["traffic"],
+                     "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
+                     "avg_launch_ms": d["avg_launch_ms"],
+                     "step_algorithmic_GBps": round(algo_total / (ms_per_step * 1e-3) / 1e9, 2),
+                     "top_stages": [stage_entry(k) for k in ranked[:3]]},
         "stages_ms": {k: round(v, 4) for k, v in stage_avg.items()},
         "valu_secondary": valu,
+        "ranks": {"seen": world, "compute_ms_per_rank": per_rank_ms,
+                  "imbalance_max_over_mean": round(max(per_rank_ms) / (sum(per_rank_ms) / len(per_rank_ms)), 4)
+                  if sum(per_rank_ms) > 0 else None,
+                  "backend": (dist.get_backend() if world > 1 else None)},
+        "host": {"library": R.loaded_library(), "runtime_stats_timed": host_stats,
+                 "torch_allocator_timed": {"device_mallocs": delta("num_device_alloc"),
+                                           "device_frees": delta("num_device_free"),
+                                           "alloc_retries": delta("num_alloc_retries"),
+                                           "peak_reserved_bytes": int(mem1.get("reserved_bytes.all.peak", 0))}},
     }
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
         try:
-            result["cpu_baseline"] = cpu_baseline(g, cam, dL, args.cpu_seconds, threads)
+            result["cpu_baseline"] = cpu_baseline(omr, g, cam, dL, args.cpu_seconds, threads, args.cpu_runs,
+                                                  args.cpu_single_config)
         except Exception as ex:  # the GPU number stands on its own; report why the baseline is missing
             result["cpu_baseline"] = {"value": None, "error": repr(ex)}
     if world == 1 and rank == 0 and not args.no_train_step:
@@ -323,6 +483,7 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 def train_step_timing(omr, g, cam, dev, steps, warmup):
@@ -363,4 +524,4 @@ def train_step_timing(omr, g, cam, dev, steps, warmup):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

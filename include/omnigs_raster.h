@@ -210,6 +210,16 @@ void omr_profile_reset(void);
 int omr_profile_read(double* total_ms, uint64_t* counts, int n);
 const char* omr_profile_stage_name(int stage);
 
+/* --- host-side runtime counters (process-wide, since load or the last reset; for bench.py / tools) ----- */
+/* 0 forwards, 1 backwards, 2 first_call_syncs (forwards that waited for num_rendered before sizing the binning
+ * buffer), 3 back_half_reruns (capacity hint too small), 4 count_wait_ns (host time waiting for num_rendered),
+ * 5 backward_wait_ns (host time waiting for the forward's error word), 6 alloc_calls, 7 alloc_bytes (allocation
+ * callbacks), 8 lookback_errors (decoupled look-backs that gave up; the call returned OMR_ERR_HIP) */
+#define OMR_NUM_RUNTIME_STATS 9
+int omr_runtime_stats(uint64_t* out, int n);
+const char* omr_runtime_stat_name(int i);
+void omr_runtime_stats_reset(void);
+
 /* --- introspection for tests / tools (read from the private scratch layout) ---------------------- */
 /* copies the sorted per-instance Gaussian indices (R entries) and tile ranges ([T] uint2) to device dst */
 int omr_debug_point_list(char* binning_buffer, int R, int width, int height, uint32_t* dst, void* stream);

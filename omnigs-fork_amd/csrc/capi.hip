@@ -7,6 +7,10 @@
 //   render backward (per-instance gradient rows) -> fused per-Gaussian backward.
 // Everything is enqueued on the caller's stream; no allocation happens outside the three callbacks.
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <deque>
+#include <mutex>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -87,7 +91,10 @@ enum Stage { ST_PREPROCESS, ST_DEPTH_SORT, ST_SCAN, ST_EMIT, ST_TILE_SORT, ST_RA
 const char* kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "scan", "emit", "tile_sort", "tile_ranges",
                                      "render_forward", "render_backward", "gaussian_backward", "row_sums"};
 
+// Diagnostic (bench.py, tests): one process-wide profiler, guarded by a mutex; its events belong to the device that
+// was current when they were created, so profile one device per process.
 struct Profiler {
+    std::mutex mu;
     bool on = false;
     uint32_t mask = ~0u;
     struct Rec {
@@ -98,7 +105,7 @@ struct Profiler {
     std::vector<hipEvent_t> pool;
     double total_ms[ST_COUNT] = {};
     uint64_t count[ST_COUNT] = {};
-    hipEvent_t get()
+    hipEvent_t get()  // caller holds mu
     {
         if (!pool.empty()) {
             hipEvent_t e = pool.back();
@@ -119,6 +126,7 @@ struct StageScope {
     StageScope(int st, hipStream_t stream) : stage(st), s(stream)
     {
         if (g_prof.on && (g_prof.mask >> st) & 1u) {
+            std::lock_guard<std::mutex> lk(g_prof.mu);
             a = g_prof.get();
             if (a) (void)hipEventRecord(a, s);
         }
@@ -126,6 +134,7 @@ struct StageScope {
     ~StageScope()
     {
         if (a) {
+            std::lock_guard<std::mutex> lk(g_prof.mu);
             hipEvent_t b = g_prof.get();
             if (b) {
                 (void)hipEventRecord(b, s);
@@ -135,22 +144,69 @@ struct StageScope {
     }
 };
 
-// pinned host words for the one device->host read of the forward (num_rendered, prefiltered flag)
-uint32_t* pinned_words()
+// Host-visible words the forward and backward read back, per (thread, device): a forward may run on any device's
+// stream, and an event can only be recorded on a stream of the device it was created on.
+//   words[0..3] <- counters[0..3] after the forward's scan (num_rendered, prefiltered flag, huge count, error word)
+//   words[4]    <- counters[3] at the start of the backward (look-back errors of the forward's back half)
+struct HostSlots {
+    int device = -1;
+    uint32_t* words = nullptr;
+    hipEvent_t ev_count = nullptr, ev_bwd = nullptr;
+};
+
+int stream_device(hipStream_t s)
 {
-    thread_local uint32_t* p = nullptr;
-    if (!p) {
-        if (hipHostMalloc(reinterpret_cast<void**>(&p), 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) p = nullptr;
+    int dev = 0;
+    if (s) {
+        hipDevice_t d;
+        if (hipStreamGetDevice(s, &d) == hipSuccess) return (int)d;
     }
-    return p;
+    (void)hipGetDevice(&dev);
+    return dev;
 }
 
-// event recorded after the num_rendered copy (one per thread; the forward waits on it at most once per call)
-hipEvent_t count_event()
+HostSlots* host_slots(hipStream_t s)
 {
-    thread_local hipEvent_t e = nullptr;
-    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
-    return e;
+    thread_local std::deque<HostSlots> slots;  // deque: pointers stay valid as devices are added
+    const int dev = stream_device(s);
+    for (auto& h : slots)
+        if (h.device == dev) return &h;
+    int cur = dev;
+    (void)hipGetDevice(&cur);
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
+    HostSlots h;
+    h.device = dev;
+    const bool ok = hipHostMalloc(reinterpret_cast<void**>(&h.words), 8 * sizeof(uint32_t), hipHostMallocPortable) == hipSuccess &&
+                    hipEventCreateWithFlags(&h.ev_count, hipEventDisableTiming) == hipSuccess &&
+                    hipEventCreateWithFlags(&h.ev_bwd, hipEventDisableTiming) == hipSuccess;
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (!ok) return nullptr;
+    slots.push_back(h);
+    return &slots.back();
+}
+
+// process-wide counters of what the host side of the rasterizer did (omr_runtime_stats): evidence for host stalls
+enum RtStat { RS_FORWARDS, RS_BACKWARDS, RS_FIRST_CALL_SYNCS, RS_BACK_HALF_RERUNS, RS_COUNT_WAIT_NS, RS_BWD_WAIT_NS,
+              RS_ALLOC_CALLS, RS_ALLOC_BYTES, RS_LOOKBACK_ERRORS, RS_COUNT };
+const char* kRtStatNames[RS_COUNT] = {"forwards", "backwards", "first_call_syncs", "back_half_reruns", "count_wait_ns",
+                                      "backward_wait_ns", "alloc_calls", "alloc_bytes", "lookback_errors"};
+std::atomic<uint64_t> g_rt[RS_COUNT];
+void rt_add(int k, uint64_t v) { g_rt[k].fetch_add(v, std::memory_order_relaxed); }
+
+// host wait on an event, timed into a runtime counter
+hipError_t timed_event_sync(hipEvent_t e, int stat)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    const hipError_t r = hipEventSynchronize(e);
+    rt_add(stat, (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+    return r;
+}
+
+void* alloc_counted(omr_alloc_fn fn, void* ctx, size_t bytes)
+{
+    rt_add(RS_ALLOC_CALLS, 1);
+    rt_add(RS_ALLOC_BYTES, bytes);
+    return fn(ctx, bytes);
 }
 
 // per-thread capacity hint for the binning buffer, by view shape (L depends mostly on the resolution and camera)
@@ -295,11 +351,11 @@ int forward_impl(const ForwardIn& in)
     const hipStream_t s = in.stream;
     const size_t P = (size_t)in.P;
 
-    char* geom_base = static_cast<char*>(in.geometry_alloc(in.geometry_ctx, GeomState::carve(nullptr, P, nullptr)));
+    char* geom_base = static_cast<char*>(alloc_counted(in.geometry_alloc, in.geometry_ctx, GeomState::carve(nullptr, P, nullptr)));
     if (!geom_base) return fail(OMR_ERR_ALLOCATION, "geometry allocation failed");
     GeomState g;
     GeomState::carve(geom_base, P, &g);
-    char* img_base = static_cast<char*>(in.image_alloc(in.image_ctx, ImageState::carve(nullptr, d.N, d.T, nullptr)));
+    char* img_base = static_cast<char*>(alloc_counted(in.image_alloc, in.image_ctx, ImageState::carve(nullptr, d.N, d.T, nullptr)));
     if (!img_base) return fail(OMR_ERR_ALLOCATION, "image allocation failed");
     ImageState im;
     ImageState::carve(img_base, d.N, d.T, &im);
@@ -308,7 +364,7 @@ int forward_impl(const ForwardIn& in)
     // counters[1] is the prefiltered-cull flag, set by preprocess itself: cleared first, and only when it can be set
     if (in.prefiltered) OMR_HIP(hipMemsetAsync(g.counters + 1, 0, sizeof(uint32_t), s));
     PreprocessArgs pa;
-    pa.zero[0] = {g.counters + 2, 2};                                  // huge-list count (scan), spare
+    pa.zero[0] = {g.counters + 2, 2};                                  // huge-list count (scan), look-back error word
     pa.zero[1] = {reinterpret_cast<uint32_t*>(im.ranges), 2 * (size_t)d.T};  // tile_ranges writes boundaries only
     pa.zero[2] = {im.tile_cost, (size_t)d.T};                          // render_forward adds into it
     pa.zero[3] = radix_zero_span(g.hist, P, DEPTH_SORT_PASSES);        // the depth sort's digit totals / tickets
@@ -327,45 +383,54 @@ int forward_impl(const ForwardIn& in)
     { StageScope st_(ST_PREPROCESS, s); launch_preprocess(in.camera_type, pa, s); }
 
     // depth order of the Gaussians (stable: ties keep index order)
-    int which; { StageScope st_(ST_DEPTH_SORT, s); which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr, nullptr, 0, DEPTH_SORT_PASSES, s, true); }
+    uint32_t* const err_dev = g.counters + 3;  // every decoupled look-back of the forward reports a give-up here
+    int which; { StageScope st_(ST_DEPTH_SORT, s); which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr, nullptr, 0, DEPTH_SORT_PASSES, s, true, err_dev); }
     g.order = which ? g.val_b : g.val_a;
-    { StageScope st_(ST_SCAN, s); launch_forward_scans(g.tiles_touched, g.order, g.offsets, g.row_first, g.huge_list, g.counters + 2, g.scan2_status, P, s); }
+    { StageScope st_(ST_SCAN, s); launch_forward_scans(g.tiles_touched, g.order, g.offsets, g.row_first, g.huge_list, g.counters + 2, g.scan2_status, g.counters, err_dev, P, s); }
 
     // num_rendered = offsets[P-1] (+ the prefiltered error flag) to pinned host memory, without waiting for it:
     // the binning buffer is sized from a capacity hint and everything after the scan reads the count on the device,
     // so the GPU never idles on this host round trip (the reference synchronises here, rasterizer_impl.cu:628).
     // The host checks the count once the rest of the forward is queued; a hint that was too small costs one
     // re-run of the back half with the exact size.
-    uint32_t* host = pinned_words();
-    hipEvent_t ev_count = count_event();
-    if (!host || !ev_count) return fail(OMR_ERR_HIP, "pinned host memory / event allocation failed");
-    const uint32_t* count_dev = g.offsets + (P - 1);
-    OMR_HIP(hipMemcpyAsync(host, count_dev, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    host[1] = 0;
-    if (in.prefiltered) OMR_HIP(hipMemcpyAsync(host + 1, g.counters + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HostSlots* hs = host_slots(s);
+    if (!hs) return fail(OMR_ERR_HIP, "pinned host memory / event allocation failed");
+    uint32_t* host = hs->words;
+    hipEvent_t ev_count = hs->ev_count;
+    const uint32_t* count_dev = g.counters;  // {num_rendered, -, -, error word}: raster_common.h binning_count
+    // one copy: num_rendered (scan), prefiltered flag (preprocess; meaningful only when prefiltered is set), huge
+    // count, look-back error word (depth sort, scan)
+    OMR_HIP(hipMemcpyAsync(host, g.counters, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     OMR_HIP(hipEventRecord(ev_count, s));
+    rt_add(RS_FORWARDS, 1);
 
     const int tile_passes = tile_sort_passes(d.T);
     size_t& hint = capacity_hint(in.width, in.height, in.camera_type);
     bool known = false;
     size_t L = 0;
     auto wait_count = [&]() -> int {
-        OMR_HIP(hipEventSynchronize(ev_count));
+        OMR_HIP(timed_event_sync(ev_count, RS_COUNT_WAIT_NS));
         if (int e = hip_check("preprocess/sort/scan")) return e;
-        if (host[1] != 0)
+        if (in.prefiltered && host[1] != 0)
             return fail(OMR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+        if (host[3] != 0) {
+            rt_add(RS_LOOKBACK_ERRORS, 1);
+            return fail(OMR_ERR_HIP, "depth sort / scan: a decoupled look-back gave up waiting for a predecessor");
+        }
         L = host[0];
         known = true;
         return OMR_OK;
     };
-    if (hint == 0)  // first call for this view shape: learn L the reference's way
+    if (hint == 0) {  // first call for this view shape: learn L the reference's way
+        rt_add(RS_FIRST_CALL_SYNCS, 1);
         if (int e = wait_count()) return e;
+    }
     size_t cap = known ? L : hint;
 
     bool rerun = false;  // a second back half must clear what the first one wrote (preprocess zeroed it once)
     auto back_half = [&](size_t capacity) -> int {
         char* bin_base = static_cast<char*>(
-            in.binning_alloc(in.binning_ctx, BinningState::carve(nullptr, capacity, nullptr, tile_passes)));
+            alloc_counted(in.binning_alloc, in.binning_ctx, BinningState::carve(nullptr, capacity, nullptr, tile_passes)));
         if (!bin_base) return fail(OMR_ERR_ALLOCATION, "binning allocation failed");
         BinningState b;
         BinningState::carve(bin_base, capacity, &b, tile_passes);
@@ -373,7 +438,7 @@ int forward_impl(const ForwardIn& in)
         {
             StageScope st_(ST_TILE_SORT, s);
             radix_sort_pairs(b.key_a, b.key_b, b.val_a, b.val_b, b.hist, b.scan_partials, capacity, count_dev,
-                             bin_base, 0, tile_passes, s);
+                             bin_base, 0, tile_passes, s, false, err_dev);
         }
         if (rerun) OMR_HIP(hipMemsetAsync(im.ranges, 0, d.T * sizeof(uint2), s));
         {
@@ -398,6 +463,7 @@ int forward_impl(const ForwardIn& in)
     if (L > cap) {  // the hint was too small: redo the back half at the exact size (outputs are overwritten)
         cap = L;
         rerun = true;
+        rt_add(RS_BACK_HALF_RERUNS, 1);
         if (int e = back_half(cap)) return e;
     }
     hint = L + L / 8 + 4096;
@@ -446,6 +512,14 @@ int backward_impl(const BackwardIn& in)
     ImageState im;
     ImageState::carve(in.image_buffer, d.N, d.T, &im);
     const int* radii = in.radii ? in.radii : geom_internal_radii(in.geom_buffer, P);
+    rt_add(RS_BACKWARDS, 1);
+    // the forward's back half (emit, tile sort) reports look-back give-ups into counters[3] after the forward
+    // returned: read it here, and wait for it only once the whole backward is queued (no GPU bubble)
+    HostSlots* hs = host_slots(s);
+    if (!hs) return fail(OMR_ERR_HIP, "pinned host memory / event allocation failed");
+    hs->words[4] = 0;
+    OMR_HIP(hipMemcpyAsync(hs->words + 4, g.counters + 3, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    OMR_HIP(hipEventRecord(hs->ev_bwd, s));
 
     RenderBwdArgs rb;
     rb.W = in.width; rb.H = in.height; rb.gx = d.gx; rb.gy = d.gy;
@@ -477,7 +551,13 @@ int backward_impl(const BackwardIn& in)
     ga.dL_dscale = in.dL_dscale; ga.dL_drot = in.dL_drot; ga.dpx_dt = in.dpx_dt; ga.dpy_dt = in.dpy_dt;
     if (!in.shs) ga.shs = nullptr;
     { StageScope st_(ST_GAUSS_BWD, s); launch_gaussian_backward(in.camera_type, ga, s); }
-    return hip_check("backward");
+    if (int e = hip_check("backward")) return e;
+    OMR_HIP(timed_event_sync(hs->ev_bwd, RS_BWD_WAIT_NS));
+    if (hs->words[4] != 0) {
+        rt_add(RS_LOOKBACK_ERRORS, 1);
+        return fail(OMR_ERR_HIP, "forward tile sort: a decoupled look-back gave up waiting for a predecessor");
+    }
+    return OMR_OK;
 }
 
 }  // namespace
@@ -822,6 +902,7 @@ void omr_profile_set_mask(uint32_t mask) { g_prof.mask = mask; }
 
 void omr_profile_reset(void)
 {
+    std::lock_guard<std::mutex> lk(g_prof.mu);
     for (auto& r : g_prof.pending) {
         (void)hipEventSynchronize(r.b);
         g_prof.pool.push_back(r.a);
@@ -836,6 +917,7 @@ void omr_profile_reset(void)
 
 int omr_profile_read(double* total_ms, uint64_t* counts, int n)
 {
+    std::lock_guard<std::mutex> lk(g_prof.mu);
     for (auto& r : g_prof.pending) {
         (void)hipEventSynchronize(r.b);
         float ms = 0.f;
@@ -853,6 +935,20 @@ int omr_profile_read(double* total_ms, uint64_t* counts, int n)
         if (counts) counts[i] = g_prof.count[i];
     }
     return m;
+}
+
+int omr_runtime_stats(uint64_t* out, int n)
+{
+    const int m = std::min(n, (int)RS_COUNT);
+    for (int i = 0; i < m; ++i) out[i] = g_rt[i].load(std::memory_order_relaxed);
+    return m;
+}
+
+const char* omr_runtime_stat_name(int i) { return (i >= 0 && i < RS_COUNT) ? kRtStatNames[i] : ""; }
+
+void omr_runtime_stats_reset(void)
+{
+    for (int i = 0; i < RS_COUNT; ++i) g_rt[i].store(0, std::memory_order_relaxed);
 }
 
 const char* omr_profile_stage_name(int stage) { return (stage >= 0 && stage < ST_COUNT) ? kStageNames[stage] : ""; }

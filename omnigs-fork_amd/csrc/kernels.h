@@ -51,17 +51,20 @@ size_t radix_partials_words(size_t n);
 // the forward's scans of tiles_touched (sort.hip): offsets = inclusive scan in depth order (gather by order),
 // row_first = exclusive scan in index order (gradient row numbering); huge_list / *huge_count (zeroed by the
 // caller) = the Gaussians with more than ROW_SUM_HUGE tiles; status: scan2_status_words(n) words, zeroed before
-// the launch (one look-back kernel)
+// the launch (one look-back kernel); *count_out = offsets[n-1] (num_rendered); err (device word, zeroed by the
+// caller; NULL = a private word) is OR-ed with 1 if a look-back gave up (sort.hip: LB_SPIN_MAX)
 size_t scan2_status_words(size_t n);
 void launch_forward_scans(const uint32_t* tiles_touched, const uint32_t* order, uint32_t* offsets, uint32_t* row_first,
-                          uint32_t* huge_list, uint32_t* huge_count, uint32_t* status, size_t n, hipStream_t s);
+                          uint32_t* huge_list, uint32_t* huge_count, uint32_t* status, uint32_t* count_out,
+                          uint32_t* err, size_t n, hipStream_t s);
 // stable LSD radix sort of (key, value) over bits [0, 8*passes); returns which buffer holds the result (0: a, 1: b).
 // n = capacity; count (device, may be NULL) = live element count <= n. canon != NULL: the last pass writes the
 // values to the canonical point list of the binning buffer at canon (raster_common.h) instead of val_a / val_b.
-// scratch_zeroed: the caller has zeroed radix_zero_span(hist, n, passes) (else the sort clears it itself)
+// scratch_zeroed: the caller has zeroed radix_zero_span(hist, n, passes) (else the sort clears it itself).
+// err (device word; NULL = a private word in the scratch) is OR-ed with 1 if a decoupled look-back gave up.
 int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* hist,
                      uint32_t* scan_partials, size_t n, const uint32_t* count, char* canon, int first_pass, int passes,
-                     hipStream_t s, bool scratch_zeroed = false);
+                     hipStream_t s, bool scratch_zeroed = false, uint32_t* err = nullptr);
 // the words of `hist` a sort of n items over `passes` passes needs zeroed before it starts (possibly none)
 ZeroSpan radix_zero_span(uint32_t* hist, size_t n, int passes);
 // duplicateWithKeys; L_cap = capacity, *count (device) = num_rendered; block_owner: emit_index_size(L_cap) words
@@ -83,7 +86,7 @@ struct RenderFwdArgs {
     const uint2* ranges;
     const uint32_t* tile_order;  // [T] schedule (launch_tile_order)
     const char* binning;         // binning buffer: the point list is at binning + canonical_list_offset(*count)
-    const uint32_t* count;       // num_rendered (device)
+    const uint32_t* count;       // device count words (GeomState::counters; raster_common.h binning_count)
     size_t capacity;             // instances the binning buffer was sized for (count > capacity: render nothing)
     const float4* splat;  // [P][SPLAT_F4] render records
     const float* bg;

@@ -81,7 +81,7 @@ struct GeomState {
     uint32_t* scan_partials;  // scan block sums
     uint32_t* scan2_status;   // look-back words of the forward scans (launch_forward_scans), zeroed by preprocess
     uint32_t* offsets;        // inclusive scan of tiles_touched in depth order
-    uint32_t* counters;       // [0] = num_rendered
+    uint32_t* counters;       // [0] num_rendered, [1] prefiltered-cull flag, [2] huge_list count, [3] look-back error
     uint32_t* order;          // depth order (points at val_a or val_b after the sort)
     uint32_t* row_first;      // first gradient row of each Gaussian (index-order exclusive scan, launch_forward_scans)
     float* row_sums;          // backward: [P][GRAD_ROW] each Gaussian's instance rows summed (launch_row_sums)
@@ -117,6 +117,15 @@ __host__ __device__ inline size_t row_valid_offset(size_t L)
 {
     return canonical_list_offset(L) + ((L * sizeof(uint32_t) + ALIGN - 1) & ~(ALIGN - 1));
 }
+// The forward's device count word: counters[0] = num_rendered, counters[3] = look-back error word (GeomState).
+// The binning kernels (sort.hip: live_count) and the forward render see 0 instances when the count exceeds the
+// capacity the binning buffer was sized for or when a decoupled look-back gave up.
+__device__ __forceinline__ size_t binning_count(const uint32_t* counters, size_t capacity)
+{
+    const uint32_t L = counters[0];
+    return (L <= capacity && counters[3] == 0u) ? (size_t)L : 0u;
+}
+
 struct BinningState {
     float* inst_grad;      // [L][GRAD_ROW] backward scratch, indexed by gradient row slot (offset 0)
     uint32_t* point_list;  // sorted Gaussian indices at base + canonical_list_offset(L) (host-known only when L is)

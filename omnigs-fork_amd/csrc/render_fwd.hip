@@ -81,8 +81,8 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
         if (__ballot(inside)) active |= 1u << b;
     }
 
-    // a count past the capacity: the binning kernels did nothing (sort.hip: live_count) and the ranges stay empty
-    const size_t L = *a.count <= a.capacity ? *a.count : 0u;
+    // a count past the capacity or a failed look-back: the binning kernels did nothing and the ranges stay empty
+    const size_t L = binning_count(a.count, a.capacity);
     const uint32_t* point_list = reinterpret_cast<const uint32_t*>(a.binning + canonical_list_offset(L));
     const uint2 range = L ? a.ranges[tile] : make_uint2(0u, 0u);
     const uint32_t n = range.y - range.x;

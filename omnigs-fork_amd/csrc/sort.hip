@@ -63,6 +63,11 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t* s
 // Tiles are handed out by a ticket; a tile publishes its total (AGG), looks back over its predecessors with one
 // wave, 64 tiles per round trip, until it meets an inclusive prefix (PRE), then publishes its own. 64-bit status
 // words, flag in bits 62-63, zeroed before the launch.
+#ifndef OMR_LB_SPIN_MAX
+#define OMR_LB_SPIN_MAX (1u << 20)
+#endif
+constexpr uint32_t LB_SPIN_MAX = OMR_LB_SPIN_MAX;  // polls of one status word before a look-back gives up and sets the
+                                                   // error word (capi.hip reports it as OMR_ERR_HIP; a test build shrinks it)
 constexpr uint64_t SLB_AGG = 1ull << 62, SLB_PRE = 2ull << 62, SLB_VAL = SLB_AGG - 1;
 
 __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src)
@@ -82,7 +87,7 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
 }
 
 // Called by all 64 lanes of one wave of tile vb: publishes `total`, returns the exclusive prefix of the tile (on every
-// lane) and publishes the inclusive one. A predecessor that never publishes ends the wait after 2^20 polls with the
+// lane) and publishes the inclusive one. A predecessor that never publishes ends the wait after LB_SPIN_MAX polls with the
 // error word set (no hang).
 __device__ uint64_t wave_lookback(uint64_t* status, uint32_t vb, uint32_t total, uint32_t lane, uint32_t* err)
 {
@@ -101,7 +106,7 @@ __device__ uint64_t wave_lookback(uint64_t* status, uint32_t vb, uint32_t total,
         const uint32_t k = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
         excl += wave_sum_u64(lane < k || (lane == k && (st & SLB_PRE)) ? (st & SLB_VAL) : 0ull);
         if (k < 64u && (shfl_u64(st, (int)k) & SLB_PRE)) break;
-        if (k == 0 && ++spins > (1u << 20)) {
+        if (k == 0 && ++spins > LB_SPIN_MAX) {
             if (lane == 0) atomicOr(err, 1u);
             break;
         }
@@ -125,7 +130,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint
                                                                       uint64_t* status_d, uint64_t* status_i,
                                                                       uint32_t* ticket, uint32_t* err,
                                                                       uint32_t* offsets, uint32_t* row_first,
-                                                                      uint32_t* huge_list, uint32_t* huge_count)
+                                                                      uint32_t* huge_list, uint32_t* huge_count,
+                                                                      uint32_t* count_out)
 {
     __shared__ uint32_t s_d[SCAN_TILE + SCAN_TILE / 32];  // +1 pad per 32 to break the 16-stride conflicts
     __shared__ uint32_t s_i[SCAN_TILE + SCAN_TILE / 32];
@@ -141,11 +147,13 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint
     const uint32_t vb = s_vb;
     const size_t base = (size_t)vb * SCAN_TILE;
     auto pad = [](uint32_t i) { return i + (i >> 5); };
+    // a depth sort whose look-back gave up may leave `order` partly unwritten: never gather through it then
+    const bool order_ok = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; ++k) {
         const uint32_t li = k * SCAN_THREADS + tid;
         const size_t i = base + li;
-        s_d[pad(li)] = i < n ? in[order[i]] : 0u;
+        s_d[pad(li)] = i < n && order_ok ? in[order[i]] : 0u;
         s_i[pad(li)] = i < n ? in[i] : 0u;
     }
     __syncthreads();
@@ -191,6 +199,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint
         const size_t i = base + li;
         if (i < n) {
             offsets[i] = s_d[pad(li)];
+            if (i == n - 1) *count_out = s_d[pad(li)];  // num_rendered next to the flag words the host reads
             row_first[i] = s_i[pad(li)];
             if (hrank[k] != 0xFFFFFFFFu) huge_list[s_huge_base + hrank[k]] = (uint32_t)i;
         }
@@ -253,12 +262,12 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_lookback_kernel(const uint3
 constexpr uint32_t SELF_SCAN_MAX_BLOCKS = 512;
 
 // ---- radix sort ------------------------------------------------------------------------------------------
-// element count: the host's n, or *count when the count lives on the device (binning, capi.hip). A device count
-// above the capacity n means the forward sized the binning buffer from a hint that was too small: every binning
-// kernel then does nothing (count 0) and the host re-runs the back half at the exact size (capi.hip).
+// element count: the host's n, or the device count word (binning, capi.hip; raster_common.h: binning_count), which
+// reads as 0 when the count is past the capacity (the host re-runs the back half at the exact size) or when a
+// look-back has given up (the call fails; nothing downstream touches possibly corrupt offsets or permutations)
 __device__ __forceinline__ size_t live_count(size_t n, const uint32_t* count)
 {
-    return count ? ((size_t)*count <= n ? (size_t)*count : 0) : n;
+    return count ? binning_count(count, n) : n;
 }
 
 // BLOCK_MAJOR: hist[block][digit] (read back by the self-scanning downsweep of small sorts); else hist[digit][block]
@@ -411,7 +420,6 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_downsweep_kernel(const uin
 // started, and no block waits on a later one: the look-back always finishes (each wait is also bounded, see below).
 // The ranking inside a block is radix_downsweep_kernel's; the result is the same stable permutation.
 constexpr uint32_t LB_AGG = 1u << 30, LB_PRE = 2u << 30, LB_COUNT = LB_AGG - 1u;
-constexpr uint32_t LB_SPIN_MAX = 1u << 20;  // polls of one status word before a block gives up (sets the error word)
 #ifndef OMR_LB_WINDOW
 #define OMR_LB_WINDOW 8
 #endif
@@ -739,14 +747,16 @@ size_t radix_partials_words(size_t n) { return 2 * scan_partials_size(radix_hist
 size_t scan2_status_words(size_t n) { return 4 * div_up(n, SCAN_TILE) + 2; }
 
 void launch_forward_scans(const uint32_t* tiles_touched, const uint32_t* order, uint32_t* offsets, uint32_t* row_first,
-                          uint32_t* huge_list, uint32_t* huge_count, uint32_t* status, size_t n, hipStream_t s)
+                          uint32_t* huge_list, uint32_t* huge_count, uint32_t* status, uint32_t* count_out,
+                          uint32_t* err, size_t n, hipStream_t s)
 {
     if (n == 0) return;
     const uint32_t nb = div_up(n, SCAN_TILE);
-    uint64_t* st = reinterpret_cast<uint64_t*>(status);  // [2][nb] 64-bit | ticket | error word
+    uint64_t* st = reinterpret_cast<uint64_t*>(status);  // [2][nb] 64-bit | ticket | own error word
     uint32_t* ticket = status + 4 * (size_t)nb;
-    scan2_lookback_kernel<<<nb, SCAN_THREADS, 0, s>>>(tiles_touched, order, n, st, st + nb, ticket, ticket + 1, offsets,
-                                                      row_first, huge_list, huge_count);
+    scan2_lookback_kernel<<<nb, SCAN_THREADS, 0, s>>>(tiles_touched, order, n, st, st + nb, ticket,
+                                                      err ? err : ticket + 1, offsets, row_first, huge_list, huge_count,
+                                                      count_out);
 }
 
 size_t radix_hist_size(size_t n) { return (size_t)RADIX * div_up(n, SORT_TILE); }
@@ -774,7 +784,7 @@ ZeroSpan radix_zero_span(uint32_t* hist, size_t n, int passes)
 
 int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* hist,
                      uint32_t* scan_partials, size_t n, const uint32_t* count, char* canon, int first_pass, int passes,
-                     hipStream_t s, bool scratch_zeroed)
+                     hipStream_t s, bool scratch_zeroed, uint32_t* err_out)
 {
     if (n == 0 || passes <= 0) return 0;
     uint32_t *ki = key_a, *ko = key_b, *vi = val_a, *vo = val_b;
@@ -785,7 +795,7 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
         uint32_t* status = hist;
         uint32_t* ghist = hist + (size_t)passes * nb * RADIX;
         uint32_t* tickets = ghist + (size_t)passes * RADIX;
-        uint32_t* err = tickets + passes;
+        uint32_t* err = err_out ? err_out : tickets + passes;
         if (!scratch_zeroed) (void)hipMemsetAsync(ghist, 0, ((size_t)passes * (RADIX + 1) + 1) * sizeof(uint32_t), s);
         onesweep_hist_kernel<<<std::min(div_up(n, SORT_THREADS), OS_HIST_BLOCKS), SORT_THREADS, 0, s>>>(
             ki, n, count, first_pass, passes, status, (size_t)passes * nb * RADIX, ghist);
@@ -816,7 +826,7 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
             radix_upsweep_kernel<false><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb, scan_partials,
                                                                     2 * nbs + 2);
             scan_lookback_kernel<<<nbs, SCAN_THREADS, 0, s>>>(hist, hist, (size_t)RADIX * nb, lb, lb_ticket,
-                                                             lb_ticket + 1);
+                                                             err_out ? err_out : lb_ticket + 1);
             radix_downsweep_kernel<false><<<nb, SORT_THREADS, 0, s>>>(ki, vi, ko, vo, n, count,
                                                                       last ? canon : nullptr, shift, hist, nb);
         }

@@ -2,46 +2,14 @@
 
 Mirrors include/loss_utils.h:31-129 (l1_loss, ssim) as combined by gaussian_trainer.cpp:88-90 and
 gaussian_mapper.cpp:403-412. `l1_ssim_loss` runs the fused HIP kernel (omr_l1_ssim_loss, csrc/ssim.hip): one pass
-computes the loss and d loss / d image, and the autograd backward scales that gradient. `l1_loss` / `ssim` are the
-reference's own formulas in torch (kept for callers that want the separate terms; they are not the hot path).
+computes the loss and d loss / d image, and the autograd backward scales that gradient. There is no torch
+formulation here: the reference's formulas in torch are the tests' checker (oracle/loss_oracle.py).
 """
 from __future__ import annotations
 
-import ctypes as C
-
 import torch
-import torch.nn.functional as F
 
 from . import rasterizer as R
-
-
-def l1_loss(network_output: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
-    """loss_utils.h:31-34."""
-    return torch.abs(network_output - gt).mean()
-
-
-def _gaussian(window_size: int, sigma: float, device) -> torch.Tensor:
-    """loss_utils.h:54-67."""
-    x = torch.arange(window_size, dtype=torch.float32, device=device) - window_size // 2
-    g = torch.exp(-(x * x) / (2.0 * sigma * sigma))
-    return g / g.sum()
-
-
-def ssim(img1: torch.Tensor, img2: torch.Tensor, window_size: int = 11, size_average: bool = True) -> torch.Tensor:
-    """loss_utils.h:69-129 with torch ops ([C,H,W] images, depthwise 11x11 Gaussian window, zero padding)."""
-    channel = img1.shape[-3]
-    g = _gaussian(window_size, 1.5, img1.device).unsqueeze(1)
-    window = (g @ g.t()).to(img1.dtype).expand(channel, 1, window_size, window_size).contiguous()
-    pad = window_size // 2
-    conv = lambda x: F.conv2d(x, window, padding=pad, groups=channel)
-    mu1, mu2 = conv(img1), conv(img2)
-    mu1_sq, mu2_sq, mu1_mu2 = mu1 * mu1, mu2 * mu2, mu1 * mu2
-    sigma1_sq = conv(img1 * img1) - mu1_sq
-    sigma2_sq = conv(img2 * img2) - mu2_sq
-    sigma12 = conv(img1 * img2) - mu1_mu2
-    C1, C2 = 0.01 ** 2, 0.03 ** 2
-    ssim_map = ((2 * mu1_mu2 + C1) * (2 * sigma12 + C2)) / ((mu1_sq + mu2_sq + C1) * (sigma1_sq + sigma2_sq + C2))
-    return ssim_map.mean() if size_average else ssim_map.mean(1).mean(1).mean(1)
 
 
 def l1_ssim_loss_and_grad(image: torch.Tensor, gt: torch.Tensor, lambda_dssim: float, grad_out=None):

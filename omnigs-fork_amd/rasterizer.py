@@ -96,6 +96,11 @@ def lib() -> C.CDLL:
         L.omr_profile_read.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_uint64), i]
         L.omr_profile_stage_name.restype = C.c_char_p
         L.omr_profile_stage_name.argtypes = [i]
+        L.omr_runtime_stats.restype = i
+        L.omr_runtime_stats.argtypes = [C.POINTER(C.c_uint64), i]
+        L.omr_runtime_stat_name.restype = C.c_char_p
+        L.omr_runtime_stat_name.argtypes = [i]
+        L.omr_runtime_stats_reset.restype = None
         _lib = L
     return _lib
 
@@ -469,6 +474,28 @@ def profile_read() -> dict:
     cnt = (C.c_uint64 * NUM_STAGES)()
     n = lib().omr_profile_read(tot, cnt, NUM_STAGES)
     return {lib().omr_profile_stage_name(i).decode(): (float(tot[i]), int(cnt[i])) for i in range(n)}
+
+
+NUM_RUNTIME_STATS = 9
+
+
+def runtime_stats() -> dict:
+    """Host-side counters of the library since load or the last reset (omr_runtime_stats): forwards, backwards,
+    first-call syncs, capacity-hint back-half re-runs, host wait (ns) for num_rendered and for the backward's error
+    word, allocation callbacks and bytes, look-back give-ups."""
+    buf = (C.c_uint64 * NUM_RUNTIME_STATS)()
+    n = lib().omr_runtime_stats(buf, NUM_RUNTIME_STATS)
+    return {lib().omr_runtime_stat_name(i).decode(): int(buf[i]) for i in range(n)}
+
+
+def runtime_stats_reset():
+    lib().omr_runtime_stats_reset()
+
+
+def loaded_library() -> str:
+    """Absolute path of the HIP library this process loaded (OMR_LIB_PATH or the in-tree build)."""
+    lib()
+    return os.path.realpath(LIB_PATH)
 
 
 def debug_wave_sum(x: torch.Tensor, rows: bool = False, lds: bool = False) -> torch.Tensor:

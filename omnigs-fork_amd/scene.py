@@ -13,6 +13,7 @@ Conventions follow the reference host:
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -26,31 +27,79 @@ CAMERA_PINHOLE = 1
 CAMERA_LONLAT = 3
 
 
+_CHUNK = 1 << 20  # values per worker task of the threaded generator
+
+
+def _pool():
+    global _POOL
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+
+        _POOL = ThreadPoolExecutor(max_workers=max(1, min(16, os.cpu_count() or 1)))
+    return _POOL
+
+
+_POOL = None
+
+
 class SplitMix64:
-    """Sequential SplitMix64 stream; uniform = (x >> 40) * 2^-24, normal = Box-Muller (cos branch)."""
+    """Sequential SplitMix64 stream; uniform = (x >> 40) * 2^-24, normal = Box-Muller (cos branch).
+
+    Value j of the stream (0-based) is mix(seed + (j + 1) * GOLDEN), so any slice can be computed on its own: long
+    draws are split over a thread pool (numpy releases the GIL in its loops) with results identical to one
+    sequential pass."""
 
     def __init__(self, seed: int):
         self.state = np.uint64(seed & 0xFFFFFFFFFFFFFFFF)
 
-    def next_u64(self, n: int) -> np.ndarray:
+    @staticmethod
+    def _mix(state, first: int, n: int) -> np.ndarray:
         with np.errstate(over="ignore"):
-            k = np.arange(1, n + 1, dtype=np.uint64)
-            z = self.state + k * GOLDEN
-            self.state = self.state + np.uint64(n) * GOLDEN
+            k = np.arange(first + 1, first + n + 1, dtype=np.uint64)
+            z = state + k * GOLDEN
             z = (z ^ (z >> np.uint64(30))) * M1
             z = (z ^ (z >> np.uint64(27))) * M2
-            z = z ^ (z >> np.uint64(31))
-        return z
+            return z ^ (z >> np.uint64(31))
 
-    def uniform(self, n: int) -> np.ndarray:
-        x = self.next_u64(n)
+    def _draw(self, n: int, per_value: int, fn) -> np.ndarray:
+        """n outputs, each from `per_value` consecutive stream values; fn maps the u64 slice to the outputs."""
+        state = self.state
+        with np.errstate(over="ignore"):
+            self.state = self.state + np.uint64(n * per_value) * GOLDEN
+        if n * per_value <= _CHUNK:
+            return fn(self._mix(state, 0, n * per_value))
+        out = np.empty(n, dtype=np.float64 if fn is not None else np.uint64)
+        step = _CHUNK // per_value
+
+        def work(i0):
+            i1 = min(n, i0 + step)
+            out[i0:i1] = fn(self._mix(state, i0 * per_value, (i1 - i0) * per_value))
+
+        list(_pool().map(work, range(0, n, step)))
+        return out
+
+    def next_u64(self, n: int) -> np.ndarray:
+        state = self.state
+        with np.errstate(over="ignore"):
+            self.state = self.state + np.uint64(n) * GOLDEN
+        return self._mix(state, 0, n)
+
+    @staticmethod
+    def _uniform(x: np.ndarray) -> np.ndarray:
         return (x >> np.uint64(40)).astype(np.float64) * (1.0 / (1 << 24))
 
-    def normal(self, n: int) -> np.ndarray:
-        u = self.uniform(2 * n)
+    @staticmethod
+    def _normal(x: np.ndarray) -> np.ndarray:
+        u = SplitMix64._uniform(x)
         u1 = 1.0 - u[0::2]  # (0, 1]
         u2 = u[1::2]
         return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * math.pi * u2)
+
+    def uniform(self, n: int) -> np.ndarray:
+        return self._draw(n, 1, self._uniform)
+
+    def normal(self, n: int) -> np.ndarray:
+        return self._draw(n, 2, self._normal)
 
 
 @dataclass

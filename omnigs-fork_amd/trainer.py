@@ -10,6 +10,7 @@ reference's loop (:436-452), through GaussianOptimizer.densify_and_prune / reset
 """
 from __future__ import annotations
 
+import math
 from typing import Optional
 
 import numpy as np
@@ -29,12 +30,23 @@ class TrainStep:
         self.dimg: Optional[torch.Tensor] = None
 
 
+def skip_bottom_rows(image_height: int, skip_bottom_ratio: float) -> int:
+    """gaussian_mapper.cpp:396: (int)std::round(image_height * skip_bottom_ratio_), half away from zero."""
+    return int(math.floor(image_height * skip_bottom_ratio + 0.5))
+
+
 def train_step(opt: O.GaussianOptimizer, viewpoint, image_height: int, image_width: int, gt_image: torch.Tensor,
                bg_color: torch.Tensor, camera_type: int = R.CAMERA_LONLAT, lambda_dssim: float = 0.2,
                densification_stats: bool = True, state: Optional[TrainStep] = None,
-               dist_info: Optional[DistInfo] = None):
+               dist_info: Optional[DistInfo] = None, mask: Optional[torch.Tensor] = None,
+               skip_bottom_ratio: float = 0.0):
     """Render `viewpoint`, take the loss against gt_image, backpropagate and step Adam. Returns
     (terms = tensor([loss, l1, ssim]), rendered image, radii).
+
+    The loss is the reference's (gaussian_mapper.cpp:387-413): the rendered image times `mask` (the undistortion
+    mask, broadcast over channels; None = all ones), and with skip_bottom_ratio > 0 the bottom
+    round(H * ratio) rows of image and gt left out of L1 and SSIM (cfg/lonlat/360roam_lonlat.yaml uses 0.063).
+    d loss / d image is the fused kernel's gradient on the kept rows, zero on the skipped ones, times the mask.
 
     View-parallel (dist_info.world_size > 1): every rank renders its own view of the replicated
     Gaussians; the compact exchange (parallel.allreduce_compact_) sums the rasterizer gradients over the views and
@@ -62,7 +74,22 @@ def train_step(opt: O.GaussianOptimizer, viewpoint, image_height: int, image_wid
         image_width, shs, pc.active_sh_degree, cp, False, camera_type)
     if state.dimg is None or state.dimg.shape != image.shape:
         state.dimg = torch.empty_like(image)
-    terms, dimg = losses.l1_ssim_loss_and_grad(image, gt_image, lambda_dssim, grad_out=state.dimg)
+    masked = image * mask if mask is not None else image
+    if skip_bottom_ratio > 0.0:
+        kept = image_height - skip_bottom_rows(image_height, skip_bottom_ratio)
+        if kept <= 0 or kept == image_height:
+            # pix == 0 makes the reference's Slice(0, -pix) empty (kept == H here), which its conv2d rejects, and so
+            # is a crop of every row
+            raise ValueError(f"skip_bottom_ratio {skip_bottom_ratio} keeps {kept} of {image_height} rows")
+        dtop = torch.empty((image.shape[0], kept, image_width), dtype=image.dtype, device=dev)
+        terms, _ = losses.l1_ssim_loss_and_grad(masked[:, :kept], gt_image[:, :kept], lambda_dssim, grad_out=dtop)
+        state.dimg[:, :kept].copy_(dtop)
+        state.dimg[:, kept:].zero_()
+        dimg = state.dimg
+    else:
+        terms, dimg = losses.l1_ssim_loss_and_grad(masked, gt_image, lambda_dssim, grad_out=state.dimg)
+    if mask is not None:
+        dimg.mul_(mask)
     if state.buf is None or state.buf.P != P or state.buf.M != Mr + 1:
         state.buf = GradBuffer(P, Mr + 1, dev)
     out = state.buf.out_dict(dev)

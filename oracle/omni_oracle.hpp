@@ -592,9 +592,11 @@ template <typename R> int forward(State<R>& s, const Args<R>& in)
     const int num_rendered = (int)s.point_offsets[P - 1];
     s.num_rendered = num_rendered;
 
-    // duplicateWithKeys (rasterizer_impl.cu:94-140)
+    // duplicateWithKeys (rasterizer_impl.cu:94-140): every Gaussian writes its own slot range, so the loop is
+    // parallel over Gaussians with the reference's per-Gaussian row-major emission order
     std::vector<uint64_t> keys_unsorted(num_rendered);
     std::vector<uint32_t> vals_unsorted(num_rendered);
+#pragma omp parallel for schedule(dynamic, 1024)
     for (int idx = 0; idx < P; ++idx) {
         if (s.radii[idx] > 0) {
             uint32_t off = (idx == 0) ? 0 : s.point_offsets[idx - 1];
@@ -610,17 +612,51 @@ template <typename R> int forward(State<R>& s, const Args<R>& in)
                 }
         }
     }
-    // SortPairs (rasterizer_impl.cu:656-661): stable LSD radix on bits [0, 32+bit). Stable sort by the
-    // masked key gives the same permutation; bits above 32+bit are zero because tile < T <= 2^bit.
-    const int bit = (int)getHigherMsb(T);
-    const uint64_t mask = (bit + 32 >= 64) ? ~0ull : ((1ull << (32 + bit)) - 1);
+    // SortPairs (rasterizer_impl.cu:656-661): stable LSD radix on bits [0, 32+bit). Its permutation is that of a
+    // stable sort by the masked key (bits above 32+bit are zero because tile < T <= 2^bit), i.e. by
+    // (tile, depth bits) with ties in emission order. Computed as a stable counting sort by tile (per-thread
+    // contiguous chunks, so placement keeps emission order), then a stable sort by depth bits inside each tile:
+    // the same permutation, in parallel.
     std::vector<uint32_t> perm(num_rendered);
-    for (int i = 0; i < num_rendered; ++i) perm[i] = i;
-    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t l, uint32_t r) {
-        return (keys_unsorted[l] & mask) < (keys_unsorted[r] & mask);
-    });
+    {
+        const int nth = omp_get_max_threads();
+        std::vector<uint32_t> cnt((size_t)nth * T, 0u);
+        std::vector<uint32_t> tile_start(T + 1, 0u);
+        const size_t L = (size_t)num_rendered;
+        auto chunk = [&](int t, size_t& lo, size_t& hi) { lo = L * t / nth; hi = L * (t + 1) / nth; };
+#pragma omp parallel num_threads(nth)
+        {
+            const int t = omp_get_thread_num();
+            size_t lo, hi;
+            chunk(t, lo, hi);
+            uint32_t* c = &cnt[(size_t)t * T];
+            for (size_t i = lo; i < hi; ++i) c[keys_unsorted[i] >> 32]++;
+#pragma omp barrier
+#pragma omp single
+            {
+                uint32_t run = 0;
+                for (uint32_t tile = 0; tile < T; ++tile) {
+                    tile_start[tile] = run;
+                    for (int q = 0; q < nth; ++q) {
+                        const uint32_t v = cnt[(size_t)q * T + tile];
+                        cnt[(size_t)q * T + tile] = run;
+                        run += v;
+                    }
+                }
+                tile_start[T] = run;
+            }
+            for (size_t i = lo; i < hi; ++i) perm[c[keys_unsorted[i] >> 32]++] = (uint32_t)i;
+        }
+#pragma omp parallel for schedule(dynamic, 16)
+        for (int tile = 0; tile < (int)T; ++tile)
+            std::stable_sort(perm.begin() + tile_start[tile], perm.begin() + tile_start[tile + 1],
+                             [&](uint32_t l, uint32_t r) {
+                                 return (uint32_t)keys_unsorted[l] < (uint32_t)keys_unsorted[r];
+                             });
+    }
     s.keys.resize(num_rendered);
     s.point_list.resize(num_rendered);
+#pragma omp parallel for schedule(static)
     for (int i = 0; i < num_rendered; ++i) {
         s.keys[i] = keys_unsorted[perm[i]];
         s.point_list[i] = vals_unsorted[perm[i]];

@@ -53,6 +53,7 @@ def lib():
         L.oracle_asinf.restype = f
         L.oracle_asinf.argtypes = [f]
         L.oracle_mark_visible.argtypes = [i, vp, vp, vp, i, vp]
+        L.oracle_ambiguity.argtypes = [vp, d, i, vp, C.POINTER(C.c_int64)]
         _lib = L
     return _lib
 
@@ -123,6 +124,15 @@ class Oracle:
                     dmean3D=self.get("dmean3D").reshape(P, 3), dcov3D=self.get("dcov3D").reshape(P, 6),
                     dsh=self.get("dsh").reshape(P, M, 3), dscale=self.get("dscale").reshape(P, 3),
                     drot=self.get("drot").reshape(P, 4))
+
+    def ambiguity(self, eps: float = 1e-5, ulps: int = 3):
+        """ambiguity.hpp on the last (float) forward: dict of counts and the [P] flip-affected mask."""
+        counts = (C.c_int64 * 4)()
+        flip = np.zeros(self.P, dtype=np.uint8)
+        if lib().oracle_ambiguity(self.h, float(eps), int(ulps), _ptr(flip), counts) != 0:
+            raise RuntimeError("ambiguity needs a float forward")
+        return dict(rect_gaussians=int(counts[0]), alpha_pixels=int(counts[1]), saturation_pixels=int(counts[2]),
+                    flip_gaussians=int(counts[3]), eps=eps, ulps=ulps), flip.astype(bool)
 
     @property
     def num_rendered(self) -> int:

@@ -4,6 +4,7 @@
 #include <cstring>
 #include <string>
 
+#include "ambiguity.hpp"
 #include "omni_oracle.hpp"
 
 namespace {
@@ -175,6 +176,21 @@ float oracle_asinf(float x) { return omni::asinf_(x); }
 void oracle_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, int camera_type, uint8_t* present)
 {
     oracle::markVisible<float>(P, means3D, viewmatrix, projmatrix, camera_type, present);
+}
+
+// ambiguity.hpp on the last float forward: counts[0] rect-ambiguous Gaussians, [1] alpha-threshold pixels,
+// [2] saturation-threshold pixels, [3] flip-affected Gaussians; flip_out [P] (may be NULL) marks the latter
+int oracle_ambiguity(void* hv, double eps, int ulps, uint8_t* flip_out, int64_t* counts)
+{
+    Handle* h = static_cast<Handle*>(hv);
+    if (h->dbl) return -1;
+    const oracle::Ambiguity a = oracle::ambiguity_scan(h->sf, eps, ulps);
+    counts[0] = a.rect_gaussians;
+    counts[1] = a.alpha_pixels;
+    counts[2] = a.sat_pixels;
+    counts[3] = a.flip_gaussians;
+    if (flip_out && !a.flip.empty()) std::memcpy(flip_out, a.flip.data(), a.flip.size());
+    return 0;
 }
 
 }  // extern "C"

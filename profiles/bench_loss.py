@@ -28,6 +28,8 @@ def main():
     import _omnigs
 
     L = _omnigs.load().losses
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import loss_oracle as LO  # the reference formulation in torch (timed beside the fused kernel)
     H, W = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 else (1024, 2048)
     g = torch.Generator(device="cuda").manual_seed(0)
     gt = torch.rand((3, H, W), device="cuda", generator=g)
@@ -41,7 +43,7 @@ def main():
 
     def reference():
         img.grad = None
-        loss = (1.0 - lam) * L.l1_loss(img, gt) + lam * (1.0 - L.ssim(img, gt))
+        loss = (1.0 - lam) * LO.l1_loss(img, gt) + lam * (1.0 - LO.ssim(img, gt))
         loss.backward()
 
     t_f, t_r = timeit(fused), timeit(reference)

@@ -1,6 +1,8 @@
 """Shared test helpers: run the same scene through the oracle (CPU, test infrastructure) and the HIP path."""
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 import _omnigs
@@ -21,7 +23,7 @@ def make_case(P, width, height, camera_type, seed, view_index=0, sh_degree=3, sp
 
 
 def oracle_run(g, cam, dL=None, bg=(0.0, 0.0, 0.0), double=False, colors_precomp=None, cov3D_precomp=None,
-               render_depth=False, prefiltered=False):
+               render_depth=False, prefiltered=False, nthreads=1):
     import oracle as O
 
     o = O.Oracle(double)
@@ -33,7 +35,7 @@ def oracle_run(g, cam, dL=None, bg=(0.0, 0.0, 0.0), double=False, colors_precomp
                   viewmatrix=cam.viewmatrix, projmatrix=cam.projmatrix, campos=cam.campos, width=cam.width,
                   height=cam.height, sh_degree=g.sh_degree, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
                   camera_type=cam.camera_type, render_depth=render_depth, prefiltered=prefiltered)
-    grads = o.backward(dL) if dL is not None else None
+    grads = o.backward(dL, nthreads) if dL is not None else None
     return o, L, grads
 
 
@@ -103,19 +105,27 @@ def blend_threshold_flip(o, width, P, x, y, rel=1e-5):
     return False
 
 
+def oracle_threads() -> int:
+    """Threads for the oracle at the full BASELINE sizes: the box's CPU share (16) or this container's CPUs."""
+    return max(1, min(16, os.cpu_count() or 1))
+
+
 def to_np(x):
     return x.detach().cpu().numpy()
 
 
-def grad_close(a, b, rtol=1e-3, atol_frac=1e-4):
+def grad_close(a, b, rtol=1e-3, atol_frac=1e-4, elementwise=False):
     """Per-element |a-b| <= rtol*|b| + atol_frac*max|b| (documented gradient tolerance: north_star 1e-3 rel, with an
-    absolute floor at 1e-4 of the tensor's largest entry for entries that cancel to ~0)."""
+    absolute floor at 1e-4 of the tensor's largest entry for entries that cancel to ~0). elementwise=True returns the
+    boolean array of entries inside the bar instead."""
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
     scale = np.abs(b).max() if b.size else 0.0
     err = np.abs(a - b)
     lim = rtol * np.abs(b) + atol_frac * scale
     bad = err > lim
+    if elementwise:
+        return ~bad
     return (not bad.any()), (float(err.max()) if err.size else 0.0), int(bad.sum())
 
 

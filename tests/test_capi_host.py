@@ -111,3 +111,16 @@ def test_libtorch_dropin_exports_reference_symbols(omr):
         assert sig in out, sig
     m = omr.rasterizer.libtorch_boundary()
     assert hasattr(m, "RasterizeGaussiansCUDA") and hasattr(m, "markVisible")
+
+
+def test_runtime_stats_without_gpu(omr):
+    """omr_runtime_stats: the host-side counters bench.py reports (first-call syncs, back-half re-runs, host waits,
+    allocation callbacks, look-back give-ups) are named, start at zero after a reset, and count the host-validated
+    calls that never reach the device."""
+    R = omr.rasterizer
+    R.runtime_stats_reset()
+    st = R.runtime_stats()
+    assert list(st) == ["forwards", "backwards", "first_call_syncs", "back_half_reruns", "count_wait_ns",
+                        "backward_wait_ns", "alloc_calls", "alloc_bytes", "lookback_errors"]
+    assert all(v == 0 for v in st.values())
+    assert R.loaded_library().endswith("libomnigs_raster.so")

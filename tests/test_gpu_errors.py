@@ -1,0 +1,74 @@
+"""Failure reporting of the binning's decoupled look-backs (sort.hip), on a test build that gives up at the first
+unanswered poll (libomnigs_raster_lbspin0.so: OMR_LB_SPIN_MAX=0, csrc/Makefile).
+
+A look-back that gives up sets the forward's error word (GeomState::counters[3]); every later binning kernel and the
+forward render then see zero instances (raster_common.h: binning_count), so nothing reads a partly written
+permutation, and the call that can see the word returns OMR_ERR_HIP: the forward for the depth sort and the scans,
+the backward for the tile sort. The run happens in a child process, which loads the variant library through
+OMR_LIB_PATH; the in-tree library is checked alongside on the same scene to return OK.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VARIANT = os.path.join(ROOT, "omnigs-fork_amd", "lib", "exp", "libomnigs_raster_lbspin0.so")
+
+CHILD = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+import numpy as np, torch
+import _omnigs
+omr = _omnigs.load()
+R = omr.rasterizer
+g, cam, dL = omr.scene.config_scene("C")
+t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).cuda()
+e = torch.empty(0, device="cuda")
+args = (t(np.zeros(3)), t(g.means3D), e, t(g.opacity), t(g.scales), t(g.rotations), 1.0, e, t(cam.viewmatrix),
+        t(cam.projmatrix), 0.0, 0.0, cam.height, cam.width, t(g.shs), 3, t(cam.campos), False, 3)
+out = []
+for it in range(4):
+    try:
+        nr, color, radii, gb, bb, ib = R.RasterizeGaussiansCUDA(*args)
+        R.RasterizeGaussiansBackwardCUDA(args[0], args[1], radii, e, args[4], args[5], 1.0, e, args[8], args[9], 0.0,
+                                         0.0, t(dL), args[14], 3, args[16], gb, nr, bb, ib, 3)
+        torch.cuda.synchronize()
+        out.append(["ok", nr])
+    except R.RasterizerError as ex:
+        torch.cuda.synchronize()
+        out.append(["error", str(ex)])
+print(json.dumps(dict(lib=R.loaded_library(), runs=out, stats=R.runtime_stats())))
+"""
+
+
+def _child(lib_path):
+    env = dict(os.environ)
+    if lib_path:
+        env["OMR_LIB_PATH"] = lib_path
+    else:
+        env.pop("OMR_LIB_PATH", None)
+    r = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT)], env=env, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_lookback_give_up_is_reported_not_silent():
+    assert os.path.exists(VARIANT), "build the test variant first (make -C omnigs-fork_amd/csrc)"
+    res = _child(VARIANT)
+    assert res["lib"] == os.path.realpath(VARIANT)
+    errors = [m for kind, m in res["runs"] if kind == "error"]
+    assert errors, res  # 245 depth-sort / scan tiles per pass at P = 1 M: some look-back meets an unpublished tile
+    assert all("look-back" in m for m in errors), errors
+    assert res["stats"]["lookback_errors"] == len(errors)
+    ok = _child(None)
+    assert all(kind == "ok" for kind, _ in ok["runs"]), ok
+    assert ok["stats"]["lookback_errors"] == 0
+    # a good call after a failed one: the variant's ok runs (if any) render the same instance count
+    n_ok = {n for kind, n in res["runs"] if kind == "ok"}
+    assert n_ok <= {ok["runs"][0][1]}

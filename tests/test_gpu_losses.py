@@ -1,5 +1,5 @@
 """Fused L1 + SSIM loss (csrc/ssim.hip) against the reference formula (include/loss_utils.h:31-129,
-gaussian_trainer.cpp:88-90) evaluated by torch autograd in float64 on the CPU: loss value and d loss / d image,
+gaussian_trainer.cpp:88-90; restated in oracle/loss_oracle.py) evaluated by torch autograd in float64 on the CPU: loss value and d loss / d image,
 on image sizes that are not multiples of the 16x16 tile (border handling of the zero padding)."""
 import numpy as np
 import pytest
@@ -11,7 +11,8 @@ pytestmark = pytest.mark.gpu
 
 
 def _reference(img, gt, lam):
-    L = omr.losses
+    import loss_oracle as L  # oracle/: the reference formula in torch (test infrastructure)
+
     x = img.detach().double().cpu().requires_grad_(True)
     y = gt.detach().double().cpu()
     loss = (1.0 - lam) * L.l1_loss(x, y) + lam * (1.0 - L.ssim(x, y))

@@ -226,10 +226,15 @@ def test_reset_opacity_vs_oracle(ceiling):
     assert not opt.exp_avg[3].any() and not opt.exp_avg_sq[3].any()
 
 
-def test_fused_train_step_matches_autograd_reference_composition():
+@pytest.mark.parametrize("masked,skip_bottom_ratio", [(False, 0.0), (True, 0.063)],
+                         ids=["plain", "mask_skip_bottom"])
+def test_fused_train_step_matches_autograd_reference_composition(masked, skip_bottom_ratio):
     """trainer.train_step (no autograd: fused loss, rasterizer backward, fused activation backward + Adam) reaches
-    the same parameters as the reference's composition: torch activations -> rasterizer autograd -> l1/ssim loss
-    in torch (loss_utils.h) -> loss.backward() -> Adam on .grad (raw mode)."""
+    the same parameters as the reference's composition: torch activations -> rasterizer autograd -> masked image,
+    optional bottom crop, l1/ssim loss in torch (gaussian_mapper.cpp:387-413, loss_utils.h; oracle/loss_oracle.py)
+    -> loss.backward() -> Adam on .grad (raw mode). 0.063 is the skip_bottom_ratio of the reference's
+    cfg/lonlat/360roam_lonlat.yaml (8 of 128 rows here)."""
+    import loss_oracle as LO
     from helpers import make_case, scene
 
     W, H = 256, 128
@@ -240,6 +245,11 @@ def test_fused_train_step_matches_autograd_reference_composition():
               g.rotations * rng.uniform(0.5, 2.0, (g.P, 1))]
     params = [np.ascontiguousarray(p, dtype=np.float32) for p in params]
     gt = torch.tensor(rng.random((3, H, W)), dtype=torch.float32, device="cuda")
+    mask = None
+    if masked:  # an undistortion mask: black border columns, the rest 1 (gaussian_mapper.cpp:389)
+        mask = torch.ones((1, H, W), device="cuda")
+        mask[:, :, :9] = 0.0
+        mask[:, :, W - 7:] = 0.0
     bg = torch.zeros(3, device="cuda")
     t = lambda a: torch.tensor(np.ascontiguousarray(a, dtype=np.float32), device="cuda")  # noqa: E731
     vp = RD.Viewpoint(t(cam.viewmatrix), t(cam.projmatrix), t(cam.campos))
@@ -255,9 +265,10 @@ def test_fused_train_step_matches_autograd_reference_composition():
     for it in range(3):
         for opt in (opt1, opt2):
             opt.update_learning_rate(it)
-        terms, img1, radii1 = omr.trainer.train_step(opt1, vp, H, W, gt, bg, lambda_dssim=0.2, state=state)
+        terms, img1, radii1 = omr.trainer.train_step(opt1, vp, H, W, gt, bg, lambda_dssim=0.2, state=state,
+                                                     mask=mask, skip_bottom_ratio=skip_bottom_ratio)
         img2, vsp, vis, radii2 = RD.render_lonlat(vp, H, W, m2, RD.PipelineParams(), bg)
-        loss = 0.8 * omr.losses.l1_loss(img2, gt) + 0.2 * (1.0 - omr.losses.ssim(img2, gt))
+        loss = LO.training_loss(img2, gt, 0.2, mask=mask, skip_bottom_ratio=skip_bottom_ratio)
         loss.backward()
         opt2.add_densification_stats(vsp.grad, radii2)
         opt2.step()

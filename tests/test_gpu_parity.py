@@ -9,14 +9,18 @@ Bars (written here, checked per case):
     a pixel over 1e-4 is accepted only when a float64 re-blend of its tile list finds such a threshold decision
     (helpers.blend_threshold_flip) and at most 1 in 1e5 pixels (at least 1) is one: config C (2 M pixels) has
     one, |err| 3.6e-4 from a Gaussian with alpha = 1/255 (1 + 3e-6);
-  * gradients: per element |gpu - oracle| <= 1e-3 |oracle| + 1e-4 max|oracle| (helpers.grad_close).
+  * gradients: per element |gpu - oracle| <= 1e-3 |oracle| + 1e-4 max|oracle| (helpers.grad_close), except on
+    Gaussians whose own blend decision sits within 1e-5 of a threshold (alpha at 1/255, T(1-alpha) at 1e-4) at some
+    pixel (oracle/ambiguity.hpp: 886 of 1 M at config C); there the two exp implementations may decide differently
+    and the Gaussian gains or loses a whole pixel term (config C: one dscale entry, 1.4e-4 off).
 """
 import os
 
 import numpy as np
 import pytest
 
-from helpers import blend_threshold_flip, grad_close, hip_run, make_case, omr, oracle_run, scene, to_np
+from helpers import (blend_threshold_flip, grad_close, hip_run, make_case, omr, oracle_run, oracle_threads, scene,
+                     to_np)
 
 pytestmark = pytest.mark.gpu
 
@@ -37,8 +41,8 @@ CASES = [
 ]
 
 
-def _compare(g, cam, dL, **kw):
-    o, L, og = oracle_run(g, cam, dL, **kw)
+def _compare(g, cam, dL, nthreads=1, **kw):
+    o, L, og = oracle_run(g, cam, dL, nthreads=nthreads, **kw)
     h = hip_run(g, cam, dL, **kw)
     st = {k: to_np(v) for k, v in h["state"].items()}
     P = g.P
@@ -71,9 +75,18 @@ def _compare(g, cam, dL, **kw):
     pairs = [("dmean2D", og["dmean2D"]), ("dcolor", og["dcolor"]), ("dopacity", og["dopacity"]),
              ("dmean3D", og["dmean3D"]), ("dcov3D", og["dcov3D"]), ("dsh", og["dsh"]), ("dscale", og["dscale"]),
              ("drot", og["drot"])]
+    flip = None
     for name, ref in pairs:
         ok, emax, nbad = grad_close(hg[name], ref)
-        assert ok, f"{name}: max abs err {emax}, {nbad} elements outside tolerance"
+        if ok:
+            continue
+        # outside the bar only where the Gaussian's own blend decision sits at a threshold (oracle/ambiguity.hpp):
+        # there v_exp and expf may decide differently and the Gaussian gains or loses a whole pixel term
+        if flip is None:
+            counts, flip = o.ambiguity()
+        bad = ~grad_close(hg[name], ref, elementwise=True).reshape(P, -1).all(axis=1)
+        assert not (bad & ~flip).any(), (f"{name}: max abs err {emax}, {nbad} elements outside tolerance, "
+                                         f"{int((bad & ~flip).sum())} of them on Gaussians without a threshold decision")
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
@@ -113,19 +126,61 @@ def test_capacity_hint_too_small_reruns_back_half():
     _compare(g, cam, dL)
 
 
-def test_config_C_forward_large_sort_paths():
-    """The bench workload itself (1 M Gaussians, 2048x1024 equirect, L = 7.9 M): the tile sort takes the large-sort
-    path (upsweep / look-back histogram scan / downsweep) that the small parity cases never reach, the row sums
-    Forward checked bit-exact (radii, instance list, ranges) and the image within 1e-4 (the backward at this size is
-    covered by the golden and smaller parity cases; the oracle backward would take minutes)."""
+@pytest.fixture
+def oracle_mt():
+    """The oracle's forward on all of the box's CPU share (its backward takes nthreads per call)."""
     import oracle as O
 
-    O.set_threads(min(16, os.cpu_count() or 1))
-    g, cam, dL = scene.config_scene("C")
-    try:
-        _compare(g, cam, None)
-    finally:
-        O.set_threads(1)
+    O.set_threads(oracle_threads())
+    yield oracle_threads()
+    O.set_threads(1)
+
+
+@pytest.mark.parametrize("name", ["B", "C", "E_pinhole", "E"])
+def test_baseline_config_full(name, oracle_mt):
+    """Every BASELINE.json single-view config at its full size, forward AND backward, against the oracle on the same
+    seeded scene (rasterizer_impl.cu:540-795 / :250-535):
+      B  100 k Gaussians @ 1024x512 equirect (L = 0.35 M: the one-launch onesweep tile sort);
+      C  1 M @ 2048x1024 equirect, the bench workload (L = 7.9 M: the upsweep / look-back scan / downsweep tile sort,
+         huge-Gaussian row sums);
+      E_pinhole  5 M @ 1920x1080 pinhole (config E's ranks 4-7; frustum culling, V = 0.6 M);
+      E  5 M @ 4096x2048 equirect (config E's ranks 0-3; L = 117 M instances, binning scratch past 4 GB, so 64-bit
+         offsets in every binning kernel).
+    Bars as in the module docstring: integers bit-exact, image 1e-4, gradients grad_close."""
+    g, cam, dL = scene.config_scene(name)
+    _compare(g, cam, dL, nthreads=oracle_mt)
+
+
+def test_config_D_standin_eight_views(oracle_mt):
+    """Config D (1 M Gaussians, 8 views one per GPU, BASELINE.json) on one GPU: the eight views of the §8(d) ring run
+    one after another. The compact exchange's result (parallel.allreduce_compact_: sum of the 44 B/G xyz / opacity /
+    scale / rotation gradients + the SH gradient rebuilt from the gathered colour gradients) must equal the sum of
+    the per-view HIP gradients (the SH part bit for bit: same arithmetic, same view order), and two of the views
+    match the oracle."""
+    import torch
+
+    R = omr.rasterizer
+    sums, dcolors, campos, dsh_sum = None, [], [], None
+    for v in range(8):
+        g, cam, dL = scene.config_scene("C", view_index=v)
+        if v in (0, 5):
+            _compare(g, cam, dL, nthreads=oracle_mt)
+        h = hip_run(g, cam, dL)
+        gr = h["grads"]
+        part = torch.cat([gr["dmean3D"].reshape(-1, 3), gr["dopacity"].reshape(-1, 1), gr["dscale"].reshape(-1, 3),
+                          gr["drot"].reshape(-1, 4)], dim=1)
+        sums = part.double() if sums is None else sums + part.double()
+        dsh_sum = gr["dsh"].clone() if dsh_sum is None else dsh_sum + gr["dsh"]
+        dcolors.append(gr["dcolor"].clone())
+        campos.append(torch.from_numpy(cam.campos).cuda())
+        del h, gr, part
+    dev = dsh_sum.device
+    means, shs = torch.from_numpy(g.means3D).to(dev), torch.from_numpy(g.shs).to(dev)
+    packed = torch.cat([torch.stack(dcolors), torch.stack(campos)[:, None, :]], dim=1).contiguous()
+    rebuilt = R.sh_grad_from_colors_packed(means, shs, g.sh_degree, packed)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(to_np(rebuilt), to_np(dsh_sum))
+    assert torch.isfinite(sums).all() and float(sums.abs().max()) > 0
 
 
 def test_white_background():
