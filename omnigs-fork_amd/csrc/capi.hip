@@ -64,6 +64,12 @@ __global__ __launch_bounds__(64) void debug_wave_sum9_lds_kernel(const float* in
     if (lane == 1) out[8] = t8;
 }
 
+__global__ __launch_bounds__(256) void debug_point_ids_kernel(const uint32_t* list, size_t n, uint32_t* out)
+{
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = list[i] & PL_GID_MASK;
+}
+
 thread_local std::string g_last_error;
 
 int fail(int code, const std::string& msg)
@@ -267,17 +273,21 @@ size_t ImageState::carve(char* base, size_t N, size_t T, ImageState* s)
     im.ranges = c.take<uint2>(T);
     im.tile_order = c.take<uint32_t>(T);
     im.tile_cost = c.take<uint32_t>(T);
+    im.max_contrib = c.take<uint32_t>(T * FWD_GROUPS);
+    im.final_C = c.take<float>(3 * N);
     if (s) *s = im;
     return c.size();
 }
 
-size_t BinningState::carve(char* base, size_t cap, BinningState* s, int tile_passes)
+size_t BinningState::carve(char* base, size_t cap, uint32_t T, BinningState* s)
 {
+    const int tile_passes = tile_sort_passes(T);
     Carver c(base);
     BinningState b;
     b.inst_grad = c.take<float>(cap * GRAD_ROW);
-    c.take<uint32_t>(cap);  // room for the canonical point list when L < cap (raster_common.h)
-    c.take<uint8_t>(cap);   // room for row_valid behind it
+    // room for the rest of the L-indexed region when L < cap (raster_common.h): point list, row_valid, the
+    // backward's checkpoints, per-segment work and schedule
+    c.take<uint8_t>(l_region_end(cap, T) - canonical_list_offset(cap));
     b.point_list = base ? reinterpret_cast<uint32_t*>(base + canonical_list_offset(cap)) : nullptr;
     b.row_valid = base ? reinterpret_cast<uint8_t*>(base + row_valid_offset(cap)) : nullptr;
     b.key_a = c.take<uint32_t>(cap);
@@ -338,6 +348,8 @@ int forward_impl(const ForwardIn& in)
         return fail(OMR_ERR_CAMERA_TYPE, "[CudaRasterizer]Invalid camera_type");
     if (in.P < 0 || in.width <= 0 || in.height <= 0) return fail(OMR_ERR_INVALID_ARGUMENT, "bad P / width / height");
     if (in.P == 0) return OMR_OK;  // rasterize_points.cu:97: nothing runs, image stays zero
+    if ((uint32_t)in.P > PL_GID_MASK + 1u)  // point list entries hold the index in 28 bits (raster_common.h)
+        return fail(OMR_ERR_INVALID_ARGUMENT, "P above 2^28 Gaussians per view");
     if (!in.means3D || !in.opacities || !in.viewmatrix || !in.background || !in.out_color)
         return fail(OMR_ERR_INVALID_ARGUMENT, "missing required input pointer");
     if (!in.colors_precomp && (!in.shs || in.M <= 0))
@@ -429,11 +441,13 @@ int forward_impl(const ForwardIn& in)
 
     bool rerun = false;  // a second back half must clear what the first one wrote (preprocess zeroed it once)
     auto back_half = [&](size_t capacity) -> int {
+        if (ckpt_bytes(capacity) >= 0x80000000ull)  // 32-bit buffer offsets of the checkpoints (raster_common.h)
+            return fail(OMR_ERR_INVALID_ARGUMENT, "more than 2^28 Gaussian x tile instances in one view");
         char* bin_base = static_cast<char*>(
-            alloc_counted(in.binning_alloc, in.binning_ctx, BinningState::carve(nullptr, capacity, nullptr, tile_passes)));
+            alloc_counted(in.binning_alloc, in.binning_ctx, BinningState::carve(nullptr, capacity, d.T, nullptr)));
         if (!bin_base) return fail(OMR_ERR_ALLOCATION, "binning allocation failed");
         BinningState b;
-        BinningState::carve(bin_base, capacity, &b, tile_passes);
+        BinningState::carve(bin_base, capacity, d.T, &b);
         { StageScope st_(ST_EMIT, s); launch_emit_instances(in.P, capacity, count_dev, g, d.gx, b.block_owner, b.key_a, b.val_a, bin_base, s); }
         {
             StageScope st_(ST_TILE_SORT, s);
@@ -452,6 +466,7 @@ int forward_impl(const ForwardIn& in)
         ra.ranges = im.ranges; ra.tile_order = im.tile_order; ra.binning = bin_base; ra.count = count_dev; ra.capacity = capacity;
         ra.splat = g.splat;
         ra.bg = in.background; ra.tile_cost = im.tile_cost; ra.final_T = im.final_T; ra.n_contrib = im.n_contrib;
+        ra.max_contrib = im.max_contrib; ra.final_C = im.final_C;
         ra.out_color = in.out_color;
         // lonlat never renders depth (rasterize_points.cu:133-156 passes render_depth to the pinhole path only)
         { StageScope st_(ST_RENDER_FWD, s); launch_render_forward(ra, in.render_depth && in.camera_type == CAM_PINHOLE, s); }
@@ -508,7 +523,7 @@ int backward_impl(const BackwardIn& in)
     GeomState g;
     GeomState::carve(in.geom_buffer, P, &g);
     BinningState b;
-    BinningState::carve(in.binning_buffer, (size_t)in.R, &b, tile_sort_passes(d.T));
+    BinningState::carve(in.binning_buffer, (size_t)in.R, d.T, &b);
     ImageState im;
     ImageState::carve(in.image_buffer, d.N, d.T, &im);
     const int* radii = in.radii ? in.radii : geom_internal_radii(in.geom_buffer, P);
@@ -521,19 +536,30 @@ int backward_impl(const BackwardIn& in)
     OMR_HIP(hipMemcpyAsync(hs->words + 4, g.counters + 3, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     OMR_HIP(hipEventRecord(hs->ev_bwd, s));
 
+    const size_t R = (size_t)in.R;
+    char* const lb = in.binning_buffer;  // the L-indexed region (raster_common.h), at offsets of R
     RenderBwdArgs rb;
     rb.W = in.width; rb.H = in.height; rb.gx = d.gx; rb.gy = d.gy;
-    rb.ranges = im.ranges; rb.tile_order = im.tile_order; rb.point_list = b.point_list; rb.splat = g.splat; rb.bg = in.background;
+    rb.ranges = im.ranges; rb.point_list = b.point_list; rb.splat = g.splat; rb.bg = in.background;
     rb.row_first = g.row_first;
-    rb.final_T = im.final_T; rb.n_contrib = im.n_contrib; rb.dL_dpix = in.dL_dpix; rb.inst_grad = b.inst_grad;
+    rb.final_T = im.final_T; rb.final_C = im.final_C; rb.n_contrib = im.n_contrib; rb.dL_dpix = in.dL_dpix;
+    rb.inst_grad = b.inst_grad;
     rb.row_valid = b.row_valid;
+    rb.ckpt = reinterpret_cast<const float4*>(lb + ckpt_offset(R));
+    uint2* units = reinterpret_cast<uint2*>(lb + units_offset(R, d.T));
+    uint32_t* unit_count = reinterpret_cast<uint32_t*>(lb + unit_words_offset(R, d.T));
+    rb.units = units;
+    rb.unit_count = unit_count;
     // b.row_valid [R] was zeroed by the forward's emit (row_valid_offset)
-    // costliest tiles first (outside the render_backward stage, so the stage, the bench's roofline duration and the
-    // rocprofv3 kernel average all time render_bwd_kernel alone)
-    launch_tile_order(im.ranges, im.tile_cost, d.T, im.tile_order, s);
+    // (tile, depth segment) units, costliest first per XCD share (outside the render_backward stage, so the stage,
+    // the bench's roofline duration and the rocprofv3 kernel average all time render_bwd_kernel alone)
+    if (R > 0)
+        launch_backward_schedule(im.ranges, im.max_contrib, d.T, reinterpret_cast<uint2*>(lb + units_tmp_offset(R, d.T)),
+                                 reinterpret_cast<uint32_t*>(lb + units_tmp_offset(R, d.T) + seg_count(R, d.T) * 8),
+                                 units, unit_count, s);
     {
         StageScope st_(ST_RENDER_BWD, s);
-        launch_render_backward(rb, s);
+        if (R > 0) launch_render_backward(rb, seg_count(R, d.T), s);
     }
 
     GaussBwdArgs ga;
@@ -873,7 +899,7 @@ size_t omr_image_bytes(int width, int height)
 size_t omr_binning_bytes(int num_rendered, int width, int height)
 {
     const Dims d = dims(width, height);
-    return BinningState::carve(nullptr, (size_t)std::max(num_rendered, 0), nullptr, tile_sort_passes(d.T));
+    return BinningState::carve(nullptr, (size_t)std::max(num_rendered, 0), d.T, nullptr);
 }
 
 int omr_debug_wave_sum9(const float* in, float* out, void* stream)
@@ -959,9 +985,10 @@ int omr_debug_point_list(char* binning_buffer, int R, int width, int height, uin
     if (R <= 0) return OMR_OK;
     const Dims d = dims(width, height);
     BinningState b;
-    BinningState::carve(binning_buffer, (size_t)R, &b, tile_sort_passes(d.T));
-    OMR_HIP(hipMemcpyAsync(dst, b.point_list, (size_t)R * sizeof(uint32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
-    return OMR_OK;
+    BinningState::carve(binning_buffer, (size_t)R, d.T, &b);
+    // the Gaussian indices alone (entries carry the instance's band mask in their top bits, raster_common.h)
+    debug_point_ids_kernel<<<div_up((size_t)R, 256), 256, 0, (hipStream_t)stream>>>(b.point_list, (size_t)R, dst);
+    return hip_check("debug_point_list");
 }
 
 int omr_debug_ranges(char* image_buffer, int width, int height, uint32_t* dst, void* stream)

@@ -85,13 +85,15 @@ struct RenderFwdArgs {
     uint32_t gx, gy;
     const uint2* ranges;
     const uint32_t* tile_order;  // [T] schedule (launch_tile_order)
-    const char* binning;         // binning buffer: the point list is at binning + canonical_list_offset(*count)
+    char* binning;               // binning buffer: point list at binning + canonical_list_offset(L); checkpoints, segment work
     const uint32_t* count;       // device count words (GeomState::counters; raster_common.h binning_count)
     size_t capacity;             // instances the binning buffer was sized for (count > capacity: render nothing)
     const float4* splat;  // [P][SPLAT_F4] render records
     const float* bg;
-    uint32_t* tile_cost;  // [T] zeroed; receives the (instance, band) pairs each tile evaluated (backward schedule)
+    uint32_t* tile_cost;  // [T] zeroed; receives the (instance, band) pairs each tile evaluated
+    uint32_t* max_contrib;  // [T][FWD_GROUPS] each wave's largest last contributor (backward schedule)
     float* final_T;
+    float* final_C;         // [3][N] colour before the background term (backward segment starts)
     uint32_t* n_contrib;
     float* out_color;
 };
@@ -102,7 +104,10 @@ struct RenderBwdArgs {
     int W, H;
     uint32_t gx, gy;
     const uint2* ranges;
-    const uint32_t* tile_order;  // [T] schedule (launch_tile_order)
+    const uint2* units;          // {tile, chunk} depth segments, longest first per XCD share (launch_backward_schedule)
+    const uint32_t* unit_count;  // device word: number of units
+    const float4* ckpt;          // the forward's checkpoints (raster_common.h: ckpt_offset)
+    const float* final_C;        // [3][N]
     const uint32_t* point_list;
     const float4* splat;  // [P][SPLAT_F4] render records
     const uint32_t* row_first;  // [P] first gradient row of each Gaussian (index-order scan, launch_forward_scans)
@@ -113,7 +118,13 @@ struct RenderBwdArgs {
     float* inst_grad;
     uint8_t* row_valid;  // [L] zeroed; 1 where inst_grad holds a row
 };
-void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
+// grid: an upper bound on the unit count (seg_count(R, T)); waves past the device count exit at once
+void launch_render_backward(const RenderBwdArgs& a, size_t max_units, hipStream_t s);
+// the backward's work list: every (tile, depth segment) below the tile's last contributor (max over the forward's
+// max_contrib words), costed by its positions, sorted longest first within each of the 8 XCD shares of the unit list
+// (the shares xcd_remap gives each XCD); writes units, *unit_count
+void launch_backward_schedule(const uint2* ranges, const uint32_t* max_contrib, uint32_t T, uint2* units_tmp,
+                              uint32_t* cost_tmp, uint2* units, uint32_t* unit_count, hipStream_t s);
 #ifdef OMR_STAMPS
 int omr_debug_stamps_bwd(uint64_t* dst, size_t bytes);  // diagnostic builds only (tile_wave.h)
 #endif

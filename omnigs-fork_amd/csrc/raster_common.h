@@ -40,7 +40,7 @@ constexpr int GRAD_ROW = 9;
 constexpr uint32_t ROW_SUM_HUGE = 256;
 
 constexpr size_t ALIGN = 256;
-inline size_t align_up(size_t x) { return (x + ALIGN - 1) & ~(ALIGN - 1); }
+__host__ __device__ inline size_t align_up(size_t x) { return (x + ALIGN - 1) & ~(ALIGN - 1); }
 inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
 struct Carver {
@@ -67,6 +67,16 @@ struct Carver {
 //   [2] rgb   = {r, g, b, w}               colour (SH or colors_precomp); w = rect width in tiles (u32 bits)
 //   [3] rect  = {x0, y0, x1, y1}           getRect (u32 bits), read by emit
 constexpr int SPLAT_F4 = 4;
+
+// ---- point list entries -------------------------------------------------------------------------------------
+// The sorted point list holds, per (tile, Gaussian) instance, the Gaussian index in the low PL_GID_BITS bits and
+// the instance's band mask in the top four: bit b set iff the Gaussian's alpha >= 1/255 ellipse can reach pixel rows
+// 4b..4b+3 of the tile (band_mask, computed once per instance by emit). Both render kernels read the mask with the
+// index and gather the Gaussian's record only when it is non-zero. Limits P to 2^28 (checked by the forward). The
+// binning buffer is private scratch (rasterizer_impl.h:37-102); omr_debug_point_list returns the indices alone.
+constexpr uint32_t PL_GID_BITS = 28;
+constexpr uint32_t PL_GID_MASK = (1u << PL_GID_BITS) - 1u;
+constexpr int PL_BANDS = 4;
 
 // ---- geometry state: P Gaussians --------------------------------------------------------------------------
 struct GeomState {
@@ -97,7 +107,9 @@ struct ImageState {
     uint32_t* n_contrib;
     uint2* ranges;      // [T] (the reference allocates N, uses T)
     uint32_t* tile_order;  // [T] render schedule: tiles by descending cost within each XCD's share (launch_tile_order)
-    uint32_t* tile_cost;   // [T] (instance, band) pairs the forward evaluated per tile: the backward's schedule key
+    uint32_t* tile_cost;   // [T] (instance, band) pairs the forward evaluated per tile (bench.py's VALU secondary)
+    uint32_t* max_contrib;  // [T][FWD_GROUPS] each forward wave's largest last contributor (backward schedule)
+    float* final_C;         // [3][N] blended colour before the background term (backward segment starts)
     static size_t carve(char* base, size_t N, size_t T, ImageState* s);
 };
 
@@ -117,6 +129,38 @@ __host__ __device__ inline size_t row_valid_offset(size_t L)
 {
     return canonical_list_offset(L) + ((L * sizeof(uint32_t) + ALIGN - 1) & ~(ALIGN - 1));
 }
+// Depth segments of the render backward: a tile's instance list is cut at the global positions that are multiples
+// of CKPT (one backward wave per (tile, segment), render_bwd.hip). The forward checkpoints every pixel's state at
+// each boundary it crosses (T and the colour accumulated in front, 16 B per pixel per boundary), so a segment's wave
+// can start there instead of at the tile's last contributor. Segment (tile t, chunk c) has the unique id t + c
+// (a later tile's chunks never precede an earlier tile's), so per-segment arrays take T + L / CKPT + 1 entries.
+// The checkpoints are addressed through a buffer descriptor with 32-bit offsets: ckpt_bytes(L) < 2^31, i.e.
+// L < 2^28 instances per view (checked by the forward).
+#ifndef OMR_BWD_CK
+#define OMR_BWD_CK 512
+#endif
+constexpr uint32_t CKPT = OMR_BWD_CK;
+// bands per forward wave (render_fwd.hip): 2 = each tile is rendered by two independent waves ("groups")
+#ifndef OMR_FWD_BANDS
+#define OMR_FWD_BANDS 2
+#endif
+constexpr int FWD_BANDS = OMR_FWD_BANDS;
+constexpr int FWD_GROUPS = 4 / FWD_BANDS;
+__host__ __device__ inline size_t ckpt_count(size_t L) { return L / CKPT + 1; }
+__host__ __device__ inline size_t seg_count(size_t L, uint32_t T) { return (size_t)T + L / CKPT + 1; }
+// the L-indexed region of the binning buffer, after row_valid: checkpoints [ckpt_count][256 pixels] float4
+// {T, C_r, C_g, C_b} (pixel = band * 64 + lane), then the backward's schedule (units uint2 {tile, chunk}
+// [seg_count], its unsorted form + costs, the unit count)
+__host__ __device__ inline size_t ckpt_offset(size_t L) { return row_valid_offset(L) + align_up(L); }
+__host__ __device__ inline size_t ckpt_bytes(size_t L) { return ckpt_count(L) * BLOCK_X * BLOCK_Y * 16; }
+__host__ __device__ inline size_t units_offset(size_t L, uint32_t T) { return ckpt_offset(L) + align_up(ckpt_bytes(L)); }
+__host__ __device__ inline size_t units_tmp_offset(size_t L, uint32_t T) { return units_offset(L, T) + align_up(seg_count(L, T) * 8); }
+__host__ __device__ inline size_t unit_words_offset(size_t L, uint32_t T)
+{
+    return units_tmp_offset(L, T) + align_up(seg_count(L, T) * 12);
+}
+__host__ __device__ inline size_t l_region_end(size_t L, uint32_t T) { return unit_words_offset(L, T) + ALIGN; }
+
 // The forward's device count word: counters[0] = num_rendered, counters[3] = look-back error word (GeomState).
 // The binning kernels (sort.hip: live_count) and the forward render see 0 instances when the count exceeds the
 // capacity the binning buffer was sized for or when a decoupled look-back gave up.
@@ -139,7 +183,7 @@ struct BinningState {
     uint8_t* row_valid;     // backward: 1 where inst_grad holds a row (at row_valid_offset(L); zeroed by emit)
     uint32_t* point_keys;  // sorted tile ids (points at key_a or key_b)
     // carve for capacity cap; point_list is set for L = cap (exact sizing: backward, debug, omr_binning_bytes)
-    static size_t carve(char* base, size_t cap, BinningState* s, int tile_passes);
+    static size_t carve(char* base, size_t cap, uint32_t T, BinningState* s);
 };
 
 // number of 8-bit passes needed for tile ids < T (rasterizer_impl.cu:651: sort end bit = 32 + getHigherMsb(T))

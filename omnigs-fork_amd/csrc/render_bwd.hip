@@ -4,8 +4,12 @@
 // back to front from the last contributor; for each contributing instance the reference accumulates, with nine
 // float atomics into per-Gaussian arrays, dL/dmean2D.xy, dL/dconic.{x,y,w}, dL/dopacity and dL/dcolour.
 //
-// Structure (MI355X): ONE wave64 per 16x16 tile, four pixels per lane (one per 16x4 band, tile_wave.h), as in
-// render_fwd.hip. For each instance the wave accumulates, per lane and over the bands the instance reaches,
+// Structure (MI355X): ONE wave64 per (16x16 tile, depth segment) unit, four pixels per lane (one per 16x4 band,
+// tile_wave.h), as in render_fwd.hip. A tile's instance list is cut at global positions that are multiples of
+// CKPT (raster_common.h); the forward stored every pixel's T and accumulated colour at each boundary it crossed,
+// so the wave of a segment starts at its upper boundary from that state (or from the final state for a pixel whose
+// last contributor lies in front of it) and replays only its own positions. Units are ordered longest first by
+// the forward's per-segment work (sort.hip: backward_schedule_kernel): long tiles no longer form the launch's tail. For each instance the wave accumulates, per lane and over the bands the instance reaches,
 // nine moments of the pixel weights u = G * dL/dalpha and the colour weights alpha * T:
 //     S_u, S_u dx, S_u dy, S_u dx^2, S_u dx dy, S_u dy^2, S_aT dpix_{r,g,b}
 // (a lane's four pixels share one column, so only S_u, S_u dy, S_u dy^2 are summed per band; the x-moments are
@@ -66,14 +70,12 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
 #endif
     __shared__ float s_floor_all[TW_WAVES][TW_BATCH];  // p2_floor(opacity)
 
-    const uint32_t wv = threadIdx.x >> 6;
-    const uint32_t rank = xcd_remap(blockIdx.x, gridDim.x) * TW_WAVES + wv;
-    if (rank >= a.gx * a.gy) return;  // wave-uniform; the block's waves never synchronise with each other
-#ifdef OMR_NO_TILE_ORDER
-    const uint32_t tile = rank;
-#else
-    const uint32_t tile = a.tile_order[rank];
-#endif
+    static_assert(TW_WAVES == 1, "one (tile, segment) unit per workgroup");
+    const uint32_t wv = 0;
+    const uint32_t nunits = *a.unit_count;
+    if (blockIdx.x >= nunits) return;  // the grid is an upper bound on the unit count
+    const uint2 unit = a.units[xcd_remap(blockIdx.x, nunits)];
+    const uint32_t tile = unit.x, chunk = unit.y;
     float4* s_geo = s_geo_all[wv];
     float4* s_quad = s_quad_all[wv];
     float4* s_rgb = s_rgb_all[wv];
@@ -94,22 +96,40 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
         const uint32_t py = tl.py(b);
         const bool inside = tl.px < (uint32_t)a.W && py < (uint32_t)a.H;
         const uint32_t pix = a.W * py + tl.px;
-        const float Tf = inside ? a.final_T[pix] : 0.f;
         const uint32_t lc = inside ? a.n_contrib[pix] : 0u;
-        const float d0 = inside ? a.dL_dpix[pix] : 0.f;
-        const float d1 = inside ? a.dL_dpix[plane + pix] : 0.f;
-        const float d2 = inside ? a.dL_dpix[2 * plane + pix] : 0.f;
         last[b] = lc;
-        dp01[b] = f2v{d0, d1};
-        dp2[b] = d2;
-        T[b] = Tf;
-        s[b] = Tf * (a.bg[0] * d0 + a.bg[1] * d1 + a.bg[2] * d2);
         band_end[b] = uniform(wave_max_u32(lc));
         max_c = max(max_c, band_end[b]);
     }
     const uint2 range = a.ranges[tile];
     const uint32_t n = range.y - range.x;
     max_c = min(max_c, n);
+    // this unit's depth segment of the list, local positions [seg_lo, seg_hi) (raster_common.h: CKPT)
+    const uint32_t seg_lo = max(range.x, chunk * CKPT) - range.x;
+    const uint32_t seg_hi = min(range.x + max_c, (chunk + 1) * CKPT) - range.x;
+    const bool resume = seg_hi < max_c;  // a boundary inside the list: some pixels blend behind it
+#pragma unroll
+    for (int b = 0; b < TW_BANDS; ++b) {
+        const uint32_t py = tl.py(b);
+        const bool inside = tl.px < (uint32_t)a.W && py < (uint32_t)a.H;
+        const uint32_t pix = a.W * py + tl.px;
+        const float Tf = inside ? a.final_T[pix] : 0.f;
+        const float d0 = inside ? a.dL_dpix[pix] : 0.f;
+        const float d1 = inside ? a.dL_dpix[plane + pix] : 0.f;
+        const float d2 = inside ? a.dL_dpix[2 * plane + pix] : 0.f;
+        dp01[b] = f2v{d0, d1};
+        dp2[b] = d2;
+        T[b] = Tf;
+        s[b] = Tf * (a.bg[0] * d0 + a.bg[1] * d1 + a.bg[2] * d2);
+        if (resume && last[b] > seg_hi) {
+            // the pixel still blends behind the boundary: start from the forward's state there, T in front of the
+            // boundary and s = bg . dL/dpix T_final + dL/dpix . (C_final - C in front of the boundary)
+            const float4 ck = a.ckpt[(size_t)(chunk + 1) * BLOCK_SIZE + b * 64 + lane];
+            T[b] = ck.x;
+            s[b] += d0 * (a.final_C[pix] - ck.y) + d1 * (a.final_C[plane + pix] - ck.z) +
+                    d2 * (a.final_C[2 * plane + pix] - ck.w);
+        }
+    }
 
     // instances behind every pixel's last contributor get no row (row_valid stays 0 for them)
 
@@ -122,28 +142,31 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
     uint32_t cnt_[5] = {0, 0, 0, 0, 0};
 #endif
 
-    // positions max_c-1 .. 0, 64 per batch, back to front: batch entry `lane` <-> position hi-1-lane
-    for (int hi = (int)max_c; hi > 0; hi -= TW_BATCH) {
-        const int cnt = min(hi, TW_BATCH);
+    // positions seg_hi-1 .. seg_lo, 64 per batch, back to front: batch entry `lane` <-> position hi-1-lane
+    for (int hi = (int)seg_hi; hi > (int)seg_lo; hi -= TW_BATCH) {
+        const int cnt = min(hi - (int)seg_lo, TW_BATCH);
         uint32_t m = 0;
         float4 p, co, c;
         uint32_t pos = 0, slot = 0;
         if ((int)lane < cnt) {
             pos = (uint32_t)(hi - 1 - (int)lane);
-            const uint32_t gid = a.point_list[range.x + pos];
-            const float4* rec = a.splat + (size_t)gid * SPLAT_F4;  // one 64-B line
-            const uint32_t first = a.row_first[gid];
-            p = rec[0];
-            co = rec[1];
-            c = rec[2];
-            const float4 rect = rec[3];
-            // gradient row of (Gaussian, tile): its rows follow its rect row-major (duplicateWithKeys order)
-            slot = first + (tl.ty - __builtin_bit_cast(uint32_t, rect.y)) * __builtin_bit_cast(uint32_t, c.w) +
-                   (tl.tx - __builtin_bit_cast(uint32_t, rect.x));
-            m = band_mask<TW_BANDS>(make_float2(p.x, p.y), co, tl.tx, tl.ty, 0);
+            const uint32_t v = a.point_list[range.x + pos];  // Gaussian index | band mask (emit)
+            m = v >> PL_GID_BITS;
 #pragma unroll
             for (int b = 0; b < TW_BANDS; ++b)
                 if (pos >= band_end[b]) m &= ~(1u << b);
+            if (m) {  // record and row base are gathered only for an instance some band still needs
+                const uint32_t gid = v & PL_GID_MASK;
+                const float4* rec = a.splat + (size_t)gid * SPLAT_F4;  // one 64-B line
+                const uint32_t first = a.row_first[gid];
+                p = rec[0];
+                co = rec[1];
+                c = rec[2];
+                const float4 rect = rec[3];
+                // gradient row of (Gaussian, tile): its rows follow its rect row-major (duplicateWithKeys order)
+                slot = first + (tl.ty - __builtin_bit_cast(uint32_t, rect.y)) * __builtin_bit_cast(uint32_t, c.w) +
+                       (tl.tx - __builtin_bit_cast(uint32_t, rect.x));
+            }
         }
         const uint64_t useful = __ballot(m != 0);
         if (m != 0) {
@@ -243,7 +266,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
         }
         wave_sync();  // the next batch overwrites the staging arrays
     }
-    OMR_STAMP_END(g_stamps_bwd, tile);
+    OMR_STAMP_END(g_stamps_bwd, blockIdx.x);
 #ifdef OMR_BWD_COUNT
     if (lane == 0)
         for (int k = 0; k < 5; ++k) atomicAdd(&g_bwd_counts[k], (unsigned long long)cnt_[k]);
@@ -271,11 +294,10 @@ extern "C" int omr_debug_bwd_counts(uint64_t* dst, int reset)
 }
 #endif
 
-void launch_render_backward(const RenderBwdArgs& a, hipStream_t s)
+void launch_render_backward(const RenderBwdArgs& a, size_t max_units, hipStream_t s)
 {
-    const uint32_t T = a.gx * a.gy;
-    if (T == 0) return;
-    render_bwd_kernel<<<div_up(T, TW_WAVES), 64 * TW_WAVES, 0, s>>>(a);
+    if (max_units == 0) return;
+    render_bwd_kernel<<<(uint32_t)max_units, 64 * TW_WAVES, 0, s>>>(a);
 }
 
 }  // namespace omr

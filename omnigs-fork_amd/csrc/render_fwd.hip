@@ -5,9 +5,10 @@
 // T * (1 - alpha) < 1e-4; C += feature * alpha * T; record the last contributor; out = C + T * bg.
 //
 // Structure (MI355X): ONE wave64 per 16x16 tile, four pixels per lane (one per 16x4 band, tile_wave.h).
-//  * Batches of 64 instances: each lane gathers one instance (point_list entry + the Gaussian's 64-B render
-//    record, raster_common.h), computes the bands its alpha >= 1/255 ellipse can reach (band_mask) and, if any,
-//    stages it in LDS at its ballot rank — a compacted, order-preserving list of the batch's useful instances.
+//  * Batches of 64 instances: each lane reads one point list entry (Gaussian index + the bands its alpha >= 1/255
+//    ellipse can reach, computed by emit) and, if it reaches one of the wave's live bands, gathers the Gaussian's
+//    64-B render record (raster_common.h) and stages it in LDS at its ballot rank — a compacted, order-preserving
+//    list of the batch's useful instances.
 //  * The wave then walks that list; for each instance the band mask is wave-uniform (readfirstlane), so
 //    unreachable bands cost one scalar branch and reachable ones ~20 VALU per lane.
 //  * A band whose 64 pixels are all saturated leaves the active set; the tile exits when none is left.
@@ -24,19 +25,14 @@ namespace omr {
 
 namespace {
 
-#ifndef OMR_FWD_BANDS
-#define OMR_FWD_BANDS 2
-#endif
-// bands per wave: 4 = one wave per tile; 2 or 1 split a tile over 2 or 4 independent waves (shorter work
-// units for load balance; each wave stages the tile's instances itself)
+// bands per wave (FWD_BANDS, raster_common.h): 4 = one wave per tile; 2 or 1 split a tile over 2 or 4 independent
+// waves (shorter work units for load balance; each wave stages the tile's instances itself)
 #ifndef OMR_FWD_MINW
 #define OMR_FWD_MINW 8
 #endif
 #ifndef OMR_FWD_PREFETCH
 #define OMR_FWD_PREFETCH 0
 #endif
-constexpr int FWD_BANDS = OMR_FWD_BANDS;
-constexpr int FWD_GROUPS = TW_BANDS / FWD_BANDS;
 
 OMR_STAMP_DECL(g_stamps_fwd)
 
@@ -61,7 +57,8 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
 #else
     const uint32_t tile = a.tile_order[unit / FWD_GROUPS];
 #endif
-    const uint32_t band0 = (unit % FWD_GROUPS) * FWD_BANDS;  // this wave's bands: band0 .. band0 + FWD_BANDS - 1
+    const uint32_t grp = unit % FWD_GROUPS;
+    const uint32_t band0 = grp * FWD_BANDS;  // this wave's bands: band0 .. band0 + FWD_BANDS - 1
     const TileLane tl(tile, a.gx);
     const uint32_t lane = tl.lane;
     const float pxf = (float)tl.px;
@@ -86,18 +83,56 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
     const uint32_t* point_list = reinterpret_cast<const uint32_t*>(a.binning + canonical_list_offset(L));
     const uint2 range = L ? a.ranges[tile] : make_uint2(0u, 0u);
     const uint32_t n = range.y - range.x;
-    for (uint32_t start = 0; start < n && active; start += TW_BATCH) {
+    // The backward's depth segments (raster_common.h: CKPT): batches never straddle a boundary, and the batch that
+    // starts at one stores this wave's pixel states there (T, colour so far). Those stores are straight-line buffer
+    // stores issued AFTER the batch's gathers and after the next batch's point-list prefetch (a batch at no boundary
+    // stores at an out-of-range offset, which the descriptor's range check drops): vector-memory counters retire in
+    // issue order, so no wait for a gather ever includes a checkpoint store.
+    const size_t ck_bytes = L ? ckpt_count(L) * BLOCK_SIZE * sizeof(float4) : 0;
+    const __amdgpu_buffer_rsrc_t ck_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        a.binning + ckpt_offset(L), (short)0, (int)(uint32_t)ck_bytes, 0x00020000);
+    auto batch_end = [&](uint32_t s0) {  // [s0, end): at most TW_BATCH positions, never past a boundary or n
+        const uint32_t nb = (range.x + s0) / CKPT * CKPT + CKPT - range.x;
+        return min(min(s0 + TW_BATCH, n), nb);
+    };
+    // checkpoint stores of the batch that starts at `start` (OOB offset = dropped); issued as the last vector-memory
+    // operations of each batch, and twice after the prologue's prefetch too, so that the loop head sees the same
+    // issue pattern from both edges and waits only for the prefetched entry (vmcnt(2)), never for the stores
+    auto store_ckpt = [&](uint32_t s0) {
+        const uint32_t g0 = range.x + s0;
+        const bool at_boundary = s0 > 0 && g0 % CKPT == 0;
+        const uint32_t base = at_boundary ? (uint32_t)(((size_t)(g0 / CKPT) * BLOCK_SIZE + band0 * 64 + lane) * 16)
+                                          : 0x80000000u;
+#pragma unroll
+        for (int b = 0; b < FWD_BANDS; ++b)
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(v4u, make_float4(fabsf(T[b]), C0[b], C1[b], C2[b])), ck_rsrc,
+                base + (uint32_t)(b * 64 * 16), 0, 0);  // distinct offsets even when dropped: no store is merged away
+    };
+    // point-list entries are loaded one batch ahead, unconditionally (index clamped into the list; lanes past the
+    // batch ignore theirs), so no exec-masked write to the prefetch register forces an early wait
+    const uint32_t last_idx = L ? (uint32_t)L - 1u : 0u;
+    uint32_t start = 0, end = n ? batch_end(0) : 0;
+    uint32_t v_next = 0;
+    if (n) {
+        v_next = point_list[min(range.x + lane, last_idx)];
+        store_ckpt(0);  // at_boundary is false for s0 = 0: two dropped stores
+    }
+    for (; start < n && active;) {
         const uint32_t k = start + lane;
-        uint32_t m = 0;
         float4 pos, co, c;
-        if (k < n) {
-            const uint32_t gid = point_list[range.x + k];
-            const float4* rec = a.splat + (size_t)gid * SPLAT_F4;  // one 64-B record per instance
+        const uint32_t v = v_next;  // Gaussian index | band mask (emit)
+        const uint32_t m = k < end ? (v >> (PL_GID_BITS + band0)) & ((1u << FWD_BANDS) - 1u) & active : 0u;
+        if (m) {  // the record is gathered only for an instance that reaches one of this wave's live bands
+            const float4* rec = a.splat + (size_t)(v & PL_GID_MASK) * SPLAT_F4;  // one 64-B record
             pos = rec[0];
             co = rec[1];
             c = DEPTH ? make_float4(pos.z, pos.z, pos.z, 0.f) : rec[2];
-            m = band_mask<FWD_BANDS>(make_float2(pos.x, pos.y), co, tl.tx, tl.ty, band0) & active;
         }
+        const uint32_t next_start = end, next_end = end < n ? batch_end(end) : end;
+        v_next = point_list[min(range.x + next_start + lane, last_idx)];
+        // the state at a boundary = after every instance in front of it (this batch has not blended yet)
+        store_ckpt(start);
         const uint64_t useful = __ballot(m != 0);
         if (m != 0) {
             const uint32_t r = mask_rank(useful);
@@ -166,22 +201,31 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
 #endif
         }
         wave_sync();  // the next batch overwrites the staging arrays
+        start = next_start;
+        end = next_end;
     }
 
     const size_t plane = (size_t)a.H * a.W;
+    uint32_t maxc = 0;
 #pragma unroll
     for (int b = 0; b < FWD_BANDS; ++b) {
         const uint32_t py = tl.py(band0 + b);
+        maxc = max(maxc, last[b]);
         if (tl.px < (uint32_t)a.W && py < (uint32_t)a.H) {
             const uint32_t pix = a.W * py + tl.px;
             const float Tf = fabsf(T[b]);
             a.final_T[pix] = Tf;
             a.n_contrib[pix] = last[b];
+            a.final_C[pix] = C0[b];
+            a.final_C[plane + pix] = C1[b];
+            a.final_C[2 * plane + pix] = C2[b];
             a.out_color[pix] = C0[b] + Tf * a.bg[0];
             a.out_color[plane + pix] = C1[b] + Tf * a.bg[1];
             a.out_color[2 * plane + pix] = C2[b] + Tf * a.bg[2];
         }
     }
+    maxc = wave_max_u32(maxc);
+    if (lane == 0) a.max_contrib[(size_t)tile * FWD_GROUPS + grp] = maxc;
     if (lane == 0 && work) atomicAdd(&a.tile_cost[tile], work);
     OMR_STAMP_END(g_stamps_fwd, unit);
 }

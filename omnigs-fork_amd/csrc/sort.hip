@@ -621,7 +621,8 @@ __global__ __launch_bounds__(256) void emit_index_kernel(int P, size_t L_cap, co
 }
 
 // duplicateWithKeys (rasterizer_impl.cu:94-140) in depth order: Gaussian order[r] owns slots
-// [offsets[r-1], offsets[r]) and its tiles are emitted row-major like the reference. One thread per INSTANCE
+// [offsets[r-1], offsets[r]) and its tiles are emitted row-major like the reference. The value carries the
+// instance's band mask next to the Gaussian index (raster_common.h: point list entries). One thread per INSTANCE
 // (not per Gaussian as in the reference): writes are fully coalesced and a polar Gaussian spanning hundreds
 // of tiles no longer serialises its wave. The block's slots belong to ranks [block_owner[B], block_owner[B+1]];
 // their slot ends are staged in LDS and each thread finds its owner by a binary search there.
@@ -661,12 +662,16 @@ __global__ __launch_bounds__(EMIT_BLOCK) void emit_kernel(int P, size_t L_cap, c
     }
     const uint32_t gid = order[r];
     const uint32_t k = (uint32_t)e - start;
-    const float4 rect = splat[(size_t)gid * SPLAT_F4 + 3];  // {x0, y0, x1, y1} from preprocess (getRect)
+    const float4* rec = splat + (size_t)gid * SPLAT_F4;  // one 64-B line: rect, position, conic + opacity
+    const float4 rect = rec[3];  // {x0, y0, x1, y1} from preprocess (getRect)
+    const float4 pos = rec[0], co = rec[1];
     const uint32_t x0 = __builtin_bit_cast(uint32_t, rect.x), y0 = __builtin_bit_cast(uint32_t, rect.y);
     const uint32_t w = __builtin_bit_cast(uint32_t, rect.z) - x0;
     const uint32_t ky = k / w;
-    tile_keys[e] = (y0 + ky) * gx + (x0 + (k - ky * w));
-    gauss_vals[e] = gid;
+    const uint32_t tx = x0 + (k - ky * w), ty = y0 + ky;
+    tile_keys[e] = ty * gx + tx;
+    // the bands of the tile this instance can reach (point list entry format, raster_common.h)
+    gauss_vals[e] = gid | (band_mask<PL_BANDS>(make_float2(pos.x, pos.y), co, tx, ty, 0) << PL_GID_BITS);
     reinterpret_cast<uint8_t*>(binning + row_valid_offset(L))[e] = 0;  // the backward's row map (render_bwd.hip)
 }
 
@@ -732,7 +737,95 @@ __global__ __launch_bounds__(ORDER_THREADS) void tile_order_kernel(const uint2* 
     for (uint32_t i = lo + threadIdx.x; i < hi; i += ORDER_THREADS) order[atomicAdd(&s_hist[bucket(i)], 1u)] = i;
 }
 
+// The render backward's work list (render_bwd.hip). Unit = (tile, chunk): the part of the tile's instance list in
+// global chunk [chunk * CKPT, (chunk + 1) * CKPT) below the tile's last contributor. Every block scans the tiles'
+// unit counts (block-wide, 1024 tiles per step), keeps the units of its own share of the list (the share xcd_remap
+// maps onto XCD blockIdx.x), costs them by their positions below the tile's last contributor and counting-sorts
+// them, longest first.
+constexpr int SCHED_THREADS = 1024;
+__device__ __forceinline__ uint32_t tile_units(const uint2* ranges, const uint32_t* max_contrib, uint32_t t,
+                                               uint32_t* rx, uint32_t* mc_out)
+{
+    uint32_t mc = 0;
+#pragma unroll
+    for (int g = 0; g < FWD_GROUPS; ++g) mc = max(mc, max_contrib[(size_t)t * FWD_GROUPS + g]);
+    const uint2 r = ranges[t];
+    mc = min(mc, r.y - r.x);
+    *rx = r.x;
+    *mc_out = mc;
+    return mc ? (r.x + mc - 1) / CKPT - r.x / CKPT + 1 : 0u;
+}
+__global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(const uint2* ranges, const uint32_t* max_contrib,
+                                                                          uint32_t T,
+                                                                          uint2* units_tmp, uint32_t* cost_tmp,
+                                                                          uint2* units, uint32_t* unit_count)
+{
+    __shared__ uint32_t s_wave[SCHED_THREADS / 64];
+    __shared__ uint32_t s_hist[RADIX];
+    __shared__ uint32_t s_max;
+    const uint32_t tid = threadIdx.x;
+    uint32_t total = 0;
+    for (uint32_t base = 0; base < T; base += SCHED_THREADS) {
+        uint32_t rx, mc;
+        const uint32_t t = base + tid;
+        const uint32_t c = t < T ? tile_units(ranges, max_contrib, t, &rx, &mc) : 0u;
+        uint32_t tot;
+        (void)block_exclusive_scan<SCHED_THREADS>(c, s_wave, &tot);
+        total += tot;
+    }
+    // this block's share of [0, total): xcd_remap's split over the 8 XCDs
+    const uint32_t q = total / gridDim.x, rem = total % gridDim.x, x = blockIdx.x;
+    const uint32_t lo = x * q + min(x, rem), hi = lo + q + (x < rem ? 1u : 0u);
+    uint32_t run = 0;
+    for (uint32_t base = 0; base < T && run < hi; base += SCHED_THREADS) {
+        uint32_t rx = 0, mc = 0;
+        const uint32_t t = base + tid;
+        const uint32_t c = t < T ? tile_units(ranges, max_contrib, t, &rx, &mc) : 0u;
+        uint32_t tot;
+        const uint32_t first = run + block_exclusive_scan<SCHED_THREADS>(c, s_wave, &tot);
+        for (uint32_t k = 0; k < c; ++k) {
+            const uint32_t u = first + k;
+            if (u < lo || u >= hi) continue;
+            const uint32_t chunk = rx / CKPT + k;
+            units_tmp[u] = make_uint2(t, chunk);
+            // cost: the segment's positions below the tile's last contributor
+            cost_tmp[u] = min(rx + mc, (chunk + 1) * CKPT) - max(rx, chunk * CKPT);
+        }
+        run += tot;
+    }
+    if (tid < RADIX) s_hist[tid] = 0;
+    if (tid == 0) s_max = 0;
+    __threadfence();  // the share's entries (written by other threads of this block) before they are read back
+    __syncthreads();
+    uint32_t mx = 0;
+    for (uint32_t u = lo + tid; u < hi; u += SCHED_THREADS) mx = max(mx, cost_tmp[u]);
+    atomicMax(&s_max, mx);
+    __syncthreads();
+    const uint64_t scale = (uint64_t)s_max + 1;
+    auto bucket = [&](uint32_t u) {  // 0 = costliest
+        return (uint32_t)(RADIX - 1) - (uint32_t)(((uint64_t)cost_tmp[u] * RADIX) / scale);
+    };
+    for (uint32_t u = lo + tid; u < hi; u += SCHED_THREADS) atomicAdd(&s_hist[bucket(u)], 1u);
+    __syncthreads();
+    {
+        const uint32_t cnt = tid < RADIX ? s_hist[tid] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan<SCHED_THREADS>(cnt, s_wave, &tot);
+        if (tid < RADIX) s_hist[tid] = lo + ex;
+    }
+    __syncthreads();
+    for (uint32_t u = lo + tid; u < hi; u += SCHED_THREADS) units[atomicAdd(&s_hist[bucket(u)], 1u)] = units_tmp[u];
+    if (x == 0 && tid == 0) *unit_count = total;
+}
+
 }  // namespace
+
+void launch_backward_schedule(const uint2* ranges, const uint32_t* max_contrib, uint32_t T, uint2* units_tmp,
+                              uint32_t* cost_tmp, uint2* units, uint32_t* unit_count, hipStream_t s)
+{
+    if (T == 0) return;
+    backward_schedule_kernel<<<8, SCHED_THREADS, 0, s>>>(ranges, max_contrib, T, units_tmp, cost_tmp, units, unit_count);
+}
 
 void launch_tile_order(const uint2* ranges, const uint32_t* cost, uint32_t T, uint32_t* order, hipStream_t s)
 {

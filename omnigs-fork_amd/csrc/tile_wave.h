@@ -12,6 +12,7 @@
 namespace omr {
 
 typedef float f2v __attribute__((ext_vector_type(2)));  // a VGPR pair for v_pk_* f32 ops
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));  // 16-B payload of raw buffer stores
 constexpr int TW_BANDS = 4;       // 16x4 bands per 16x16 tile = pixels per lane
 constexpr int TW_BATCH = 64;      // instances staged per batch (one per lane)
 constexpr float LOG2E = 1.4426950408889634f;

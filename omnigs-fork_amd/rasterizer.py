@@ -149,20 +149,29 @@ def _stream(device: torch.device) -> int:
 
 class _ByteBuffer:
     """Allocation callback backed by a torch uint8 tensor (plays the role of resizeFunctional,
-    src/rasterize_points.cu:41-47)."""
+    src/rasterize_points.cu:41-47).
+
+    The callback closes over a one-element list, not over `self`: a closure that referenced the buffer object would
+    form a reference cycle (object -> callback -> closure -> object), so every step's scratch tensors (0.7 GB at
+    config C, 7.6 GB at E) would wait for Python's cyclic GC instead of returning to the caching allocator when the
+    caller drops them, and the allocator would keep calling hipMalloc for new blocks."""
 
     def __init__(self, device: torch.device):
-        self.device = device
-        self.tensor = torch.empty(0, dtype=torch.uint8, device=device)
+        holder = [torch.empty(0, dtype=torch.uint8, device=device)]
 
         def _cb(ctx, nbytes):
             try:
-                self.tensor = torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
-                return self.tensor.data_ptr()
+                holder[0] = torch.empty(int(nbytes), dtype=torch.uint8, device=device)
+                return holder[0].data_ptr()
             except Exception:  # out of memory -> NULL -> OMR_ERR_ALLOCATION
                 return None
 
+        self._holder = holder
         self.fn = _ALLOC_FN(_cb)
+
+    @property
+    def tensor(self) -> torch.Tensor:
+        return self._holder[0]
 
 
 def RasterizeGaussiansCUDA(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,

@@ -124,3 +124,25 @@ def test_runtime_stats_without_gpu(omr):
                         "backward_wait_ns", "alloc_calls", "alloc_bytes", "lookback_errors"]
     assert all(v == 0 for v in st.values())
     assert R.loaded_library().endswith("libomnigs_raster.so")
+
+
+def test_scratch_buffers_free_without_cyclic_gc(omr):
+    """The allocation callbacks' byte buffers must not sit in a reference cycle: otherwise each step's scratch
+    tensors (0.7 GB at config C, 7.6 GB at E) outlive the step until Python's cyclic GC runs, and the caching
+    allocator has to hipMalloc fresh blocks every step (bench.py reports device_mallocs in the timed region)."""
+    import gc
+    import weakref
+
+    import torch
+
+    gc.disable()
+    try:
+        b = omr.rasterizer._ByteBuffer(torch.device("cpu"))
+        ref = weakref.ref(b)
+        assert b.fn(None, 64)
+        t = b.tensor
+        assert t.numel() == 64
+        del b
+        assert ref() is None
+    finally:
+        gc.enable()

@@ -17,7 +17,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VARIANT = os.path.join(ROOT, "omnigs-fork_amd", "lib", "exp", "libomnigs_raster_lbspin0.so")
+VARIANT = os.path.join(ROOT, "omnigs-fork_amd", "lib", "test", "libomnigs_raster_lbspin0.so")
 
 CHILD = r"""
 import json, sys
