@@ -4,6 +4,8 @@
   lib/librasterize_points.so            RasterizeGaussiansCUDA / RasterizeGaussiansBackwardCUDA / markVisible
                                         (C++ symbols, CXX11 ABI as PyTorch-ROCm), linked to libomnigs_raster.so
   lib/_rasterize_points<ext-suffix>     pybind11 module exposing the same three functions (tests)
+  tests/cpp/build/reference_host_caller  test program: the reference host's torch::autograd::Function over the
+                                        drop-in (tests/test_gpu_libtorch_cpp.py); test infrastructure only
 
 Host-only C++ (no device code: kernels live in libomnigs_raster.so), so plain g++ against the torch headers.
 Skips work when outputs are newer than their inputs.
@@ -48,6 +50,15 @@ def main():
         cmd = ["g++", *common, pyinc, "-DTORCH_EXTENSION_NAME=_rasterize_points", "-DTORCH_API_INCLUDE_EXTENSION_H",
                "-shared", "-o", ext, bsrc, f"-L{LIB}", "-lrasterize_points", "-Wl,-rpath,$ORIGIN", *torch_libs,
                "-ltorch_python"]
+        subprocess.run(cmd, check=True)
+    tdir = os.path.join(ROOT, "tests", "cpp")
+    tsrc = os.path.join(tdir, "reference_host_caller.cpp")
+    texe = os.path.join(tdir, "build", "reference_host_caller")
+    if os.path.exists(tsrc) and _stale(texe, [tsrc, core] + hdrs):
+        os.makedirs(os.path.dirname(texe), exist_ok=True)
+        # --no-as-needed: nothing here names a torch_hip symbol, but the CUDA(HIP) device registers from it
+        cmd = ["g++", *common, "-o", texe, tsrc, "-Wl,--no-as-needed", f"-L{LIB}", "-lrasterize_points",
+               "-Wl,-rpath,$ORIGIN/../../../omnigs-fork_amd/lib", *torch_libs]
         subprocess.run(cmd, check=True)
     return 0
 
