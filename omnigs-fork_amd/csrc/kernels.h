@@ -68,7 +68,12 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
 // the words of `hist` a sort of n items over `passes` passes needs zeroed before it starts (possibly none)
 ZeroSpan radix_zero_span(uint32_t* hist, size_t n, int passes);
 // duplicateWithKeys; L_cap = capacity, *count (device) = num_rendered; block_owner: emit_index_size(L_cap) words
-constexpr int EMIT_BLOCK = 256;
+constexpr int EMIT_THREADS = 256;
+#ifndef OMR_EMIT_PER
+#define OMR_EMIT_PER 4
+#endif
+constexpr int EMIT_PER = OMR_EMIT_PER;                // consecutive instance slots per emit thread (1, 2 or 4)
+constexpr int EMIT_SLOTS = EMIT_THREADS * EMIT_PER;   // slots per emit block (block_owner granularity)
 size_t emit_index_size(size_t L_cap);
 // also zeroes the backward's row_valid bytes at binning + row_valid_offset(L)
 void launch_emit_instances(int P, size_t L_cap, const uint32_t* count, const GeomState& g, uint32_t gx,

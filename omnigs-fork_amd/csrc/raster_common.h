@@ -22,7 +22,10 @@ constexpr int CAM_LONLAT = 3;
 
 // radix sort geometry (sort.hip)
 constexpr int SORT_THREADS = 256;
-constexpr int SORT_ITEMS = 16;  // items per thread per block tile
+#ifndef OMR_SORT_ITEMS
+#define OMR_SORT_ITEMS 16
+#endif
+constexpr int SORT_ITEMS = OMR_SORT_ITEMS;  // items per thread per block tile of the multi-launch passes
 constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;
 constexpr int RADIX_BITS = 8;
 constexpr int RADIX = 1 << RADIX_BITS;
@@ -179,7 +182,7 @@ struct BinningState {
     uint32_t* val_b;
     uint32_t* hist;        // radix histograms
     uint32_t* scan_partials;
-    uint32_t* block_owner;  // emit index: owner rank of every EMIT_BLOCK-th slot
+    uint32_t* block_owner;  // emit index: owner rank of every EMIT_SLOTS-th slot
     uint8_t* row_valid;     // backward: 1 where inst_grad holds a row (at row_valid_offset(L); zeroed by emit)
     uint32_t* point_keys;  // sorted tile ids (points at key_a or key_b)
     // carve for capacity cap; point_list is set for L = cap (exact sizing: backward, debug, omr_binning_bytes)

@@ -260,6 +260,14 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_lookback_kernel(const uint3
 // sorts of at most this many 4096-item blocks (the depth sort up to 2M Gaussians) let each downsweep block derive
 // its digit offsets from the raw histogram: <= 512 KiB of L2 reads per block instead of three scan launches
 constexpr uint32_t SELF_SCAN_MAX_BLOCKS = 512;
+#ifndef OMR_SORT_ITEMS_LARGE
+#define OMR_SORT_ITEMS_LARGE 32
+#endif
+#ifndef OMR_SORT_LARGE_MIN
+#define OMR_SORT_LARGE_MIN (1u << 25)
+#endif
+constexpr int SORT_ITEMS_LARGE = OMR_SORT_ITEMS_LARGE;  // items per thread of the multi-launch passes of large sorts
+constexpr size_t SORT_LARGE_MIN = OMR_SORT_LARGE_MIN;
 
 // ---- radix sort ------------------------------------------------------------------------------------------
 // element count: the host's n, or the device count word (binning, capi.hip; raster_common.h: binning_count), which
@@ -270,12 +278,17 @@ __device__ __forceinline__ size_t live_count(size_t n, const uint32_t* count)
     return count ? binning_count(count, n) : n;
 }
 
-// BLOCK_MAJOR: hist[block][digit] (read back by the self-scanning downsweep of small sorts); else hist[digit][block]
-template <bool BLOCK_MAJOR>
+#ifndef OMR_UPSWEEP_V4
+#define OMR_UPSWEEP_V4 2
+#endif
+// BLOCK_MAJOR: hist[block][digit] (read back by the self-scanning downsweep of small sorts); else hist[digit][block].
+// Key arrays are 16-B aligned (Carver) for the 16-B loads.
+template <bool BLOCK_MAJOR, int ITEMS>
 __global__ __launch_bounds__(SORT_THREADS) void radix_upsweep_kernel(const uint32_t* keys, size_t n_cap,
                                                                      const uint32_t* count, int shift, uint32_t* hist,
                                                                      uint32_t nblocks, uint32_t* zero, uint32_t nzero)
 {
+    constexpr int TILE_N = SORT_THREADS * ITEMS;
     {   // the look-back words of the histogram scan that follows (scan_lookback_kernel)
         const uint32_t z = blockIdx.x * SORT_THREADS + threadIdx.x;
         if (z < nzero) zero[z] = 0u;
@@ -284,12 +297,55 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_upsweep_kernel(const uint3
     __shared__ uint32_t s_hist[RADIX];
     s_hist[threadIdx.x] = 0;
     __syncthreads();
-    const size_t base = (size_t)blockIdx.x * SORT_TILE;
+    const size_t base = (size_t)blockIdx.x * TILE_N;
+#if OMR_UPSWEEP_V4
+    // 16-B loads (4 per thread, each wave instruction one contiguous KiB), and one LDS add per distinct digit of
+    // each 64-key group (8-ballot match, as the downsweep ranks): same-address adds within one ds_add serialise,
+    // and neighbouring instances often share a digit
+    static_assert(ITEMS % 4 == 0, "16-B key loads");
+    uint32_t kv[ITEMS];
+    const bool full = base + TILE_N <= n;
 #pragma unroll
-    for (int k = 0; k < SORT_ITEMS; ++k) {
+    for (int k = 0; k < ITEMS / 4; ++k) {
+        const size_t i = base + 4 * ((size_t)k * SORT_THREADS + threadIdx.x);
+        uint4 q;
+        if (full) q = *reinterpret_cast<const uint4*>(keys + i);
+        else {
+            q.x = i < n ? keys[i] : 0u;
+            q.y = i + 1 < n ? keys[i + 1] : 0u;
+            q.z = i + 2 < n ? keys[i + 2] : 0u;
+            q.w = i + 3 < n ? keys[i + 3] : 0u;
+        }
+        kv[4 * k] = q.x;
+        kv[4 * k + 1] = q.y;
+        kv[4 * k + 2] = q.z;
+        kv[4 * k + 3] = q.w;
+    }
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const size_t i = base + 4 * ((size_t)(j >> 2) * SORT_THREADS + threadIdx.x) + (j & 3);
+        const bool valid = i < n;
+        const uint32_t d = (kv[j] >> shift) & (RADIX - 1);
+        if (OMR_UPSWEEP_V4 == 2) {
+            if (valid) atomicAdd(&s_hist[d], 1u);
+            continue;
+        }
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < RADIX_BITS; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        if (valid && mask_rank(peers) == 0) atomicAdd(&s_hist[d], (uint32_t)__popcll(peers));
+    }
+#else
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
         const size_t i = base + (size_t)k * SORT_THREADS + threadIdx.x;
         if (i < n) atomicAdd(&s_hist[(keys[i] >> shift) & (RADIX - 1)], 1u);
     }
+#endif
     __syncthreads();
     if (BLOCK_MAJOR) hist[(size_t)blockIdx.x * RADIX + threadIdx.x] = s_hist[threadIdx.x];
     else hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = s_hist[threadIdx.x];
@@ -304,27 +360,28 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_upsweep_kernel(const uint3
 // SELF_SCAN (small sorts, few blocks): hist is the raw block-major histogram and each block derives its global
 // digit offsets itself (column prefix over the blocks before it + scan of the digit totals), which saves the
 // three scan launches per pass; else hist is the scanned [digit][block] histogram.
-template <bool SELF_SCAN>
+template <bool SELF_SCAN, int ITEMS>
 __global__ __launch_bounds__(SORT_THREADS) void radix_downsweep_kernel(const uint32_t* keys_in, const uint32_t* vals_in,
                                                                        uint32_t* keys_out, uint32_t* vals_out,
                                                                        size_t n_cap, const uint32_t* count, char* canon,
                                                                        int shift, const uint32_t* hist_scanned,
                                                                        uint32_t nblocks)
 {
+    constexpr int TILE_N = SORT_THREADS * ITEMS;
     constexpr int WAVES = SORT_THREADS / 64;
-    constexpr int PER_WAVE = SORT_TILE / WAVES;
+    constexpr int PER_WAVE = TILE_N / WAVES;
     constexpr int ROUNDS = PER_WAVE / 64;
     __shared__ uint32_t s_whist[WAVES][RADIX];  // running digit counts per wave, then per-wave digit offsets
     __shared__ uint32_t s_dstart[RADIX];        // block-local start of each digit's run
     __shared__ uint32_t s_gbase[RADIX];         // global start of this block's run of each digit
     __shared__ uint32_t s_wave[SORT_THREADS / 64];
-    __shared__ uint32_t s_k[SORT_TILE];
-    __shared__ uint32_t s_v[SORT_TILE];
+    __shared__ uint32_t s_k[TILE_N];
+    __shared__ uint32_t s_v[TILE_N];
     const size_t n = live_count(n_cap, count);
     if (canon) vals_out = reinterpret_cast<uint32_t*>(canon + canonical_list_offset(n));
     const uint32_t tid = threadIdx.x;
     const uint32_t w = tid >> 6, lane = tid & 63;
-    const size_t tile0 = (size_t)blockIdx.x * SORT_TILE;
+    const size_t tile0 = (size_t)blockIdx.x * TILE_N;
 #pragma unroll
     for (int q = 0; q < WAVES; ++q) s_whist[q][tid] = 0;
     if (SELF_SCAN) {
@@ -401,7 +458,7 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_downsweep_kernel(const uin
         }
     }
     __syncthreads();
-    const uint32_t nvalid = (uint32_t)min((size_t)SORT_TILE, n > tile0 ? n - tile0 : (size_t)0);
+    const uint32_t nvalid = (uint32_t)min((size_t)TILE_N, n > tile0 ? n - tile0 : (size_t)0);
     for (uint32_t j = tid; j < nvalid; j += SORT_THREADS) {
         const uint32_t kk = s_k[j];
         const uint32_t d = (kk >> shift) & (RADIX - 1);
@@ -427,12 +484,15 @@ constexpr int LB_WINDOW = OMR_LB_WINDOW;  // predecessors read per look-back rou
 
 // scratch words for a sort of n items over `passes` passes: status [passes][blocks][RADIX], digit totals
 // [passes][RADIX], tickets [passes], error word
-constexpr int OS_TILE = SORT_TILE;                   // keys per onesweep block (smaller tiles measured slower)
+constexpr int OS_TILE = SORT_THREADS * 16;                   // keys per onesweep block (smaller tiles measured slower)
 constexpr uint32_t OS_HIST_BLOCKS = 128;             // histogram blocks: each digit total takes <= 128 global adds
 // Onesweep only for sorts of at most this many tiles (the depth sort up to 2 M Gaussians: 0.100 vs 0.122 ms at
 // 1 M). Past that the look-back chains and the same-address ticket / histogram adds cost more than the launches
 // they save (the 7.9 M-instance tile sort: 0.185 vs 0.142 ms), and the upsweep / scan / downsweep passes run.
-constexpr uint32_t OS_MAX_BLOCKS = 512;
+#ifndef OMR_OS_MAX_BLOCKS
+#define OMR_OS_MAX_BLOCKS 512
+#endif
+constexpr uint32_t OS_MAX_BLOCKS = OMR_OS_MAX_BLOCKS;
 
 __host__ __device__ inline size_t onesweep_words(size_t n, int passes)
 {
@@ -609,89 +669,153 @@ __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* offsets, uin
     return lo;
 }
 
-// Emission index: block_owner[B] = the depth rank owning slot B * EMIT_BLOCK (the rank whose slot range
+// Emission index: block_owner[B] = the depth rank owning slot B * EMIT_SLOTS (the rank whose slot range
 // [offsets[r-1], offsets[r]) contains it). One thread per rank; only ranks containing a block start write.
 __global__ __launch_bounds__(256) void emit_index_kernel(int P, size_t L_cap, const uint32_t* count,
                                                          const uint32_t* offsets, uint32_t* block_owner)
 {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= P || live_count(L_cap, count) == 0) return;  // block_owner holds L_cap / EMIT_BLOCK + 1 words
+    if (r >= P || live_count(L_cap, count) == 0) return;  // block_owner holds L_cap / EMIT_SLOTS + 1 words
     const uint32_t lo = r == 0 ? 0u : offsets[r - 1], hi = offsets[r];
-    for (uint32_t B = (lo + EMIT_BLOCK - 1) / EMIT_BLOCK; B * EMIT_BLOCK < hi; ++B) block_owner[B] = (uint32_t)r;
+    for (uint32_t B = (lo + EMIT_SLOTS - 1) / EMIT_SLOTS; B * EMIT_SLOTS < hi; ++B) block_owner[B] = (uint32_t)r;
 }
 
-// duplicateWithKeys (rasterizer_impl.cu:94-140) in depth order: Gaussian order[r] owns slots
-// [offsets[r-1], offsets[r]) and its tiles are emitted row-major like the reference. The value carries the
-// instance's band mask next to the Gaussian index (raster_common.h: point list entries). One thread per INSTANCE
-// (not per Gaussian as in the reference): writes are fully coalesced and a polar Gaussian spanning hundreds
-// of tiles no longer serialises its wave. The block's slots belong to ranks [block_owner[B], block_owner[B+1]];
-// their slot ends are staged in LDS and each thread finds its owner by a binary search there.
-__global__ __launch_bounds__(EMIT_BLOCK) void emit_kernel(int P, size_t L_cap, const uint32_t* count,
-                                                          const uint32_t* order, const uint32_t* offsets,
-                                                          const uint32_t* block_owner, const float4* splat, uint32_t gx,
-                                                          uint32_t* tile_keys, uint32_t* gauss_vals, char* binning)
+// the tile and point-list entry of instance k of Gaussian gid (its tiles row-major over its rect)
+__device__ __forceinline__ void emit_one(const float4* splat, uint32_t gid, uint32_t k, uint32_t gx, uint32_t* key,
+                                         uint32_t* val)
 {
-    __shared__ uint32_t s_end[EMIT_BLOCK];
-    __shared__ uint32_t s_start0;
-    const size_t L = live_count(L_cap, count);
-    const uint32_t B = blockIdx.x;
-    const size_t e0 = (size_t)B * EMIT_BLOCK;
-    if (e0 >= L) return;  // block-uniform
-    const size_t e = e0 + threadIdx.x;
-    const uint32_t r_lo = block_owner[B];
-    const uint32_t r_hi = e0 + EMIT_BLOCK < L ? block_owner[B + 1] + 1 : (uint32_t)P;  // exclusive
-    const uint32_t nr = r_hi - r_lo;
-    const bool staged = nr <= EMIT_BLOCK;  // block-uniform; more only with runs of empty (culled) segments
-    if (staged && threadIdx.x < nr) s_end[threadIdx.x] = offsets[r_lo + threadIdx.x];
-    if (threadIdx.x == 0) s_start0 = r_lo == 0 ? 0u : offsets[r_lo - 1];
-    __syncthreads();
-    if (e >= L) return;
-    uint32_t r, start;
-    if (staged) {
-        uint32_t lo = 0, hi = nr;  // first i with s_end[i] > e
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (s_end[mid] > (uint32_t)e) hi = mid;
-            else lo = mid + 1;
-        }
-        r = r_lo + lo;
-        start = lo == 0 ? s_start0 : s_end[lo - 1];
-    } else {
-        r = upper_bound_u32(offsets, r_lo, r_hi, (uint32_t)e);
-        start = r == 0 ? 0u : offsets[r - 1];
-    }
-    const uint32_t gid = order[r];
-    const uint32_t k = (uint32_t)e - start;
     const float4* rec = splat + (size_t)gid * SPLAT_F4;  // one 64-B line: rect, position, conic + opacity
     const float4 rect = rec[3];  // {x0, y0, x1, y1} from preprocess (getRect)
     const float4 pos = rec[0], co = rec[1];
     const uint32_t x0 = __builtin_bit_cast(uint32_t, rect.x), y0 = __builtin_bit_cast(uint32_t, rect.y);
     const uint32_t w = __builtin_bit_cast(uint32_t, rect.z) - x0;
-    const uint32_t ky = k / w;
-    const uint32_t tx = x0 + (k - ky * w), ty = y0 + ky;
-    tile_keys[e] = ty * gx + tx;
+    // k / w through the f32 reciprocal (a u32 division is ~40 VALU): for k < 2^20 the truncated quotient is off by at
+    // most one, which the remainder test corrects exactly
+    uint32_t ky, kx;
+    if (k < (1u << 20)) {
+        ky = (uint32_t)((float)k * __builtin_amdgcn_rcpf((float)w));
+        int rem = (int)k - (int)(ky * w);
+        if (rem < 0) { --ky; rem += (int)w; }
+        else if (rem >= (int)w) { ++ky; rem -= (int)w; }
+        kx = (uint32_t)rem;
+    } else {
+        ky = k / w;
+        kx = k - ky * w;
+    }
+    const uint32_t tx = x0 + kx, ty = y0 + ky;
+    *key = ty * gx + tx;
     // the bands of the tile this instance can reach (point list entry format, raster_common.h)
-    gauss_vals[e] = gid | (band_mask<PL_BANDS>(make_float2(pos.x, pos.y), co, tx, ty, 0) << PL_GID_BITS);
-    reinterpret_cast<uint8_t*>(binning + row_valid_offset(L))[e] = 0;  // the backward's row map (render_bwd.hip)
+    *val = gid | (band_mask<PL_BANDS>(make_float2(pos.x, pos.y), co, tx, ty, 0) << PL_GID_BITS);
 }
 
-// identifyTileRanges (rasterizer_impl.cu:145-167)
+// duplicateWithKeys (rasterizer_impl.cu:94-140) in depth order: Gaussian order[r] owns slots
+// [offsets[r-1], offsets[r]) and its tiles are emitted row-major like the reference. The value carries the
+// instance's band mask next to the Gaussian index (raster_common.h: point list entries). Per INSTANCE work (not per
+// Gaussian as in the reference), EMIT_PER consecutive slots per thread: the stores are 16-B per lane and fully
+// coalesced, a polar Gaussian spanning hundreds of tiles no longer serialises its wave, and each thread has
+// EMIT_PER independent record gathers in flight (the kernel waits on memory, not on its ALU). The block's slots
+// belong to ranks [block_owner[B], block_owner[B+1]]; their slot ends are staged in LDS, each thread finds the owner
+// of its first slot by a binary search there and steps forward for the others.
+__global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap, const uint32_t* count,
+                                                            const uint32_t* order, const uint32_t* offsets,
+                                                            const uint32_t* block_owner, const float4* splat,
+                                                            uint32_t gx, uint32_t* tile_keys, uint32_t* gauss_vals,
+                                                            char* binning)
+{
+    __shared__ uint32_t s_end[EMIT_SLOTS];
+    __shared__ uint32_t s_start0;
+    const size_t L = live_count(L_cap, count);
+    const uint32_t B = blockIdx.x;
+    const size_t e0 = (size_t)B * EMIT_SLOTS;
+    if (e0 >= L) return;  // block-uniform
+    const uint32_t r_lo = block_owner[B];
+    const uint32_t r_hi = e0 + EMIT_SLOTS < L ? block_owner[B + 1] + 1 : (uint32_t)P;  // exclusive
+    const uint32_t nr = r_hi - r_lo;
+    const bool staged = nr <= EMIT_SLOTS;  // block-uniform; more only with runs of empty (culled) segments
+    if (staged)
+        for (uint32_t i = threadIdx.x; i < nr; i += EMIT_THREADS) s_end[i] = offsets[r_lo + i];
+    if (threadIdx.x == 0) s_start0 = r_lo == 0 ? 0u : offsets[r_lo - 1];
+    __syncthreads();
+    const size_t eb = e0 + (size_t)threadIdx.x * EMIT_PER;
+    if (eb >= L) return;
+    const uint32_t nmine = (uint32_t)min((size_t)EMIT_PER, L - eb);
+    uint32_t rr[EMIT_PER], kk[EMIT_PER];
+    if (staged) {
+        uint32_t lo = 0, hi = nr;  // first i with s_end[i] > eb
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_end[mid] > (uint32_t)eb) hi = mid;
+            else lo = mid + 1;
+        }
+#pragma unroll
+        for (int j = 0; j < EMIT_PER; ++j) {
+            const uint32_t e = (uint32_t)eb + (uint32_t)j;
+            if (j > 0 && (uint32_t)j < nmine)
+                while (s_end[lo] <= e) ++lo;  // the last owner's end is past every slot of the block
+            rr[j] = r_lo + lo;
+            kk[j] = e - (lo == 0 ? s_start0 : s_end[lo - 1]);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < EMIT_PER; ++j) {
+            const uint32_t e = (uint32_t)eb + (uint32_t)min((uint32_t)j, nmine - 1);
+            const uint32_t r = upper_bound_u32(offsets, r_lo, r_hi, e);
+            rr[j] = r;
+            kk[j] = e - (r == 0 ? 0u : offsets[r - 1]);
+        }
+    }
+    uint32_t gid[EMIT_PER], key[EMIT_PER], val[EMIT_PER];
+#pragma unroll
+    for (int j = 0; j < EMIT_PER; ++j) gid[j] = order[rr[j]];
+#pragma unroll
+    for (int j = 0; j < EMIT_PER; ++j) emit_one(splat, gid[j], kk[j], gx, &key[j], &val[j]);
+    uint8_t* row_valid = reinterpret_cast<uint8_t*>(binning + row_valid_offset(L));  // the backward's row map
+    if (EMIT_PER == 4 && nmine == 4) {
+        *reinterpret_cast<uint4*>(tile_keys + eb) = make_uint4(key[0], key[1], key[2], key[3]);
+        *reinterpret_cast<uint4*>(gauss_vals + eb) = make_uint4(val[0], val[1], val[2], val[3]);
+        *reinterpret_cast<uint32_t*>(row_valid + eb) = 0u;  // row_valid_offset is 256-B aligned
+    } else {
+#pragma unroll
+        for (int j = 0; j < EMIT_PER; ++j) {
+            if ((uint32_t)j >= nmine) break;
+            tile_keys[eb + j] = key[j];
+            gauss_vals[eb + j] = val[j];
+            row_valid[eb + j] = 0;
+        }
+    }
+}
+
+// identifyTileRanges (rasterizer_impl.cu:145-167). Four sorted keys per thread through one 16-B load (key arrays
+// are 16-B aligned), the predecessor of the first from the neighbouring lane.
+constexpr int RANGES_ITEMS = 4;
 __global__ __launch_bounds__(256) void tile_ranges_kernel(size_t L_cap, const uint32_t* count, const uint32_t* tiles,
                                                           uint2* ranges)
 {
     const size_t L = live_count(L_cap, count);
-    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= L) return;
-    const uint32_t curr = tiles[idx];
-    if (idx == 0) ranges[curr].x = 0;
-    else {
-        const uint32_t prev = tiles[idx - 1];
-        if (curr != prev) {
+    const size_t i0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * RANGES_ITEMS;
+    if (i0 >= L) return;
+    uint32_t k[RANGES_ITEMS];
+    if (i0 + RANGES_ITEMS <= L) {
+        const uint4 q = *reinterpret_cast<const uint4*>(tiles + i0);
+        k[0] = q.x; k[1] = q.y; k[2] = q.z; k[3] = q.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < RANGES_ITEMS; ++j) k[j] = i0 + j < L ? tiles[i0 + j] : 0u;
+    }
+    uint32_t prev = i0 == 0 ? 0u : tiles[i0 - 1];
+#pragma unroll
+    for (int j = 0; j < RANGES_ITEMS; ++j) {
+        const size_t idx = i0 + j;
+        if (idx >= L) break;
+        const uint32_t curr = k[j];
+        if (idx == 0) ranges[curr].x = 0;
+        else if (curr != prev) {
             ranges[prev].y = (uint32_t)idx;
             ranges[curr].x = (uint32_t)idx;
         }
+        if (idx == L - 1) ranges[curr].y = (uint32_t)L;
+        prev = curr;
     }
-    if (idx == L - 1) ranges[curr].y = (uint32_t)L;
 }
 
 // Longest-first render schedule. The render kernels run one wave per tile (or half tile) and launch more waves
@@ -764,34 +888,36 @@ __global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(const 
     __shared__ uint32_t s_hist[RADIX];
     __shared__ uint32_t s_max;
     const uint32_t tid = threadIdx.x;
-    uint32_t total = 0;
-    for (uint32_t base = 0; base < T; base += SCHED_THREADS) {
+    // thread tid owns the contiguous tiles [t0, t1): one block scan of the per-thread unit counts (their loads are
+    // independent, so all are in flight at once) instead of a scan per 1024 tiles — 2 x T/1024 dependent
+    // load + barrier rounds cost 32 us at config C
+    const uint32_t per = (T + SCHED_THREADS - 1) / SCHED_THREADS;
+    const uint32_t t0 = min(T, tid * per), t1 = min(T, t0 + per);
+    uint32_t mine = 0;
+    for (uint32_t t = t0; t < t1; ++t) {
         uint32_t rx, mc;
-        const uint32_t t = base + tid;
-        const uint32_t c = t < T ? tile_units(ranges, max_contrib, t, &rx, &mc) : 0u;
-        uint32_t tot;
-        (void)block_exclusive_scan<SCHED_THREADS>(c, s_wave, &tot);
-        total += tot;
+        mine += tile_units(ranges, max_contrib, t, &rx, &mc);
     }
+    uint32_t total;
+    const uint32_t first0 = block_exclusive_scan<SCHED_THREADS>(mine, s_wave, &total);
     // this block's share of [0, total): xcd_remap's split over the 8 XCDs
     const uint32_t q = total / gridDim.x, rem = total % gridDim.x, x = blockIdx.x;
     const uint32_t lo = x * q + min(x, rem), hi = lo + q + (x < rem ? 1u : 0u);
-    uint32_t run = 0;
-    for (uint32_t base = 0; base < T && run < hi; base += SCHED_THREADS) {
-        uint32_t rx = 0, mc = 0;
-        const uint32_t t = base + tid;
-        const uint32_t c = t < T ? tile_units(ranges, max_contrib, t, &rx, &mc) : 0u;
-        uint32_t tot;
-        const uint32_t first = run + block_exclusive_scan<SCHED_THREADS>(c, s_wave, &tot);
-        for (uint32_t k = 0; k < c; ++k) {
-            const uint32_t u = first + k;
-            if (u < lo || u >= hi) continue;
-            const uint32_t chunk = rx / CKPT + k;
-            units_tmp[u] = make_uint2(t, chunk);
-            // cost: the segment's positions below the tile's last contributor
-            cost_tmp[u] = min(rx + mc, (chunk + 1) * CKPT) - max(rx, chunk * CKPT);
+    if (first0 < hi && first0 + mine > lo) {
+        uint32_t first = first0;
+        for (uint32_t t = t0; t < t1 && first < hi; ++t) {
+            uint32_t rx, mc;
+            const uint32_t c = tile_units(ranges, max_contrib, t, &rx, &mc);
+            for (uint32_t k = 0; k < c; ++k) {
+                const uint32_t u = first + k;
+                if (u < lo || u >= hi) continue;
+                const uint32_t chunk = rx / CKPT + k;
+                units_tmp[u] = make_uint2(t, chunk);
+                // cost: the segment's positions below the tile's last contributor
+                cost_tmp[u] = min(rx + mc, (chunk + 1) * CKPT) - max(rx, chunk * CKPT);
+            }
+            first += c;
         }
-        run += tot;
     }
     if (tid < RADIX) s_hist[tid] = 0;
     if (tid == 0) s_max = 0;
@@ -903,25 +1029,45 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
         }
         return cur;
     }
-    const uint32_t nb = div_up(n, SORT_TILE);
+    // large sorts (config E's 117 M instances) take 8192-key tiles: digit runs twice as long per block, so the
+    // scattered stores fill whole lines more often (tile sort 1.98 -> 1.64 ms there); below the threshold 4096-key
+    // tiles are faster (0.136 vs 0.152 ms at config C's 7.9 M)
+    const bool large = n >= SORT_LARGE_MIN;
+    const uint32_t nb = div_up(n, large ? SORT_THREADS * SORT_ITEMS_LARGE : SORT_TILE);
     for (int p = first_pass; p < first_pass + passes; ++p) {
         const int shift = p * RADIX_BITS;
         const bool last = p == first_pass + passes - 1;
         if (nb <= SELF_SCAN_MAX_BLOCKS) {
-            radix_upsweep_kernel<true><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb, nullptr, 0);
-            radix_downsweep_kernel<true><<<nb, SORT_THREADS, 0, s>>>(ki, vi, ko, vo, n, count, last ? canon : nullptr,
-                                                                     shift, hist, nb);
+            if (large) {
+                radix_upsweep_kernel<true, SORT_ITEMS_LARGE><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb,
+                                                                                        nullptr, 0);
+                radix_downsweep_kernel<true, SORT_ITEMS_LARGE><<<nb, SORT_THREADS, 0, s>>>(
+                    ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
+            } else {
+                radix_upsweep_kernel<true, SORT_ITEMS><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb,
+                                                                                  nullptr, 0);
+                radix_downsweep_kernel<true, SORT_ITEMS><<<nb, SORT_THREADS, 0, s>>>(
+                    ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
+            }
         } else {
             // scan_partials: look-back status [nbs] (64-bit) | ticket | error word, zeroed by the upsweep
             const uint32_t nbs = div_up((size_t)RADIX * nb, SCAN_TILE);
             uint64_t* lb = reinterpret_cast<uint64_t*>(scan_partials);
             uint32_t* lb_ticket = scan_partials + 2 * (size_t)nbs;
-            radix_upsweep_kernel<false><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb, scan_partials,
-                                                                    2 * nbs + 2);
+            if (large)
+                radix_upsweep_kernel<false, SORT_ITEMS_LARGE><<<nb, SORT_THREADS, 0, s>>>(
+                    ki, n, count, shift, hist, nb, scan_partials, 2 * nbs + 2);
+            else
+                radix_upsweep_kernel<false, SORT_ITEMS><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb,
+                                                                                   scan_partials, 2 * nbs + 2);
             scan_lookback_kernel<<<nbs, SCAN_THREADS, 0, s>>>(hist, hist, (size_t)RADIX * nb, lb, lb_ticket,
                                                              err_out ? err_out : lb_ticket + 1);
-            radix_downsweep_kernel<false><<<nb, SORT_THREADS, 0, s>>>(ki, vi, ko, vo, n, count,
-                                                                      last ? canon : nullptr, shift, hist, nb);
+            if (large)
+                radix_downsweep_kernel<false, SORT_ITEMS_LARGE><<<nb, SORT_THREADS, 0, s>>>(
+                    ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
+            else
+                radix_downsweep_kernel<false, SORT_ITEMS><<<nb, SORT_THREADS, 0, s>>>(
+                    ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
         }
         std::swap(ki, ko);
         std::swap(vi, vo);
@@ -930,7 +1076,7 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
     return cur;
 }
 
-size_t emit_index_size(size_t L_cap) { return div_up(L_cap, EMIT_BLOCK) + 1; }
+size_t emit_index_size(size_t L_cap) { return div_up(L_cap, EMIT_SLOTS) + 1; }
 
 void launch_emit_instances(int P, size_t L_cap, const uint32_t* count, const GeomState& g, uint32_t gx,
                            uint32_t* block_owner, uint32_t* tile_keys, uint32_t* gauss_vals, char* binning,
@@ -938,14 +1084,14 @@ void launch_emit_instances(int P, size_t L_cap, const uint32_t* count, const Geo
 {
     if (P <= 0 || L_cap == 0) return;
     emit_index_kernel<<<div_up(P, 256), 256, 0, s>>>(P, L_cap, count, g.offsets, block_owner);
-    emit_kernel<<<div_up(L_cap, EMIT_BLOCK), EMIT_BLOCK, 0, s>>>(P, L_cap, count, g.order, g.offsets, block_owner,
+    emit_kernel<<<div_up(L_cap, EMIT_SLOTS), EMIT_THREADS, 0, s>>>(P, L_cap, count, g.order, g.offsets, block_owner,
                                                                  g.splat, gx, tile_keys, gauss_vals, binning);
 }
 
 void launch_tile_ranges(size_t L_cap, const uint32_t* count, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s)
 {
     if (L_cap == 0) return;
-    tile_ranges_kernel<<<div_up(L_cap, 256), 256, 0, s>>>(L_cap, count, sorted_tiles, ranges);
+    tile_ranges_kernel<<<div_up(L_cap, 256 * RANGES_ITEMS), 256, 0, s>>>(L_cap, count, sorted_tiles, ranges);
 }
 
 }  // namespace omr
