@@ -293,13 +293,20 @@ def main():
                 (out if name == "dL_dcolors" else grads.views)[name].copy_(gr[idx])
         return nr, radii, ib
 
+    # compact exchange: the colour all-gather overlaps the backward's per-Gaussian stage (parallel.CompactExchange);
+    # the LibTorch boundary has no event hook, so it exchanges after the backward
+    cx = None
+    if world > 1 and args.exchange == "compact":
+        cx = par.CompactExchange(grads, info, campos,
+                                 lambda pk, out: R.sh_grad_from_colors_packed(means3D, shs, g.sh_degree, pk, out=out),
+                                 dev, overlap=LT is None)
+    bwd_kwargs = cx.backward_kwargs() if cx is not None else {}
+
     def exchange():
-        if args.exchange == "compact":
-            par.allreduce_compact_(grads, info, out["dL_dcolors"], campos,
-                                   lambda c, d, out: R.sh_grad_from_colors(means3D, shs, g.sh_degree, c, d, out=out),
-                                   rebuild_packed=lambda pk, out: R.sh_grad_from_colors_packed(means3D, shs,
-                                                                                              g.sh_degree, pk, out=out))
-        else:
+        if cx is not None:
+            cx.start()
+            cx.finish()
+        elif world > 1:
             par.allreduce_(grads, info, average=False, bucket_bytes=bucket)
 
     def step():
@@ -314,7 +321,7 @@ def main():
                 shs, g.sh_degree, campos, False, cam.camera_type, False)
             R.RasterizeGaussiansBackwardCUDA(bg, means3D, radii, empty, scales, rots, 1.0, empty, view, proj,
                                              cam.tanfovx, cam.tanfovy, dL_dout, shs, g.sh_degree, campos, gb, nr, bb,
-                                             ib, cam.camera_type, out=out)
+                                             ib, cam.camera_type, out=out, **bwd_kwargs)
         if record["on"]:
             ev[1].record(stream)
             compute_events.append(ev)

@@ -26,11 +26,15 @@
  *   - scratch memory comes from three allocation callbacks (geometry, binning, image) replacing the
  *     reference's std::function<char*(size_t)>; the returned memory must stay valid and be passed back
  *     unchanged to the backward call together with R = *num_rendered; its layout is private;
- *   - `stream` is a hipStream_t (NULL = legacy default stream). The forward synchronises the stream once,
- *     after the scan, to size the binning buffer (as the reference's cudaMemcpy, rasterizer_impl.cu:628);
+ *   - `stream` is a hipStream_t (NULL = legacy default stream). The forward does not wait for the GPU before it
+ *     has queued all its kernels: the binning buffer is sized from a capacity hint (the last num_rendered of the
+ *     view shape + 12.5 %) instead of the reference's mid-forward cudaMemcpy (rasterizer_impl.cu:628); the call
+ *     then waits for num_rendered to return it (and re-runs the binning at the exact size if the hint was short);
  *   - ADDED vs the reference: the backward writes EVERY element of its gradient outputs (zeros where the
  *     reference leaves its zero-initialised tensors untouched), so they need not be zeroed by the caller.
- *     dL_dconic ([P,4], slots 0,1,3) and, for lonlat, dpx_dt / dpy_dt ([P,3]) are optional (NULL = skip);
+ *     dL_dconic ([P,4], slots 0,1,3) and, for lonlat, dpx_dt / dpy_dt ([P,3]) are optional (NULL = skip), and
+ *     so is dL_dsh (its SH backward still feeds dL_dmean3D; a view-parallel host rebuilds the summed SH gradient
+ *     from the colour gradients instead, omr_sh_grad_from_colors_packed);
  *   - errors: calls return OMR_OK (0) or an OMR_ERR_* code; omr_last_error() gives the message of the last
  *     failing call on this thread. The reference throws std::runtime_error / traps instead.
  */
@@ -105,6 +109,11 @@ int omr_lonlat_backward(int P, int D, int M, int R, const float* background, int
                         float* dL_dsh, float* dL_dscale, float* dL_drot, float* dpx_dt, float* dpy_dt, void* stream);
 
 /* --- view-parallel data parallelism (extension, not in the reference; omnigs-fork_amd/parallel.py) -- */
+/* The next omr_*_backward call on this thread records `event` (a hipEvent_t) on its stream as soon as dL_dcolor is
+ * final — after the per-Gaussian row sums, before the per-Gaussian backward (gaussian_bwd) — and forgets it. A
+ * view-parallel host starts the all-gather of the colour gradients on another stream waiting on that event, so the
+ * collective overlaps the rest of the backward. NULL clears a pending event. */
+void omr_backward_colors_event(void* event);
 /* dL_dsh [P,M,3] = sum over nviews views of the SH gradient the backward computes for each, rebuilt from each
  * view's dL_dcolors ([nviews][P][3], RasterizeGaussiansBackwardCUDA's second output) and camera position
  * (campos [nviews][3]) with the backward's own SH arithmetic. Lets view-parallel ranks exchange 12 B per

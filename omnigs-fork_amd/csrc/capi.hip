@@ -71,6 +71,8 @@ __global__ __launch_bounds__(256) void debug_point_ids_kernel(const uint32_t* li
 }
 
 thread_local std::string g_last_error;
+// omr_backward_colors_event: recorded by this thread's next backward once dL_dcolor is final, then cleared
+thread_local hipEvent_t t_colors_event = nullptr;
 
 int fail(int code, const std::string& msg)
 {
@@ -506,6 +508,8 @@ struct BackwardIn {
 
 int backward_impl(const BackwardIn& in)
 {
+    const hipEvent_t colors_event = t_colors_event;  // omr_backward_colors_event applies to this call only
+    t_colors_event = nullptr;
     g_last_error.clear();
     if (in.camera_type != CAM_PINHOLE && in.camera_type != CAM_LONLAT)
         return fail(OMR_ERR_CAMERA_TYPE, "[CudaRasterizer]Invalid camera_type");
@@ -515,7 +519,7 @@ int backward_impl(const BackwardIn& in)
         return fail(OMR_ERR_INVALID_ARGUMENT, "missing scratch buffer or dL_dpix");
     if (!in.dL_dmean2D || !in.dL_dopacity || !in.dL_dcolor || !in.dL_dmean3D || !in.dL_dcov3D || !in.dL_dscale || !in.dL_drot)
         return fail(OMR_ERR_INVALID_ARGUMENT, "missing gradient output pointer");
-    if (in.M > 0 && !in.dL_dsh) return fail(OMR_ERR_INVALID_ARGUMENT, "missing dL_dsh");
+    // dL_dsh == NULL with M > 0: not written (omnigs_raster.h; the view-parallel compact exchange rebuilds it)
     if ((in.dpx_dt == nullptr) != (in.dpy_dt == nullptr)) return fail(OMR_ERR_INVALID_ARGUMENT, "dpx_dt / dpy_dt: both or neither");
     const Dims d = dims(in.width, in.height);
     const hipStream_t s = in.stream;
@@ -571,7 +575,8 @@ int backward_impl(const BackwardIn& in)
     ga.focal_x = (float)in.width / (2.0f * in.tan_fovx);
     ga.clamped = g.clamped;
     ga.row_sums = g.row_sums;
-    { StageScope st_(ST_ROW_SUMS, s); launch_row_sums(in.P, g.row_first, g.tiles_touched, g.huge_list, g.counters + 2, b.inst_grad, b.row_valid, (uint32_t)in.R, g.row_sums, s); }
+    { StageScope st_(ST_ROW_SUMS, s); launch_row_sums(in.P, g.row_first, g.tiles_touched, g.huge_list, g.counters + 2, b.inst_grad, b.row_valid, (uint32_t)in.R, g.row_sums, in.dL_dcolor, s); }
+    if (colors_event) OMR_HIP(hipEventRecord(colors_event, s));  // dL_dcolor is final from here on
     ga.dL_dmean2D = in.dL_dmean2D; ga.dL_dconic = in.dL_dconic; ga.dL_dopacity = in.dL_dopacity; ga.dL_dcolor = in.dL_dcolor;
     ga.dL_dmean3D = in.dL_dmean3D; ga.dL_dcov3D = in.dL_dcov3D; ga.dL_dsh = in.M > 0 ? in.dL_dsh : nullptr;
     ga.dL_dscale = in.dL_dscale; ga.dL_drot = in.dL_drot; ga.dpx_dt = in.dpx_dt; ga.dpy_dt = in.dpy_dt;
@@ -594,6 +599,7 @@ using namespace omr;
 extern "C" {
 
 int omr_abi_version(void) { return OMR_ABI_VERSION; }
+void omr_backward_colors_event(void* event) { t_colors_event = static_cast<hipEvent_t>(event); }
 const char* omr_last_error(void) { return g_last_error.c_str(); }
 
 int omr_rasterizer_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -269,6 +269,7 @@ struct RowSumArgs {
     const float* inst_grad;
     const uint8_t* row_valid;
     float* row_sums;
+    float* dL_dcolor;  // [P][3] = row_sums[:, 6:9], written here so that it is final before gaussian_bwd runs
 };
 
 // one workgroup per huge Gaussian (the first RS_HUGE_BLOCKS blocks of the grid): thread t adds rows t, t + 256, ... (RS_HUGE_STEP in flight), then
@@ -300,9 +301,12 @@ __device__ __forceinline__ void huge_row_sums(const RowSumArgs& a, uint32_t hb, 
         if ((lane & 7) == 0) s_red[wv * GRAD_ROW + (lane >> 3)] = tv;
         if (lane == 1) s_red[wv * GRAD_ROW + 8] = t8;
         __syncthreads();
-        if (tid < GRAD_ROW)
-            a.row_sums[(size_t)idx * GRAD_ROW + tid] =
+        if (tid < GRAD_ROW) {
+            const float tot =
                 ((s_red[tid] + s_red[GRAD_ROW + tid]) + s_red[2 * GRAD_ROW + tid]) + s_red[3 * GRAD_ROW + tid];
+            a.row_sums[(size_t)idx * GRAD_ROW + tid] = tot;
+            if (tid >= 6) a.dL_dcolor[(size_t)idx * 3 + (tid - 6)] = tot;
+        }
         __syncthreads();
     }
 }
@@ -412,6 +416,10 @@ __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
         float* out = a.row_sums + (size_t)idx * GRAD_ROW;
 #pragma unroll
         for (int c = 0; c < GRAD_ROW; ++c) out[c] = acc[c];
+        // dL/dcolour (backward.cu:805-808 sums) is final here: the view-parallel exchange can gather it while
+        // gaussian_bwd still runs (parallel.py); zeros for a culled Gaussian, which has no rows
+#pragma unroll
+        for (int c = 0; c < 3; ++c) a.dL_dcolor[(size_t)idx * 3 + c] = acc[6 + c];
     }
 }
 
@@ -433,10 +441,7 @@ __device__ __forceinline__ void gaussian_bwd_point(const GaussBwdArgs& a, int id
     a.dL_dmean2D[3 * idx + 0] = g[0];
     a.dL_dmean2D[3 * idx + 1] = g[1];
     a.dL_dmean2D[3 * idx + 2] = 0.f;
-    a.dL_dopacity[idx] = g[5];
-    a.dL_dcolor[3 * idx + 0] = g[6];
-    a.dL_dcolor[3 * idx + 1] = g[7];
-    a.dL_dcolor[3 * idx + 2] = g[8];
+    a.dL_dopacity[idx] = g[5];  // dL_dcolor = g[6..8] was written by row_sum_kernel
     if (a.dL_dconic) {
         a.dL_dconic[4 * idx + 0] = g[2];
         a.dL_dconic[4 * idx + 1] = g[3];
@@ -602,8 +607,7 @@ __device__ __forceinline__ void gaussian_bwd_culled(const GaussBwdArgs& a, int i
     const int Mr = MC > 0 ? MC : a.M;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        a.dL_dmean2D[3 * idx + c] = 0.f;
-        a.dL_dcolor[3 * idx + c] = 0.f;
+        a.dL_dmean2D[3 * idx + c] = 0.f;  // dL_dcolor: zeros from row_sum_kernel
         a.dL_dmean3D[3 * idx + c] = 0.f;
         a.dL_dscale[3 * idx + c] = 0.f;
     }
@@ -765,7 +769,7 @@ void launch_sh_grad_from_colors(int P, int D, int M, int nviews, const float* me
 
 void launch_row_sums(int P, const uint32_t* row_first, const uint32_t* tiles_touched, const uint32_t* huge_list,
                      const uint32_t* huge_count, const float* inst_grad, const uint8_t* row_valid, uint32_t R,
-                     float* row_sums, hipStream_t s)
+                     float* row_sums, float* dL_dcolor, hipStream_t s)
 {
     if (P <= 0) return;
     RowSumArgs a;
@@ -779,6 +783,7 @@ void launch_row_sums(int P, const uint32_t* row_first, const uint32_t* tiles_tou
     a.inst_grad = inst_grad;
     a.row_valid = row_valid;
     a.row_sums = row_sums;
+    a.dL_dcolor = dL_dcolor;
     row_sum_kernel<<<a.main_blocks + RS_HUGE_BLOCKS, 256, 0, s>>>(a);
 }
 

@@ -16,12 +16,16 @@ is no pack/unpack copy before or after the collective.
 
 Two exchanges give the same summed gradients (up to the order of the float additions):
   * allreduce_          one RCCL all-reduce of the whole 236 B/Gaussian buffer;
-  * allreduce_compact_  (default in bench.py) all-reduce of the first 44 B/Gaussian (xyz, opacity, scale,
+  * allreduce_compact_  all-reduce of the first 44 B/Gaussian (xyz, opacity, scale,
                         rotation) and ONE all-gather of each view's colour gradient (12 B/Gaussian) with its camera
                         position appended as an extra row; every rank then rebuilds the summed SH gradient with the backward's own SH
                         arithmetic (omr_sh_grad_from_colors). Per rank on a ring of n: 2(n-1)/n * 236 B/G vs
                         2(n-1)/n * 44 + (n-1) * 12 B/G — at n = 8, 413 vs 161 MB for 1 M Gaussians, at n = 2 236 vs
                         56 MB. xGMI is point-to-point (a 2-GPU job has ONE link), so bytes are the scaling cost.
+  * CompactExchange     (default in bench.py) the compact exchange overlapped with the backward: the row sums write
+                        dL_dcolors before the per-Gaussian backward runs, the backward records an event there
+                        (omr_backward_colors_event), and the colour all-gather starts on a side stream as soon as it
+                        fires; the per-view dL_dsh is not written at all (skip_dsh), since the rebuild replaces it.
 """
 from __future__ import annotations
 
@@ -126,3 +130,46 @@ def allreduce_compact_(buf: GradBuffer, info: DistInfo, dL_dcolors: torch.Tensor
         rebuild(packed_all[:, P].contiguous(), packed_all[:, :P].contiguous(), out=buf.views["dL_dsh"])
     if average:
         buf.flat.div_(n)
+
+
+class CompactExchange:
+    """allreduce_compact_ with the colour all-gather overlapped with the rest of the backward (module docstring).
+
+    Per step: call the backward with **backward_kwargs() (event + skip_dsh), then start() (queues the all-gather on a
+    side stream behind the event), then finish() (all-reduce of the 44 B/G prefix on the current stream once the
+    backward is done, then the SH rebuild behind both collectives). Over gloo (CPU rehearsals), or when `overlap` is
+    False (e.g. a host that cannot pass the event), it falls back to allreduce_compact_ inside finish()."""
+
+    def __init__(self, buf: GradBuffer, info: DistInfo, campos: torch.Tensor, rebuild_packed, device,
+                 overlap: bool = True):
+        self.buf, self.info, self.rebuild_packed = buf, info, rebuild_packed
+        self.campos = campos
+        P = buf.P
+        buf.out_dict(device)  # creates colors_ext [P + 1, 3]
+        buf.colors_ext[P].copy_(campos.reshape(3).to(buf.colors_ext.dtype))
+        self.overlap = bool(overlap and info.enabled and dist.get_backend() == "nccl")
+        if self.overlap:
+            self.event = torch.cuda.Event()
+            self.comm = torch.cuda.Stream(device)
+            self.packed_all = torch.empty((info.world_size, P + 1, 3), dtype=buf.colors_ext.dtype, device=device)
+
+    def backward_kwargs(self) -> dict:
+        return dict(colors_event=self.event, skip_dsh=True) if self.overlap else {}
+
+    def start(self):
+        if not self.overlap:
+            return
+        with torch.cuda.stream(self.comm):
+            self.comm.wait_event(self.event)
+            dist.all_gather_into_tensor(self.packed_all, self.buf.colors_ext)
+
+    def finish(self):
+        if not self.info.enabled:
+            return
+        if not self.overlap:
+            allreduce_compact_(self.buf, self.info, self.buf.colors_ext[:self.buf.P], self.campos, None,
+                               rebuild_packed=self.rebuild_packed)
+            return
+        dist.all_reduce(self.buf.flat[:REDUCED_FLOATS * self.buf.P], op=dist.ReduceOp.SUM)
+        torch.cuda.current_stream().wait_stream(self.comm)
+        self.rebuild_packed(self.packed_all, out=self.buf.views["dL_dsh"])

@@ -60,6 +60,8 @@ def lib() -> C.CDLL:
         L.omr_image_bytes.argtypes = [i, i]
         L.omr_binning_bytes.restype = sz
         L.omr_binning_bytes.argtypes = [i, i, i]
+        L.omr_backward_colors_event.argtypes = [vp]
+        L.omr_backward_colors_event.restype = None
         L.omr_debug_point_list.argtypes = [vp, i, i, i, vp, vp]
         L.omr_debug_ranges.argtypes = [vp, i, i, vp, vp]
         L.omr_debug_image_state.argtypes = [vp, i, i, vp, vp, vp]
@@ -217,13 +219,18 @@ def RasterizeGaussiansCUDA(background, means3D, colors, opacity, scales, rotatio
 
 def RasterizeGaussiansBackwardCUDA(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp,
                                    viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos,
-                                   geomBuffer, R, binningBuffer, imageBuffer, camera_type=CAMERA_PINHOLE, out=None):
+                                   geomBuffer, R, binningBuffer, imageBuffer, camera_type=CAMERA_PINHOLE, out=None,
+                                   colors_event=None, skip_dsh=False):
     """rasterize_points.cu:166-285. Returns (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh,
     dL_dscales, dL_drotations).
 
-    `out` (extension): optional dict of preallocated, contiguous float32 tensors keyed by those names, written in
-    place (every element is written) — lets a data-parallel host place the gradients inside one flat all-reduce
-    buffer."""
+    Extensions for a data-parallel host (parallel.CompactExchange):
+      `out`          optional dict of preallocated, contiguous float32 tensors keyed by those names, written in place
+                     (every element is written): the gradients land inside one flat all-reduce buffer;
+      `colors_event` a torch.cuda.Event recorded on the stream as soon as dL_dcolors is final (after the row sums,
+                     before the per-Gaussian backward): the colour all-gather can wait on it and overlap the rest;
+      `skip_dsh`     dL_dsh is not written (returned as None): the compact exchange rebuilds the summed SH gradient
+                     from the gathered colour gradients, so the per-view one would be overwritten unread."""
     if camera_type not in (CAMERA_PINHOLE, CAMERA_LONLAT):
         raise RasterizerError("[CudaRasterizer]Invalid camera_type")
     dev = means3D.device
@@ -234,6 +241,9 @@ def RasterizeGaussiansBackwardCUDA(background, means3D, radii, colors, scales, r
                   dL_dsh=(P, M, 3), dL_dscales=(P, 3), dL_drotations=(P, 4))
     o = {}
     for k, shp in shapes.items():
+        if k == "dL_dsh" and skip_dsh:
+            o[k] = None
+            continue
         t = None if out is None else out.get(k)
         if t is None:
             t = (torch.zeros if P == 0 else torch.empty)(shp, dtype=torch.float32, device=dev)
@@ -250,6 +260,10 @@ def RasterizeGaussiansBackwardCUDA(background, means3D, radii, colors, scales, r
         a = args_common
         rad = radii.contiguous()
         gb, bb, ib = geomBuffer.data_ptr(), binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr()
+        if colors_event is not None:
+            if colors_event.cuda_event == 0:  # torch creates the HIP event at its first record
+                colors_event.record(torch.cuda.current_stream(dev))
+            L.omr_backward_colors_event(C.c_void_p(colors_event.cuda_event))
         if camera_type == CAMERA_PINHOLE:
             pm = _dev_f32(projmatrix, "projmatrix")
             rc = L.omr_rasterizer_backward(P, int(degree), M, int(R), _ptr(a["bg"]), W, H, _ptr(a["m"]), _ptr(a["shc"]),

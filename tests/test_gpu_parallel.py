@@ -49,3 +49,42 @@ def test_sh_rebuild_argument_checks():
     sh = torch.zeros((10, 16, 3), device="cuda")
     with pytest.raises(R.RasterizerError):
         R.sh_grad_from_colors(m, sh, 3, torch.zeros((2, 3), device="cuda"), torch.zeros((3, 10, 3), device="cuda"))
+
+
+@pytest.mark.parametrize("cam_type", [scene.CAMERA_LONLAT, scene.CAMERA_PINHOLE])
+def test_colors_event_fires_when_colour_gradients_are_final(cam_type):
+    """parallel.CompactExchange's overlap: the backward records colors_event once dL_dcolors is final (row sums),
+    before the per-Gaussian backward. A side stream that waits on the event and copies dL_dcolors right away must see
+    the final values; skip_dsh leaves dL_dsh unwritten and every other output equal to the plain backward."""
+    R = omr.rasterizer
+    W, H = (512, 256) if cam_type == scene.CAMERA_LONLAT else (320, 180)
+    g, cam, dL = make_case(20000, W, H, cam_type, 17, view_index=2)
+    ref = hip_run(g, cam, dL)
+    dev = torch.device("cuda")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)
+    m, sc, rot, sh, op = t(g.means3D), t(g.scales), t(g.rotations), t(g.shs), t(g.opacity)
+    vm, pm, cp, bg, dl = t(cam.viewmatrix), t(cam.projmatrix), t(cam.campos), torch.zeros(3, device=dev), t(dL)
+    e = torch.empty(0, device=dev)
+    nr, color, radii, gb, bb, ib = R.RasterizeGaussiansCUDA(bg, m, e, op, sc, rot, 1.0, e, vm, pm, cam.tanfovx,
+                                                            cam.tanfovy, H, W, sh, g.sh_degree, cp, False,
+                                                            cam.camera_type, False)
+    ev = torch.cuda.Event()
+    side = torch.cuda.Stream(dev)
+    grads = R.RasterizeGaussiansBackwardCUDA(bg, m, radii, e, sc, rot, 1.0, e, vm, pm, cam.tanfovx, cam.tanfovy, dl,
+                                             sh, g.sh_degree, cp, gb, nr, bb, ib, cam.camera_type,
+                                             colors_event=ev, skip_dsh=True)
+    with torch.cuda.stream(side):
+        side.wait_event(ev)
+        early = grads[1].clone()
+    torch.cuda.synchronize()
+    assert grads[5] is None
+    np.testing.assert_array_equal(to_np(early), to_np(ref["grads"]["dcolor"]))
+    for i, name in enumerate(["dmean2D", "dcolor", "dopacity", "dmean3D", "dcov3D"]):
+        np.testing.assert_array_equal(to_np(grads[i]), to_np(ref["grads"][name]), err_msg=name)
+    np.testing.assert_array_equal(to_np(grads[6]), to_np(ref["grads"]["dscale"]))
+    np.testing.assert_array_equal(to_np(grads[7]), to_np(ref["grads"]["drot"]))
+    # the event is consumed by that call: a second backward without one records nothing and must still work
+    again = R.RasterizeGaussiansBackwardCUDA(bg, m, radii, e, sc, rot, 1.0, e, vm, pm, cam.tanfovx, cam.tanfovy, dl,
+                                             sh, g.sh_degree, cp, gb, nr, bb, ib, cam.camera_type)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(to_np(again[5]), to_np(ref["grads"]["dsh"]))

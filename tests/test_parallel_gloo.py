@@ -63,8 +63,19 @@ def _worker(rank, world, port, bucket, average, q, compact=False):
                 out.copy_(torch.from_numpy(sh_grad_from_colors_np(grads["means3D"], grads["shs"], grads["deg"],
                                                                   campos_all.numpy(), dcolors_all.numpy())))
 
-            par.allreduce_compact_(buf, info, torch.from_numpy(grads["dL_dcolors"]),
-                                   torch.from_numpy(grads["campos"]), rebuild, average=average)
+            if compact == "cx":  # parallel.CompactExchange: over gloo it takes the non-overlapped path
+                def rebuild_packed(pk, out):
+                    rebuild(pk[:, buf.P].contiguous(), pk[:, :buf.P].contiguous(), out)
+
+                cx = par.CompactExchange(buf, info, torch.from_numpy(grads["campos"]), rebuild_packed,
+                                         torch.device("cpu"))
+                assert not cx.overlap and cx.backward_kwargs() == {}
+                buf.colors_ext[:buf.P].copy_(torch.from_numpy(grads["dL_dcolors"]))  # the backward's output slot
+                cx.start()
+                cx.finish()
+            else:
+                par.allreduce_compact_(buf, info, torch.from_numpy(grads["dL_dcolors"]),
+                                       torch.from_numpy(grads["campos"]), rebuild, average=average)
         else:
             par.allreduce_(buf, info, average=average, bucket_bytes=bucket)
         q.put((rank, {k: v.numpy().copy() for k, v in buf.views.items()}))
@@ -73,7 +84,7 @@ def _worker(rank, world, port, bucket, average, q, compact=False):
 
 
 @pytest.mark.parametrize("bucket,average,compact", [(0, False, False), (4096, False, False), (0, True, False),
-                                                    (0, False, True), (0, True, True)])
+                                                    (0, False, True), (0, True, True), (0, False, "cx")])
 def test_allreduce_equals_sum_of_views(bucket, average, compact, oracle_mod):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
