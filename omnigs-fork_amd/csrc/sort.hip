@@ -260,13 +260,17 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_lookback_kernel(const uint3
 // sorts of at most this many 4096-item blocks (the depth sort up to 2M Gaussians) let each downsweep block derive
 // its digit offsets from the raw histogram: <= 512 KiB of L2 reads per block instead of three scan launches
 constexpr uint32_t SELF_SCAN_MAX_BLOCKS = 512;
+#ifndef OMR_SORT_THREADS_LARGE
+#define OMR_SORT_THREADS_LARGE 512
+#endif
 #ifndef OMR_SORT_ITEMS_LARGE
-#define OMR_SORT_ITEMS_LARGE 32
+#define OMR_SORT_ITEMS_LARGE (8192 / OMR_SORT_THREADS_LARGE)
 #endif
 #ifndef OMR_SORT_LARGE_MIN
 #define OMR_SORT_LARGE_MIN (1u << 25)
 #endif
-constexpr int SORT_ITEMS_LARGE = OMR_SORT_ITEMS_LARGE;  // items per thread of the multi-launch passes of large sorts
+constexpr int SORT_THREADS_LARGE = OMR_SORT_THREADS_LARGE;  // block size of the multi-launch passes of large sorts
+constexpr int SORT_ITEMS_LARGE = OMR_SORT_ITEMS_LARGE;      // items per thread there (8192-key tiles)
 constexpr size_t SORT_LARGE_MIN = OMR_SORT_LARGE_MIN;
 
 // ---- radix sort ------------------------------------------------------------------------------------------
@@ -283,19 +287,20 @@ __device__ __forceinline__ size_t live_count(size_t n, const uint32_t* count)
 #endif
 // BLOCK_MAJOR: hist[block][digit] (read back by the self-scanning downsweep of small sorts); else hist[digit][block].
 // Key arrays are 16-B aligned (Carver) for the 16-B loads.
-template <bool BLOCK_MAJOR, int ITEMS>
-__global__ __launch_bounds__(SORT_THREADS) void radix_upsweep_kernel(const uint32_t* keys, size_t n_cap,
+template <bool BLOCK_MAJOR, int ITEMS, int THREADS>
+__global__ __launch_bounds__(THREADS) void radix_upsweep_kernel(const uint32_t* keys, size_t n_cap,
                                                                      const uint32_t* count, int shift, uint32_t* hist,
                                                                      uint32_t nblocks, uint32_t* zero, uint32_t nzero)
 {
-    constexpr int TILE_N = SORT_THREADS * ITEMS;
+    constexpr int TILE_N = THREADS * ITEMS;
     {   // the look-back words of the histogram scan that follows (scan_lookback_kernel)
-        const uint32_t z = blockIdx.x * SORT_THREADS + threadIdx.x;
+        const uint32_t z = blockIdx.x * THREADS + threadIdx.x;
         if (z < nzero) zero[z] = 0u;
     }
     const size_t n = live_count(n_cap, count);
+    static_assert(THREADS % RADIX == 0, "thread = digit phases");
     __shared__ uint32_t s_hist[RADIX];
-    s_hist[threadIdx.x] = 0;
+    if (threadIdx.x < RADIX) s_hist[threadIdx.x] = 0;
     __syncthreads();
     const size_t base = (size_t)blockIdx.x * TILE_N;
 #if OMR_UPSWEEP_V4
@@ -307,7 +312,7 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_upsweep_kernel(const uint3
     const bool full = base + TILE_N <= n;
 #pragma unroll
     for (int k = 0; k < ITEMS / 4; ++k) {
-        const size_t i = base + 4 * ((size_t)k * SORT_THREADS + threadIdx.x);
+        const size_t i = base + 4 * ((size_t)k * THREADS + threadIdx.x);
         uint4 q;
         if (full) q = *reinterpret_cast<const uint4*>(keys + i);
         else {
@@ -323,7 +328,7 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_upsweep_kernel(const uint3
     }
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
-        const size_t i = base + 4 * ((size_t)(j >> 2) * SORT_THREADS + threadIdx.x) + (j & 3);
+        const size_t i = base + 4 * ((size_t)(j >> 2) * THREADS + threadIdx.x) + (j & 3);
         const bool valid = i < n;
         const uint32_t d = (kv[j] >> shift) & (RADIX - 1);
         if (OMR_UPSWEEP_V4 == 2) {
@@ -342,13 +347,15 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_upsweep_kernel(const uint3
 #else
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) {
-        const size_t i = base + (size_t)k * SORT_THREADS + threadIdx.x;
+        const size_t i = base + (size_t)k * THREADS + threadIdx.x;
         if (i < n) atomicAdd(&s_hist[(keys[i] >> shift) & (RADIX - 1)], 1u);
     }
 #endif
     __syncthreads();
-    if (BLOCK_MAJOR) hist[(size_t)blockIdx.x * RADIX + threadIdx.x] = s_hist[threadIdx.x];
-    else hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = s_hist[threadIdx.x];
+    if (threadIdx.x < RADIX) {
+        if (BLOCK_MAJOR) hist[(size_t)blockIdx.x * RADIX + threadIdx.x] = s_hist[threadIdx.x];
+        else hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = s_hist[threadIdx.x];
+    }
 }
 
 // One block sorts its 4096-item tile by the pass's digit in LDS, then writes each digit's run to its global
@@ -360,21 +367,21 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_upsweep_kernel(const uint3
 // SELF_SCAN (small sorts, few blocks): hist is the raw block-major histogram and each block derives its global
 // digit offsets itself (column prefix over the blocks before it + scan of the digit totals), which saves the
 // three scan launches per pass; else hist is the scanned [digit][block] histogram.
-template <bool SELF_SCAN, int ITEMS>
-__global__ __launch_bounds__(SORT_THREADS) void radix_downsweep_kernel(const uint32_t* keys_in, const uint32_t* vals_in,
+template <bool SELF_SCAN, int ITEMS, int THREADS>
+__global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const uint32_t* keys_in, const uint32_t* vals_in,
                                                                        uint32_t* keys_out, uint32_t* vals_out,
                                                                        size_t n_cap, const uint32_t* count, char* canon,
                                                                        int shift, const uint32_t* hist_scanned,
                                                                        uint32_t nblocks)
 {
-    constexpr int TILE_N = SORT_THREADS * ITEMS;
-    constexpr int WAVES = SORT_THREADS / 64;
+    constexpr int TILE_N = THREADS * ITEMS;
+    constexpr int WAVES = THREADS / 64;
     constexpr int PER_WAVE = TILE_N / WAVES;
     constexpr int ROUNDS = PER_WAVE / 64;
     __shared__ uint32_t s_whist[WAVES][RADIX];  // running digit counts per wave, then per-wave digit offsets
     __shared__ uint32_t s_dstart[RADIX];        // block-local start of each digit's run
     __shared__ uint32_t s_gbase[RADIX];         // global start of this block's run of each digit
-    __shared__ uint32_t s_wave[SORT_THREADS / 64];
+    __shared__ uint32_t s_wave[THREADS / 64];
     __shared__ uint32_t s_k[TILE_N];
     __shared__ uint32_t s_v[TILE_N];
     const size_t n = live_count(n_cap, count);
@@ -382,29 +389,33 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_downsweep_kernel(const uin
     const uint32_t tid = threadIdx.x;
     const uint32_t w = tid >> 6, lane = tid & 63;
     const size_t tile0 = (size_t)blockIdx.x * TILE_N;
-#pragma unroll
-    for (int q = 0; q < WAVES; ++q) s_whist[q][tid] = 0;
+    static_assert(THREADS % RADIX == 0, "thread = digit phases");
+    const bool dig = tid < RADIX;  // this thread also owns digit tid in the per-digit phases
+    for (uint32_t i = tid; i < (uint32_t)(WAVES * RADIX); i += THREADS) (&s_whist[0][0])[i] = 0;
     if (SELF_SCAN) {
         uint32_t before = 0, total = 0;
-        uint32_t b = 0;
-        for (; b + 8 <= nblocks; b += 8) {  // 8 coalesced 1-KiB row loads in flight
-            uint32_t c[8];
+        if (dig) {
+            uint32_t b = 0;
+            for (; b + 8 <= nblocks; b += 8) {  // 8 coalesced 1-KiB row loads in flight
+                uint32_t c[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) c[q] = hist_scanned[(size_t)(b + q) * RADIX + tid];
+                for (int q = 0; q < 8; ++q) c[q] = hist_scanned[(size_t)(b + q) * RADIX + tid];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                before += b + q < blockIdx.x ? c[q] : 0u;
-                total += c[q];
+                for (int q = 0; q < 8; ++q) {
+                    before += b + q < blockIdx.x ? c[q] : 0u;
+                    total += c[q];
+                }
+            }
+            for (; b < nblocks; ++b) {
+                const uint32_t c = hist_scanned[(size_t)b * RADIX + tid];
+                before += b < blockIdx.x ? c : 0u;
+                total += c;
             }
         }
-        for (; b < nblocks; ++b) {
-            const uint32_t c = hist_scanned[(size_t)b * RADIX + tid];
-            before += b < blockIdx.x ? c : 0u;
-            total += c;
-        }
         uint32_t all;
-        s_gbase[tid] = before + block_exclusive_scan(total, s_wave, &all);
-    } else {
+        const uint32_t ex = block_exclusive_scan<THREADS>(total, s_wave, &all);
+        if (dig) s_gbase[tid] = before + ex;
+    } else if (dig) {
         s_gbase[tid] = hist_scanned[(size_t)tid * nblocks + blockIdx.x];
     }
     const size_t base = tile0 + (size_t)w * PER_WAVE + lane;
@@ -438,14 +449,17 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_downsweep_kernel(const uin
     __syncthreads();
     {   // thread = digit: per-wave exclusive offsets, then the block-wide exclusive scan of the digit totals
         uint32_t run = 0;
+        if (dig) {
 #pragma unroll
-        for (int q = 0; q < WAVES; ++q) {
-            const uint32_t c = s_whist[q][tid];
-            s_whist[q][tid] = run;
-            run += c;
+            for (int q = 0; q < WAVES; ++q) {
+                const uint32_t c = s_whist[q][tid];
+                s_whist[q][tid] = run;
+                run += c;
+            }
         }
         uint32_t total;
-        s_dstart[tid] = block_exclusive_scan(run, s_wave, &total);
+        const uint32_t ex = block_exclusive_scan<THREADS>(run, s_wave, &total);
+        if (dig) s_dstart[tid] = ex;
     }
     __syncthreads();
 #pragma unroll
@@ -459,7 +473,7 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_downsweep_kernel(const uin
     }
     __syncthreads();
     const uint32_t nvalid = (uint32_t)min((size_t)TILE_N, n > tile0 ? n - tile0 : (size_t)0);
-    for (uint32_t j = tid; j < nvalid; j += SORT_THREADS) {
+    for (uint32_t j = tid; j < nvalid; j += THREADS) {
         const uint32_t kk = s_k[j];
         const uint32_t d = (kk >> shift) & (RADIX - 1);
         const uint32_t dst = s_gbase[d] + (j - s_dstart[d]);
@@ -1033,20 +1047,20 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
     // scattered stores fill whole lines more often (tile sort 1.98 -> 1.64 ms there); below the threshold 4096-key
     // tiles are faster (0.136 vs 0.152 ms at config C's 7.9 M)
     const bool large = n >= SORT_LARGE_MIN;
-    const uint32_t nb = div_up(n, large ? SORT_THREADS * SORT_ITEMS_LARGE : SORT_TILE);
+    const uint32_t nb = div_up(n, large ? SORT_THREADS_LARGE * SORT_ITEMS_LARGE : SORT_TILE);
     for (int p = first_pass; p < first_pass + passes; ++p) {
         const int shift = p * RADIX_BITS;
         const bool last = p == first_pass + passes - 1;
         if (nb <= SELF_SCAN_MAX_BLOCKS) {
             if (large) {
-                radix_upsweep_kernel<true, SORT_ITEMS_LARGE><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb,
+                radix_upsweep_kernel<true, SORT_ITEMS_LARGE, SORT_THREADS_LARGE><<<nb, SORT_THREADS_LARGE, 0, s>>>(ki, n, count, shift, hist, nb,
                                                                                         nullptr, 0);
-                radix_downsweep_kernel<true, SORT_ITEMS_LARGE><<<nb, SORT_THREADS, 0, s>>>(
+                radix_downsweep_kernel<true, SORT_ITEMS_LARGE, SORT_THREADS_LARGE><<<nb, SORT_THREADS_LARGE, 0, s>>>(
                     ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
             } else {
-                radix_upsweep_kernel<true, SORT_ITEMS><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb,
+                radix_upsweep_kernel<true, SORT_ITEMS, SORT_THREADS><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb,
                                                                                   nullptr, 0);
-                radix_downsweep_kernel<true, SORT_ITEMS><<<nb, SORT_THREADS, 0, s>>>(
+                radix_downsweep_kernel<true, SORT_ITEMS, SORT_THREADS><<<nb, SORT_THREADS, 0, s>>>(
                     ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
             }
         } else {
@@ -1055,18 +1069,18 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
             uint64_t* lb = reinterpret_cast<uint64_t*>(scan_partials);
             uint32_t* lb_ticket = scan_partials + 2 * (size_t)nbs;
             if (large)
-                radix_upsweep_kernel<false, SORT_ITEMS_LARGE><<<nb, SORT_THREADS, 0, s>>>(
+                radix_upsweep_kernel<false, SORT_ITEMS_LARGE, SORT_THREADS_LARGE><<<nb, SORT_THREADS_LARGE, 0, s>>>(
                     ki, n, count, shift, hist, nb, scan_partials, 2 * nbs + 2);
             else
-                radix_upsweep_kernel<false, SORT_ITEMS><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb,
+                radix_upsweep_kernel<false, SORT_ITEMS, SORT_THREADS><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb,
                                                                                    scan_partials, 2 * nbs + 2);
             scan_lookback_kernel<<<nbs, SCAN_THREADS, 0, s>>>(hist, hist, (size_t)RADIX * nb, lb, lb_ticket,
                                                              err_out ? err_out : lb_ticket + 1);
             if (large)
-                radix_downsweep_kernel<false, SORT_ITEMS_LARGE><<<nb, SORT_THREADS, 0, s>>>(
+                radix_downsweep_kernel<false, SORT_ITEMS_LARGE, SORT_THREADS_LARGE><<<nb, SORT_THREADS_LARGE, 0, s>>>(
                     ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
             else
-                radix_downsweep_kernel<false, SORT_ITEMS><<<nb, SORT_THREADS, 0, s>>>(
+                radix_downsweep_kernel<false, SORT_ITEMS, SORT_THREADS><<<nb, SORT_THREADS, 0, s>>>(
                     ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
         }
         std::swap(ki, ko);
