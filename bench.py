@@ -416,9 +416,13 @@ def main():
         ms_k = ms_l / cnt_l if (cnt_l and live_ok) else stage_avg[k]
         ach = b / (ms_k * 1e-3) / 1e9 if ms_k > 0 else 0.0
         tr = pmc.get(k, {}).get("hbm_bytes_per_launch")
+        lo = pmc.get(k, {}).get("hbm_bytes_lower")
+        # traffic = (2 FETCH + WRITE): exact for 16-B/lane streams, an upper bound for gathers, which
+        # profiles/calib_fetch.hip shows FETCH counting 1:1 (traffic_lower = FETCH + WRITE)
         return {"stage": k, "avg_launch_ms": round(ms_k, 4), "algorithmic_bytes_per_launch": b,
                 "achieved_GBps": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": tr,
-                "traffic_over_algorithmic": round(tr / b, 3) if (tr and b) else None}
+                "traffic_lower": lo, "traffic_over_algorithmic": round(tr / b, 3) if (tr and b) else None,
+                "traffic_lower_over_algorithmic": round(lo / b, 3) if (lo and b) else None}
 
     d = stage_entry(dom)
     algo_total = sum(stage_bytes(s, P, V, L, N, T, M, g.sh_degree) for s in stage_avg)

@@ -75,8 +75,11 @@ def main():
         rows.append([name, n, round(fk, 1), round(wk, 1), int(hbm)])
         for frag, stage in STAGES.items():
             if frag in name:
+                # lower bound: FETCH counted 1:1, as profiles/calib_fetch.hip measures for random 64-B record
+                # gathers and 4-B gathers (a 64-B request each); the x2 upper bound holds for 16-B/lane streams
                 kernels[stage] = {"kernel": name, "fetch_kib_raw": round(fk, 1), "write_kib": round(wk, 1),
-                                  "hbm_bytes_per_launch": int(hbm), "dispatches": n}
+                                  "hbm_bytes_per_launch": int(hbm), "hbm_bytes_lower": int((fk + wk) * 1024),
+                                  "dispatches": n}
     with open(os.path.join(HERE, f"{tag}_pmc.csv"), "w", newline="") as f:
         w = csv.writer(f)
         w.writerow(["kernel", "dispatches", "FETCH_SIZE_KiB_avg", "WRITE_SIZE_KiB_avg", "hbm_bytes_per_launch"])
