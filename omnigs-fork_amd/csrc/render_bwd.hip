@@ -90,15 +90,23 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
     float dp2[TW_BANDS];
     uint32_t last[TW_BANDS];
     uint32_t band_end[TW_BANDS];  // wave-uniform: max last contributor of the band
-    uint32_t max_c = 0;
+    // the four bands' per-pixel loads are issued together (addresses clamped to pixel 0 outside the image, the
+    // values masked after), so the prologue waits for one round trip per group instead of one per band
+    bool inside[TW_BANDS];
+    uint32_t pix[TW_BANDS];
 #pragma unroll
     for (int b = 0; b < TW_BANDS; ++b) {
         const uint32_t py = tl.py(b);
-        const bool inside = tl.px < (uint32_t)a.W && py < (uint32_t)a.H;
-        const uint32_t pix = a.W * py + tl.px;
-        const uint32_t lc = inside ? a.n_contrib[pix] : 0u;
-        last[b] = lc;
-        band_end[b] = uniform(wave_max_u32(lc));
+        inside[b] = tl.px < (uint32_t)a.W && py < (uint32_t)a.H;
+        pix[b] = inside[b] ? a.W * py + tl.px : 0u;
+    }
+    uint32_t max_c = 0;
+#pragma unroll
+    for (int b = 0; b < TW_BANDS; ++b) last[b] = a.n_contrib[pix[b]];
+#pragma unroll
+    for (int b = 0; b < TW_BANDS; ++b) {
+        last[b] = inside[b] ? last[b] : 0u;
+        band_end[b] = uniform(wave_max_u32(last[b]));
         max_c = max(max_c, band_end[b]);
     }
     const uint2 range = a.ranges[tile];
@@ -108,26 +116,37 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
     const uint32_t seg_lo = max(range.x, chunk * CKPT) - range.x;
     const uint32_t seg_hi = min(range.x + max_c, (chunk + 1) * CKPT) - range.x;
     const bool resume = seg_hi < max_c;  // a boundary inside the list: some pixels blend behind it
+    float Tf[TW_BANDS], d0[TW_BANDS], d1[TW_BANDS], d2[TW_BANDS];
 #pragma unroll
     for (int b = 0; b < TW_BANDS; ++b) {
-        const uint32_t py = tl.py(b);
-        const bool inside = tl.px < (uint32_t)a.W && py < (uint32_t)a.H;
-        const uint32_t pix = a.W * py + tl.px;
-        const float Tf = inside ? a.final_T[pix] : 0.f;
-        const float d0 = inside ? a.dL_dpix[pix] : 0.f;
-        const float d1 = inside ? a.dL_dpix[plane + pix] : 0.f;
-        const float d2 = inside ? a.dL_dpix[2 * plane + pix] : 0.f;
-        dp01[b] = f2v{d0, d1};
-        dp2[b] = d2;
-        T[b] = Tf;
-        s[b] = Tf * (a.bg[0] * d0 + a.bg[1] * d1 + a.bg[2] * d2);
+        Tf[b] = a.final_T[pix[b]];
+        d0[b] = a.dL_dpix[pix[b]];
+        d1[b] = a.dL_dpix[plane + pix[b]];
+        d2[b] = a.dL_dpix[2 * plane + pix[b]];
+    }
+    float4 ck[TW_BANDS];
+    float fc0[TW_BANDS], fc1[TW_BANDS], fc2[TW_BANDS];
+    if (resume) {  // wave-uniform; the checkpoint row (chunk + 1) exists: its boundary lies inside this tile's list
+#pragma unroll
+        for (int b = 0; b < TW_BANDS; ++b) {
+            ck[b] = a.ckpt[(size_t)(chunk + 1) * BLOCK_SIZE + b * 64 + lane];
+            fc0[b] = a.final_C[pix[b]];
+            fc1[b] = a.final_C[plane + pix[b]];
+            fc2[b] = a.final_C[2 * plane + pix[b]];
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < TW_BANDS; ++b) {
+        const float e0 = inside[b] ? d0[b] : 0.f, e1 = inside[b] ? d1[b] : 0.f, e2 = inside[b] ? d2[b] : 0.f;
+        dp01[b] = f2v{e0, e1};
+        dp2[b] = e2;
+        T[b] = inside[b] ? Tf[b] : 0.f;
+        s[b] = T[b] * (a.bg[0] * e0 + a.bg[1] * e1 + a.bg[2] * e2);
         if (resume && last[b] > seg_hi) {
             // the pixel still blends behind the boundary: start from the forward's state there, T in front of the
             // boundary and s = bg . dL/dpix T_final + dL/dpix . (C_final - C in front of the boundary)
-            const float4 ck = a.ckpt[(size_t)(chunk + 1) * BLOCK_SIZE + b * 64 + lane];
-            T[b] = ck.x;
-            s[b] += d0 * (a.final_C[pix] - ck.y) + d1 * (a.final_C[plane + pix] - ck.z) +
-                    d2 * (a.final_C[2 * plane + pix] - ck.w);
+            T[b] = ck[b].x;
+            s[b] += e0 * (fc0[b] - ck[b].y) + e1 * (fc1[b] - ck[b].z) + e2 * (fc2[b] - ck[b].w);
         }
     }
 

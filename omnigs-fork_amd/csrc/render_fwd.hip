@@ -62,6 +62,8 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
     const TileLane tl(tile, a.gx);
     const uint32_t lane = tl.lane;
     const float pxf = (float)tl.px;
+    // read before any store: the compiler cannot prove the stores below miss a.bg and would reload it after each
+    const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
 
     // T carries the pixel's "done" state in its sign: a saturated (or out-of-image) pixel holds -T, so the per-band
     // test is one compare and no bool array lives in VGPRs; |T| is the transmittance
@@ -219,9 +221,9 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
             a.final_C[pix] = C0[b];
             a.final_C[plane + pix] = C1[b];
             a.final_C[2 * plane + pix] = C2[b];
-            a.out_color[pix] = C0[b] + Tf * a.bg[0];
-            a.out_color[plane + pix] = C1[b] + Tf * a.bg[1];
-            a.out_color[2 * plane + pix] = C2[b] + Tf * a.bg[2];
+            a.out_color[pix] = C0[b] + Tf * bg0;
+            a.out_color[plane + pix] = C1[b] + Tf * bg1;
+            a.out_color[2 * plane + pix] = C2[b] + Tf * bg2;
         }
     }
     maxc = wave_max_u32(maxc);

@@ -881,6 +881,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void tile_order_kernel(const uint2* 
 // maps onto XCD blockIdx.x), costs them by their positions below the tile's last contributor and counting-sorts
 // them, longest first.
 constexpr int SCHED_THREADS = 1024;
+constexpr int SCHED_LDS_UNITS = 4096;  // 48 KiB of LDS
 __device__ __forceinline__ uint32_t tile_units(const uint2* ranges, const uint32_t* max_contrib, uint32_t t,
                                                uint32_t* rx, uint32_t* mc_out)
 {
@@ -901,6 +902,8 @@ __global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(const 
     __shared__ uint32_t s_wave[SCHED_THREADS / 64];
     __shared__ uint32_t s_hist[RADIX];
     __shared__ uint32_t s_max;
+    __shared__ uint2 s_units[SCHED_LDS_UNITS];
+    __shared__ uint32_t s_cost[SCHED_LDS_UNITS];
     const uint32_t tid = threadIdx.x;
     // thread tid owns the contiguous tiles [t0, t1): one block scan of the per-thread unit counts (their loads are
     // independent, so all are in flight at once) instead of a scan per 1024 tiles — 2 x T/1024 dependent
@@ -908,6 +911,7 @@ __global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(const 
     const uint32_t per = (T + SCHED_THREADS - 1) / SCHED_THREADS;
     const uint32_t t0 = min(T, tid * per), t1 = min(T, t0 + per);
     uint32_t mine = 0;
+#pragma unroll 4
     for (uint32_t t = t0; t < t1; ++t) {
         uint32_t rx, mc;
         mine += tile_units(ranges, max_contrib, t, &rx, &mc);
@@ -917,6 +921,12 @@ __global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(const 
     // this block's share of [0, total): xcd_remap's split over the 8 XCDs
     const uint32_t q = total / gridDim.x, rem = total % gridDim.x, x = blockIdx.x;
     const uint32_t lo = x * q + min(x, rem), hi = lo + q + (x < rem ? 1u : 0u);
+    // the share's unsorted units and costs: in LDS when they fit (config C: ~3 k units per share), which saves the
+    // global round trips of the three passes below; else in the global scratch
+    const bool in_lds = hi - lo <= (uint32_t)SCHED_LDS_UNITS;  // block-uniform
+    uint2* uu = in_lds ? s_units : units_tmp;
+    uint32_t* cc = in_lds ? s_cost : cost_tmp;
+    const uint32_t ub = in_lds ? lo : 0u;  // index of unit u = u - ub
     if (first0 < hi && first0 + mine > lo) {
         uint32_t first = first0;
         for (uint32_t t = t0; t < t1 && first < hi; ++t) {
@@ -926,24 +936,24 @@ __global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(const 
                 const uint32_t u = first + k;
                 if (u < lo || u >= hi) continue;
                 const uint32_t chunk = rx / CKPT + k;
-                units_tmp[u] = make_uint2(t, chunk);
+                uu[u - ub] = make_uint2(t, chunk);
                 // cost: the segment's positions below the tile's last contributor
-                cost_tmp[u] = min(rx + mc, (chunk + 1) * CKPT) - max(rx, chunk * CKPT);
+                cc[u - ub] = min(rx + mc, (chunk + 1) * CKPT) - max(rx, chunk * CKPT);
             }
             first += c;
         }
     }
     if (tid < RADIX) s_hist[tid] = 0;
     if (tid == 0) s_max = 0;
-    __threadfence();  // the share's entries (written by other threads of this block) before they are read back
+    if (!in_lds) __threadfence();  // the share's entries (written by other threads of this block) before they are read back
     __syncthreads();
     uint32_t mx = 0;
-    for (uint32_t u = lo + tid; u < hi; u += SCHED_THREADS) mx = max(mx, cost_tmp[u]);
+    for (uint32_t u = lo + tid; u < hi; u += SCHED_THREADS) mx = max(mx, cc[u - ub]);
     atomicMax(&s_max, mx);
     __syncthreads();
     const uint64_t scale = (uint64_t)s_max + 1;
     auto bucket = [&](uint32_t u) {  // 0 = costliest
-        return (uint32_t)(RADIX - 1) - (uint32_t)(((uint64_t)cost_tmp[u] * RADIX) / scale);
+        return (uint32_t)(RADIX - 1) - (uint32_t)(((uint64_t)cc[u - ub] * RADIX) / scale);
     };
     for (uint32_t u = lo + tid; u < hi; u += SCHED_THREADS) atomicAdd(&s_hist[bucket(u)], 1u);
     __syncthreads();
@@ -954,7 +964,7 @@ __global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(const 
         if (tid < RADIX) s_hist[tid] = lo + ex;
     }
     __syncthreads();
-    for (uint32_t u = lo + tid; u < hi; u += SCHED_THREADS) units[atomicAdd(&s_hist[bucket(u)], 1u)] = units_tmp[u];
+    for (uint32_t u = lo + tid; u < hi; u += SCHED_THREADS) units[atomicAdd(&s_hist[bucket(u)], 1u)] = uu[u - ub];
     if (x == 0 && tid == 0) *unit_count = total;
 }
 

@@ -72,11 +72,27 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t orig, uint32_t nwg)
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
+// Max over the full wave, on every lane: DPP inside each 16-lane row (quad_perm xor1 / xor2, row_ror 4 / 8), then
+// v_permlane16_swap / v_permlane32_swap across rows (see wave_ops.h: cross_row_sum) — no LDS round trip per level,
+// unlike the ds_bpermute shuffles of __shfl_xor. All 64 lanes must be active.
+template <int CTRL>
+__device__ __forceinline__ uint32_t max_dpp(uint32_t v)
+{
+    return max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, true));
+}
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return v;
+    v = max_dpp<0xb1>(v);   // quad_perm [1,0,3,2]
+    v = max_dpp<0x4e>(v);   // quad_perm [2,3,0,1]
+    v = max_dpp<0x124>(v);  // row_ror:4
+    v = max_dpp<0x128>(v);  // row_ror:8
+    uint32_t a = v, b = v;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    v = max(a, b);
+    a = v;
+    b = v;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    return max(a, b);
 }
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
