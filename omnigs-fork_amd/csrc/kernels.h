@@ -68,7 +68,10 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
 // the words of `hist` a sort of n items over `passes` passes needs zeroed before it starts (possibly none)
 ZeroSpan radix_zero_span(uint32_t* hist, size_t n, int passes);
 // duplicateWithKeys; L_cap = capacity, *count (device) = num_rendered; block_owner: emit_index_size(L_cap) words
-constexpr int EMIT_THREADS = 256;
+#ifndef OMR_EMIT_THREADS
+#define OMR_EMIT_THREADS 256
+#endif
+constexpr int EMIT_THREADS = OMR_EMIT_THREADS;
 #ifndef OMR_EMIT_PER
 #define OMR_EMIT_PER 4
 #endif
