@@ -1,7 +1,7 @@
 """View-parallel training step (trainer.train_step with dist_info) on ONE GPU: 2 ranks over gloo, both on cuda:0
 (the exchange path of bench.py --rehearse). Each rank renders its own view; after the compact exchange every rank
-must take the same Adam step: parameters identical on both ranks, and equal to a single-process step on the summed
-gradients of both views (same kernels, so to within float summation order).
+must take the same Adam step: parameters identical on both ranks, and bitwise equal to a single-process step on the
+summed gradients of both views.
 """
 import os
 import socket
@@ -105,7 +105,7 @@ def test_view_parallel_train_step_replicas_agree_with_summed_views():
         opt.step(raster_grads={k: v.contiguous() for k, v in total.items()})
     torch.cuda.synchronize()
     for k, (p, ref) in enumerate(zip(opt.params(), res[0][0])):
-        # Adam (eps 1e-15) turns rounding-level gradient differences into +-lr moves: compare the moves
-        d_ref = ref - p.detach().cpu().numpy()
-        bad = np.abs(d_ref) > 1e-6 * (1 + np.abs(ref))
-        assert bad.mean() <= 2e-3, (k, int(bad.sum()), bad.size)
+        # bitwise: the compact exchange sums two views exactly as the single process does (all-reduce of two floats;
+        # the SH rebuild equals the sum of the per-view SH gradients bit for bit, tests/test_gpu_parallel.py), and
+        # every kernel is deterministic
+        np.testing.assert_array_equal(ref, p.detach().cpu().numpy(), err_msg=f"parameter group {k}")
