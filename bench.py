@@ -299,7 +299,7 @@ def main():
     if world > 1 and args.exchange == "compact":
         cx = par.CompactExchange(grads, info, campos,
                                  lambda pk, out: R.sh_grad_from_colors_packed(means3D, shs, g.sh_degree, pk, out=out),
-                                 dev, overlap=LT is None)
+                                 dev, overlap=LT is None, any_backend=args.rehearse)
     bwd_kwargs = cx.backward_kwargs() if cx is not None else {}
 
     def exchange():

@@ -141,13 +141,15 @@ class CompactExchange:
     False (e.g. a host that cannot pass the event), it falls back to allreduce_compact_ inside finish()."""
 
     def __init__(self, buf: GradBuffer, info: DistInfo, campos: torch.Tensor, rebuild_packed, device,
-                 overlap: bool = True):
+                 overlap: bool = True, any_backend: bool = False):
         self.buf, self.info, self.rebuild_packed = buf, info, rebuild_packed
         self.campos = campos
         P = buf.P
         buf.out_dict(device)  # creates colors_ext [P + 1, 3]
         buf.colors_ext[P].copy_(campos.reshape(3).to(buf.colors_ext.dtype))
-        self.overlap = bool(overlap and info.enabled and dist.get_backend() == "nccl")
+        # any_backend: also overlap over gloo (ranks sharing one GPU in tests and `bench.py --rehearse`: the same
+        # event / side-stream / collective sequence as over RCCL, with gloo's host copies)
+        self.overlap = bool(overlap and info.enabled and (any_backend or dist.get_backend() == "nccl"))
         if self.overlap:
             self.event = torch.cuda.Event()
             self.comm = torch.cuda.Stream(device)
@@ -161,7 +163,10 @@ class CompactExchange:
             return
         with torch.cuda.stream(self.comm):
             self.comm.wait_event(self.event)
-            dist.all_gather_into_tensor(self.packed_all, self.buf.colors_ext)
+            if dist.get_backend() == "nccl":
+                dist.all_gather_into_tensor(self.packed_all, self.buf.colors_ext)
+            else:  # gloo: list form
+                dist.all_gather(list(self.packed_all.unbind(0)), self.buf.colors_ext)
 
     def finish(self):
         if not self.info.enabled:
