@@ -499,7 +499,12 @@ constexpr int LB_WINDOW = OMR_LB_WINDOW;  // predecessors read per look-back rou
 // scratch words for a sort of n items over `passes` passes: status [passes][blocks][RADIX], digit totals
 // [passes][RADIX], tickets [passes], error word
 constexpr int OS_TILE = SORT_THREADS * 16;                   // keys per onesweep block (smaller tiles measured slower)
-constexpr uint32_t OS_HIST_BLOCKS = 128;             // histogram blocks: each digit total takes <= 128 global adds
+#ifndef OMR_OS_HIST_BLOCKS
+#define OMR_OS_HIST_BLOCKS 256
+#endif
+// histogram blocks: each digit total takes <= this many global adds (64 / 128 / 256 / 512 blocks at 1 M keys:
+// 0.109 / 0.098 / 0.0945 / 0.098 ms for the whole depth sort)
+constexpr uint32_t OS_HIST_BLOCKS = OMR_OS_HIST_BLOCKS;
 // Onesweep only for sorts of at most this many tiles (the depth sort up to 2 M Gaussians: 0.100 vs 0.122 ms at
 // 1 M). Past that the look-back chains and the same-address ticket / histogram adds cost more than the launches
 // they save (the 7.9 M-instance tile sort: 0.185 vs 0.142 ms), and the upsweep / scan / downsweep passes run.
