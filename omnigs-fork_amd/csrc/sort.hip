@@ -498,7 +498,16 @@ constexpr int LB_WINDOW = OMR_LB_WINDOW;  // predecessors read per look-back rou
 
 // scratch words for a sort of n items over `passes` passes: status [passes][blocks][RADIX], digit totals
 // [passes][RADIX], tickets [passes], error word
-constexpr int OS_TILE = SORT_THREADS * 16;                   // keys per onesweep block (smaller tiles measured slower)
+// keys per onesweep block: 4096, or 2048 for sorts of fewer than OS_SMALL_N keys, which then spread over more blocks
+// (config B: depth sort of 100 k keys 0.059 -> 0.050 ms, tile sort of 0.35 M 0.048 -> 0.044; at config C's 1 M-key
+// depth sort 2048-key tiles are slower, 0.110 vs 0.095 ms)
+constexpr int OS_TILE = SORT_THREADS * 16;
+constexpr int OS_TILE_SMALL = SORT_THREADS * 8;
+#ifndef OMR_OS_SMALL_N
+#define OMR_OS_SMALL_N (1u << 19)
+#endif
+constexpr size_t OS_SMALL_N = OMR_OS_SMALL_N;
+__host__ __device__ inline size_t os_tile(size_t n) { return n < OS_SMALL_N ? OS_TILE_SMALL : OS_TILE; }
 #ifndef OMR_OS_HIST_BLOCKS
 #define OMR_OS_HIST_BLOCKS 256
 #endif
@@ -515,7 +524,7 @@ constexpr uint32_t OS_MAX_BLOCKS = OMR_OS_MAX_BLOCKS;
 
 __host__ __device__ inline size_t onesweep_words(size_t n, int passes)
 {
-    const size_t nb = (n + OS_TILE - 1) / OS_TILE;
+    const size_t nb = (n + os_tile(n) - 1) / os_tile(n);
     return (size_t)passes * (nb * RADIX + RADIX + 1) + 1;
 }
 
@@ -552,6 +561,7 @@ __device__ __forceinline__ uint32_t lb_load(const uint32_t* p)
 }
 
 // one pass: status = this pass's [blocks][RADIX] words (zeroed), ghist = its digit totals, ticket = its tile counter
+template <int TILE_N>
 __global__ __launch_bounds__(SORT_THREADS) void onesweep_kernel(const uint32_t* keys_in, const uint32_t* vals_in,
                                                                 uint32_t* keys_out, uint32_t* vals_out, size_t n_cap,
                                                                 const uint32_t* count, char* canon, int shift,
@@ -559,14 +569,14 @@ __global__ __launch_bounds__(SORT_THREADS) void onesweep_kernel(const uint32_t* 
                                                                 uint32_t* ticket, uint32_t* err)
 {
     constexpr int WAVES = SORT_THREADS / 64;
-    constexpr int PER_WAVE = OS_TILE / WAVES;
+    constexpr int PER_WAVE = TILE_N / WAVES;
     constexpr int ROUNDS = PER_WAVE / 64;
     __shared__ uint32_t s_whist[WAVES][RADIX];  // running digit counts per wave, then per-wave digit offsets
     __shared__ uint32_t s_dstart[RADIX];        // block-local start of each digit's run
     __shared__ uint32_t s_gbase[RADIX];         // global start of this block's run of each digit
     __shared__ uint32_t s_wave[SORT_THREADS / 64];
-    __shared__ uint32_t s_k[OS_TILE];
-    __shared__ uint32_t s_v[OS_TILE];
+    __shared__ uint32_t s_k[TILE_N];
+    __shared__ uint32_t s_v[TILE_N];
     __shared__ uint32_t s_vb;
     const uint32_t tid = threadIdx.x;
     if (tid == 0) s_vb = atomicAdd(ticket, 1u);
@@ -577,7 +587,7 @@ __global__ __launch_bounds__(SORT_THREADS) void onesweep_kernel(const uint32_t* 
     for (int q = 0; q < WAVES; ++q) s_whist[q][tid] = 0;
     __syncthreads();
     const uint32_t vb = s_vb;
-    const size_t tile0 = (size_t)vb * OS_TILE;
+    const size_t tile0 = (size_t)vb * TILE_N;
     if (tile0 >= n) return;  // block-uniform; no block looks back at a tile past the live count
     uint32_t total_unused;
     const uint32_t gstart = block_exclusive_scan(ghist[tid], s_wave, &total_unused);  // thread = digit
@@ -666,7 +676,7 @@ __global__ __launch_bounds__(SORT_THREADS) void onesweep_kernel(const uint32_t* 
         }
     }
     __syncthreads();
-    const uint32_t nvalid = (uint32_t)min((size_t)OS_TILE, n - tile0);
+    const uint32_t nvalid = (uint32_t)min((size_t)TILE_N, n - tile0);
     for (uint32_t j = tid; j < nvalid; j += SORT_THREADS) {
         const uint32_t kk = s_k[j];
         const uint32_t d = (kk >> shift) & (RADIX - 1);
@@ -1016,7 +1026,7 @@ size_t radix_hist_size(size_t n) { return (size_t)RADIX * div_up(n, SORT_TILE); 
 #define OMR_ONESWEEP 1
 #endif
 
-static bool use_onesweep(size_t n) { return OMR_ONESWEEP && div_up(n, OS_TILE) <= OS_MAX_BLOCKS; }
+static bool use_onesweep(size_t n) { return OMR_ONESWEEP && div_up(n, os_tile(n)) <= OS_MAX_BLOCKS; }
 
 size_t radix_scratch_words(size_t n, int passes)
 {
@@ -1028,7 +1038,7 @@ ZeroSpan radix_zero_span(uint32_t* hist, size_t n, int passes)
     ZeroSpan z;
     if (n == 0 || passes <= 0 || !use_onesweep(n)) return z;
     // digit totals [passes][RADIX] | tickets [passes] | error word, after the status words
-    z.p = hist + (size_t)passes * div_up(n, OS_TILE) * RADIX;
+    z.p = hist + (size_t)passes * div_up(n, os_tile(n)) * RADIX;
     z.n = (size_t)passes * (RADIX + 1) + 1;
     return z;
 }
@@ -1041,7 +1051,7 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
     uint32_t *ki = key_a, *ko = key_b, *vi = val_a, *vo = val_b;
     int cur = 0;
     if (use_onesweep(n)) {
-        const uint32_t nb = div_up(n, OS_TILE);
+        const uint32_t nb = div_up(n, os_tile(n));
         // scratch: status [passes][nb][RADIX] | ghist [passes][RADIX] | tickets [passes] | error word
         uint32_t* status = hist;
         uint32_t* ghist = hist + (size_t)passes * nb * RADIX;
@@ -1052,9 +1062,10 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
             ki, n, count, first_pass, passes, status, (size_t)passes * nb * RADIX, ghist);
         for (int p = 0; p < passes; ++p) {
             const bool last = p == passes - 1;
-            onesweep_kernel<<<nb, SORT_THREADS, 0, s>>>(ki, vi, ko, vo, n, count, last ? canon : nullptr,
-                                                        (first_pass + p) * RADIX_BITS, status + (size_t)p * nb * RADIX,
-                                                        ghist + (size_t)p * RADIX, tickets + p, err);
+            auto kern = os_tile(n) == OS_TILE ? onesweep_kernel<OS_TILE> : onesweep_kernel<OS_TILE_SMALL>;
+            kern<<<nb, SORT_THREADS, 0, s>>>(ki, vi, ko, vo, n, count, last ? canon : nullptr,
+                                            (first_pass + p) * RADIX_BITS, status + (size_t)p * nb * RADIX,
+                                            ghist + (size_t)p * RADIX, tickets + p, err);
             std::swap(ki, ko);
             std::swap(vi, vo);
             cur ^= 1;
