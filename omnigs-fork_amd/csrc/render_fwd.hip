@@ -33,6 +33,9 @@ namespace {
 #ifndef OMR_FWD_PREFETCH
 #define OMR_FWD_PREFETCH 0
 #endif
+#ifndef OMR_FWD_LESS_SALU
+#define OMR_FWD_LESS_SALU 1
+#endif
 
 OMR_STAMP_DECL(g_stamps_fwd)
 
@@ -172,7 +175,13 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
                 const float dy = dy0 - (float)(4 * b);
                 const float p2 = falloff_p2(kq, dy);
                 const bool live = T[b] > 0.0f;
+#if OMR_FWD_LESS_SALU
+                // a done pixel (T < 0) may evaluate: its test_T is negative, so sat holds, wgt = 0, T keeps -|T| and
+                // `last` stays (wgt > 0 below) — the same results with one scalar AND less per band
+                bool ok = p2 <= 0.0f && p2 >= pfloor;  // alpha >= 1/255 (tile_wave.h: p2_floor)
+#else
                 bool ok = live && p2 <= 0.0f && p2 >= pfloor;  // alpha >= 1/255 (tile_wave.h: p2_floor)
+#endif
                 // a lane that is not ok gets alpha = 0: test_T = T, wgt = 0
                 const float alpha = fminf(0.99f, qo.w * __builtin_amdgcn_exp2f(ok ? p2 : -__builtin_inff()));
                 const float test_T = T[b] * (1.0f - alpha);
@@ -182,13 +191,18 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
                 // newly saturated = live && sat (a live lane that is not ok keeps test_T = T >= 1e-4); two ballots of
                 // plain compares stay in SGPRs, a ballot of their conjunction goes through a VGPR
                 sat_any |= __ballot(live) & __ballot(sat);
-                ok = ok && !sat;
                 const float wgt = sat ? 0.0f : alpha * T[b];
                 C0[b] = __builtin_fmaf(f.x, wgt, C0[b]);
                 C1[b] = __builtin_fmaf(f.y, wgt, C1[b]);
                 C2[b] = __builtin_fmaf(f.z, wgt, C2[b]);
                 T[b] = sat ? -fabsf(T[b]) : test_T;  // done: keeps the last live T, negated
+#if OMR_FWD_LESS_SALU
+                // blended iff wgt > 0: alpha >= 1/255 and T >= 1e-4 make wgt >= 3.9e-7 on every contributing lane
+                last[b] = wgt > 0.0f ? contributor : last[b];
+#else
+                ok = ok && !sat;
                 last[b] = ok ? contributor : last[b];
+#endif
             }
             if (sat_any) {  // some pixel saturated: drop bands with no live pixel left
 #pragma unroll
