@@ -224,7 +224,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
                 const float dy = dy0 - (float)(4 * b);
                 const float p2 = falloff_p2(kq, dy);
                 // backward.cu:770-781: skip positions at/after the pixel's last contributor, power > 0, alpha < 1/255
-                const bool contrib = ipos < lastb && p2 <= 0.0f && p2 >= pfloor;
+                const bool contrib = ipos < lastb && p2_in_band(p2, pfloor);
                 BWD_COUNT(1, 1);
                 if (!__ballot(contrib)) continue;
                 BWD_COUNT(2, 1);

@@ -73,7 +73,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
     float T[FWD_BANDS], C0[FWD_BANDS], C1[FWD_BANDS], C2[FWD_BANDS];
     uint32_t last[FWD_BANDS];
     uint32_t active = 0;  // local bands with at least one unsaturated in-image pixel (wave-uniform)
-    uint32_t work = 0;    // (instance, band) pairs evaluated: the backward's schedule key
+    uint32_t work = 0;    // (instance, band) pairs staged for evaluation (omr_debug_tile_cost, bench.py's VALU secondary)
 #pragma unroll
     for (int b = 0; b < FWD_BANDS; ++b) {
         const bool inside = tl.px < (uint32_t)a.W && tl.py(band0 + b) < (uint32_t)a.H;
@@ -139,6 +139,10 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
         // the state at a boundary = after every instance in front of it (this batch has not blended yet)
         store_ckpt(start);
         const uint64_t useful = __ballot(m != 0);
+        // counted per batch from the staging masks (two scalar ops per instance less in the blend loop); a band that
+        // saturates inside the batch is still counted for the batch's later instances
+#pragma unroll
+        for (int b = 0; b < FWD_BANDS; ++b) work += (uint32_t)__popcll(__ballot((m >> b) & 1u));
         if (m != 0) {
             const uint32_t r = mask_rank(useful);
             const Quad q = quad_of_conic(co);
@@ -162,7 +166,6 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
 #endif
             const float pfloor = s_floor[j];
             const uint32_t mb = uniform(__builtin_bit_cast(uint32_t, g.w)) & active;
-            work += (uint32_t)__builtin_popcount(mb);
             const uint32_t contributor = __builtin_bit_cast(uint32_t, g.z) + 1u;
             const Quad q = {qo.x, qo.y, qo.z};
             const float dx = g.x - pxf;
@@ -178,9 +181,9 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
 #if OMR_FWD_LESS_SALU
                 // a done pixel (T < 0) may evaluate: its test_T is negative, so sat holds, wgt = 0, T keeps -|T| and
                 // `last` stays (wgt > 0 below) — the same results with one scalar AND less per band
-                bool ok = p2 <= 0.0f && p2 >= pfloor;  // alpha >= 1/255 (tile_wave.h: p2_floor)
+                bool ok = p2_in_band(p2, pfloor);  // alpha >= 1/255 (tile_wave.h: p2_floor)
 #else
-                bool ok = live && p2 <= 0.0f && p2 >= pfloor;  // alpha >= 1/255 (tile_wave.h: p2_floor)
+                bool ok = live && p2_in_band(p2, pfloor);  // alpha >= 1/255 (tile_wave.h: p2_floor)
 #endif
                 // a lane that is not ok gets alpha = 0: test_T = T, wgt = 0
                 const float alpha = fminf(0.99f, qo.w * __builtin_amdgcn_exp2f(ok ? p2 : -__builtin_inff()));

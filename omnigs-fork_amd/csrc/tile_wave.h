@@ -47,7 +47,26 @@ __device__ __forceinline__ float falloff_p2(const ColQuad& k, float dy)
 // p2 <= 0 && p2 >= p2_floor BEFORE v_exp_f32 and feed v_exp -inf for a pixel that does not contribute, so G, alpha
 // and every product built from them are exactly 0 there without per-result selects. v_log_f32 is within an ulp,
 // so the boundary moves by < 1e-6 relative in alpha (the same class as v_exp_f32 vs expf).
-__device__ __forceinline__ float p2_floor(float opacity) { return -__builtin_amdgcn_logf(255.0f * opacity); }
+// Clamped to <= 0: instances with 255 o < 1 are never staged (band_mask is 0 for them), and the clamp keeps the
+// in_band test below exact for every staged one.
+__device__ __forceinline__ float p2_floor(float opacity)
+{
+    return fminf(-__builtin_amdgcn_logf(255.0f * opacity), 0.0f);
+}
+// p2 <= 0 && p2 >= floor as ONE vector compare (floor <= 0): v_med3 returns one of its inputs, and p2 itself exactly
+// when it lies in [floor, 0]; a NaN p2 compares unequal. Two v_cmp and an s_and otherwise — the scalar unit is the
+// render forward's tighter issue port.
+#ifndef OMR_MED3_TEST
+#define OMR_MED3_TEST 1
+#endif
+__device__ __forceinline__ bool p2_in_band(float p2, float floor)
+{
+#if OMR_MED3_TEST
+    return __builtin_amdgcn_fmed3f(p2, floor, 0.0f) == p2;
+#else
+    return p2 <= 0.0f && p2 >= floor;
+#endif
+}
 
 // one lane's view of a tile: pixel coordinates of its band pixels; band b of the tile = rows 4b..4b+3
 struct TileLane {
