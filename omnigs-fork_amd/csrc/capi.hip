@@ -575,6 +575,7 @@ int backward_impl(const BackwardIn& in)
     ga.focal_x = (float)in.width / (2.0f * in.tan_fovx);
     ga.clamped = g.clamped;
     ga.row_sums = g.row_sums;
+    ga.splat = g.splat;
     { StageScope st_(ST_ROW_SUMS, s); launch_row_sums(in.P, g.row_first, g.tiles_touched, g.huge_list, g.counters + 2, b.inst_grad, b.row_valid, (uint32_t)in.R, g.row_sums, in.dL_dcolor, s); }
     if (colors_event) OMR_HIP(hipEventRecord(colors_event, s));  // dL_dcolor is final from here on
     ga.dL_dmean2D = in.dL_dmean2D; ga.dL_dconic = in.dL_dconic; ga.dL_dopacity = in.dL_dopacity; ga.dL_dcolor = in.dL_dcolor;

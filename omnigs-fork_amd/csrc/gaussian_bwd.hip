@@ -15,6 +15,7 @@
 // rasterize_points.cu:200-208).
 #include "kernels.h"
 #include "sh_eval.h"
+#include "tile_wave.h"
 #include "wave_ops.h"
 #include "wave_rows.h"
 
@@ -648,9 +649,11 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
     if (wave_first >= a.P) return;  // wave-uniform
     const int idx = wave_first + (int)lane;
     float g[GRAD_ROW];
+    float4 co = make_float4(0.f, 0.f, 0.f, 0.f);  // conic + opacity of the render record (raw-moment rows)
     if (idx < a.P) {
 #pragma unroll
         for (int c = 0; c < GRAD_ROW; ++c) g[c] = a.row_sums[(size_t)idx * GRAD_ROW + c];
+        if (OMR_BWD_RAW_MOMENTS) co = a.splat[(size_t)idx * SPLAT_F4 + 1];
     }
     const bool valid = idx < a.P;
     const bool vis = valid && a.radii[idx] > 0;
@@ -666,7 +669,10 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
             wave_sync();
         }
     }
-    if (vis) gaussian_bwd_point<CAM, MC>(a, idx, g, sh4, dsh4);
+    if (vis) {
+        if (OMR_BWD_RAW_MOMENTS) raw_row_to_grads(g, co, a.W, a.H);
+        gaussian_bwd_point<CAM, MC>(a, idx, g, sh4, dsh4);
+    }
     else if (valid) gaussian_bwd_culled<MC>(a, idx, dsh4);
     if constexpr (STAGED) {
         if (a.dL_dsh) {

@@ -36,8 +36,15 @@ constexpr int SCAN_ITEMS = 16;
 constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
 
 // per-instance gradient row written by the render backward (render_bwd.hip) and reduced per Gaussian
-// (gaussian_bwd.hip): dmean2D.x, dmean2D.y, dconic.x, dconic.y, dconic.w, dopacity, dcolor.rgb
+// (gaussian_bwd.hip). With OMR_BWD_RAW_MOMENTS (default) the row holds the instance's raw pixel-weight moments
+// S_u dx, S_u dy, S_u dx^2, S_u dx dy, S_u dy^2, S_u, then dcolor.rgb: every factor of backward.cu:805-840 that is
+// the same for all of a Gaussian's instances (conic, opacity, W/2, H/2) is applied once to the Gaussian's sums by
+// gaussian_bwd (raw_row_to_grads), not once per instance. Without it: dmean2D.x, dmean2D.y, dconic.x, dconic.y,
+// dconic.w, dopacity, dcolor.rgb.
 constexpr int GRAD_ROW = 9;
+#ifndef OMR_BWD_RAW_MOMENTS
+#define OMR_BWD_RAW_MOMENTS 1
+#endif
 // a Gaussian touching more tiles than this gets a whole workgroup for its row sums (gaussian_bwd.hip); the
 // forward's scan lists these Gaussians (sort.hip: scan2_downsweep_kernel)
 constexpr uint32_t ROW_SUM_HUGE = 256;

@@ -15,8 +15,9 @@
 // (a lane's four pixels share one column, so only S_u, S_u dy, S_u dy^2 are summed per band; the x-moments are
 // their dx-multiples)
 // The per-Gaussian constants of the reference's expressions (conic, opacity, 0.5 W, 0.5 H, -1/2) are linear
-// factors, so they are applied once per instance to the lane's sums — not once per pixel — and the nine values
-// are then summed over the wave: eight transposed through LDS, the ninth by v_permlane{16,32}_swap + DPP (wave_ops.h).
+// factors that every instance of the Gaussian shares, so they are applied neither per pixel nor per instance but
+// once to the Gaussian's summed rows (raster_common.h: OMR_BWD_RAW_MOMENTS); the nine values of an instance are
+// summed over the wave: eight transposed through LDS, the ninth by v_permlane{16,32}_swap + DPP (wave_ops.h).
 // Lanes 0..8 store the instance's 36-B gradient row, indexed by its row slot (Gaussian-index-major: row_first), with
 // plain stores, and lane 0 marks the slot in row_valid (zeroed before the launch); an instance no pixel takes a contribution from writes
 // nothing — at dense configs most instances lie behind every pixel's last contributor. gaussian_bwd.hip sums each
@@ -59,7 +60,12 @@ __device__ unsigned long long g_bwd_counts[5];
 #define OMR_BWD_ROWS_RED 2
 #endif
 
-__global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel(RenderBwdArgs a)
+#ifdef OMR_BWD_WPE
+#define OMR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(OMR_BWD_WPE)))
+#else
+#define OMR_BWD_ATTR
+#endif
+__global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) OMR_BWD_ATTR void render_bwd_kernel(RenderBwdArgs a)
 {
     OMR_STAMP_BEGIN
     __shared__ float4 s_geo_all[TW_WAVES][TW_BATCH];   // x, y, position in range (u32 bits), band mask (u32 bits)
@@ -152,8 +158,10 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
 
     // instances behind every pixel's last contributor get no row (row_valid stays 0 for them)
 
+#if !OMR_BWD_RAW_MOMENTS
     // ddelx_dx, ddely_dy (backward.cu:700-701) = W/2, H/2, with the 2 / log2(e) of the staged conic folded in
     const float kx = (float)a.W / LOG2E, ky = (float)a.H / LOG2E;
+#endif
 #if !OMR_BWD_ROWS_RED
     const uint32_t slot_of_lane = transposed_slot_of_lane(lane);
 #endif
@@ -252,19 +260,25 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
             if (!any) continue;  // no pixel took a contribution: no row
             BWD_COUNT(3, 1);
             if (lane == 0) a.row_valid[slot_j] = 1;
-            // per-instance factors of backward.cu:805-840 (dG/ddelx = -G (dx a + dy b), ...). With the staged
-            // quadratic form q = (-a/2, -b, -c/2) log2(e):  -(a sux + b suy) = (2 / log2 e) (qa sux + qb/2 suy),
-            // so dL/dmean2D.x = o W/2 (2 / log2 e) (qa sux + qb/2 suy), likewise y with (qc, qb/2) and H/2
-            const float o = qo.w;
             const float su = s_uy.x, suy = s_uy.y;
             const float sux = su * dx, suxx = sux * dx, suxy = suy * dx;
-            const float hb = 0.5f * q.qb, mo = -0.5f * o;
             float v[8];
+#if OMR_BWD_RAW_MOMENTS
+            // the raw moments: their per-Gaussian factors are applied once to the Gaussian's sums (raw_row_to_grads)
+            v[0] = sux;
+            v[1] = suy;
+            v[2] = suxx;
+            v[3] = suxy;
+            v[4] = suyy;
+#else
+            const float o = qo.w;
+            const float hb = 0.5f * q.qb, mo = -0.5f * o;
             v[0] = (o * kx) * __builtin_fmaf(q.qa, sux, hb * suy);  // dL/dmean2D.x
             v[1] = (o * ky) * __builtin_fmaf(q.qc, suy, hb * sux);  // dL/dmean2D.y
             v[2] = mo * suxx;                                        // dL/dconic.x
             v[3] = mo * suxy;                                        // dL/dconic.y (the reference's half-weight slot)
             v[4] = mo * suyy;                                        // dL/dconic.w
+#endif
             v[5] = su;                                         // dL/dopacity
             v[6] = sc01.x;                                     // dL/dcolour
             v[7] = sc01.y;

@@ -68,6 +68,23 @@ __device__ __forceinline__ bool p2_in_band(float p2, float floor)
 #endif
 }
 
+// The per-Gaussian factors of backward.cu:805-840 applied to a Gaussian's summed raw moments g[0..5] = S_u dx,
+// S_u dy, S_u dx^2, S_u dx dy, S_u dy^2, S_u (OMR_BWD_RAW_MOMENTS rows): dG/ddelx = -G (a dx + b dy), ... With the
+// staged quadratic form q = (-a/2, -b, -c/2) log2(e):  -(a S_ux + b S_uy) = (2 / log2 e) (qa S_ux + qb/2 S_uy), so
+// dL/dmean2D.x = o W/2 (2 / log2 e) (qa S_ux + qb/2 S_uy), likewise y with (qc, qb/2) and H/2; dL/dconic = -o/2 x
+// the second moments (the reference's half-weight dconic.y slot); dL/dopacity = S_u. In place.
+__device__ __forceinline__ void raw_row_to_grads(float (&g)[9], float4 co, int W, int H)
+{
+    const Quad q = quad_of_conic(co);
+    const float o = co.w, kx = (float)W / LOG2E, ky = (float)H / LOG2E;
+    const float sux = g[0], suy = g[1], hb = 0.5f * q.qb, mo = -0.5f * o;
+    g[0] = (o * kx) * __builtin_fmaf(q.qa, sux, hb * suy);
+    g[1] = (o * ky) * __builtin_fmaf(q.qc, suy, hb * sux);
+    g[2] = mo * g[2];
+    g[3] = mo * g[3];
+    g[4] = mo * g[4];
+}
+
 // one lane's view of a tile: pixel coordinates of its band pixels; band b of the tile = rows 4b..4b+3
 struct TileLane {
     uint32_t tx, ty, lane;
