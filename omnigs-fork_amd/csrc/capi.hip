@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/omnigs_raster.h"
@@ -99,6 +100,9 @@ enum Stage { ST_PREPROCESS, ST_DEPTH_SORT, ST_SCAN, ST_EMIT, ST_TILE_SORT, ST_RA
 const char* kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "scan", "emit", "tile_sort", "tile_ranges",
                                      "render_forward", "render_backward", "gaussian_backward", "row_sums"};
 
+#ifndef OMR_EXT_STAGE_EVENTS
+#define OMR_EXT_STAGE_EVENTS 1
+#endif
 // Diagnostic (bench.py, tests): one process-wide profiler, guarded by a mutex; its events belong to the device that
 // was current when they were created, so profile one device per process.
 struct Profiler {
@@ -120,34 +124,49 @@ struct Profiler {
             pool.pop_back();
             return e;
         }
+        // timing only: no system-scope fence (an L2 writeback + invalidate, about 5 us of GPU idle per event)
         hipEvent_t e = nullptr;
-        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&e, OMR_EXT_STAGE_EVENTS ? hipEventDisableSystemFence : hipEventDefault) != hipSuccess)
+            return nullptr;
         return e;
     }
 };
 Profiler g_prof;
 
+// A stage of several launches is bracketed by two event records. Each is a marker packet whose system-scope release
+// writes back the L2 (about 6 us of GPU idle at config C, profiles/gaps.py), so a single-kernel stage (single = true)
+// instead hands its pair to the launch (start(), stop()), which attaches it to the dispatch packet
+// (hipExtLaunchKernelGGL): the timed pass that measures the roofline kernel then costs no idle time.
 struct StageScope {
     int stage;
     hipStream_t s;
-    hipEvent_t a = nullptr;
-    StageScope(int st, hipStream_t stream) : stage(st), s(stream)
+    bool single;
+    hipEvent_t a = nullptr, b = nullptr;
+    StageScope(int st, hipStream_t stream, bool single_kernel = false)
+        : stage(st), s(stream), single(single_kernel && OMR_EXT_STAGE_EVENTS)
     {
         if (g_prof.on && (g_prof.mask >> st) & 1u) {
             std::lock_guard<std::mutex> lk(g_prof.mu);
             a = g_prof.get();
-            if (a) (void)hipEventRecord(a, s);
+            if (a && single) {
+                b = g_prof.get();
+                if (!b) a = nullptr;
+            } else if (a) {
+                (void)hipEventRecord(a, s);
+            }
         }
     }
+    hipEvent_t start() const { return single ? a : nullptr; }
+    hipEvent_t stop() const { return single ? b : nullptr; }
     ~StageScope()
     {
         if (a) {
             std::lock_guard<std::mutex> lk(g_prof.mu);
-            hipEvent_t b = g_prof.get();
-            if (b) {
-                (void)hipEventRecord(b, s);
-                g_prof.pending.push_back({stage, a, b});
+            if (!single) {
+                b = g_prof.get();
+                if (b) (void)hipEventRecord(b, s);
             }
+            if (b) g_prof.pending.push_back({stage, a, b});
         }
     }
 };
@@ -156,10 +175,73 @@ struct StageScope {
 // stream, and an event can only be recorded on a stream of the device it was created on.
 //   words[0..3] <- counters[0..3] after the forward's scan (num_rendered, prefiltered flag, huge count, error word)
 //   words[4]    <- counters[3] at the start of the backward (look-back errors of the forward's back half)
+//   words[6], words[7]: the sequence numbers written after them (HostRead)
+// The words the host reads back (num_rendered etc.) are written by the GPU straight into pinned fine-grained memory
+// with system-scope stores by the first wave of a kernel that runs anyway, followed by a sequence number the host
+// spins on (kernels.h: HostWords): no blit kernel and no event. Either of those costs a dispatch and ends in a
+// system-scope release that writes back the L2 — about 5 us of GPU idle each at config C (profiles/gaps.py).
+// OMR_HOST_WORDS_KERNEL=0: hipMemcpyAsync + event record + event wait.
+#ifndef OMR_HOST_WORDS_KERNEL
+#define OMR_HOST_WORDS_KERNEL 1
+#endif
+// one host read-back: data words + the sequence word the GPU writes after them
+struct HostRead {
+    uint32_t* host;       // data, host address
+    uint32_t* dev;        // data, device address
+    uint32_t* seq_host;   // sequence word
+    uint32_t* seq_dev;
+    uint32_t seq = 0;     // last value requested
+    hipEvent_t ev = nullptr;  // OMR_HOST_WORDS_KERNEL=0 only
+};
+
+// Requests src_dev[0..n) into r's words. Returns what the next launch that carries host words (emit_index,
+// backward_schedule) must write, or dst == NULL when the request is already queued (copy + event, or own kernel).
+HostWords read_to_host(HostRead& r, const uint32_t* src_dev, int n, hipStream_t s, bool own_kernel, hipError_t* err)
+{
+    HostWords h;
+    *err = hipSuccess;
+    if (!OMR_HOST_WORDS_KERNEL) {
+        *err = hipMemcpyAsync(r.host, src_dev, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+        if (*err == hipSuccess) *err = hipEventRecord(r.ev, s);
+        return h;
+    }
+    h.dst = r.dev;
+    h.src = src_dev;
+    h.n = n;
+    h.seq_dst = r.seq_dev;
+    h.seq = ++r.seq;
+    if (own_kernel) {
+        launch_host_words(h, s);
+        *err = hipGetLastError();
+        h.dst = nullptr;
+    }
+    return h;
+}
+
+// waits for the words of the last read_to_host. The stream is queried only after 50 ms of polling (a stream
+// query enqueues a marker, which costs the GPU the same idle time as an event): it fails the wait if the stream
+// reports an error or has drained without the words.
+hipError_t wait_host_read(const HostRead& r, hipStream_t s)
+{
+    if (!OMR_HOST_WORDS_KERNEL) return hipEventSynchronize(r.ev);
+    const auto t0 = std::chrono::steady_clock::now();
+    uint32_t polls = 0;
+    while (__atomic_load_n(r.seq_host, __ATOMIC_ACQUIRE) != r.seq) {
+        if ((++polls & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q != hipSuccess && q != hipErrorNotReady) return q;
+            if (q == hipSuccess && __atomic_load_n(r.seq_host, __ATOMIC_ACQUIRE) != r.seq) return hipErrorUnknown;
+            std::this_thread::sleep_for(std::chrono::microseconds(100));
+        }
+    }
+    return hipSuccess;
+}
+
 struct HostSlots {
     int device = -1;
     uint32_t* words = nullptr;
-    hipEvent_t ev_count = nullptr, ev_bwd = nullptr;
+    uint32_t* words_dev = nullptr;  // the same words as the device addresses them
+    HostRead fwd, bwd;              // words[0..3] | words[4], sequence words[6] | words[7]
 };
 
 int stream_device(hipStream_t s)
@@ -184,9 +266,22 @@ HostSlots* host_slots(hipStream_t s)
     if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
     HostSlots h;
     h.device = dev;
-    const bool ok = hipHostMalloc(reinterpret_cast<void**>(&h.words), 8 * sizeof(uint32_t), hipHostMallocPortable) == hipSuccess &&
-                    hipEventCreateWithFlags(&h.ev_count, hipEventDisableTiming) == hipSuccess &&
-                    hipEventCreateWithFlags(&h.ev_bwd, hipEventDisableTiming) == hipSuccess;
+    const bool ok = hipHostMalloc(reinterpret_cast<void**>(&h.words), 8 * sizeof(uint32_t),
+                                  hipHostMallocPortable | hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess &&
+                    hipHostGetDevicePointer(reinterpret_cast<void**>(&h.words_dev), h.words, 0) == hipSuccess &&
+                    hipEventCreateWithFlags(&h.fwd.ev, hipEventDisableTiming) == hipSuccess &&
+                    hipEventCreateWithFlags(&h.bwd.ev, hipEventDisableTiming) == hipSuccess;
+    if (ok) {
+        std::memset(h.words, 0, 8 * sizeof(uint32_t));
+        h.fwd.host = h.words;
+        h.fwd.dev = h.words_dev;
+        h.fwd.seq_host = h.words + 6;
+        h.fwd.seq_dev = h.words_dev + 6;
+        h.bwd.host = h.words + 4;
+        h.bwd.dev = h.words_dev + 4;
+        h.bwd.seq_host = h.words + 7;
+        h.bwd.seq_dev = h.words_dev + 7;
+    }
     if (cur != dev) (void)hipSetDevice(cur);
     if (!ok) return nullptr;
     slots.push_back(h);
@@ -202,10 +297,10 @@ std::atomic<uint64_t> g_rt[RS_COUNT];
 void rt_add(int k, uint64_t v) { g_rt[k].fetch_add(v, std::memory_order_relaxed); }
 
 // host wait on an event, timed into a runtime counter
-hipError_t timed_event_sync(hipEvent_t e, int stat)
+hipError_t timed_wait(const HostRead& hr, hipStream_t s, int stat)
 {
     const auto t0 = std::chrono::steady_clock::now();
-    const hipError_t r = hipEventSynchronize(e);
+    const hipError_t r = wait_host_read(hr, s);
     rt_add(stat, (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
     return r;
 }
@@ -410,12 +505,14 @@ int forward_impl(const ForwardIn& in)
     HostSlots* hs = host_slots(s);
     if (!hs) return fail(OMR_ERR_HIP, "pinned host memory / event allocation failed");
     uint32_t* host = hs->words;
-    hipEvent_t ev_count = hs->ev_count;
     const uint32_t* count_dev = g.counters;  // {num_rendered, -, -, error word}: raster_common.h binning_count
     // one copy: num_rendered (scan), prefiltered flag (preprocess; meaningful only when prefiltered is set), huge
     // count, look-back error word (depth sort, scan)
-    OMR_HIP(hipMemcpyAsync(host, g.counters, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    OMR_HIP(hipEventRecord(ev_count, s));
+    hipError_t rerr;
+    // carried by the back half's first kernel; on the first call for a view shape (the count is needed before the
+    // back half is sized) by its own kernel
+    HostWords count_words = read_to_host(hs->fwd, g.counters, 4, s, capacity_hint(in.width, in.height, in.camera_type) == 0, &rerr);
+    OMR_HIP(rerr);
     rt_add(RS_FORWARDS, 1);
 
     const int tile_passes = tile_sort_passes(d.T);
@@ -423,7 +520,7 @@ int forward_impl(const ForwardIn& in)
     bool known = false;
     size_t L = 0;
     auto wait_count = [&]() -> int {
-        OMR_HIP(timed_event_sync(ev_count, RS_COUNT_WAIT_NS));
+        OMR_HIP(timed_wait(hs->fwd, s, RS_COUNT_WAIT_NS));
         if (int e = hip_check("preprocess/sort/scan")) return e;
         if (in.prefiltered && host[1] != 0)
             return fail(OMR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
@@ -450,7 +547,7 @@ int forward_impl(const ForwardIn& in)
         if (!bin_base) return fail(OMR_ERR_ALLOCATION, "binning allocation failed");
         BinningState b;
         BinningState::carve(bin_base, capacity, d.T, &b);
-        { StageScope st_(ST_EMIT, s); launch_emit_instances(in.P, capacity, count_dev, g, d.gx, b.block_owner, b.key_a, b.val_a, bin_base, s); }
+        { StageScope st_(ST_EMIT, s); launch_emit_instances(count_words, in.P, capacity, count_dev, g, d.gx, b.block_owner, b.key_a, b.val_a, bin_base, s); }
         {
             StageScope st_(ST_TILE_SORT, s);
             radix_sort_pairs(b.key_a, b.key_b, b.val_a, b.val_b, b.hist, b.scan_partials, capacity, count_dev,
@@ -537,8 +634,9 @@ int backward_impl(const BackwardIn& in)
     HostSlots* hs = host_slots(s);
     if (!hs) return fail(OMR_ERR_HIP, "pinned host memory / event allocation failed");
     hs->words[4] = 0;
-    OMR_HIP(hipMemcpyAsync(hs->words + 4, g.counters + 3, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    OMR_HIP(hipEventRecord(hs->ev_bwd, s));
+    hipError_t rerr;
+    HostWords err_words = read_to_host(hs->bwd, g.counters + 3, 1, s, in.R == 0, &rerr);  // carried by backward_schedule
+    OMR_HIP(rerr);
 
     const size_t R = (size_t)in.R;
     char* const lb = in.binning_buffer;  // the L-indexed region (raster_common.h), at offsets of R
@@ -558,12 +656,12 @@ int backward_impl(const BackwardIn& in)
     // (tile, depth segment) units, costliest first per XCD share (outside the render_backward stage, so the stage,
     // the bench's roofline duration and the rocprofv3 kernel average all time render_bwd_kernel alone)
     if (R > 0)
-        launch_backward_schedule(im.ranges, im.max_contrib, d.T, reinterpret_cast<uint2*>(lb + units_tmp_offset(R, d.T)),
+        launch_backward_schedule(err_words, im.ranges, im.max_contrib, d.T, reinterpret_cast<uint2*>(lb + units_tmp_offset(R, d.T)),
                                  reinterpret_cast<uint32_t*>(lb + units_tmp_offset(R, d.T) + seg_count(R, d.T) * 8),
                                  units, unit_count, s);
     {
-        StageScope st_(ST_RENDER_BWD, s);
-        if (R > 0) launch_render_backward(rb, seg_count(R, d.T), s);
+        StageScope st_(ST_RENDER_BWD, s, true);
+        if (R > 0) launch_render_backward(rb, seg_count(R, d.T), s, st_.start(), st_.stop());
     }
 
     GaussBwdArgs ga;
@@ -582,9 +680,9 @@ int backward_impl(const BackwardIn& in)
     ga.dL_dmean3D = in.dL_dmean3D; ga.dL_dcov3D = in.dL_dcov3D; ga.dL_dsh = in.M > 0 ? in.dL_dsh : nullptr;
     ga.dL_dscale = in.dL_dscale; ga.dL_drot = in.dL_drot; ga.dpx_dt = in.dpx_dt; ga.dpy_dt = in.dpy_dt;
     if (!in.shs) ga.shs = nullptr;
-    { StageScope st_(ST_GAUSS_BWD, s); launch_gaussian_backward(in.camera_type, ga, s); }
+    { StageScope st_(ST_GAUSS_BWD, s, true); launch_gaussian_backward(in.camera_type, ga, s, st_.start(), st_.stop()); }
     if (int e = hip_check("backward")) return e;
-    OMR_HIP(timed_event_sync(hs->ev_bwd, RS_BWD_WAIT_NS));
+    OMR_HIP(timed_wait(hs->bwd, s, RS_BWD_WAIT_NS));
     if (hs->words[4] != 0) {
         rt_add(RS_LOOKBACK_ERRORS, 1);
         return fail(OMR_ERR_HIP, "forward tile sort: a decoupled look-back gave up waiting for a predecessor");

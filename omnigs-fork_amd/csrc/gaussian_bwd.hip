@@ -793,19 +793,17 @@ void launch_row_sums(int P, const uint32_t* row_first, const uint32_t* tiles_tou
     row_sum_kernel<<<a.main_blocks + RS_HUGE_BLOCKS, 256, 0, s>>>(a);
 }
 
-void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s)
+void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s, hipEvent_t ev_start,
+                              hipEvent_t ev_stop)
 {
     if (a.P <= 0) return;
     const dim3 grid(div_up(a.P, 256));
     const bool m16 = a.M == 16 && (reinterpret_cast<uintptr_t>(a.dL_dsh) % 16) == 0 &&
                      (reinterpret_cast<uintptr_t>(a.shs) % 16) == 0;
-    if (camera_type == CAM_LONLAT) {
-        if (m16) gaussian_bwd_kernel<CAM_LONLAT, 16><<<grid, 256, 0, s>>>(a);
-        else gaussian_bwd_kernel<CAM_LONLAT, 0><<<grid, 256, 0, s>>>(a);
-    } else {
-        if (m16) gaussian_bwd_kernel<CAM_PINHOLE, 16><<<grid, 256, 0, s>>>(a);
-        else gaussian_bwd_kernel<CAM_PINHOLE, 0><<<grid, 256, 0, s>>>(a);
-    }
+    auto k = camera_type == CAM_LONLAT ? (m16 ? gaussian_bwd_kernel<CAM_LONLAT, 16> : gaussian_bwd_kernel<CAM_LONLAT, 0>)
+                                       : (m16 ? gaussian_bwd_kernel<CAM_PINHOLE, 16> : gaussian_bwd_kernel<CAM_PINHOLE, 0>);
+    if (ev_start || ev_stop) hipExtLaunchKernelGGL(k, grid, dim3(256), 0, s, ev_start, ev_stop, 0, a);
+    else k<<<grid, 256, 0, s>>>(a);
 }
 
 }  // namespace omr

@@ -3,6 +3,8 @@
 
 #include <string>
 
+#include <hip/hip_ext.h>
+
 #include "raster_common.h"
 
 namespace omr {
@@ -79,7 +81,28 @@ constexpr int EMIT_PER = OMR_EMIT_PER;                // consecutive instance sl
 constexpr int EMIT_SLOTS = EMIT_THREADS * EMIT_PER;   // slots per emit block (block_owner granularity)
 size_t emit_index_size(size_t L_cap);
 // also zeroes the backward's row_valid bytes at binning + row_valid_offset(L)
-void launch_emit_instances(int P, size_t L_cap, const uint32_t* count, const GeomState& g, uint32_t gx,
+// Words the host reads back (capi.hip: HostRead): src[0..n) into pinned fine-grained memory at dst, then seq into
+// seq_dst once they are acknowledged, with system-scope vector stores. Written by the first wave of a kernel that runs
+// anyway (emit_index, backward_schedule), or by host_words_kernel; dst == NULL: nothing to write.
+struct HostWords {
+    uint32_t* dst = nullptr;
+    const uint32_t* src = nullptr;
+    int n = 0;
+    uint32_t* seq_dst = nullptr;
+    uint32_t seq = 0;
+};
+#if defined(__HIPCC__)
+__device__ __forceinline__ void write_host_words(const HostWords& h, uint32_t lane)  // all 64 lanes of one wave
+{
+    if (lane < (uint32_t)h.n) __hip_atomic_store(h.dst + lane, h.src[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_s_waitcnt(0);  // the data stores are acknowledged before the sequence number is written
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) __hip_atomic_store(h.seq_dst, h.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+#endif
+void launch_host_words(const HostWords& h, hipStream_t s);
+
+void launch_emit_instances(const HostWords& hw, int P, size_t L_cap, const uint32_t* count, const GeomState& g, uint32_t gx,
                            uint32_t* block_owner, uint32_t* tile_keys, uint32_t* gauss_vals, char* binning,
                            hipStream_t s);
 void launch_tile_ranges(size_t L_cap, const uint32_t* count, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s);
@@ -127,11 +150,14 @@ struct RenderBwdArgs {
     uint8_t* row_valid;  // [L] zeroed; 1 where inst_grad holds a row
 };
 // grid: an upper bound on the unit count (seg_count(R, T)); waves past the device count exit at once
-void launch_render_backward(const RenderBwdArgs& a, size_t max_units, hipStream_t s);
+// ev_start / ev_stop (optional): timing events carried by the dispatch packet itself (hipExtLaunchKernelGGL), so
+// profiling the stage inserts no marker packets around it (each costs a system-scope release: GPU idle, capi.hip)
+void launch_render_backward(const RenderBwdArgs& a, size_t max_units, hipStream_t s, hipEvent_t ev_start = nullptr,
+                            hipEvent_t ev_stop = nullptr);
 // the backward's work list: every (tile, depth segment) below the tile's last contributor (max over the forward's
 // max_contrib words), costed by its positions, sorted longest first within each of the 8 XCD shares of the unit list
 // (the shares xcd_remap gives each XCD); writes units, *unit_count
-void launch_backward_schedule(const uint2* ranges, const uint32_t* max_contrib, uint32_t T, uint2* units_tmp,
+void launch_backward_schedule(const HostWords& hw, const uint2* ranges, const uint32_t* max_contrib, uint32_t T, uint2* units_tmp,
                               uint32_t* cost_tmp, uint2* units, uint32_t* unit_count, hipStream_t s);
 #ifdef OMR_STAMPS
 int omr_debug_stamps_bwd(uint64_t* dst, size_t bytes);  // diagnostic builds only (tile_wave.h)
@@ -166,7 +192,8 @@ struct GaussBwdArgs {
     float* dpx_dt;       // [P,3] optional (lonlat only; may be null)
     float* dpy_dt;       // [P,3] optional
 };
-void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s);
+void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s, hipEvent_t ev_start = nullptr,
+                              hipEvent_t ev_stop = nullptr);
 // Per-Gaussian sums of the render backward's instance rows: Gaussian i owns rows [row_first[i], row_first[i] +
 // tiles_touched[i]) of inst_grad (index-order numbering, launch_forward_scans); only rows marked in row_valid are read.
 // Gaussians in huge_list (*huge_count of them) are summed by whole workgroups. Also writes dL_dcolor [P][3] (the

@@ -327,10 +327,15 @@ extern "C" int omr_debug_bwd_counts(uint64_t* dst, int reset)
 }
 #endif
 
-void launch_render_backward(const RenderBwdArgs& a, size_t max_units, hipStream_t s)
+void launch_render_backward(const RenderBwdArgs& a, size_t max_units, hipStream_t s, hipEvent_t ev_start,
+                            hipEvent_t ev_stop)
 {
     if (max_units == 0) return;
-    render_bwd_kernel<<<(uint32_t)max_units, 64 * TW_WAVES, 0, s>>>(a);
+    if (ev_start || ev_stop)
+        hipExtLaunchKernelGGL(render_bwd_kernel, dim3((uint32_t)max_units), dim3(64 * TW_WAVES), 0, s, ev_start, ev_stop,
+                              0, a);
+    else
+        render_bwd_kernel<<<(uint32_t)max_units, 64 * TW_WAVES, 0, s>>>(a);
 }
 
 }  // namespace omr

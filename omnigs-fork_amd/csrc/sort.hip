@@ -700,9 +700,10 @@ __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* offsets, uin
 
 // Emission index: block_owner[B] = the depth rank owning slot B * EMIT_SLOTS (the rank whose slot range
 // [offsets[r-1], offsets[r]) contains it). One thread per rank; only ranks containing a block start write.
-__global__ __launch_bounds__(256) void emit_index_kernel(int P, size_t L_cap, const uint32_t* count,
+__global__ __launch_bounds__(256) void emit_index_kernel(HostWords hw, int P, size_t L_cap, const uint32_t* count,
                                                          const uint32_t* offsets, uint32_t* block_owner)
 {
+    if (hw.dst && blockIdx.x == 0 && threadIdx.x < 64) write_host_words(hw, threadIdx.x);  // the forward's count words
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= P || live_count(L_cap, count) == 0) return;  // block_owner holds L_cap / EMIT_SLOTS + 1 words
     const uint32_t lo = r == 0 ? 0u : offsets[r - 1], hi = offsets[r];
@@ -912,11 +913,12 @@ __device__ __forceinline__ uint32_t tile_units(const uint2* ranges, const uint32
     *mc_out = mc;
     return mc ? (r.x + mc - 1) / CKPT - r.x / CKPT + 1 : 0u;
 }
-__global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(const uint2* ranges, const uint32_t* max_contrib,
-                                                                          uint32_t T,
+__global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(HostWords hw, const uint2* ranges,
+                                                                          const uint32_t* max_contrib, uint32_t T,
                                                                           uint2* units_tmp, uint32_t* cost_tmp,
                                                                           uint2* units, uint32_t* unit_count)
 {
+    if (hw.dst && blockIdx.x == 0 && threadIdx.x < 64) write_host_words(hw, threadIdx.x);  // the backward's error word
     __shared__ uint32_t s_wave[SCHED_THREADS / 64];
     __shared__ uint32_t s_hist[RADIX];
     __shared__ uint32_t s_max;
@@ -988,12 +990,20 @@ __global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(const 
 
 }  // namespace
 
-void launch_backward_schedule(const uint2* ranges, const uint32_t* max_contrib, uint32_t T, uint2* units_tmp,
-                              uint32_t* cost_tmp, uint2* units, uint32_t* unit_count, hipStream_t s)
+void launch_backward_schedule(const HostWords& hw, const uint2* ranges, const uint32_t* max_contrib, uint32_t T,
+                              uint2* units_tmp, uint32_t* cost_tmp, uint2* units, uint32_t* unit_count, hipStream_t s)
 {
-    if (T == 0) return;
-    backward_schedule_kernel<<<8, SCHED_THREADS, 0, s>>>(ranges, max_contrib, T, units_tmp, cost_tmp, units, unit_count);
+    if (T == 0) {
+        if (hw.dst) launch_host_words(hw, s);
+        return;
+    }
+    backward_schedule_kernel<<<8, SCHED_THREADS, 0, s>>>(hw, ranges, max_contrib, T, units_tmp, cost_tmp, units,
+                                                         unit_count);
 }
+
+__global__ void host_words_kernel(HostWords hw) { write_host_words(hw, threadIdx.x); }
+
+void launch_host_words(const HostWords& h, hipStream_t s) { host_words_kernel<<<1, 64, 0, s>>>(h); }
 
 void launch_tile_order(const uint2* ranges, const uint32_t* cost, uint32_t T, uint32_t* order, hipStream_t s)
 {
@@ -1121,12 +1131,15 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
 
 size_t emit_index_size(size_t L_cap) { return div_up(L_cap, EMIT_SLOTS) + 1; }
 
-void launch_emit_instances(int P, size_t L_cap, const uint32_t* count, const GeomState& g, uint32_t gx,
-                           uint32_t* block_owner, uint32_t* tile_keys, uint32_t* gauss_vals, char* binning,
+void launch_emit_instances(const HostWords& hw, int P, size_t L_cap, const uint32_t* count, const GeomState& g,
+                           uint32_t gx, uint32_t* block_owner, uint32_t* tile_keys, uint32_t* gauss_vals, char* binning,
                            hipStream_t s)
 {
-    if (P <= 0 || L_cap == 0) return;
-    emit_index_kernel<<<div_up(P, 256), 256, 0, s>>>(P, L_cap, count, g.offsets, block_owner);
+    if (P <= 0 || L_cap == 0) {
+        if (hw.dst) launch_host_words(hw, s);
+        return;
+    }
+    emit_index_kernel<<<div_up(P, 256), 256, 0, s>>>(hw, P, L_cap, count, g.offsets, block_owner);
     emit_kernel<<<div_up(L_cap, EMIT_SLOTS), EMIT_THREADS, 0, s>>>(P, L_cap, count, g.order, g.offsets, block_owner,
                                                                  g.splat, gx, tile_keys, gauss_vals, binning);
 }
