@@ -181,6 +181,9 @@ struct StageScope {
 // spins on (kernels.h: HostWords): no blit kernel and no event. Either of those costs a dispatch and ends in a
 // system-scope release that writes back the L2 — about 5 us of GPU idle each at config C (profiles/gaps.py).
 // OMR_HOST_WORDS_KERNEL=0: hipMemcpyAsync + event record + event wait.
+#ifndef OMR_TILE_KEYS16
+#define OMR_TILE_KEYS16 1
+#endif
 #ifndef OMR_HOST_WORDS_KERNEL
 #define OMR_HOST_WORDS_KERNEL 1
 #endif
@@ -516,6 +519,8 @@ int forward_impl(const ForwardIn& in)
     rt_add(RS_FORWARDS, 1);
 
     const int tile_passes = tile_sort_passes(d.T);
+    // tile ids below 2^16: the tile sort moves 16-bit keys (emit, both passes and the ranges read 2 B less per key)
+    const bool keys16 = OMR_TILE_KEYS16 && d.T <= 65536u;
     size_t& hint = capacity_hint(in.width, in.height, in.camera_type);
     bool known = false;
     size_t L = 0;
@@ -547,16 +552,21 @@ int forward_impl(const ForwardIn& in)
         if (!bin_base) return fail(OMR_ERR_ALLOCATION, "binning allocation failed");
         BinningState b;
         BinningState::carve(bin_base, capacity, d.T, &b);
-        { StageScope st_(ST_EMIT, s); launch_emit_instances(count_words, in.P, capacity, count_dev, g, d.gx, b.block_owner, b.key_a, b.val_a, bin_base, s); }
+        { StageScope st_(ST_EMIT, s); launch_emit_instances(count_words, in.P, capacity, count_dev, g, d.gx, b.block_owner, b.key_a, keys16, b.val_a, bin_base, s); }
         {
             StageScope st_(ST_TILE_SORT, s);
-            radix_sort_pairs(b.key_a, b.key_b, b.val_a, b.val_b, b.hist, b.scan_partials, capacity, count_dev,
-                             bin_base, 0, tile_passes, s, false, err_dev);
+            if (keys16)
+                radix_sort_pairs(reinterpret_cast<uint16_t*>(b.key_a), reinterpret_cast<uint16_t*>(b.key_b), b.val_a,
+                                 b.val_b, b.hist, b.scan_partials, capacity, count_dev, bin_base, 0, tile_passes, s,
+                                 false, err_dev);
+            else
+                radix_sort_pairs(b.key_a, b.key_b, b.val_a, b.val_b, b.hist, b.scan_partials, capacity, count_dev,
+                                 bin_base, 0, tile_passes, s, false, err_dev);
         }
         if (rerun) OMR_HIP(hipMemsetAsync(im.ranges, 0, d.T * sizeof(uint2), s));
         {
             StageScope st_(ST_RANGES, s);
-            launch_tile_ranges(capacity, count_dev, b.point_keys, im.ranges, s);
+            launch_tile_ranges(capacity, count_dev, b.point_keys, keys16, im.ranges, s);
             launch_tile_order(im.ranges, nullptr, d.T, im.tile_order, s);
         }
         if (rerun) OMR_HIP(hipMemsetAsync(im.tile_cost, 0, d.T * sizeof(uint32_t), s));

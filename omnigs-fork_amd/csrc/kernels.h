@@ -64,9 +64,12 @@ void launch_forward_scans(const uint32_t* tiles_touched, const uint32_t* order, 
 // values to the canonical point list of the binning buffer at canon (raster_common.h) instead of val_a / val_b.
 // scratch_zeroed: the caller has zeroed radix_zero_span(hist, n, passes) (else the sort clears it itself).
 // err (device word; NULL = a private word in the scratch) is OR-ed with 1 if a decoupled look-back gave up.
-int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* hist,
-                     uint32_t* scan_partials, size_t n, const uint32_t* count, char* canon, int first_pass, int passes,
-                     hipStream_t s, bool scratch_zeroed = false, uint32_t* err = nullptr);
+// K = uint32_t, or uint16_t for keys below 2^16 (the tile sort of views with at most 65536 tiles: 2 B less per key
+// and pass read and written).
+template <typename K>
+int radix_sort_pairs(K* key_a, K* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* hist, uint32_t* scan_partials,
+                     size_t n, const uint32_t* count, char* canon, int first_pass, int passes, hipStream_t s,
+                     bool scratch_zeroed = false, uint32_t* err = nullptr);
 // the words of `hist` a sort of n items over `passes` passes needs zeroed before it starts (possibly none)
 ZeroSpan radix_zero_span(uint32_t* hist, size_t n, int passes);
 // duplicateWithKeys; L_cap = capacity, *count (device) = num_rendered; block_owner: emit_index_size(L_cap) words
@@ -102,10 +105,12 @@ __device__ __forceinline__ void write_host_words(const HostWords& h, uint32_t la
 #endif
 void launch_host_words(const HostWords& h, hipStream_t s);
 
-void launch_emit_instances(const HostWords& hw, int P, size_t L_cap, const uint32_t* count, const GeomState& g, uint32_t gx,
-                           uint32_t* block_owner, uint32_t* tile_keys, uint32_t* gauss_vals, char* binning,
-                           hipStream_t s);
-void launch_tile_ranges(size_t L_cap, const uint32_t* count, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s);
+// tile_keys: uint16_t[L_cap] when keys16 (at most 65536 tiles), else uint32_t[L_cap]
+void launch_emit_instances(const HostWords& hw, int P, size_t L_cap, const uint32_t* count, const GeomState& g,
+                           uint32_t gx, uint32_t* block_owner, void* tile_keys, bool keys16, uint32_t* gauss_vals,
+                           char* binning, hipStream_t s);
+void launch_tile_ranges(size_t L_cap, const uint32_t* count, const void* sorted_tiles, bool keys16, uint2* ranges,
+                        hipStream_t s);
 // render schedule: within each of 8 contiguous shares of the tiles (one per XCD), tiles by descending cost
 // (cost[t] if cost != NULL, else the instance count ranges[t].y - ranges[t].x)
 void launch_tile_order(const uint2* ranges, const uint32_t* cost, uint32_t T, uint32_t* order, hipStream_t s);

@@ -287,8 +287,8 @@ __device__ __forceinline__ size_t live_count(size_t n, const uint32_t* count)
 #endif
 // BLOCK_MAJOR: hist[block][digit] (read back by the self-scanning downsweep of small sorts); else hist[digit][block].
 // Key arrays are 16-B aligned (Carver) for the 16-B loads.
-template <bool BLOCK_MAJOR, int ITEMS, int THREADS>
-__global__ __launch_bounds__(THREADS) void radix_upsweep_kernel(const uint32_t* keys, size_t n_cap,
+template <typename K, bool BLOCK_MAJOR, int ITEMS, int THREADS>
+__global__ __launch_bounds__(THREADS) void radix_upsweep_kernel(const K* keys, size_t n_cap,
                                                                      const uint32_t* count, int shift, uint32_t* hist,
                                                                      uint32_t nblocks, uint32_t* zero, uint32_t nzero)
 {
@@ -307,28 +307,27 @@ __global__ __launch_bounds__(THREADS) void radix_upsweep_kernel(const uint32_t* 
     // 16-B loads (4 per thread, each wave instruction one contiguous KiB), and one LDS add per distinct digit of
     // each 64-key group (8-ballot match, as the downsweep ranks): same-address adds within one ds_add serialise,
     // and neighbouring instances often share a digit
-    static_assert(ITEMS % 4 == 0, "16-B key loads");
+    constexpr int KPL = 16 / (int)sizeof(K);  // keys per 16-B load
+    static_assert(ITEMS % KPL == 0, "16-B key loads");
     uint32_t kv[ITEMS];
     const bool full = base + TILE_N <= n;
 #pragma unroll
-    for (int k = 0; k < ITEMS / 4; ++k) {
-        const size_t i = base + 4 * ((size_t)k * THREADS + threadIdx.x);
-        uint4 q;
-        if (full) q = *reinterpret_cast<const uint4*>(keys + i);
-        else {
-            q.x = i < n ? keys[i] : 0u;
-            q.y = i + 1 < n ? keys[i + 1] : 0u;
-            q.z = i + 2 < n ? keys[i + 2] : 0u;
-            q.w = i + 3 < n ? keys[i + 3] : 0u;
+    for (int k = 0; k < ITEMS / KPL; ++k) {
+        const size_t i = base + KPL * ((size_t)k * THREADS + threadIdx.x);
+        if (full) {
+            const uint4 q = *reinterpret_cast<const uint4*>(keys + i);
+            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int j = 0; j < KPL; ++j)
+                kv[KPL * k + j] = sizeof(K) == 4 ? w[j] : (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+        } else {
+#pragma unroll
+            for (int j = 0; j < KPL; ++j) kv[KPL * k + j] = i + j < n ? (uint32_t)keys[i + j] : 0u;
         }
-        kv[4 * k] = q.x;
-        kv[4 * k + 1] = q.y;
-        kv[4 * k + 2] = q.z;
-        kv[4 * k + 3] = q.w;
     }
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
-        const size_t i = base + 4 * ((size_t)(j >> 2) * THREADS + threadIdx.x) + (j & 3);
+        const size_t i = base + KPL * ((size_t)(j / KPL) * THREADS + threadIdx.x) + (j % KPL);
         const bool valid = i < n;
         const uint32_t d = (kv[j] >> shift) & (RADIX - 1);
         if (OMR_UPSWEEP_V4 == 2) {
@@ -367,9 +366,9 @@ __global__ __launch_bounds__(THREADS) void radix_upsweep_kernel(const uint32_t* 
 // SELF_SCAN (small sorts, few blocks): hist is the raw block-major histogram and each block derives its global
 // digit offsets itself (column prefix over the blocks before it + scan of the digit totals), which saves the
 // three scan launches per pass; else hist is the scanned [digit][block] histogram.
-template <bool SELF_SCAN, int ITEMS, int THREADS>
-__global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const uint32_t* keys_in, const uint32_t* vals_in,
-                                                                       uint32_t* keys_out, uint32_t* vals_out,
+template <typename K, bool SELF_SCAN, int ITEMS, int THREADS>
+__global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const K* keys_in, const uint32_t* vals_in,
+                                                                       K* keys_out, uint32_t* vals_out,
                                                                        size_t n_cap, const uint32_t* count, char* canon,
                                                                        int shift, const uint32_t* hist_scanned,
                                                                        uint32_t nblocks)
@@ -382,7 +381,7 @@ __global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const uint32_t
     __shared__ uint32_t s_dstart[RADIX];        // block-local start of each digit's run
     __shared__ uint32_t s_gbase[RADIX];         // global start of this block's run of each digit
     __shared__ uint32_t s_wave[THREADS / 64];
-    __shared__ uint32_t s_k[TILE_N];
+    __shared__ K s_k[TILE_N];
     __shared__ uint32_t s_v[TILE_N];
     const size_t n = live_count(n_cap, count);
     if (canon) vals_out = reinterpret_cast<uint32_t*>(canon + canonical_list_offset(n));
@@ -467,7 +466,7 @@ __global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const uint32_t
         if (base + 64 * r < n) {
             const uint32_t d = (k[r] >> shift) & (RADIX - 1);
             const uint32_t lp = s_dstart[d] + s_whist[w][d] + lr[r];
-            s_k[lp] = k[r];
+            s_k[lp] = (K)k[r];
             s_v[lp] = v[r];
         }
     }
@@ -477,7 +476,7 @@ __global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const uint32_t
         const uint32_t kk = s_k[j];
         const uint32_t d = (kk >> shift) & (RADIX - 1);
         const uint32_t dst = s_gbase[d] + (j - s_dstart[d]);
-        keys_out[dst] = kk;
+        keys_out[dst] = (K)kk;
         vals_out[dst] = s_v[j];
     }
 }
@@ -530,7 +529,8 @@ __host__ __device__ inline size_t onesweep_words(size_t n, int passes)
 
 // digit totals of every pass (ghist, zeroed by the caller; OS_HIST_BLOCKS blocks, grid-stride, so every total
 // takes at most OS_HIST_BLOCKS same-address global adds) and the zeroed status words of every pass
-__global__ __launch_bounds__(SORT_THREADS) void onesweep_hist_kernel(const uint32_t* keys, size_t n_cap,
+template <typename K>
+__global__ __launch_bounds__(SORT_THREADS) void onesweep_hist_kernel(const K* keys, size_t n_cap,
                                                                      const uint32_t* count, int first_pass, int passes,
                                                                      uint32_t* status, size_t status_words,
                                                                      uint32_t* ghist)
@@ -561,9 +561,9 @@ __device__ __forceinline__ uint32_t lb_load(const uint32_t* p)
 }
 
 // one pass: status = this pass's [blocks][RADIX] words (zeroed), ghist = its digit totals, ticket = its tile counter
-template <int TILE_N>
-__global__ __launch_bounds__(SORT_THREADS) void onesweep_kernel(const uint32_t* keys_in, const uint32_t* vals_in,
-                                                                uint32_t* keys_out, uint32_t* vals_out, size_t n_cap,
+template <typename K, int TILE_N>
+__global__ __launch_bounds__(SORT_THREADS) void onesweep_kernel(const K* keys_in, const uint32_t* vals_in,
+                                                                K* keys_out, uint32_t* vals_out, size_t n_cap,
                                                                 const uint32_t* count, char* canon, int shift,
                                                                 uint32_t* status, const uint32_t* ghist,
                                                                 uint32_t* ticket, uint32_t* err)
@@ -575,7 +575,7 @@ __global__ __launch_bounds__(SORT_THREADS) void onesweep_kernel(const uint32_t* 
     __shared__ uint32_t s_dstart[RADIX];        // block-local start of each digit's run
     __shared__ uint32_t s_gbase[RADIX];         // global start of this block's run of each digit
     __shared__ uint32_t s_wave[SORT_THREADS / 64];
-    __shared__ uint32_t s_k[TILE_N];
+    __shared__ K s_k[TILE_N];
     __shared__ uint32_t s_v[TILE_N];
     __shared__ uint32_t s_vb;
     const uint32_t tid = threadIdx.x;
@@ -671,7 +671,7 @@ __global__ __launch_bounds__(SORT_THREADS) void onesweep_kernel(const uint32_t* 
         if (base + 64 * r < n) {
             const uint32_t d = (k[r] >> shift) & (RADIX - 1);
             const uint32_t lp = s_dstart[d] + s_whist[w][d] + lr[r];
-            s_k[lp] = k[r];
+            s_k[lp] = (K)k[r];
             s_v[lp] = v[r];
         }
     }
@@ -681,7 +681,7 @@ __global__ __launch_bounds__(SORT_THREADS) void onesweep_kernel(const uint32_t* 
         const uint32_t kk = s_k[j];
         const uint32_t d = (kk >> shift) & (RADIX - 1);
         const uint32_t dst = s_gbase[d] + (j - s_dstart[d]);
-        keys_out[dst] = kk;
+        keys_out[dst] = (K)kk;
         vals_out[dst] = s_v[j];
     }
 }
@@ -746,10 +746,11 @@ __device__ __forceinline__ void emit_one(const float4* splat, uint32_t gid, uint
 // EMIT_PER independent record gathers in flight (the kernel waits on memory, not on its ALU). The block's slots
 // belong to ranks [block_owner[B], block_owner[B+1]]; their slot ends are staged in LDS, each thread finds the owner
 // of its first slot by a binary search there and steps forward for the others.
+template <typename K>
 __global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap, const uint32_t* count,
                                                             const uint32_t* order, const uint32_t* offsets,
                                                             const uint32_t* block_owner, const float4* splat,
-                                                            uint32_t gx, uint32_t* tile_keys, uint32_t* gauss_vals,
+                                                            uint32_t gx, K* tile_keys, uint32_t* gauss_vals,
                                                             char* binning)
 {
     __shared__ uint32_t s_end[EMIT_SLOTS];
@@ -803,7 +804,11 @@ __global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap,
     if (EMIT_PER % 4 == 0 && nmine == (uint32_t)EMIT_PER) {
 #pragma unroll
         for (int q = 0; q < EMIT_PER; q += 4) {
-            *reinterpret_cast<uint4*>(tile_keys + eb + q) = make_uint4(key[q], key[q + 1], key[q + 2], key[q + 3]);
+            if (sizeof(K) == 4)
+                *reinterpret_cast<uint4*>(tile_keys + eb + q) = make_uint4(key[q], key[q + 1], key[q + 2], key[q + 3]);
+            else
+                *reinterpret_cast<uint2*>(tile_keys + eb + q) =
+                    make_uint2(key[q] | (key[q + 1] << 16), key[q + 2] | (key[q + 3] << 16));
             *reinterpret_cast<uint4*>(gauss_vals + eb + q) = make_uint4(val[q], val[q + 1], val[q + 2], val[q + 3]);
             *reinterpret_cast<uint32_t*>(row_valid + eb + q) = 0u;  // row_valid_offset is 256-B aligned
         }
@@ -811,7 +816,7 @@ __global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap,
 #pragma unroll
         for (int j = 0; j < EMIT_PER; ++j) {
             if ((uint32_t)j >= nmine) break;
-            tile_keys[eb + j] = key[j];
+            tile_keys[eb + j] = (K)key[j];
             gauss_vals[eb + j] = val[j];
             row_valid[eb + j] = 0;
         }
@@ -821,7 +826,8 @@ __global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap,
 // identifyTileRanges (rasterizer_impl.cu:145-167). Four sorted keys per thread through one 16-B load (key arrays
 // are 16-B aligned), the predecessor of the first from the neighbouring lane.
 constexpr int RANGES_ITEMS = 4;
-__global__ __launch_bounds__(256) void tile_ranges_kernel(size_t L_cap, const uint32_t* count, const uint32_t* tiles,
+template <typename K>
+__global__ __launch_bounds__(256) void tile_ranges_kernel(size_t L_cap, const uint32_t* count, const K* tiles,
                                                           uint2* ranges)
 {
     const size_t L = live_count(L_cap, count);
@@ -829,8 +835,13 @@ __global__ __launch_bounds__(256) void tile_ranges_kernel(size_t L_cap, const ui
     if (i0 >= L) return;
     uint32_t k[RANGES_ITEMS];
     if (i0 + RANGES_ITEMS <= L) {
-        const uint4 q = *reinterpret_cast<const uint4*>(tiles + i0);
-        k[0] = q.x; k[1] = q.y; k[2] = q.z; k[3] = q.w;
+        if (sizeof(K) == 4) {
+            const uint4 q = *reinterpret_cast<const uint4*>(tiles + i0);
+            k[0] = q.x; k[1] = q.y; k[2] = q.z; k[3] = q.w;
+        } else {
+            const uint2 q = *reinterpret_cast<const uint2*>(tiles + i0);
+            k[0] = q.x & 0xFFFFu; k[1] = q.x >> 16; k[2] = q.y & 0xFFFFu; k[3] = q.y >> 16;
+        }
     } else {
 #pragma unroll
         for (int j = 0; j < RANGES_ITEMS; ++j) k[j] = i0 + j < L ? tiles[i0 + j] : 0u;
@@ -1053,12 +1064,14 @@ ZeroSpan radix_zero_span(uint32_t* hist, size_t n, int passes)
     return z;
 }
 
-int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* hist,
-                     uint32_t* scan_partials, size_t n, const uint32_t* count, char* canon, int first_pass, int passes,
-                     hipStream_t s, bool scratch_zeroed, uint32_t* err_out)
+template <typename K>
+int radix_sort_pairs(K* key_a, K* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* hist, uint32_t* scan_partials,
+                     size_t n, const uint32_t* count, char* canon, int first_pass, int passes, hipStream_t s,
+                     bool scratch_zeroed, uint32_t* err_out)
 {
     if (n == 0 || passes <= 0) return 0;
-    uint32_t *ki = key_a, *ko = key_b, *vi = val_a, *vo = val_b;
+    K *ki = key_a, *ko = key_b;
+    uint32_t *vi = val_a, *vo = val_b;
     int cur = 0;
     if (use_onesweep(n)) {
         const uint32_t nb = div_up(n, os_tile(n));
@@ -1068,11 +1081,11 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
         uint32_t* tickets = ghist + (size_t)passes * RADIX;
         uint32_t* err = err_out ? err_out : tickets + passes;
         if (!scratch_zeroed) (void)hipMemsetAsync(ghist, 0, ((size_t)passes * (RADIX + 1) + 1) * sizeof(uint32_t), s);
-        onesweep_hist_kernel<<<std::min(div_up(n, SORT_THREADS), OS_HIST_BLOCKS), SORT_THREADS, 0, s>>>(
+        onesweep_hist_kernel<K><<<std::min(div_up(n, SORT_THREADS), OS_HIST_BLOCKS), SORT_THREADS, 0, s>>>(
             ki, n, count, first_pass, passes, status, (size_t)passes * nb * RADIX, ghist);
         for (int p = 0; p < passes; ++p) {
             const bool last = p == passes - 1;
-            auto kern = os_tile(n) == OS_TILE ? onesweep_kernel<OS_TILE> : onesweep_kernel<OS_TILE_SMALL>;
+            auto kern = os_tile(n) == OS_TILE ? onesweep_kernel<K, OS_TILE> : onesweep_kernel<K, OS_TILE_SMALL>;
             kern<<<nb, SORT_THREADS, 0, s>>>(ki, vi, ko, vo, n, count, last ? canon : nullptr,
                                             (first_pass + p) * RADIX_BITS, status + (size_t)p * nb * RADIX,
                                             ghist + (size_t)p * RADIX, tickets + p, err);
@@ -1092,14 +1105,14 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
         const bool last = p == first_pass + passes - 1;
         if (nb <= SELF_SCAN_MAX_BLOCKS) {
             if (large) {
-                radix_upsweep_kernel<true, SORT_ITEMS_LARGE, SORT_THREADS_LARGE><<<nb, SORT_THREADS_LARGE, 0, s>>>(ki, n, count, shift, hist, nb,
+                radix_upsweep_kernel<K, true, SORT_ITEMS_LARGE, SORT_THREADS_LARGE><<<nb, SORT_THREADS_LARGE, 0, s>>>(ki, n, count, shift, hist, nb,
                                                                                         nullptr, 0);
-                radix_downsweep_kernel<true, SORT_ITEMS_LARGE, SORT_THREADS_LARGE><<<nb, SORT_THREADS_LARGE, 0, s>>>(
+                radix_downsweep_kernel<K, true, SORT_ITEMS_LARGE, SORT_THREADS_LARGE><<<nb, SORT_THREADS_LARGE, 0, s>>>(
                     ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
             } else {
-                radix_upsweep_kernel<true, SORT_ITEMS, SORT_THREADS><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb,
+                radix_upsweep_kernel<K, true, SORT_ITEMS, SORT_THREADS><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb,
                                                                                   nullptr, 0);
-                radix_downsweep_kernel<true, SORT_ITEMS, SORT_THREADS><<<nb, SORT_THREADS, 0, s>>>(
+                radix_downsweep_kernel<K, true, SORT_ITEMS, SORT_THREADS><<<nb, SORT_THREADS, 0, s>>>(
                     ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
             }
         } else {
@@ -1108,18 +1121,18 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
             uint64_t* lb = reinterpret_cast<uint64_t*>(scan_partials);
             uint32_t* lb_ticket = scan_partials + 2 * (size_t)nbs;
             if (large)
-                radix_upsweep_kernel<false, SORT_ITEMS_LARGE, SORT_THREADS_LARGE><<<nb, SORT_THREADS_LARGE, 0, s>>>(
+                radix_upsweep_kernel<K, false, SORT_ITEMS_LARGE, SORT_THREADS_LARGE><<<nb, SORT_THREADS_LARGE, 0, s>>>(
                     ki, n, count, shift, hist, nb, scan_partials, 2 * nbs + 2);
             else
-                radix_upsweep_kernel<false, SORT_ITEMS, SORT_THREADS><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb,
+                radix_upsweep_kernel<K, false, SORT_ITEMS, SORT_THREADS><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb,
                                                                                    scan_partials, 2 * nbs + 2);
             scan_lookback_kernel<<<nbs, SCAN_THREADS, 0, s>>>(hist, hist, (size_t)RADIX * nb, lb, lb_ticket,
                                                              err_out ? err_out : lb_ticket + 1);
             if (large)
-                radix_downsweep_kernel<false, SORT_ITEMS_LARGE, SORT_THREADS_LARGE><<<nb, SORT_THREADS_LARGE, 0, s>>>(
+                radix_downsweep_kernel<K, false, SORT_ITEMS_LARGE, SORT_THREADS_LARGE><<<nb, SORT_THREADS_LARGE, 0, s>>>(
                     ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
             else
-                radix_downsweep_kernel<false, SORT_ITEMS, SORT_THREADS><<<nb, SORT_THREADS, 0, s>>>(
+                radix_downsweep_kernel<K, false, SORT_ITEMS, SORT_THREADS><<<nb, SORT_THREADS, 0, s>>>(
                     ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
         }
         std::swap(ki, ko);
@@ -1129,25 +1142,42 @@ int radix_sort_pairs(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t
     return cur;
 }
 
+template int radix_sort_pairs<uint32_t>(uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, size_t,
+                                        const uint32_t*, char*, int, int, hipStream_t, bool, uint32_t*);
+template int radix_sort_pairs<uint16_t>(uint16_t*, uint16_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, size_t,
+                                        const uint32_t*, char*, int, int, hipStream_t, bool, uint32_t*);
+
 size_t emit_index_size(size_t L_cap) { return div_up(L_cap, EMIT_SLOTS) + 1; }
 
 void launch_emit_instances(const HostWords& hw, int P, size_t L_cap, const uint32_t* count, const GeomState& g,
-                           uint32_t gx, uint32_t* block_owner, uint32_t* tile_keys, uint32_t* gauss_vals, char* binning,
-                           hipStream_t s)
+                           uint32_t gx, uint32_t* block_owner, void* tile_keys, bool keys16, uint32_t* gauss_vals,
+                           char* binning, hipStream_t s)
 {
     if (P <= 0 || L_cap == 0) {
         if (hw.dst) launch_host_words(hw, s);
         return;
     }
     emit_index_kernel<<<div_up(P, 256), 256, 0, s>>>(hw, P, L_cap, count, g.offsets, block_owner);
-    emit_kernel<<<div_up(L_cap, EMIT_SLOTS), EMIT_THREADS, 0, s>>>(P, L_cap, count, g.order, g.offsets, block_owner,
-                                                                 g.splat, gx, tile_keys, gauss_vals, binning);
+    if (keys16)
+        emit_kernel<uint16_t><<<div_up(L_cap, EMIT_SLOTS), EMIT_THREADS, 0, s>>>(
+            P, L_cap, count, g.order, g.offsets, block_owner, g.splat, gx, static_cast<uint16_t*>(tile_keys), gauss_vals,
+            binning);
+    else
+        emit_kernel<uint32_t><<<div_up(L_cap, EMIT_SLOTS), EMIT_THREADS, 0, s>>>(
+            P, L_cap, count, g.order, g.offsets, block_owner, g.splat, gx, static_cast<uint32_t*>(tile_keys), gauss_vals,
+            binning);
 }
 
-void launch_tile_ranges(size_t L_cap, const uint32_t* count, const uint32_t* sorted_tiles, uint2* ranges, hipStream_t s)
+void launch_tile_ranges(size_t L_cap, const uint32_t* count, const void* sorted_tiles, bool keys16, uint2* ranges,
+                        hipStream_t s)
 {
     if (L_cap == 0) return;
-    tile_ranges_kernel<<<div_up(L_cap, 256 * RANGES_ITEMS), 256, 0, s>>>(L_cap, count, sorted_tiles, ranges);
+    if (keys16)
+        tile_ranges_kernel<<<div_up(L_cap, 256 * RANGES_ITEMS), 256, 0, s>>>(
+            L_cap, count, static_cast<const uint16_t*>(sorted_tiles), ranges);
+    else
+        tile_ranges_kernel<<<div_up(L_cap, 256 * RANGES_ITEMS), 256, 0, s>>>(
+            L_cap, count, static_cast<const uint32_t*>(sorted_tiles), ranges);
 }
 
 }  // namespace omr
