@@ -272,6 +272,12 @@ constexpr uint32_t SELF_SCAN_MAX_BLOCKS = 512;
 constexpr int SORT_THREADS_LARGE = OMR_SORT_THREADS_LARGE;  // block size of the multi-launch passes of large sorts
 constexpr int SORT_ITEMS_LARGE = OMR_SORT_ITEMS_LARGE;      // items per thread there (8192-key tiles)
 constexpr size_t SORT_LARGE_MIN = OMR_SORT_LARGE_MIN;
+// 16-bit keys take the large tiles from 4 M keys on (config C's 7.9 M-key tile sort: 0.1315 -> 0.1217 ms; with
+// 32-bit keys 8192-key tiles are slower there, 0.152 vs 0.137 ms)
+#ifndef OMR_SORT_LARGE_MIN16
+#define OMR_SORT_LARGE_MIN16 (1u << 22)
+#endif
+constexpr size_t SORT_LARGE_MIN16 = OMR_SORT_LARGE_MIN16;
 
 // ---- radix sort ------------------------------------------------------------------------------------------
 // element count: the host's n, or the device count word (binning, capi.hip; raster_common.h: binning_count), which
@@ -307,16 +313,23 @@ __global__ __launch_bounds__(THREADS) void radix_upsweep_kernel(const K* keys, s
     // 16-B loads (4 per thread, each wave instruction one contiguous KiB), and one LDS add per distinct digit of
     // each 64-key group (8-ballot match, as the downsweep ranks): same-address adds within one ds_add serialise,
     // and neighbouring instances often share a digit
-    constexpr int KPL = 16 / (int)sizeof(K);  // keys per 16-B load
-    static_assert(ITEMS % KPL == 0, "16-B key loads");
+    // keys per load: 16 B of them, or 8 B (4 16-bit keys) when ITEMS is not a multiple of 8
+    constexpr int KPL = ITEMS % (16 / (int)sizeof(K)) == 0 ? 16 / (int)sizeof(K) : 4;
+    static_assert(ITEMS % KPL == 0, "vector key loads");
     uint32_t kv[ITEMS];
     const bool full = base + TILE_N <= n;
 #pragma unroll
     for (int k = 0; k < ITEMS / KPL; ++k) {
         const size_t i = base + KPL * ((size_t)k * THREADS + threadIdx.x);
         if (full) {
-            const uint4 q = *reinterpret_cast<const uint4*>(keys + i);
-            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+            uint32_t w[4];
+            if (KPL * sizeof(K) == 16) {
+                const uint4 q = *reinterpret_cast<const uint4*>(keys + i);
+                w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w;
+            } else {
+                const uint2 q = *reinterpret_cast<const uint2*>(keys + i);
+                w[0] = q.x; w[1] = q.y; w[2] = w[3] = 0u;
+            }
 #pragma unroll
             for (int j = 0; j < KPL; ++j)
                 kv[KPL * k + j] = sizeof(K) == 4 ? w[j] : (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
@@ -1098,7 +1111,7 @@ int radix_sort_pairs(K* key_a, K* key_b, uint32_t* val_a, uint32_t* val_b, uint3
     // large sorts (config E's 117 M instances) take 8192-key tiles: digit runs twice as long per block, so the
     // scattered stores fill whole lines more often (tile sort 1.98 -> 1.64 ms there); below the threshold 4096-key
     // tiles are faster (0.136 vs 0.152 ms at config C's 7.9 M)
-    const bool large = n >= SORT_LARGE_MIN;
+    const bool large = n >= (sizeof(K) == 2 ? SORT_LARGE_MIN16 : SORT_LARGE_MIN);
     const uint32_t nb = div_up(n, large ? SORT_THREADS_LARGE * SORT_ITEMS_LARGE : SORT_TILE);
     for (int p = first_pass; p < first_pass + passes; ++p) {
         const int shift = p * RADIX_BITS;
