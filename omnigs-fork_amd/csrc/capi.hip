@@ -350,6 +350,7 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s)
     g.counters = c.take<uint32_t>(4);
     g.row_first = c.take<uint32_t>(P);
     g.row_sums = c.take<float>(P * GRAD_ROW);
+    g.conic_op = c.take<float4>(P);
     g.huge_list = c.take<uint32_t>(P);
     g.internal_radii = c.take<int>(P);
     g.order = g.val_a;  // the depth sort runs DEPTH_SORT_PASSES (even) passes, so its result lands in val_a
@@ -683,7 +684,7 @@ int backward_impl(const BackwardIn& in)
     ga.focal_x = (float)in.width / (2.0f * in.tan_fovx);
     ga.clamped = g.clamped;
     ga.row_sums = g.row_sums;
-    ga.splat = g.splat;
+    ga.conic_op = g.conic_op;
     { StageScope st_(ST_ROW_SUMS, s); launch_row_sums(in.P, g.row_first, g.tiles_touched, g.huge_list, g.counters + 2, b.inst_grad, b.row_valid, (uint32_t)in.R, g.row_sums, in.dL_dcolor, s); }
     if (colors_event) OMR_HIP(hipEventRecord(colors_event, s));  // dL_dcolor is final from here on
     ga.dL_dmean2D = in.dL_dmean2D; ga.dL_dconic = in.dL_dconic; ga.dL_dopacity = in.dL_dopacity; ga.dL_dcolor = in.dL_dcolor;

@@ -653,7 +653,7 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
     if (idx < a.P) {
 #pragma unroll
         for (int c = 0; c < GRAD_ROW; ++c) g[c] = a.row_sums[(size_t)idx * GRAD_ROW + c];
-        if (OMR_BWD_RAW_MOMENTS) co = a.splat[(size_t)idx * SPLAT_F4 + 1];
+        if (OMR_BWD_RAW_MOMENTS) co = a.conic_op[idx];
     }
     const bool valid = idx < a.P;
     const bool vis = valid && a.radii[idx] > 0;

@@ -184,7 +184,7 @@ struct GaussBwdArgs {
     float tan_fovx, tan_fovy, focal_x, focal_y;
     const uint8_t* clamped;
     const float* row_sums;  // [P][GRAD_ROW] each Gaussian's instance rows summed (launch_row_sums)
-    const float4* splat;    // [P][SPLAT_F4] render records: conic + opacity for the raw-moment rows
+    const float4* conic_op;  // [P] conic + opacity (GeomState) for the raw-moment rows
     float* dL_dmean2D;   // [P,3]
     float* dL_dconic;    // [P,4] optional (may be null)
     float* dL_dopacity;  // [P]

@@ -272,7 +272,10 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
         g.tiles_touched[idx] = vis ? o.area : 0u;
         g.key_a[idx] = vis ? __float_as_uint(o.depth) : 0xFFFFFFFFu;  // culled Gaussians sort last, emit nothing
         g.val_a[idx] = (uint32_t)idx;
-        if (vis) g.clamped[idx] = o.clamp_bits;
+        if (vis) {
+            g.clamped[idx] = o.clamp_bits;
+            if (OMR_BWD_RAW_MOMENTS) g.conic_op[idx] = o.rec[1];  // the backward's per-Gaussian factors
+        }
     }
     // the render record of a visible Gaussian (culled records are never read)
     if (OMR_PRE_STAGE) {

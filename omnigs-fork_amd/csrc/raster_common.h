@@ -105,6 +105,8 @@ struct GeomState {
     uint32_t* order;          // depth order (points at val_a or val_b after the sort)
     uint32_t* row_first;      // first gradient row of each Gaussian (index-order exclusive scan, launch_forward_scans)
     float* row_sums;          // backward: [P][GRAD_ROW] each Gaussian's instance rows summed (launch_row_sums)
+    float4* conic_op;         // [P] conic + opacity (= splat record slot 1), contiguous for gaussian_bwd's coalesced
+                              // read (raw-moment rows: raster_common.h OMR_BWD_RAW_MOMENTS)
     uint32_t* huge_list;      // Gaussians with more than ROW_SUM_HUGE tiles, any order; count in counters[2]
     int* internal_radii;      // used when the caller passes radii == NULL (rasterizer_impl.cu:284-287)
 
