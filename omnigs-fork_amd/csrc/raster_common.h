@@ -247,6 +247,44 @@ __device__ __forceinline__ void getRect(float2 p, int max_radius, uint32_t gx, u
     y1 = min(gy, (uint32_t)max(0, (int)((p.y + r + (float)BLOCK_Y - 1.0f) / (float)BLOCK_Y)));
 }
 
+// The per-Gaussian part of band_mask: threshold t and the completed-square terms. A Gaussian with 255 o < 1 gets
+// t = -inf (no band), a degenerate conic a = k = dd = 0 and t = +inf (every band), so band_mask_of needs no branch.
+struct BandConsts {
+    float t, k, dd, a;
+};
+__device__ __forceinline__ BandConsts band_consts(float4 co)
+{
+    if (!(co.w * 255.0f >= 1.0f)) return {-__builtin_inff(), 0.f, 0.f, 0.f};  // even G = 1 gives alpha < 1/255
+    const float a = co.x, b = co.y, c = co.z;
+    if (!(a * c - b * b > 0.0f) || !(a > 0.0f)) return {__builtin_inff(), 0.f, 0.f, 0.f};  // degenerate: every band
+    const float t = 2.0f * __logf(255.0f * co.w) * 1.002f + 0.02f;
+    // completed square: q = a (dx - k dy)^2 + (det / a) dy^2 with k = -b / a (no cancellation between large terms)
+    const float ra = __builtin_amdgcn_rcpf(a);
+    return {t, -b * ra, (a * c - b * b) * ra, a};
+}
+template <int NB>
+__device__ __forceinline__ uint32_t band_mask_of(const BandConsts& bc, float2 xy, uint32_t tx, uint32_t ty,
+                                                 uint32_t band0)
+{
+    const float x0 = (float)(tx * BLOCK_X);
+    const float lo = xy.x - (x0 + (float)(BLOCK_X - 1)), hi = xy.x - x0;  // dx over the tile's columns
+    const float dy0 = xy.y - (float)(ty * BLOCK_Y + 4 * band0);
+    uint32_t m = 0;
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+        bool hit = false;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float dy = dy0 - (float)(4 * bb + r);
+            const float kdy = bc.k * dy;
+            const float e = __builtin_amdgcn_fmed3f(kdy, lo, hi) - kdy;  // the strip's column nearest the row minimum
+            const float q = __builtin_fmaf(bc.a * e, e, bc.dd * dy * dy);
+            hit = hit || q <= bc.t;
+        }
+        if (hit) m |= 1u << bb;
+    }
+    return m;
+}
 // Which of the bands band0 .. band0 + NB - 1 of tile (tx, ty) (band b = pixel rows 4b..4b+3 of the tile, 16
 // columns: the pixels of one wave's lanes, tile_wave.h) contain a pixel where alpha = min(0.99, o * exp(power))
 // >= 1/255 can hold. With d = mean - pixel, that is q(d) = a dx^2 + 2 b dx dy + c dy^2 <= t = 2 ln(255 o). Along
@@ -258,31 +296,7 @@ __device__ __forceinline__ void getRect(float2 p, int max_radius, uint32_t gx, u
 template <int NB>
 __device__ __forceinline__ uint32_t band_mask(float2 xy, float4 co, uint32_t tx, uint32_t ty, uint32_t band0)
 {
-    if (!(co.w * 255.0f >= 1.0f)) return 0u;  // even G = 1 gives alpha < 1/255
-    const float a = co.x, b = co.y, c = co.z;
-    if (!(a * c - b * b > 0.0f) || !(a > 0.0f)) return (1u << NB) - 1u;  // degenerate: every band
-    const float t = 2.0f * __logf(255.0f * co.w) * 1.002f + 0.02f;
-    const float x0 = (float)(tx * BLOCK_X);
-    const float lo = xy.x - (x0 + (float)(BLOCK_X - 1)), hi = xy.x - x0;  // dx over the tile's columns
-    // completed square: q = a (dx - k dy)^2 + (det / a) dy^2 with k = -b / a (no cancellation between large terms)
-    const float ra = __builtin_amdgcn_rcpf(a);
-    const float k = -b * ra, dd = (a * c - b * b) * ra;
-    const float dy0 = xy.y - (float)(ty * BLOCK_Y + 4 * band0);
-    uint32_t m = 0;
-#pragma unroll
-    for (int bb = 0; bb < NB; ++bb) {
-        bool hit = false;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float dy = dy0 - (float)(4 * bb + r);
-            const float kdy = k * dy;
-            const float e = __builtin_amdgcn_fmed3f(kdy, lo, hi) - kdy;  // the strip's column nearest the row minimum
-            const float q = __builtin_fmaf(a * e, e, dd * dy * dy);
-            hit = hit || q <= t;
-        }
-        if (hit) m |= 1u << bb;
-    }
-    return m;
+    return band_mask_of<NB>(band_consts(co), xy, tx, ty, band0);
 }
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }

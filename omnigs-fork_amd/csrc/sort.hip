@@ -711,6 +711,11 @@ __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* offsets, uin
     return lo;
 }
 
+#ifndef OMR_EMIT_OWN_MAX
+#define OMR_EMIT_OWN_MAX 256
+#endif
+constexpr uint32_t EMIT_OWN_MAX = OMR_EMIT_OWN_MAX;  // 0: every instance gathers its owner's record itself
+
 // Emission index: block_owner[B] = the depth rank owning slot B * EMIT_SLOTS (the rank whose slot range
 // [offsets[r-1], offsets[r]) contains it). One thread per rank; only ranks containing a block start write.
 __global__ __launch_bounds__(256) void emit_index_kernel(HostWords hw, int P, size_t L_cap, const uint32_t* count,
@@ -723,18 +728,11 @@ __global__ __launch_bounds__(256) void emit_index_kernel(HostWords hw, int P, si
     for (uint32_t B = (lo + EMIT_SLOTS - 1) / EMIT_SLOTS; B * EMIT_SLOTS < hi; ++B) block_owner[B] = (uint32_t)r;
 }
 
-// the tile and point-list entry of instance k of Gaussian gid (its tiles row-major over its rect)
-__device__ __forceinline__ void emit_one(const float4* splat, uint32_t gid, uint32_t k, uint32_t gx, uint32_t* key,
-                                         uint32_t* val)
+// instance k of a Gaussian whose rect is w tiles wide: row ky, column kx of the rect (row-major). k / w through the
+// f32 reciprocal (a u32 division is ~40 VALU): for k < 2^20 the truncated quotient is off by at most one, which the
+// remainder test corrects exactly
+__device__ __forceinline__ void rect_slot(uint32_t k, uint32_t w, uint32_t& kx, uint32_t& ky)
 {
-    const float4* rec = splat + (size_t)gid * SPLAT_F4;  // one 64-B line: rect, position, conic + opacity
-    const float4 rect = rec[3];  // {x0, y0, x1, y1} from preprocess (getRect)
-    const float4 pos = rec[0], co = rec[1];
-    const uint32_t x0 = __builtin_bit_cast(uint32_t, rect.x), y0 = __builtin_bit_cast(uint32_t, rect.y);
-    const uint32_t w = __builtin_bit_cast(uint32_t, rect.z) - x0;
-    // k / w through the f32 reciprocal (a u32 division is ~40 VALU): for k < 2^20 the truncated quotient is off by at
-    // most one, which the remainder test corrects exactly
-    uint32_t ky, kx;
     if (k < (1u << 20)) {
         ky = (uint32_t)((float)k * __builtin_amdgcn_rcpf((float)w));
         int rem = (int)k - (int)(ky * w);
@@ -745,6 +743,19 @@ __device__ __forceinline__ void emit_one(const float4* splat, uint32_t gid, uint
         ky = k / w;
         kx = k - ky * w;
     }
+}
+
+// the tile and point-list entry of instance k of Gaussian gid (its tiles row-major over its rect)
+__device__ __forceinline__ void emit_one(const float4* splat, uint32_t gid, uint32_t k, uint32_t gx, uint32_t* key,
+                                         uint32_t* val)
+{
+    const float4* rec = splat + (size_t)gid * SPLAT_F4;  // one 64-B line: rect, position, conic + opacity
+    const float4 rect = rec[3];  // {x0, y0, x1, y1} from preprocess (getRect)
+    const float4 pos = rec[0], co = rec[1];
+    const uint32_t x0 = __builtin_bit_cast(uint32_t, rect.x), y0 = __builtin_bit_cast(uint32_t, rect.y);
+    const uint32_t w = __builtin_bit_cast(uint32_t, rect.z) - x0;
+    uint32_t ky, kx;
+    rect_slot(k, w, kx, ky);
     const uint32_t tx = x0 + kx, ty = y0 + ky;
     *key = ty * gx + tx;
     // the bands of the tile this instance can reach (point list entry format, raster_common.h)
@@ -768,6 +779,11 @@ __global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap,
 {
     __shared__ uint32_t s_end[EMIT_SLOTS];
     __shared__ uint32_t s_start0;
+    // the block's owners themselves when there are few (EMIT_OWN_MAX): their record, band-mask constants and rect
+    // are gathered once per Gaussian, not once per instance
+    __shared__ float4 s_own_a[EMIT_OWN_MAX > 0 ? EMIT_OWN_MAX : 1];  // x, y, t, k
+    __shared__ float4 s_own_b[EMIT_OWN_MAX > 0 ? EMIT_OWN_MAX : 1];  // dd, a, x0 (bits), y0 (bits)
+    __shared__ uint2 s_own_c[EMIT_OWN_MAX > 0 ? EMIT_OWN_MAX : 1];   // rect width, Gaussian index
     const size_t L = live_count(L_cap, count);
     const uint32_t B = blockIdx.x;
     const size_t e0 = (size_t)B * EMIT_SLOTS;
@@ -776,8 +792,20 @@ __global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap,
     const uint32_t r_hi = e0 + EMIT_SLOTS < L ? block_owner[B + 1] + 1 : (uint32_t)P;  // exclusive
     const uint32_t nr = r_hi - r_lo;
     const bool staged = nr <= EMIT_SLOTS;  // block-uniform; more only with runs of empty (culled) segments
+    const bool owners = nr <= EMIT_OWN_MAX;  // block-uniform
     if (staged)
         for (uint32_t i = threadIdx.x; i < nr; i += EMIT_THREADS) s_end[i] = offsets[r_lo + i];
+    if (owners)
+        for (uint32_t i = threadIdx.x; i < nr; i += EMIT_THREADS) {
+            // an owner with an empty segment (culled: never written) is staged too and never read
+            const uint32_t gid = order[r_lo + i];
+            const float4* rec = splat + (size_t)gid * SPLAT_F4;
+            const float4 pos = rec[0], co = rec[1], rect = rec[3];
+            const BandConsts bc = band_consts(co);
+            s_own_a[i] = make_float4(pos.x, pos.y, bc.t, bc.k);
+            s_own_b[i] = make_float4(bc.dd, bc.a, rect.x, rect.y);
+            s_own_c[i] = make_uint2(__builtin_bit_cast(uint32_t, rect.z) - __builtin_bit_cast(uint32_t, rect.x), gid);
+        }
     if (threadIdx.x == 0) s_start0 = r_lo == 0 ? 0u : offsets[r_lo - 1];
     __syncthreads();
     const size_t eb = e0 + (size_t)threadIdx.x * EMIT_PER;
@@ -808,11 +836,27 @@ __global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap,
             kk[j] = e - (r == 0 ? 0u : offsets[r - 1]);
         }
     }
-    uint32_t gid[EMIT_PER], key[EMIT_PER], val[EMIT_PER];
+    uint32_t key[EMIT_PER], val[EMIT_PER];
+    if (owners) {
 #pragma unroll
-    for (int j = 0; j < EMIT_PER; ++j) gid[j] = order[rr[j]];
+        for (int j = 0; j < EMIT_PER; ++j) {
+            const uint32_t l = rr[j] - r_lo;
+            const float4 oa = s_own_a[l], ob = s_own_b[l];
+            const uint2 oc = s_own_c[l];
+            uint32_t kx, ky;
+            rect_slot(kk[j], oc.x, kx, ky);
+            const uint32_t tx = __builtin_bit_cast(uint32_t, ob.z) + kx, ty = __builtin_bit_cast(uint32_t, ob.w) + ky;
+            key[j] = ty * gx + tx;
+            const BandConsts bc = {oa.z, oa.w, ob.x, ob.y};
+            val[j] = oc.y | (band_mask_of<PL_BANDS>(bc, make_float2(oa.x, oa.y), tx, ty, 0) << PL_GID_BITS);
+        }
+    } else {
+        uint32_t gid[EMIT_PER];
 #pragma unroll
-    for (int j = 0; j < EMIT_PER; ++j) emit_one(splat, gid[j], kk[j], gx, &key[j], &val[j]);
+        for (int j = 0; j < EMIT_PER; ++j) gid[j] = order[rr[j]];
+#pragma unroll
+        for (int j = 0; j < EMIT_PER; ++j) emit_one(splat, gid[j], kk[j], gx, &key[j], &val[j]);
+    }
     uint8_t* row_valid = reinterpret_cast<uint8_t*>(binning + row_valid_offset(L));  // the backward's row map
     if (EMIT_PER % 4 == 0 && nmine == (uint32_t)EMIT_PER) {
 #pragma unroll
