@@ -880,32 +880,31 @@ __global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap,
     }
 }
 
-// identifyTileRanges (rasterizer_impl.cu:145-167). Four sorted keys per thread through one 16-B load (key arrays
-// are 16-B aligned), the predecessor of the first from the neighbouring lane.
-constexpr int RANGES_ITEMS = 4;
+// identifyTileRanges (rasterizer_impl.cu:145-167). The sorted keys of one 16-B load per thread (4 32-bit or 8 16-bit
+// keys; key arrays are 16-B aligned), the predecessor of the first from the neighbouring lane.
+template <typename K>
+constexpr int ranges_items() { return 16 / (int)sizeof(K); }
 template <typename K>
 __global__ __launch_bounds__(256) void tile_ranges_kernel(size_t L_cap, const uint32_t* count, const K* tiles,
                                                           uint2* ranges)
 {
+    constexpr int ITEMS = ranges_items<K>();
     const size_t L = live_count(L_cap, count);
-    const size_t i0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * RANGES_ITEMS;
+    const size_t i0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * ITEMS;
     if (i0 >= L) return;
-    uint32_t k[RANGES_ITEMS];
-    if (i0 + RANGES_ITEMS <= L) {
-        if (sizeof(K) == 4) {
-            const uint4 q = *reinterpret_cast<const uint4*>(tiles + i0);
-            k[0] = q.x; k[1] = q.y; k[2] = q.z; k[3] = q.w;
-        } else {
-            const uint2 q = *reinterpret_cast<const uint2*>(tiles + i0);
-            k[0] = q.x & 0xFFFFu; k[1] = q.x >> 16; k[2] = q.y & 0xFFFFu; k[3] = q.y >> 16;
-        }
+    uint32_t k[ITEMS];
+    if (i0 + ITEMS <= L) {
+        const uint4 q = *reinterpret_cast<const uint4*>(tiles + i0);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) k[j] = sizeof(K) == 4 ? w[j] : (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
     } else {
 #pragma unroll
-        for (int j = 0; j < RANGES_ITEMS; ++j) k[j] = i0 + j < L ? tiles[i0 + j] : 0u;
+        for (int j = 0; j < ITEMS; ++j) k[j] = i0 + j < L ? (uint32_t)tiles[i0 + j] : 0u;
     }
-    uint32_t prev = i0 == 0 ? 0u : tiles[i0 - 1];
+    uint32_t prev = i0 == 0 ? 0u : (uint32_t)tiles[i0 - 1];
 #pragma unroll
-    for (int j = 0; j < RANGES_ITEMS; ++j) {
+    for (int j = 0; j < ITEMS; ++j) {
         const size_t idx = i0 + j;
         if (idx >= L) break;
         const uint32_t curr = k[j];
@@ -1230,10 +1229,10 @@ void launch_tile_ranges(size_t L_cap, const uint32_t* count, const void* sorted_
 {
     if (L_cap == 0) return;
     if (keys16)
-        tile_ranges_kernel<<<div_up(L_cap, 256 * RANGES_ITEMS), 256, 0, s>>>(
+        tile_ranges_kernel<<<div_up(L_cap, 256 * ranges_items<uint16_t>()), 256, 0, s>>>(
             L_cap, count, static_cast<const uint16_t*>(sorted_tiles), ranges);
     else
-        tile_ranges_kernel<<<div_up(L_cap, 256 * RANGES_ITEMS), 256, 0, s>>>(
+        tile_ranges_kernel<<<div_up(L_cap, 256 * ranges_items<uint32_t>()), 256, 0, s>>>(
             L_cap, count, static_cast<const uint32_t*>(sorted_tiles), ranges);
 }
 
