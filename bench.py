@@ -122,13 +122,14 @@ def dist_check(args) -> int:
 def stage_bytes(stage, P, V, L, N, T, M=16, D=3):
     """Algorithmic HBM bytes of one launch of each stage (SURVEY.md §8(d) accounting)."""
     sh = 12 * (D + 1) ** 2
+    kb = 2 if T <= 65536 else 4  # tile-id bytes: 16-bit keys up to 65536 tiles (capi.hip: keys16)
     return {
         "preprocess": 28 * P + (40 + sh + 45) * V,
         "depth_sort": 4 * 2 * 8 * P,               # 4 passes x (key+value read + write)
         "scan": 16 * P,                            # tiles_touched read in depth and index order; two scans written
-        "emit": 8 * P + 12 * V + 8 * L,
-        "tile_sort": 2 * 2 * 8 * L,                # 2 passes x (tile id + index, read + write)
-        "tile_ranges": 4 * L + 16 * T,
+        "emit": 8 * P + 12 * V + (kb + 4) * L,
+        "tile_sort": 2 * 2 * (kb + 4) * L,         # 2 passes x (tile id + point-list entry, read + write)
+        "tile_ranges": kb * L + 16 * T,
         "render_forward": 40 * L + 20 * N + 8 * T,
         "render_backward": 40 * L + 20 * N + 8 * T + 88 * V,
         # tiles_touched + row_first + row_valid bytes + one 36-B sum row written per Gaussian; the marked 36-B
@@ -277,6 +278,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     compute_events = []  # per step: (start, end of this rank's forward + backward), before the exchange
     record = {"on": False}
+    COMPUTE_EVENT_STEPS = 3
 
     LT = R.libtorch_boundary() if args.boundary == "libtorch" else None
 
@@ -310,7 +312,11 @@ def main():
             par.allreduce_(grads, info, average=False, bucket_bytes=bucket)
 
     def step():
-        if record["on"]:
+        # per-rank compute time (N > 1) from the first COMPUTE_EVENT_STEPS timed steps only: every event record ends
+        # in a system-scope release (an L2 writeback, ~5 us of GPU idle), so timing every step would
+        # slow the steps it measures
+        timed = record["on"] and len(compute_events) < COMPUTE_EVENT_STEPS
+        if timed:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record(stream)
         if LT is not None:
@@ -322,7 +328,7 @@ def main():
             R.RasterizeGaussiansBackwardCUDA(bg, means3D, radii, empty, scales, rots, 1.0, empty, view, proj,
                                              cam.tanfovx, cam.tanfovy, dL_dout, shs, g.sh_degree, campos, gb, nr, bb,
                                              ib, cam.camera_type, out=out, **bwd_kwargs)
-        if record["on"]:
+        if timed:
             ev[1].record(stream)
             compute_events.append(ev)
         exchange()
