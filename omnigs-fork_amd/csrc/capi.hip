@@ -685,12 +685,18 @@ int backward_impl(const BackwardIn& in)
     ga.clamped = g.clamped;
     ga.row_sums = g.row_sums;
     ga.conic_op = g.conic_op;
-    { StageScope st_(ST_ROW_SUMS, s); launch_row_sums(in.P, g.row_first, g.tiles_touched, g.huge_list, g.counters + 2, b.inst_grad, b.row_valid, (uint32_t)in.R, g.row_sums, in.dL_dcolor, s); }
-    if (colors_event) OMR_HIP(hipEventRecord(colors_event, s));  // dL_dcolor is final from here on
     ga.dL_dmean2D = in.dL_dmean2D; ga.dL_dconic = in.dL_dconic; ga.dL_dopacity = in.dL_dopacity; ga.dL_dcolor = in.dL_dcolor;
     ga.dL_dmean3D = in.dL_dmean3D; ga.dL_dcov3D = in.dL_dcov3D; ga.dL_dsh = in.M > 0 ? in.dL_dsh : nullptr;
     ga.dL_dscale = in.dL_dscale; ga.dL_drot = in.dL_drot; ga.dpx_dt = in.dpx_dt; ga.dpy_dt = in.dpy_dt;
     if (!in.shs) ga.shs = nullptr;
+    {
+        StageScope st_(ST_ROW_SUMS, s);
+        launch_row_sums(0, in.P, true, g.row_first, g.tiles_touched, g.huge_list, g.counters + 2, b.inst_grad,
+                        b.row_valid, (uint32_t)in.R, g.row_sums, in.dL_dcolor, s);
+    }
+    if (colors_event) OMR_HIP(hipEventRecord(colors_event, s));  // dL_dcolor is final from here on
+    ga.g_begin = 0;
+    ga.g_end = in.P;
     { StageScope st_(ST_GAUSS_BWD, s, true); launch_gaussian_backward(in.camera_type, ga, s, st_.start(), st_.stop()); }
     if (int e = hip_check("backward")) return e;
     OMR_HIP(timed_wait(hs->bwd, s, RS_BWD_WAIT_NS));

@@ -260,9 +260,9 @@ __device__ __forceinline__ void add_marked_row(float* acc, const float* __restri
 }
 
 struct RowSumArgs {
-    int P;
+    int g_begin, g_end;     // the Gaussians [g_begin, g_end) of this launch (g_begin a multiple of 256)
+    uint32_t huge_blocks;   // RS_HUGE_BLOCKS workgroups for the huge Gaussians at the start of the grid, or 0
     uint32_t R;
-    uint32_t main_blocks;
     const uint32_t* row_first;
     const uint32_t* tiles_touched;
     const uint32_t* huge_list;
@@ -315,18 +315,18 @@ __device__ __forceinline__ void huge_row_sums(const RowSumArgs& a, uint32_t hb, 
 __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
 {
     __shared__ float s_rows_all[4][RS_ROWS * GRAD_ROW];  // row-major, 9 floats per row (odd stride: no conflicts)
-    if (blockIdx.x < RS_HUGE_BLOCKS) {  // dispatched first: the huge Gaussians overlap the rest of the grid
+    if (blockIdx.x < a.huge_blocks) {  // dispatched first: the huge Gaussians overlap the rest of the grid
         huge_row_sums(a, blockIdx.x, &s_rows_all[0][0]);
         return;
     }
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const int g0 = (int)((blockIdx.x - RS_HUGE_BLOCKS) * 256u + wv * 64u);
-    if (g0 >= a.P) return;  // wave-uniform
+    const int g0 = a.g_begin + (int)((blockIdx.x - a.huge_blocks) * 256u + wv * 64u);
+    if (g0 >= a.g_end) return;  // wave-uniform
     float* s_rows = s_rows_all[wv];
     const int idx = g0 + (int)lane;
     uint32_t n = 0, s = 0;
     bool huge = false;
-    if (idx < a.P) {
+    if (idx < a.g_end) {
         n = a.tiles_touched[idx];
         s = a.row_first[idx];
         huge = n > ROW_SUM_HUGE;  // summed by the workgroups at the end of the grid
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
         }
         wave_sync();  // the next chunk overwrites the staging rows
     }
-    if (idx < a.P && !huge) {
+    if (idx < a.g_end && !huge) {
         float* out = a.row_sums + (size_t)idx * GRAD_ROW;
 #pragma unroll
         for (int c = 0; c < GRAD_ROW; ++c) out[c] = acc[c];
@@ -645,17 +645,17 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
     constexpr bool STAGED = MC == 16 && OMR_GBWD_STAGE;
     __shared__ float4 s_stage[4][STAGED ? stage_f4<SH_F4>() : 1];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const int wave_first = (int)(blockIdx.x * 256u + wv * 64u);
-    if (wave_first >= a.P) return;  // wave-uniform
+    const int wave_first = a.g_begin + (int)(blockIdx.x * 256u + wv * 64u);
+    if (wave_first >= a.g_end) return;  // wave-uniform
     const int idx = wave_first + (int)lane;
     float g[GRAD_ROW];
     float4 co = make_float4(0.f, 0.f, 0.f, 0.f);  // conic + opacity of the render record (raw-moment rows)
-    if (idx < a.P) {
+    if (idx < a.g_end) {
 #pragma unroll
         for (int c = 0; c < GRAD_ROW; ++c) g[c] = a.row_sums[(size_t)idx * GRAD_ROW + c];
         if (OMR_BWD_RAW_MOMENTS) co = a.conic_op[idx];
     }
-    const bool valid = idx < a.P;
+    const bool valid = idx < a.g_end;
     const bool vis = valid && a.radii[idx] > 0;
     float4* stage = s_stage[wv];
     // MC == 16 only (the MC == 0 path reads and writes the rows itself)
@@ -773,15 +773,17 @@ void launch_sh_grad_from_colors(int P, int D, int M, int nviews, const float* me
                                                            dc_stride, dL_dsh);
 }
 
-void launch_row_sums(int P, const uint32_t* row_first, const uint32_t* tiles_touched, const uint32_t* huge_list,
-                     const uint32_t* huge_count, const float* inst_grad, const uint8_t* row_valid, uint32_t R,
-                     float* row_sums, float* dL_dcolor, hipStream_t s)
+void launch_row_sums(int g_begin, int g_end, bool huge, const uint32_t* row_first, const uint32_t* tiles_touched,
+                     const uint32_t* huge_list, const uint32_t* huge_count, const float* inst_grad,
+                     const uint8_t* row_valid, uint32_t R, float* row_sums, float* dL_dcolor, hipStream_t s)
 {
-    if (P <= 0) return;
+    if (g_end <= g_begin && !huge) return;
     RowSumArgs a;
-    a.P = P;
+    a.g_begin = g_begin;
+    a.g_end = g_end;
+    a.huge_blocks = huge ? RS_HUGE_BLOCKS : 0u;
     a.R = R;
-    a.main_blocks = div_up(P, 256);  // after the RS_HUGE_BLOCKS huge-Gaussian workgroups
+    const uint32_t main_blocks = g_end > g_begin ? div_up(g_end - g_begin, 256) : 0u;  // after the huge workgroups
     a.row_first = row_first;
     a.tiles_touched = tiles_touched;
     a.huge_list = huge_list;
@@ -790,14 +792,14 @@ void launch_row_sums(int P, const uint32_t* row_first, const uint32_t* tiles_tou
     a.row_valid = row_valid;
     a.row_sums = row_sums;
     a.dL_dcolor = dL_dcolor;
-    row_sum_kernel<<<a.main_blocks + RS_HUGE_BLOCKS, 256, 0, s>>>(a);
+    row_sum_kernel<<<main_blocks + a.huge_blocks, 256, 0, s>>>(a);
 }
 
 void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s, hipEvent_t ev_start,
                               hipEvent_t ev_stop)
 {
-    if (a.P <= 0) return;
-    const dim3 grid(div_up(a.P, 256));
+    if (a.g_end <= a.g_begin) return;
+    const dim3 grid(div_up(a.g_end - a.g_begin, 256));
     const bool m16 = a.M == 16 && (reinterpret_cast<uintptr_t>(a.dL_dsh) % 16) == 0 &&
                      (reinterpret_cast<uintptr_t>(a.shs) % 16) == 0;
     auto k = camera_type == CAM_LONLAT ? (m16 ? gaussian_bwd_kernel<CAM_LONLAT, 16> : gaussian_bwd_kernel<CAM_LONLAT, 0>)

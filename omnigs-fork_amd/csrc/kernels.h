@@ -171,6 +171,7 @@ int omr_debug_stamps_bwd(uint64_t* dst, size_t bytes);  // diagnostic builds onl
 // gaussian_bwd.hip
 struct GaussBwdArgs {
     int P, D, M, W, H;
+    int g_begin, g_end;  // the Gaussians of this launch, [g_begin, g_end) (g_begin a multiple of 256)
     const float* means3D;
     const int* radii;
     const float* shs;
@@ -202,10 +203,11 @@ void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_
 // Per-Gaussian sums of the render backward's instance rows: Gaussian i owns rows [row_first[i], row_first[i] +
 // tiles_touched[i]) of inst_grad (index-order numbering, launch_forward_scans); only rows marked in row_valid are read.
 // Gaussians in huge_list (*huge_count of them) are summed by whole workgroups. Also writes dL_dcolor [P][3] (the
-// colour part of the sums; zeros for culled Gaussians), which gaussian_bwd then leaves alone.
-void launch_row_sums(int P, const uint32_t* row_first, const uint32_t* tiles_touched, const uint32_t* huge_list,
-                     const uint32_t* huge_count, const float* inst_grad, const uint8_t* row_valid, uint32_t R,
-                     float* row_sums, float* dL_dcolor, hipStream_t s);
+// colour part of the sums; zeros for culled Gaussians), which gaussian_bwd then leaves alone. One launch covers the
+// Gaussians [g_begin, g_end); huge = it also sums the huge_list ones (the first launch of a split backward).
+void launch_row_sums(int g_begin, int g_end, bool huge, const uint32_t* row_first, const uint32_t* tiles_touched,
+                     const uint32_t* huge_list, const uint32_t* huge_count, const float* inst_grad,
+                     const uint8_t* row_valid, uint32_t R, float* row_sums, float* dL_dcolor, hipStream_t s);
 // view-parallel DP: dL_dsh[P,M,3] = sum over views of dL/dsh rebuilt from dL_dcolors [nviews][P][3] + campos [nviews][3]
 // view v's colour gradient at dL_dcolors + v * dc_stride, its camera position at campos + v * cp_stride (floats)
 void launch_sh_grad_from_colors(int P, int D, int M, int nviews, const float* means3D, const float* shs,
