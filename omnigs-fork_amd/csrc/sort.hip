@@ -513,8 +513,12 @@ constexpr int LB_WINDOW = OMR_LB_WINDOW;  // predecessors read per look-back rou
 // keys per onesweep block: 4096, or 2048 for sorts of fewer than OS_SMALL_N keys, which then spread over more blocks
 // (config B: depth sort of 100 k keys 0.059 -> 0.050 ms, tile sort of 0.35 M 0.048 -> 0.044; at config C's 1 M-key
 // depth sort 2048-key tiles are slower, 0.110 vs 0.095 ms)
-constexpr int OS_TILE = SORT_THREADS * 16;
-constexpr int OS_TILE_SMALL = SORT_THREADS * 8;
+#ifndef OMR_OS_THREADS
+#define OMR_OS_THREADS 512
+#endif
+constexpr int OS_THREADS = OMR_OS_THREADS;  // block size of the onesweep passes
+constexpr int OS_TILE = 4096;
+constexpr int OS_TILE_SMALL = 2048;
 #ifndef OMR_OS_SMALL_N
 #define OMR_OS_SMALL_N (1u << 19)
 #endif
@@ -575,19 +579,19 @@ __device__ __forceinline__ uint32_t lb_load(const uint32_t* p)
 
 // one pass: status = this pass's [blocks][RADIX] words (zeroed), ghist = its digit totals, ticket = its tile counter
 template <typename K, int TILE_N>
-__global__ __launch_bounds__(SORT_THREADS) void onesweep_kernel(const K* keys_in, const uint32_t* vals_in,
+__global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, const uint32_t* vals_in,
                                                                 K* keys_out, uint32_t* vals_out, size_t n_cap,
                                                                 const uint32_t* count, char* canon, int shift,
                                                                 uint32_t* status, const uint32_t* ghist,
                                                                 uint32_t* ticket, uint32_t* err)
 {
-    constexpr int WAVES = SORT_THREADS / 64;
+    constexpr int WAVES = OS_THREADS / 64;
     constexpr int PER_WAVE = TILE_N / WAVES;
     constexpr int ROUNDS = PER_WAVE / 64;
     __shared__ uint32_t s_whist[WAVES][RADIX];  // running digit counts per wave, then per-wave digit offsets
     __shared__ uint32_t s_dstart[RADIX];        // block-local start of each digit's run
     __shared__ uint32_t s_gbase[RADIX];         // global start of this block's run of each digit
-    __shared__ uint32_t s_wave[SORT_THREADS / 64];
+    __shared__ uint32_t s_wave[OS_THREADS / 64];
     __shared__ K s_k[TILE_N];
     __shared__ uint32_t s_v[TILE_N];
     __shared__ uint32_t s_vb;
@@ -596,14 +600,15 @@ __global__ __launch_bounds__(SORT_THREADS) void onesweep_kernel(const K* keys_in
     const size_t n = live_count(n_cap, count);
     if (canon) vals_out = reinterpret_cast<uint32_t*>(canon + canonical_list_offset(n));
     const uint32_t w = tid >> 6, lane = tid & 63;
-#pragma unroll
-    for (int q = 0; q < WAVES; ++q) s_whist[q][tid] = 0;
+    static_assert(OS_THREADS % RADIX == 0, "thread = digit phases");
+    const bool dig = tid < RADIX;  // this thread also owns digit tid in the per-digit phases
+    for (uint32_t i = tid; i < (uint32_t)(WAVES * RADIX); i += OS_THREADS) (&s_whist[0][0])[i] = 0;
     __syncthreads();
     const uint32_t vb = s_vb;
     const size_t tile0 = (size_t)vb * TILE_N;
     if (tile0 >= n) return;  // block-uniform; no block looks back at a tile past the live count
     uint32_t total_unused;
-    const uint32_t gstart = block_exclusive_scan(ghist[tid], s_wave, &total_unused);  // thread = digit
+    const uint32_t gstart = block_exclusive_scan<OS_THREADS>(dig ? ghist[tid] : 0u, s_wave, &total_unused);
     const size_t base = tile0 + (size_t)w * PER_WAVE + lane;
     uint32_t k[ROUNDS], v[ROUNDS], lr[ROUNDS];
 #pragma unroll
@@ -633,50 +638,55 @@ __global__ __launch_bounds__(SORT_THREADS) void onesweep_kernel(const K* keys_in
     __syncthreads();
     {   // thread = digit: per-wave exclusive offsets, block-local digit starts, then the look-back
         uint32_t run = 0;
+        if (dig) {
 #pragma unroll
-        for (int q = 0; q < WAVES; ++q) {
-            const uint32_t c = s_whist[q][tid];
-            s_whist[q][tid] = run;
-            run += c;
+            for (int q = 0; q < WAVES; ++q) {
+                const uint32_t c = s_whist[q][tid];
+                s_whist[q][tid] = run;
+                run += c;
+            }
         }
         uint32_t total;
-        s_dstart[tid] = block_exclusive_scan(run, s_wave, &total);
-        uint32_t* mine = status + (size_t)vb * RADIX + tid;
-        uint32_t excl = 0;
-        if (vb == 0) {
-            lb_store(mine, LB_PRE | run);
-        } else {
-            lb_store(mine, LB_AGG | run);
-            // look back LB_WINDOW blocks per round trip: blocks j-1, j-2, ... (nearest first) until a PRE word;
-            // an unpublished word ends the window and is polled again
-            uint32_t j = vb, spins = 0;
-            while (true) {
-                uint32_t st[LB_WINDOW];
+        const uint32_t ex = block_exclusive_scan<OS_THREADS>(run, s_wave, &total);
+        if (dig) {
+            s_dstart[tid] = ex;
+            uint32_t* mine = status + (size_t)vb * RADIX + tid;
+            uint32_t excl = 0;
+            if (vb == 0) {
+                lb_store(mine, LB_PRE | run);
+            } else {
+                lb_store(mine, LB_AGG | run);
+                // look back LB_WINDOW blocks per round trip: blocks j-1, j-2, ... (nearest first) until a PRE word;
+                // an unpublished word ends the window and is polled again
+                uint32_t j = vb, spins = 0;
+                while (true) {
+                    uint32_t st[LB_WINDOW];
 #pragma unroll
-                for (int q = 0; q < LB_WINDOW; ++q)
-                    st[q] = j > (uint32_t)q ? lb_load(status + (size_t)(j - 1 - q) * RADIX + tid) : LB_PRE;
-                uint32_t used = 0;
-                bool done = false;
+                    for (int q = 0; q < LB_WINDOW; ++q)
+                        st[q] = j > (uint32_t)q ? lb_load(status + (size_t)(j - 1 - q) * RADIX + tid) : LB_PRE;
+                    uint32_t used = 0;
+                    bool done = false;
 #pragma unroll
-                for (int q = 0; q < LB_WINDOW; ++q) {
-                    if (done || used != (uint32_t)q || (st[q] & ~LB_COUNT) == 0) continue;
-                    excl += st[q] & LB_COUNT;
-                    ++used;
-                    done = (st[q] & LB_PRE) != 0;  // block 0 always publishes PRE: j never passes it
-                }
-                if (done) break;
-                j -= used;
-                if (used == 0) {
-                    if (++spins > LB_SPIN_MAX) {
-                        atomicOr(err, 1u);
-                        break;
+                    for (int q = 0; q < LB_WINDOW; ++q) {
+                        if (done || used != (uint32_t)q || (st[q] & ~LB_COUNT) == 0) continue;
+                        excl += st[q] & LB_COUNT;
+                        ++used;
+                        done = (st[q] & LB_PRE) != 0;  // block 0 always publishes PRE: j never passes it
                     }
-                    __builtin_amdgcn_s_sleep(1);
+                    if (done) break;
+                    j -= used;
+                    if (used == 0) {
+                        if (++spins > LB_SPIN_MAX) {
+                            atomicOr(err, 1u);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
                 }
+                lb_store(mine, LB_PRE | (excl + run));
             }
-            lb_store(mine, LB_PRE | (excl + run));
+            s_gbase[tid] = gstart + excl;
         }
-        s_gbase[tid] = gstart + excl;
     }
     __syncthreads();
 #pragma unroll
@@ -690,7 +700,7 @@ __global__ __launch_bounds__(SORT_THREADS) void onesweep_kernel(const K* keys_in
     }
     __syncthreads();
     const uint32_t nvalid = (uint32_t)min((size_t)TILE_N, n - tile0);
-    for (uint32_t j = tid; j < nvalid; j += SORT_THREADS) {
+    for (uint32_t j = tid; j < nvalid; j += OS_THREADS) {
         const uint32_t kk = s_k[j];
         const uint32_t d = (kk >> shift) & (RADIX - 1);
         const uint32_t dst = s_gbase[d] + (j - s_dstart[d]);
@@ -1142,7 +1152,7 @@ int radix_sort_pairs(K* key_a, K* key_b, uint32_t* val_a, uint32_t* val_b, uint3
         for (int p = 0; p < passes; ++p) {
             const bool last = p == passes - 1;
             auto kern = os_tile(n) == OS_TILE ? onesweep_kernel<K, OS_TILE> : onesweep_kernel<K, OS_TILE_SMALL>;
-            kern<<<nb, SORT_THREADS, 0, s>>>(ki, vi, ko, vo, n, count, last ? canon : nullptr,
+            kern<<<nb, OS_THREADS, 0, s>>>(ki, vi, ko, vo, n, count, last ? canon : nullptr,
                                             (first_pass + p) * RADIX_BITS, status + (size_t)p * nb * RADIX,
                                             ghist + (size_t)p * RADIX, tickets + p, err);
             std::swap(ki, ko);
