@@ -272,6 +272,12 @@ constexpr uint32_t SELF_SCAN_MAX_BLOCKS = 512;
 constexpr int SORT_THREADS_LARGE = OMR_SORT_THREADS_LARGE;  // block size of the multi-launch passes of large sorts
 constexpr int SORT_ITEMS_LARGE = OMR_SORT_ITEMS_LARGE;      // items per thread there (8192-key tiles)
 constexpr size_t SORT_LARGE_MIN = OMR_SORT_LARGE_MIN;
+// block shape of the multi-launch passes below the large-sort threshold: SORT_TILE (4096) keys either way
+#ifndef OMR_SORT_THREADS_S
+#define OMR_SORT_THREADS_S 512
+#endif
+constexpr int SORT_THREADS_S = OMR_SORT_THREADS_S;
+constexpr int SORT_ITEMS_S = SORT_TILE / SORT_THREADS_S;
 // 16-bit keys take the large tiles from 4 M keys on (config C's 7.9 M-key tile sort: 0.1315 -> 0.1217 ms; with
 // 32-bit keys 8192-key tiles are slower there, 0.152 vs 0.137 ms)
 #ifndef OMR_SORT_LARGE_MIN16
@@ -1176,9 +1182,9 @@ int radix_sort_pairs(K* key_a, K* key_b, uint32_t* val_a, uint32_t* val_b, uint3
                 radix_downsweep_kernel<K, true, SORT_ITEMS_LARGE, SORT_THREADS_LARGE><<<nb, SORT_THREADS_LARGE, 0, s>>>(
                     ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
             } else {
-                radix_upsweep_kernel<K, true, SORT_ITEMS, SORT_THREADS><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb,
+                radix_upsweep_kernel<K, true, SORT_ITEMS_S, SORT_THREADS_S><<<nb, SORT_THREADS_S, 0, s>>>(ki, n, count, shift, hist, nb,
                                                                                   nullptr, 0);
-                radix_downsweep_kernel<K, true, SORT_ITEMS, SORT_THREADS><<<nb, SORT_THREADS, 0, s>>>(
+                radix_downsweep_kernel<K, true, SORT_ITEMS_S, SORT_THREADS_S><<<nb, SORT_THREADS_S, 0, s>>>(
                     ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
             }
         } else {
@@ -1190,7 +1196,7 @@ int radix_sort_pairs(K* key_a, K* key_b, uint32_t* val_a, uint32_t* val_b, uint3
                 radix_upsweep_kernel<K, false, SORT_ITEMS_LARGE, SORT_THREADS_LARGE><<<nb, SORT_THREADS_LARGE, 0, s>>>(
                     ki, n, count, shift, hist, nb, scan_partials, 2 * nbs + 2);
             else
-                radix_upsweep_kernel<K, false, SORT_ITEMS, SORT_THREADS><<<nb, SORT_THREADS, 0, s>>>(ki, n, count, shift, hist, nb,
+                radix_upsweep_kernel<K, false, SORT_ITEMS_S, SORT_THREADS_S><<<nb, SORT_THREADS_S, 0, s>>>(ki, n, count, shift, hist, nb,
                                                                                    scan_partials, 2 * nbs + 2);
             scan_lookback_kernel<<<nbs, SCAN_THREADS, 0, s>>>(hist, hist, (size_t)RADIX * nb, lb, lb_ticket,
                                                              err_out ? err_out : lb_ticket + 1);
@@ -1198,7 +1204,7 @@ int radix_sort_pairs(K* key_a, K* key_b, uint32_t* val_a, uint32_t* val_b, uint3
                 radix_downsweep_kernel<K, false, SORT_ITEMS_LARGE, SORT_THREADS_LARGE><<<nb, SORT_THREADS_LARGE, 0, s>>>(
                     ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
             else
-                radix_downsweep_kernel<K, false, SORT_ITEMS, SORT_THREADS><<<nb, SORT_THREADS, 0, s>>>(
+                radix_downsweep_kernel<K, false, SORT_ITEMS_S, SORT_THREADS_S><<<nb, SORT_THREADS_S, 0, s>>>(
                     ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
         }
         std::swap(ki, ko);
