@@ -31,9 +31,12 @@ constexpr int RADIX_BITS = 8;
 constexpr int RADIX = 1 << RADIX_BITS;
 constexpr int DEPTH_SORT_PASSES = 4;  // the depth sort's 32-bit keys (float bits of the depth)
 // scan geometry
-constexpr int SCAN_THREADS = 256;
-constexpr int SCAN_ITEMS = 16;
-constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
+#ifndef OMR_SCAN_THREADS
+#define OMR_SCAN_THREADS 1024
+#endif
+constexpr int SCAN_THREADS = OMR_SCAN_THREADS;
+constexpr int SCAN_TILE = 4096;
+constexpr int SCAN_ITEMS = SCAN_TILE / SCAN_THREADS;
 
 // per-instance gradient row written by the render backward (render_bwd.hip) and reduced per Gaussian
 // (gaussian_bwd.hip). With OMR_BWD_RAW_MOMENTS (default) the row holds the instance's raw pixel-weight moments
