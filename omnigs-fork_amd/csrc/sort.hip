@@ -536,6 +536,10 @@ __host__ __device__ inline size_t os_tile(size_t n) { return n < OS_SMALL_N ? OS
 // histogram blocks: each digit total takes <= this many global adds (64 / 128 / 256 / 512 blocks at 1 M keys:
 // 0.109 / 0.098 / 0.0945 / 0.098 ms for the whole depth sort)
 constexpr uint32_t OS_HIST_BLOCKS = OMR_OS_HIST_BLOCKS;
+#ifndef OMR_OS_HIST_THREADS
+#define OMR_OS_HIST_THREADS 1024
+#endif
+constexpr int OS_HIST_THREADS = OMR_OS_HIST_THREADS;
 // Onesweep only for sorts of at most this many tiles (the depth sort up to 2 M Gaussians: 0.100 vs 0.122 ms at
 // 1 M). Past that the look-back chains and the same-address ticket / histogram adds cost more than the launches
 // they save (the 7.9 M-instance tile sort: 0.185 vs 0.142 ms), and the upsweep / scan / downsweep passes run.
@@ -553,7 +557,7 @@ __host__ __device__ inline size_t onesweep_words(size_t n, int passes)
 // digit totals of every pass (ghist, zeroed by the caller; OS_HIST_BLOCKS blocks, grid-stride, so every total
 // takes at most OS_HIST_BLOCKS same-address global adds) and the zeroed status words of every pass
 template <typename K>
-__global__ __launch_bounds__(SORT_THREADS) void onesweep_hist_kernel(const K* keys, size_t n_cap,
+__global__ __launch_bounds__(OS_HIST_THREADS) void onesweep_hist_kernel(const K* keys, size_t n_cap,
                                                                      const uint32_t* count, int first_pass, int passes,
                                                                      uint32_t* status, size_t status_words,
                                                                      uint32_t* ghist)
@@ -561,17 +565,18 @@ __global__ __launch_bounds__(SORT_THREADS) void onesweep_hist_kernel(const K* ke
     __shared__ uint32_t s_h[4][RADIX];
     const size_t n = live_count(n_cap, count);
     const uint32_t tid = threadIdx.x;
-    const size_t stride = (size_t)gridDim.x * SORT_THREADS;
-    for (size_t i = (size_t)blockIdx.x * SORT_THREADS + tid; i < status_words; i += stride) status[i] = 0;
-    for (int p = 0; p < passes; ++p) s_h[p][tid] = 0;
+    const size_t stride = (size_t)gridDim.x * OS_HIST_THREADS;
+    for (size_t i = (size_t)blockIdx.x * OS_HIST_THREADS + tid; i < status_words; i += stride) status[i] = 0;
+    for (uint32_t i = tid; i < 4u * RADIX; i += OS_HIST_THREADS) (&s_h[0][0])[i] = 0;
     __syncthreads();
-    for (size_t i = (size_t)blockIdx.x * SORT_THREADS + tid; i < n; i += stride) {
+    for (size_t i = (size_t)blockIdx.x * OS_HIST_THREADS + tid; i < n; i += stride) {
         const uint32_t key = keys[i];
         for (int p = 0; p < passes; ++p) atomicAdd(&s_h[p][(key >> ((first_pass + p) * RADIX_BITS)) & (RADIX - 1)], 1u);
     }
     __syncthreads();
-    for (int p = 0; p < passes; ++p)
-        if (s_h[p][tid]) atomicAdd(&ghist[p * RADIX + tid], s_h[p][tid]);
+    if (tid < RADIX)
+        for (int p = 0; p < passes; ++p)
+            if (s_h[p][tid]) atomicAdd(&ghist[p * RADIX + tid], s_h[p][tid]);
 }
 
 __device__ __forceinline__ void lb_store(uint32_t* p, uint32_t v)
@@ -1153,7 +1158,7 @@ int radix_sort_pairs(K* key_a, K* key_b, uint32_t* val_a, uint32_t* val_b, uint3
         uint32_t* tickets = ghist + (size_t)passes * RADIX;
         uint32_t* err = err_out ? err_out : tickets + passes;
         if (!scratch_zeroed) (void)hipMemsetAsync(ghist, 0, ((size_t)passes * (RADIX + 1) + 1) * sizeof(uint32_t), s);
-        onesweep_hist_kernel<K><<<std::min(div_up(n, SORT_THREADS), OS_HIST_BLOCKS), SORT_THREADS, 0, s>>>(
+        onesweep_hist_kernel<K><<<std::min(div_up(n, OS_HIST_THREADS), OS_HIST_BLOCKS), OS_HIST_THREADS, 0, s>>>(
             ki, n, count, first_pass, passes, status, (size_t)passes * nb * RADIX, ghist);
         for (int p = 0; p < passes; ++p) {
             const bool last = p == passes - 1;
