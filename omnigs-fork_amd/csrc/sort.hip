@@ -732,6 +732,9 @@ __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* offsets, uin
     return lo;
 }
 
+#ifndef OMR_EMIT_FAST_MASK
+#define OMR_EMIT_FAST_MASK 1
+#endif
 #ifndef OMR_EMIT_OWN_MAX
 #define OMR_EMIT_OWN_MAX 256
 #endif
@@ -802,9 +805,9 @@ __global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap,
     __shared__ uint32_t s_start0;
     // the block's owners themselves when there are few (EMIT_OWN_MAX): their record, band-mask constants and rect
     // are gathered once per Gaussian, not once per instance
-    __shared__ float4 s_own_a[EMIT_OWN_MAX > 0 ? EMIT_OWN_MAX : 1];  // x, y, t, k
-    __shared__ float4 s_own_b[EMIT_OWN_MAX > 0 ? EMIT_OWN_MAX : 1];  // dd, a, x0 (bits), y0 (bits)
-    __shared__ uint2 s_own_c[EMIT_OWN_MAX > 0 ? EMIT_OWN_MAX : 1];   // rect width, Gaussian index
+    __shared__ float4 s_own_a[EMIT_OWN_MAX > 0 ? EMIT_OWN_MAX : 1];  // x, y, t, k    | fast: x, y, k Dt, a k
+    __shared__ float4 s_own_b[EMIT_OWN_MAX > 0 ? EMIT_OWN_MAX : 1];  // dd, a, x0, y0 | fast: a dd, A t, 1/A, -
+    __shared__ uint4 s_own_c[EMIT_OWN_MAX > 0 ? EMIT_OWN_MAX : 1];   // x0, y0, rect width, Gaussian index
     const size_t L = live_count(L_cap, count);
     const uint32_t B = blockIdx.x;
     const size_t e0 = (size_t)B * EMIT_SLOTS;
@@ -823,9 +826,16 @@ __global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap,
             const float4* rec = splat + (size_t)gid * SPLAT_F4;
             const float4 pos = rec[0], co = rec[1], rect = rec[3];
             const BandConsts bc = band_consts(co);
-            s_own_a[i] = make_float4(pos.x, pos.y, bc.t, bc.k);
-            s_own_b[i] = make_float4(bc.dd, bc.a, rect.x, rect.y);
-            s_own_c[i] = make_uint2(__builtin_bit_cast(uint32_t, rect.z) - __builtin_bit_cast(uint32_t, rect.x), gid);
+            if (OMR_EMIT_FAST_MASK) {
+                const BandSpan sp = band_span_consts(bc);
+                s_own_a[i] = make_float4(pos.x, pos.y, sp.kDt, sp.ak);
+                s_own_b[i] = make_float4(sp.adt, sp.At, sp.invA, 0.f);
+            } else {
+                s_own_a[i] = make_float4(pos.x, pos.y, bc.t, bc.k);
+                s_own_b[i] = make_float4(bc.dd, bc.a, 0.f, 0.f);
+            }
+            s_own_c[i] = make_uint4(__builtin_bit_cast(uint32_t, rect.x), __builtin_bit_cast(uint32_t, rect.y),
+                                    __builtin_bit_cast(uint32_t, rect.z) - __builtin_bit_cast(uint32_t, rect.x), gid);
         }
     if (threadIdx.x == 0) s_start0 = r_lo == 0 ? 0u : offsets[r_lo - 1];
     __syncthreads();
@@ -863,13 +873,20 @@ __global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap,
         for (int j = 0; j < EMIT_PER; ++j) {
             const uint32_t l = rr[j] - r_lo;
             const float4 oa = s_own_a[l], ob = s_own_b[l];
-            const uint2 oc = s_own_c[l];
+            const uint4 oc = s_own_c[l];
             uint32_t kx, ky;
-            rect_slot(kk[j], oc.x, kx, ky);
-            const uint32_t tx = __builtin_bit_cast(uint32_t, ob.z) + kx, ty = __builtin_bit_cast(uint32_t, ob.w) + ky;
+            rect_slot(kk[j], oc.z, kx, ky);
+            const uint32_t tx = oc.x + kx, ty = oc.y + ky;
             key[j] = ty * gx + tx;
-            const BandConsts bc = {oa.z, oa.w, ob.x, ob.y};
-            val[j] = oc.y | (band_mask_of<PL_BANDS>(bc, make_float2(oa.x, oa.y), tx, ty, 0) << PL_GID_BITS);
+            uint32_t m;
+            if (OMR_EMIT_FAST_MASK) {
+                const BandSpan sp = {oa.z, oa.w, ob.x, ob.y, ob.z};
+                m = band_mask_span<PL_BANDS>(sp, make_float2(oa.x, oa.y), tx, ty);
+            } else {
+                const BandConsts bc = {oa.z, oa.w, ob.x, ob.y};
+                m = band_mask_of<PL_BANDS>(bc, make_float2(oa.x, oa.y), tx, ty, 0);
+            }
+            val[j] = oc.w | (m << PL_GID_BITS);
         }
     } else {
         uint32_t gid[EMIT_PER];
