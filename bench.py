@@ -361,15 +361,19 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     R.profile_reset()
-    # OMR_BENCH_LIVE=0 (diagnostic only: profiles/gaps.py): no events in the timed loop; the roofline then falls back
-    # to the per-stage pass's average
-    R.profile_enable(os.environ.get("OMR_BENCH_LIVE", "1") != "0", stages=[dom])
+    # The roofline kernel's launches are timed live on every LIVE_EVERY-th timed step (every step: sampling every
+    # 4th measured no faster, 1718-1721 vs 1721-1724 MP/s). OMR_BENCH_LIVE=0 (diagnostic only: profiles/gaps.py): no
+    # events in the timed loop; the roofline then falls back to the per-stage pass's average.
+    live_on = os.environ.get("OMR_BENCH_LIVE", "1") != "0"
+    LIVE_EVERY = 1
+    R.profile_enable(live_on, stages=[dom])
     R.runtime_stats_reset()
     torch.cuda.reset_peak_memory_stats(dev)
     mem0 = torch.cuda.memory_stats(dev)
     record["on"] = world > 1
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        R.profile_set_on(live_on and i % LIVE_EVERY == 0)
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -427,7 +431,8 @@ def main():
         lo = pmc.get(k, {}).get("hbm_bytes_lower")
         # traffic = (2 FETCH + WRITE): exact for 16-B/lane streams, an upper bound for gathers, which
         # profiles/calib_fetch.hip shows FETCH counting 1:1 (traffic_lower = FETCH + WRITE)
-        return {"stage": k, "avg_launch_ms": round(ms_k, 4), "algorithmic_bytes_per_launch": b,
+        return {"stage": k, "avg_launch_ms": round(ms_k, 4), "timed_launches": int(cnt_l) if live_ok else 0,
+                "algorithmic_bytes_per_launch": b,
                 "achieved_GBps": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": tr,
                 "traffic_lower": lo, "traffic_over_algorithmic": round(tr / b, 3) if (tr and b) else None,
                 "traffic_lower_over_algorithmic": round(lo / b, 3) if (lo and b) else None}
@@ -471,7 +476,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": d["achieved_GBps"], "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": d["frac"], "traffic": d["traffic"],
                      "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
-                     "avg_launch_ms": d["avg_launch_ms"],
+                     "avg_launch_ms": d["avg_launch_ms"], "timed_launches": d["timed_launches"],
                      "step_algorithmic_GBps": round(algo_total / (ms_per_step * 1e-3) / 1e9, 2),
                      "top_stages": [stage_entry(k) for k in ranked[:3]]},
         "stages_ms": {k: round(v, 4) for k, v in stage_avg.items()},

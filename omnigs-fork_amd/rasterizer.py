@@ -487,6 +487,11 @@ def profile_enable(on: bool = True, stages=None):
     lib().omr_profile_enable(1 if on else 0)
 
 
+def profile_set_on(on: bool):
+    """Turn the stage profiler on or off, keeping the stage mask (one cheap call per step)."""
+    lib().omr_profile_enable(1 if on else 0)
+
+
 def profile_reset():
     lib().omr_profile_reset()
 
