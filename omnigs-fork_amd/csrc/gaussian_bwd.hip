@@ -312,9 +312,42 @@ __device__ __forceinline__ void huge_row_sums(const RowSumArgs& a, uint32_t hb, 
     }
 }
 
+#ifndef OMR_RS_COMPACT
+#define OMR_RS_COMPACT 1
+#endif
+#if OMR_RS_COMPACT
+constexpr uint32_t RS_WIN = 512;  // rows whose marks a wave compacts at once (8 per lane, one 8-B load)
+#endif
+
+__device__ __forceinline__ uint32_t wave_exclusive_scan_u32(uint32_t x, uint32_t lane, uint32_t* total)
+{
+    uint32_t inc = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    *total = (uint32_t)__shfl((int)inc, 63, 64);
+    return inc - x;
+}
+
+// first position p in [lo, hi) of the sorted list with list[p] >= v
+__device__ __forceinline__ uint32_t lds_lower_bound(const uint32_t* list, uint32_t lo, uint32_t hi, uint32_t v)
+{
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (list[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
 __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
 {
     __shared__ float s_rows_all[4][RS_ROWS * GRAD_ROW];  // row-major, 9 floats per row (odd stride: no conflicts)
+#if OMR_RS_COMPACT
+    __shared__ uint32_t s_list_all[4][RS_WIN];
+#endif
     if (blockIdx.x < a.huge_blocks) {  // dispatched first: the huge Gaussians overlap the rest of the grid
         huge_row_sums(a, blockIdx.x, &s_rows_all[0][0]);
         return;
@@ -324,10 +357,10 @@ __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
     if (g0 >= a.g_end) return;  // wave-uniform
     float* s_rows = s_rows_all[wv];
     const int idx = g0 + (int)lane;
-    uint32_t n = 0, s = 0;
+    uint32_t n = 0, s = 0, n_all = 0;
     bool huge = false;
     if (idx < a.g_end) {
-        n = a.tiles_touched[idx];
+        n = n_all = a.tiles_touched[idx];
         s = a.row_first[idx];
         huge = n > ROW_SUM_HUGE;  // summed by the workgroups at the end of the grid
         if (huge || (n != 0 && (s >= a.R || n > a.R - s))) n = 0;  // the latter: never for a consistent forward
@@ -335,11 +368,106 @@ __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
     const uint32_t e = s + n;
     const uint32_t lo = __builtin_amdgcn_readfirstlane(wave_min_u32(n ? s : 0xFFFFFFFFu));
     const uint32_t hi = __builtin_amdgcn_readfirstlane(wave_max_u32(n ? e : 0u));
-    const bool is_long = n > RS_LONG;
     float acc[GRAD_ROW];
 #pragma unroll
     for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
 
+#if OMR_RS_COMPACT
+    // Sparse rows (config C: 24 % of the rows are marked, config E: 4 %): the wave compacts the marked rows of
+    // each 512-row window of its span into an LDS list (one 8-B load of marks per lane, a wave scan), then
+    // streams the list in chunks of RS_ROWS marked rows: one HBM round trip per 128 marked rows instead of one
+    // per 128 rows. Each Gaussian's marked rows are a contiguous run of the sorted list; the sums keep row order.
+    uint32_t* s_list = s_list_all[wv];
+    const uint64_t huges = __ballot(huge && idx < a.g_end && s < a.R);
+    for (uint32_t w0 = lo & ~7u; w0 < hi; w0 += RS_WIN) {  // lo > hi when the wave owns no rows
+        const uint32_t r0 = w0 + 8u * lane;
+        uint32_t m = 0;  // bit j: row r0 + j is marked, inside [lo, hi) and not a huge Gaussian's
+        if (r0 < hi) {
+            uint32_t fx = 0, fy = 0;
+            if (r0 + 8u <= a.R) {
+                const uint2 f = *reinterpret_cast<const uint2*>(a.row_valid + r0);  // row_valid is 256-B aligned
+                fx = f.x;
+                fy = f.y;
+            } else {
+                for (uint32_t j = 0; j < 8u && r0 + j < a.R; ++j)
+                    (j < 4 ? fx : fy) |= (uint32_t)a.row_valid[r0 + j] << (8u * (j & 3u));
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < 8u; ++j) {
+                const uint32_t r = r0 + j;
+                const uint32_t byte = ((j < 4 ? fx : fy) >> (8u * (j & 3u))) & 0xFFu;
+                if (byte != 0 && r >= lo && r < hi) m |= 1u << j;
+            }
+            for (uint64_t hb = huges; hb; hb &= hb - 1) {  // rare: a huge Gaussian's rows inside the span
+                const int jl = __builtin_ctzll(hb);
+                const uint32_t hs = __builtin_amdgcn_readlane(s, jl), he = hs + __builtin_amdgcn_readlane(n_all, jl);
+#pragma unroll
+                for (uint32_t j = 0; j < 8u; ++j)
+                    if (r0 + j >= hs && r0 + j < he) m &= ~(1u << j);
+            }
+        }
+        uint32_t total;
+        uint32_t k = wave_exclusive_scan_u32((uint32_t)__popc(m), lane, &total);
+        for (uint32_t mm = m; mm; mm &= mm - 1) s_list[k++] = r0 + (uint32_t)__builtin_ctz(mm);
+        wave_sync();
+        for (uint32_t c0 = 0; c0 < total; c0 += RS_ROWS) {
+            const uint32_t c1 = min(total, c0 + RS_ROWS);
+            float x[RS_Q][GRAD_ROW];
+#pragma unroll
+            for (int q = 0; q < RS_Q; ++q) {
+                const uint32_t p = c0 + (uint32_t)q * 64u + lane;
+#pragma unroll
+                for (int c = 0; c < GRAD_ROW; ++c) x[q][c] = 0.f;
+                add_marked_row(x[q], a.inst_grad, p < c1 ? s_list[p] : 0u, p < c1);
+            }
+#pragma unroll
+            for (int q = 0; q < RS_Q; ++q)
+#pragma unroll
+                for (int c = 0; c < GRAD_ROW; ++c) s_rows[(q * 64 + lane) * GRAD_ROW + c] = x[q][c];
+            // this lane's Gaussian's marked rows in the chunk: list positions [pa, pb)
+            const uint32_t first = s_list[c0], last = s_list[c1 - 1];
+            uint32_t pa = c0, pb = c0;
+            if (n != 0 && s <= last && e > first) {
+                pa = lds_lower_bound(s_list, c0, c1, s);
+                pb = lds_lower_bound(s_list, pa, c1, e);
+            }
+            wave_sync();
+            const bool is_long = pb - pa > RS_LONG;
+            if (!is_long)
+                for (uint32_t j = pa - c0; j < pb - c0; ++j)
+#pragma unroll
+                    for (int c = 0; c < GRAD_ROW; ++c) acc[c] += s_rows[j * GRAD_ROW + c];
+            // long runs: the whole wave, one Gaussian at a time
+            uint64_t longs = __ballot(is_long);
+            while (longs) {
+                const int jl = __builtin_ctzll(longs);
+                longs &= longs - 1;
+                const uint32_t sj = __builtin_amdgcn_readlane(pa, jl) - c0, ej = __builtin_amdgcn_readlane(pb, jl) - c0;
+                float v[GRAD_ROW];
+#pragma unroll
+                for (int c = 0; c < GRAD_ROW; ++c) v[c] = 0.f;
+#pragma unroll
+                for (int q = 0; q < RS_Q; ++q) {
+                    const uint32_t pos = (uint32_t)q * 64u + lane;
+                    if (pos >= sj && pos < ej)
+#pragma unroll
+                        for (int c = 0; c < GRAD_ROW; ++c) v[c] += x[q][c];
+                }
+                float t8;
+                const float tv = wave_sum9_rows(v, v[8], lane, &t8);  // lane l: total of value (l >> 3) & 7
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const float tc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tv), 8 * c));
+                    if ((int)lane == jl) acc[c] += tc;
+                }
+                if ((int)lane == jl) acc[8] += t8;
+            }
+            wave_sync();  // the next chunk overwrites the staging rows
+        }
+        wave_sync();  // the next window overwrites the list
+    }
+#else
+    const bool is_long = n > RS_LONG;
     // row_valid bytes of the first chunk; each iteration requests the next chunk's with its rows
     uint32_t flag[RS_Q];
 #pragma unroll
@@ -413,6 +541,7 @@ __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
         }
         wave_sync();  // the next chunk overwrites the staging rows
     }
+#endif
     if (idx < a.g_end && !huge) {
         float* out = a.row_sums + (size_t)idx * GRAD_ROW;
 #pragma unroll
