@@ -316,7 +316,13 @@ __device__ __forceinline__ void huge_row_sums(const RowSumArgs& a, uint32_t hb, 
 #define OMR_RS_COMPACT 1
 #endif
 #if OMR_RS_COMPACT
-constexpr uint32_t RS_WIN = 512;  // rows whose marks a wave compacts at once (8 per lane, one 8-B load)
+#ifndef OMR_RS_WIN
+#define OMR_RS_WIN 512
+#endif
+constexpr uint32_t RS_WIN = OMR_RS_WIN;  // rows whose marks a wave compacts at once (8 or 16 per lane, one load;
+                                         // 512: C 0.056 / E 0.37 ms, 1024: 0.060 / 0.40)
+constexpr uint32_t RS_RPL = RS_WIN / 64;
+static_assert(RS_RPL == 8 || RS_RPL == 16, "8-B or 16-B mark loads");
 #endif
 
 __device__ __forceinline__ uint32_t wave_exclusive_scan_u32(uint32_t x, uint32_t lane, uint32_t* total)
@@ -379,30 +385,38 @@ __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
     // per 128 rows. Each Gaussian's marked rows are a contiguous run of the sorted list; the sums keep row order.
     uint32_t* s_list = s_list_all[wv];
     const uint64_t huges = __ballot(huge && idx < a.g_end && s < a.R);
-    for (uint32_t w0 = lo & ~7u; w0 < hi; w0 += RS_WIN) {  // lo > hi when the wave owns no rows
-        const uint32_t r0 = w0 + 8u * lane;
+    for (uint32_t w0 = lo & ~(RS_RPL - 1u); w0 < hi; w0 += RS_WIN) {  // lo > hi when the wave owns no rows
+        const uint32_t r0 = w0 + RS_RPL * lane;
         uint32_t m = 0;  // bit j: row r0 + j is marked, inside [lo, hi) and not a huge Gaussian's
         if (r0 < hi) {
-            uint32_t fx = 0, fy = 0;
-            if (r0 + 8u <= a.R) {
-                const uint2 f = *reinterpret_cast<const uint2*>(a.row_valid + r0);  // row_valid is 256-B aligned
-                fx = f.x;
-                fy = f.y;
+            uint32_t fw[RS_RPL / 4] = {};
+            if (r0 + RS_RPL <= a.R) {  // row_valid is 256-B aligned
+                if constexpr (RS_RPL == 8) {
+                    const uint2 f = *reinterpret_cast<const uint2*>(a.row_valid + r0);
+                    fw[0] = f.x;
+                    fw[1] = f.y;
+                } else {
+                    const uint4 f = *reinterpret_cast<const uint4*>(a.row_valid + r0);
+                    fw[0] = f.x;
+                    fw[1] = f.y;
+                    fw[2] = f.z;
+                    fw[3] = f.w;
+                }
             } else {
-                for (uint32_t j = 0; j < 8u && r0 + j < a.R; ++j)
-                    (j < 4 ? fx : fy) |= (uint32_t)a.row_valid[r0 + j] << (8u * (j & 3u));
+                for (uint32_t j = 0; j < RS_RPL && r0 + j < a.R; ++j)
+                    fw[j >> 2] |= (uint32_t)a.row_valid[r0 + j] << (8u * (j & 3u));
             }
 #pragma unroll
-            for (uint32_t j = 0; j < 8u; ++j) {
+            for (uint32_t j = 0; j < RS_RPL; ++j) {
                 const uint32_t r = r0 + j;
-                const uint32_t byte = ((j < 4 ? fx : fy) >> (8u * (j & 3u))) & 0xFFu;
+                const uint32_t byte = (fw[j >> 2] >> (8u * (j & 3u))) & 0xFFu;
                 if (byte != 0 && r >= lo && r < hi) m |= 1u << j;
             }
             for (uint64_t hb = huges; hb; hb &= hb - 1) {  // rare: a huge Gaussian's rows inside the span
                 const int jl = __builtin_ctzll(hb);
                 const uint32_t hs = __builtin_amdgcn_readlane(s, jl), he = hs + __builtin_amdgcn_readlane(n_all, jl);
 #pragma unroll
-                for (uint32_t j = 0; j < 8u; ++j)
+                for (uint32_t j = 0; j < RS_RPL; ++j)
                     if (r0 + j >= hs && r0 + j < he) m &= ~(1u << j);
             }
         }
