@@ -152,7 +152,7 @@ __host__ __device__ inline size_t row_valid_offset(size_t L)
 // The checkpoints are addressed through a buffer descriptor with 32-bit offsets: ckpt_bytes(L) < 2^31, i.e.
 // L < 2^28 instances per view (checked by the forward).
 #ifndef OMR_BWD_CK
-#define OMR_BWD_CK 512
+#define OMR_BWD_CK 1024
 #endif
 constexpr uint32_t CKPT = OMR_BWD_CK;
 // bands per forward wave (render_fwd.hip): 2 = each tile is rendered by two independent waves ("groups")
