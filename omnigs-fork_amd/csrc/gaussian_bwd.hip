@@ -557,9 +557,12 @@ __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
     }
 #endif
     if (idx < a.g_end && !huge) {
-        float* out = a.row_sums + (size_t)idx * GRAD_ROW;
+        // a Gaussian without instances (culled: radii 0) has no sums to keep; gaussian_bwd does not read them
+        if (!OMR_SKIP_CULLED_SUMS || n_all != 0) {
+            float* out = a.row_sums + (size_t)idx * GRAD_ROW;
 #pragma unroll
-        for (int c = 0; c < GRAD_ROW; ++c) out[c] = acc[c];
+            for (int c = 0; c < GRAD_ROW; ++c) out[c] = acc[c];
+        }
         // dL/dcolour (backward.cu:805-808 sums) is final here: the view-parallel exchange can gather it while
         // gaussian_bwd still runs (parallel.py); zeros for a culled Gaussian, which has no rows
 #pragma unroll
@@ -793,13 +796,15 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
     const int idx = wave_first + (int)lane;
     float g[GRAD_ROW];
     float4 co = make_float4(0.f, 0.f, 0.f, 0.f);  // conic + opacity of the render record (raw-moment rows)
-    if (idx < a.g_end) {
+    const bool valid = idx < a.g_end;
+    const bool vis = valid && a.radii[idx] > 0;
+    // sums and conic are read for visible Gaussians only (radii > 0 implies instances, preprocess.hip, so
+    // row_sum_kernel wrote the row): at config E pinhole 88 % of the Gaussians are culled
+    if (OMR_SKIP_CULLED_SUMS ? vis : valid) {
 #pragma unroll
         for (int c = 0; c < GRAD_ROW; ++c) g[c] = a.row_sums[(size_t)idx * GRAD_ROW + c];
         if (OMR_BWD_RAW_MOMENTS) co = a.conic_op[idx];
     }
-    const bool valid = idx < a.g_end;
-    const bool vis = valid && a.radii[idx] > 0;
     float4* stage = s_stage[wv];
     // MC == 16 only (the MC == 0 path reads and writes the rows itself)
     float4* dsh4 = STAGED ? stage + lane * stage_stride<SH_F4>() : reinterpret_cast<float4*>(a.dL_dsh) + (size_t)idx * SH_F4;

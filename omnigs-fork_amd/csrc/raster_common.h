@@ -48,6 +48,10 @@ constexpr int GRAD_ROW = 9;
 #ifndef OMR_BWD_RAW_MOMENTS
 #define OMR_BWD_RAW_MOMENTS 1
 #endif
+// row sums of Gaussians without instances are neither written (row_sum_kernel) nor read (gaussian_bwd_kernel)
+#ifndef OMR_SKIP_CULLED_SUMS
+#define OMR_SKIP_CULLED_SUMS 1
+#endif
 // a Gaussian touching more tiles than this gets a whole workgroup for its row sums (gaussian_bwd.hip); the
 // forward's scan lists these Gaussians (sort.hip: scan2_downsweep_kernel)
 constexpr uint32_t ROW_SUM_HUGE = 256;
