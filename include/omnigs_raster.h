@@ -241,7 +241,8 @@ int omr_debug_tile_cost(char* image_buffer, int width, int height, uint32_t* dst
 /* one wave64 through the render backward's gradient reduction: in [64][9] -> out [9] (column sums) */
 int omr_debug_wave_sum(const float* in, float* out, void* stream);
 int omr_debug_wave_sum9(const float* in, float* out, void* stream); /* wave_sum9_rows */
-int omr_debug_wave_sum9_lds(const float* in, float* out, void* stream); /* wave_sum9_lds (render backward) */
+int omr_debug_wave_sum9_lds(const float* in, float* out, void* stream); /* wave_sum9_lds (render backward, unpaired) */
+int omr_debug_wave_sum9x2(const float* in, float* out, void* stream); /* wave_sum9x2_stored: [2][64][9] -> [2][9] (render backward) */
 int omr_debug_geometry(char* geom_buffer, int P, float* means2D, float* conic_opacity, float* rgb, float* depths,
                        uint32_t* tiles_touched, void* stream);
 

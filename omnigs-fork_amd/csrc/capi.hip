@@ -65,6 +65,21 @@ __global__ __launch_bounds__(64) void debug_wave_sum9_lds_kernel(const float* in
     if (lane == 1) out[8] = t8;
 }
 
+// two instances' rows through wave_sum9x2_stored (the render backward's paired reduction, OMR_BWD_PAIR): in is
+// [2][64][9], out [2][9]
+__global__ __launch_bounds__(64) void debug_wave_sum9x2_kernel(const float* in, float* out)
+{
+    __shared__ __attribute__((aligned(16))) float s_red[16 * WS_LDS_STRIDE];
+    const uint32_t lane = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s_red[k * WS_LDS_STRIDE + lane] = in[(k >> 3) * 576 + lane * 9 + (k & 7)];
+    float t8;
+    const float tv = wave_sum9x2_stored(in[lane * 9 + 8], in[576 + lane * 9 + 8], lane, s_red, &t8);
+    const uint32_t k = lane >> 2;
+    if ((lane & 3) == 0) out[(k >> 3) * 9 + (k & 7)] = tv;
+    if ((lane & 31) == 1) out[(lane >> 5) * 9 + 8] = t8;
+}
+
 __global__ __launch_bounds__(256) void debug_point_ids_kernel(const uint32_t* list, size_t n, uint32_t* out)
 {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -1036,6 +1051,13 @@ int omr_debug_wave_sum9_lds(const float* in, float* out, void* stream)
     g_last_error.clear();
     debug_wave_sum9_lds_kernel<<<1, 64, 0, (hipStream_t)stream>>>(in, out);
     return hip_check("debug_wave_sum9_lds");
+}
+
+int omr_debug_wave_sum9x2(const float* in, float* out, void* stream)
+{
+    g_last_error.clear();
+    debug_wave_sum9x2_kernel<<<1, 64, 0, (hipStream_t)stream>>>(in, out);
+    return hip_check("debug_wave_sum9x2");
 }
 
 int omr_debug_wave_sum(const float* in, float* out, void* stream)

@@ -18,6 +18,8 @@
 // factors that every instance of the Gaussian shares, so they are applied neither per pixel nor per instance but
 // once to the Gaussian's summed rows (raster_common.h: OMR_BWD_RAW_MOMENTS); the nine values of an instance are
 // summed over the wave: eight transposed through LDS, the ninth by v_permlane{16,32}_swap + DPP (wave_ops.h).
+// Contributing instances are summed in pairs (OMR_BWD_PAIR): the first one's eight values wait in LDS rows 0-7
+// until the second's fill rows 8-15, then one pass sums both (wave_sum9x2_stored).
 // Lanes 0..8 store the instance's 36-B gradient row, indexed by its row slot (Gaussian-index-major: row_first), with
 // plain stores, and lane 0 marks the slot in row_valid (zeroed before the launch); an instance no pixel takes a contribution from writes
 // nothing — at dense configs most instances lie behind every pixel's last contributor. gaussian_bwd.hip sums each
@@ -59,6 +61,14 @@ __device__ unsigned long long g_bwd_counts[5];
 #ifndef OMR_BWD_ROWS_RED
 #define OMR_BWD_ROWS_RED 2
 #endif
+// with the LDS reduction: reduce the rows of two contributing instances together (wave_sum9x2_lds), the first one
+// held in registers until the second arrives or the unit ends
+#ifndef OMR_BWD_PAIR
+#define OMR_BWD_PAIR 1
+#endif
+#if OMR_BWD_PAIR && OMR_BWD_ROWS_RED != 2
+#error "OMR_BWD_PAIR needs the LDS reduction (OMR_BWD_ROWS_RED 2)"
+#endif
 
 #ifdef OMR_BWD_WPE
 #define OMR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(OMR_BWD_WPE)))
@@ -72,7 +82,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) OMR_BWD_ATTR void rend
     __shared__ float4 s_quad_all[TW_WAVES][TW_BATCH];  // qa, qb, qc, opacity
     __shared__ float4 s_rgb_all[TW_WAVES][TW_BATCH];   // colour, gradient row slot (u32 bits)
 #if OMR_BWD_ROWS_RED == 2
-    __shared__ __attribute__((aligned(16))) float s_red_all[TW_WAVES][8 * WS_LDS_STRIDE];  // wave_sum9_lds rows
+    __shared__ __attribute__((aligned(16))) float s_red_all[TW_WAVES][(OMR_BWD_PAIR ? 16 : 8) * WS_LDS_STRIDE];
 #endif
     __shared__ float s_floor_all[TW_WAVES][TW_BATCH];  // p2_floor(opacity)
 
@@ -167,6 +177,10 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) OMR_BWD_ATTR void rend
 #endif
 #ifdef OMR_BWD_COUNT
     uint32_t cnt_[5] = {0, 0, 0, 0, 0};
+#endif
+#if OMR_BWD_PAIR
+    float pv8 = 0.f;        // the held instance's 9th value (its first eight wait in rows 0-7 of s_red)
+    float* prow = nullptr;  // its gradient row (wave-uniform); null: nothing held
 #endif
 
     // positions seg_hi-1 .. seg_lo, 64 per batch, back to front: batch entry `lane` <-> position hi-1-lane
@@ -283,7 +297,25 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) OMR_BWD_ATTR void rend
             v[6] = sc01.x;                                     // dL/dcolour
             v[7] = sc01.y;
             float t8;
-#if OMR_BWD_ROWS_RED
+#if OMR_BWD_PAIR
+            float* s_red = s_red_all[wv];
+            const uint32_t base = prow ? 8u * WS_LDS_STRIDE : 0u;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s_red[base + k * WS_LDS_STRIDE + lane] = v[k];
+            if (!prow) {
+                pv8 = sc2;
+                prow = row;
+                continue;
+            }
+            {
+                const float tv = wave_sum9x2_stored(pv8, sc2, lane, s_red, &t8);
+                // lane 4k holds value k (k < 8 the held row's, k >= 8 this one's); lanes 1 and 33 the 9th values
+                const bool lead = (lane & 3) == 0;
+                float* dst = (lane < 32) ? prow : row;
+                if (lead || (lane & 31) == 1) dst[lead ? ((lane >> 2) & 7u) : 8u] = lead ? tv : t8;
+                prow = nullptr;
+            }
+#elif OMR_BWD_ROWS_RED
 #if OMR_BWD_ROWS_RED == 2
             const float tv = wave_sum9_lds(v, sc2, lane, s_red_all[wv], &t8);
 #else
@@ -299,6 +331,17 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) OMR_BWD_ATTR void rend
         }
         wave_sync();  // the next batch overwrites the staging arrays
     }
+#if OMR_BWD_PAIR
+    if (prow) {  // the unit's last contributing instance had no partner: sum its rows 0-7 alone
+        float v[8], t8;
+        const float* r8 = s_red_all[wv];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = r8[k * WS_LDS_STRIDE + lane];
+        const float tv = wave_sum9_lds(v, pv8, lane, s_red_all[wv], &t8);
+        const bool lead = (lane & 7) == 0;
+        if (lead || lane == 1) prow[lead ? (lane >> 3) : 8u] = lead ? tv : t8;
+    }
+#endif
     OMR_STAMP_END(g_stamps_bwd, blockIdx.x);
 #ifdef OMR_BWD_COUNT
     if (lane == 0)

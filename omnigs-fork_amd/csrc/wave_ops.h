@@ -127,6 +127,36 @@ __device__ __forceinline__ float wave_sum9_lds(const float v[8], float v8, uint3
     return add_dpp<DPP_HALF_MIRROR>(c, c);
 }
 
+// Wave-sums of two instances' nine values, the first eight of each already stored by the caller: a's in rows 0-7 of
+// s_red (float[16 * WS_LDS_STRIDE]), b's in rows 8-15 (row k, lane l at k * WS_LDS_STRIDE + l). Lane l sums 16
+// consecutive partials of value l >> 2 and two DPP steps finish the 4-lane groups, so lane 4k returns value k
+// (k < 8: a's, k >= 8: b's). The 9th values share one permlane/DPP chain: v_permlane32_swap with a in the first
+// operand and b in the second leaves a's pair sums in lanes 0-31 and b's in 32-63, and the rest of the chain stays
+// inside each half, so *t8 = sum a8 on lanes 0-31 and sum b8 on lanes 32-63.
+__device__ __forceinline__ float wave_sum9x2_stored(float va8, float vb8, uint32_t lane, const float* s_red, float* t8)
+{
+    float u0 = va8, u1 = vb8;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(u0), "+v"(u1));
+    float u = u0 + u1;
+    u0 = u;
+    u1 = u;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(u0), "+v"(u1));
+    u = u0 + u1;
+    u = add_dpp<DPP_ROR8>(u, u);
+    u = add_dpp<DPP_XOR1>(u, u);
+    u = add_dpp<DPP_XOR2>(u, u);
+    *t8 = add_dpp<DPP_HALF_MIRROR>(u, u);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const float4* seg = reinterpret_cast<const float4*>(s_red + (lane >> 2) * WS_LDS_STRIDE + (lane & 3) * 16);
+    const float4 a = seg[0], b = seg[1], c = seg[2], d = seg[3];
+    float s = (((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w))) +
+              (((c.x + c.y) + (c.z + c.w)) + ((d.x + d.y) + (d.z + d.w)));
+    s = add_dpp<DPP_XOR1>(s, s);
+    return add_dpp<DPP_XOR2>(s, s);
+}
+
 // lane l < 8 holds value index bitrev3(l) after wave_sum8_transposed; lane 8 is used for the 9th value
 __device__ __forceinline__ uint32_t transposed_slot_of_lane(uint32_t lane)
 {

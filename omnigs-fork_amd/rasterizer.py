@@ -70,6 +70,7 @@ def lib() -> C.CDLL:
         L.omr_debug_wave_sum.argtypes = [vp, vp, vp]
         L.omr_debug_wave_sum9.argtypes = [vp, vp, vp]
         L.omr_debug_wave_sum9_lds.argtypes = [vp, vp, vp]
+        L.omr_debug_wave_sum9x2.argtypes = [vp, vp, vp]
         L.omr_profile_enable.argtypes = [i]
         L.omr_sh_grad_from_colors.argtypes = [i, i, i, i, vp, vp, vp, vp, vp, vp]
         L.omr_sh_grad_from_colors_packed.restype = i
@@ -535,4 +536,14 @@ def debug_wave_sum(x: torch.Tensor, rows: bool = False, lds: bool = False) -> to
     out = torch.empty(9, dtype=torch.float32, device=x.device)
     fn = lib().omr_debug_wave_sum9_lds if lds else (lib().omr_debug_wave_sum9 if rows else lib().omr_debug_wave_sum)
     _check(fn(x.data_ptr(), out.data_ptr(), _stream(x.device)), "debug_wave_sum")
+    return out
+
+
+def debug_wave_sum_pair(x: torch.Tensor) -> torch.Tensor:
+    """Column sums of two [64, 9] float32 blocks (x: [2, 64, 9] on the device) through wave_sum9x2_stored, the
+    render backward's paired reduction: returns [2, 9]."""
+    x = _dev_f32(x, "x")
+    assert tuple(x.shape) == (2, 64, 9)
+    out = torch.empty((2, 9), dtype=torch.float32, device=x.device)
+    _check(lib().omr_debug_wave_sum9x2(x.data_ptr(), out.data_ptr(), _stream(x.device)), "debug_wave_sum_pair")
     return out

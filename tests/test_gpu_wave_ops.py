@@ -33,3 +33,25 @@ def test_wave_sum_lane_identity(mode, omr):
     got = omr.rasterizer.debug_wave_sum(torch.from_numpy(x).cuda(), **mode).cpu().numpy()
     ref = x.astype(np.float64).sum(axis=0)
     np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_wave_sum_pair_matches_column_sums(seed, omr):
+    """wave_sum9x2_stored (render_bwd.hip, OMR_BWD_PAIR): two instances' rows summed in one pass."""
+    import torch
+
+    rng = np.random.default_rng(10 + seed)
+    x = rng.standard_normal((2, 64, 9)).astype(np.float32)
+    if seed == 2:
+        x[rng.uniform(size=x.shape) < 0.85] = 0.0
+    got = omr.rasterizer.debug_wave_sum_pair(torch.from_numpy(x).cuda()).cpu().numpy()
+    np.testing.assert_allclose(got, x.astype(np.float64).sum(axis=1), rtol=1e-5, atol=1e-5)
+
+
+def test_wave_sum_pair_lane_identity(omr):
+    import torch
+
+    x = np.array([[[(i * 9 + c + 1) * 1000 + l for c in range(9)] for l in range(64)] for i in range(2)],
+                 dtype=np.float32)
+    got = omr.rasterizer.debug_wave_sum_pair(torch.from_numpy(x).cuda()).cpu().numpy()
+    np.testing.assert_array_equal(got, x.astype(np.float64).sum(axis=1))
