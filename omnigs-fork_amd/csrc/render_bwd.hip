@@ -180,7 +180,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) OMR_BWD_ATTR void rend
 #endif
 #if OMR_BWD_PAIR
     float pv8 = 0.f;        // the held instance's 9th value (its first eight wait in rows 0-7 of s_red)
-    float* prow = nullptr;  // its gradient row (wave-uniform); null: nothing held
+    uint32_t pslot = ~0u;   // its gradient row slot (wave-uniform: an SGPR); ~0: nothing held
 #endif
 
     // positions seg_hi-1 .. seg_lo, 64 per batch, back to front: batch entry `lane` <-> position hi-1-lane
@@ -270,10 +270,14 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) OMR_BWD_ATTR void rend
                 sc2 = __builtin_fmaf(wc, dp2b, sc2);
             }
             const uint32_t slot_j = __builtin_bit_cast(uint32_t, f.w);
+#if !OMR_BWD_PAIR
             float* row = a.inst_grad + (size_t)slot_j * GRAD_ROW;
+#endif
             if (!any) continue;  // no pixel took a contribution: no row
             BWD_COUNT(3, 1);
-            if (lane == 0) a.row_valid[slot_j] = 1;
+#if !OMR_BWD_PAIR
+            if (lane == 0) a.row_valid[slot_j] = 1;  // paired: marked with the pair's row stores
+#endif
             const float su = s_uy.x, suy = s_uy.y;
             const float sux = su * dx, suxx = sux * dx, suxy = suy * dx;
             float v[8];
@@ -299,21 +303,25 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) OMR_BWD_ATTR void rend
             float t8;
 #if OMR_BWD_PAIR
             float* s_red = s_red_all[wv];
-            const uint32_t base = prow ? 8u * WS_LDS_STRIDE : 0u;
+            const uint32_t slot_u = uniform(slot_j);
+            const bool held = pslot != ~0u;  // scalar
+            const uint32_t base = held ? 8u * WS_LDS_STRIDE : 0u;
 #pragma unroll
             for (int k = 0; k < 8; ++k) s_red[base + k * WS_LDS_STRIDE + lane] = v[k];
-            if (!prow) {
+            if (!held) {
                 pv8 = sc2;
-                prow = row;
+                pslot = slot_u;
                 continue;
             }
             {
                 const float tv = wave_sum9x2_stored(pv8, sc2, lane, s_red, &t8);
                 // lane 4k holds value k (k < 8 the held row's, k >= 8 this one's); lanes 1 and 33 the 9th values
                 const bool lead = (lane & 3) == 0;
-                float* dst = (lane < 32) ? prow : row;
-                if (lead || (lane & 31) == 1) dst[lead ? ((lane >> 2) & 7u) : 8u] = lead ? tv : t8;
-                prow = nullptr;
+                const uint32_t dslot = (lane < 32) ? pslot : slot_u;
+                if (lead || (lane & 31) == 1)
+                    a.inst_grad[(size_t)dslot * GRAD_ROW + (lead ? ((lane >> 2) & 7u) : 8u)] = lead ? tv : t8;
+                if ((lane & 31) == 0) a.row_valid[dslot] = 1;
+                pslot = ~0u;
             }
 #elif OMR_BWD_ROWS_RED
 #if OMR_BWD_ROWS_RED == 2
@@ -332,14 +340,15 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) OMR_BWD_ATTR void rend
         wave_sync();  // the next batch overwrites the staging arrays
     }
 #if OMR_BWD_PAIR
-    if (prow) {  // the unit's last contributing instance had no partner: sum its rows 0-7 alone
+    if (pslot != ~0u) {  // the unit's last contributing instance had no partner: sum its rows 0-7 alone
         float v[8], t8;
         const float* r8 = s_red_all[wv];
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = r8[k * WS_LDS_STRIDE + lane];
         const float tv = wave_sum9_lds(v, pv8, lane, s_red_all[wv], &t8);
         const bool lead = (lane & 7) == 0;
-        if (lead || lane == 1) prow[lead ? (lane >> 3) : 8u] = lead ? tv : t8;
+        if (lead || lane == 1) a.inst_grad[(size_t)pslot * GRAD_ROW + (lead ? (lane >> 3) : 8u)] = lead ? tv : t8;
+        if (lane == 0) a.row_valid[pslot] = 1;
     }
 #endif
     OMR_STAMP_END(g_stamps_bwd, blockIdx.x);
