@@ -60,7 +60,8 @@ def parse():
                    help="skip the extra whole-training-iteration timing (N = 1 only; not part of `value`)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     p.add_argument("--ambiguity-json", default=os.path.join(ROOT, "profiles", "ambiguity.json"),
-                   help="boundary-ambiguous Gaussian counts per config (oracle/ambiguity.py), reported as "
+                   help="parity allowance counts per config and the FMA-contracted reference proxies' differences "
+                        "(oracle/contraction.py), reported as "
                         "config.ambiguous")
     p.add_argument("--cpu-runs", type=int, default=10, help="CPU-oracle runs per baseline leg (median reported)")
     p.add_argument("--cpu-single-config", default="B",
@@ -168,6 +169,9 @@ def cpu_model() -> str:
     return "unknown"
 
 
+CPU_VARIANT = "fast"  # oracle/Makefile: -O3 -march=x86-64-v3; the parity build is -O2
+
+
 def _oracle_leg(O, g, cam, dL, threads, runs, seconds):
     """Median seconds of `runs` oracle fwd+bwd passes (stopping early once `seconds` is spent, after >= 3 runs)."""
     import numpy as np
@@ -177,7 +181,7 @@ def _oracle_leg(O, g, cam, dL, threads, runs, seconds):
     t_start = time.perf_counter()
     while len(times) < runs:
         t0 = time.perf_counter()
-        o = O.Oracle(False)
+        o = O.Oracle(False, CPU_VARIANT)
         o.forward(background=np.zeros(3), means3D=g.means3D, opacity=g.opacity, scales=g.scales,
                   rotations=g.rotations, shs=g.shs, viewmatrix=cam.viewmatrix, projmatrix=cam.projmatrix,
                   campos=cam.campos, width=cam.width, height=cam.height, sh_degree=g.sh_degree,
@@ -200,7 +204,7 @@ def cpu_baseline(omr, g, cam, dL, seconds, threads, runs, single_config):
     med, times = _oracle_leg(O, g, cam, dL, threads, runs, seconds)
     N = cam.width * cam.height
     out = {"value": round(N / med / 1e6, 4), "unit": "Mpixels/s", "cores": threads, "kind": "port",
-           "cpu_model": cpu_model(),
+           "cpu_model": cpu_model(), "build": "oracle/_build/liboracle_fast.so (g++ -O3 -march=x86-64-v3 -fopenmp)",
            "sample": f"median of {len(times)} fwd+bwd of the bench view ({cam.width}x{cam.height}, P={g.P}, same "
                      f"scene as the GPU run) on {threads} OpenMP threads: {med:.2f} s (min {min(times):.2f}, max "
                      f"{max(times):.2f}); oracle/ restatement, no CPU reference exists"}
@@ -211,6 +215,15 @@ def cpu_baseline(omr, g, cam, dL, seconds, threads, runs, single_config):
             "value": round(cam1.width * cam1.height / med1 / 1e6, 4), "unit": "Mpixels/s", "cores": 1,
             "sample": f"median of {len(t1)} fwd+bwd of config {single_config} ({cam1.width}x{cam1.height}, "
                       f"P={g1.P}) on one thread: {med1:.2f} s"}
+    # config A (10 k Gaussians @ 512x256, the reference's own CPU-runnable case) on one thread and
+    # on all cores
+    gA, camA, dLA = omr.scene.config_scene("A")
+    NA = camA.width * camA.height
+    out["config_A"] = {}
+    for leg, th in (("single_thread", 1), ("all_cores", threads)):
+        mA, tA = _oracle_leg(O, gA, camA, dLA, th, runs, seconds)
+        out["config_A"][leg] = {"value": round(NA / mA / 1e6, 4), "unit": "Mpixels/s", "cores": th,
+                                "sample": f"median of {len(tA)} fwd+bwd of config A (512x256, P={gA.P}): {mA:.3f} s"}
     O.set_threads(1)
     return out
 
@@ -413,12 +426,13 @@ def main():
 
     # dominant kernel: the largest stage of the per-stage pass; its launch duration from the timed pass (HIP events
     # on the launch stream around that kernel alone)
-    pmc = {}
+    pmc, pmc_file = {}, None
     try:
         with open(args.traffic_json) as f:
             pj = json.load(f)
         if pj.get("config") == cfg_name and pj.get("P") == P:
             pmc = pj.get("kernels", {})
+            pmc_file = pj.get("kernel_stats_file")
     except (OSError, ValueError):
         pass
 
@@ -429,13 +443,19 @@ def main():
         ach = b / (ms_k * 1e-3) / 1e9 if ms_k > 0 else 0.0
         tr = pmc.get(k, {}).get("hbm_bytes_per_launch")
         lo = pmc.get(k, {}).get("hbm_bytes_lower")
+        # the committed rocprofv3 --stats average of the same kernel (profiles/<tag>_kernel_stats.csv, all launches of
+        # that run including warm-up): `frac` recomputes from it as algorithmic bytes / avg / peak
+        rp = pmc.get(k, {}).get("rocprof_avg_ms")
+        ach_rp = b / (rp * 1e-3) / 1e9 if rp else None
         # traffic = (2 FETCH + WRITE): exact for 16-B/lane streams, an upper bound for gathers, which
         # profiles/calib_fetch.hip shows FETCH counting 1:1 (traffic_lower = FETCH + WRITE)
         return {"stage": k, "avg_launch_ms": round(ms_k, 4), "timed_launches": int(cnt_l) if live_ok else 0,
                 "algorithmic_bytes_per_launch": b,
                 "achieved_GBps": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": tr,
                 "traffic_lower": lo, "traffic_over_algorithmic": round(tr / b, 3) if (tr and b) else None,
-                "traffic_lower_over_algorithmic": round(lo / b, 3) if (lo and b) else None}
+                "traffic_lower_over_algorithmic": round(lo / b, 3) if (lo and b) else None,
+                "avg_launch_ms_rocprof": rp, "frac_rocprof": round(ach_rp / HBM_PEAK_GBS, 5) if ach_rp else None,
+                "rocprof_file": pmc_file if rp else None}
 
     d = stage_entry(dom)
     algo_total = sum(stage_bytes(s, P, V, L, N, T, M, g.sh_degree) for s in stage_avg)
@@ -451,8 +471,17 @@ def main():
     ambiguous = None
     try:
         with open(args.ambiguity_json) as f:
-            ambiguous = json.load(f).get("configs", {}).get(scene_name if world == 1 else cfg_name)
-    except (OSError, ValueError):
+            amb = json.load(f).get("configs", {}).get(scene_name if world == 1 else cfg_name)
+        if amb:  # oracle/contraction.py: the allowance counts and, per FMA-contracted build, what actually changed
+            keep = ("num_rendered_delta", "depths_changed", "point_list_positions_changed", "pixels_over_1e-4",
+                    "image_max_abs_err", "grad_entries_outside_bar", "grad_entries_on_owners")
+            ambiguous = {"allowance": amb.get("allowance"),
+                         "contracted_reference_proxies": {
+                             v: dict({k: r.get(k) for k in keep},
+                                     unexplained=sum(x for k, x in r.items() if k.endswith("_unexplained")))
+                             for v, r in amb.get("variants", {}).items()},
+                         "source": os.path.relpath(args.ambiguity_json, ROOT)}
+    except (OSError, ValueError, AttributeError):
         pass
     delta = lambda k: int(mem1.get(k, 0) - mem0.get(k, 0))
     result = {
@@ -477,6 +506,8 @@ def main():
                      "unit": "GB/s", "frac": d["frac"], "traffic": d["traffic"],
                      "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
                      "avg_launch_ms": d["avg_launch_ms"], "timed_launches": d["timed_launches"],
+                     "avg_launch_ms_rocprof": d["avg_launch_ms_rocprof"], "frac_rocprof": d["frac_rocprof"],
+                     "rocprof_file": d["rocprof_file"],
                      "step_algorithmic_GBps": round(algo_total / (ms_per_step * 1e-3) / 1e9, 2),
                      "top_stages": [stage_entry(k) for k in ranked[:3]]},
         "stages_ms": {k: round(v, 4) for k, v in stage_avg.items()},

@@ -108,6 +108,12 @@ int omr_lonlat_backward(int P, int D, int M, int R, const float* background, int
                         float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D,
                         float* dL_dsh, float* dL_dscale, float* dL_drot, float* dpx_dt, float* dpy_dt, void* stream);
 
+/* Status of a forward's device-side binning (emit, tile sort), which may still be running when omr_*_forward
+ * returns. A decoupled look-back of the tile sort that gave up makes that view render background only; the next
+ * omr_*_backward on the same buffers returns OMR_ERR_HIP for it, and a forward-only caller (evaluation, inference)
+ * checks it here: synchronises `stream`, returns OMR_OK or OMR_ERR_HIP (message in omr_last_error). Extension. */
+int omr_forward_status(char* geom_buffer, int P, void* stream);
+
 /* --- view-parallel data parallelism (extension, not in the reference; omnigs-fork_amd/parallel.py) -- */
 /* The next omr_*_backward call on this thread records `event` (a hipEvent_t) on its stream as soon as dL_dcolor is
  * final — after the per-Gaussian row sums, before the per-Gaussian backward (gaussian_bwd) — and forgets it. A
@@ -239,7 +245,6 @@ int omr_debug_image_state(char* image_buffer, int width, int height, float* fina
 int omr_debug_tile_cost(char* image_buffer, int width, int height, uint32_t* dst, void* stream);
 /* per-Gaussian pixel centre [P,2], conic+opacity [P,4], rgb [P,3], depth [P], tiles_touched [P] */
 /* one wave64 through the render backward's gradient reduction: in [64][9] -> out [9] (column sums) */
-int omr_debug_wave_sum(const float* in, float* out, void* stream);
 int omr_debug_wave_sum9(const float* in, float* out, void* stream); /* wave_sum9_rows */
 int omr_debug_wave_sum9_lds(const float* in, float* out, void* stream); /* wave_sum9_lds (render backward, unpaired) */
 int omr_debug_wave_sum9x2(const float* in, float* out, void* stream); /* wave_sum9x2_stored: [2][64][9] -> [2][9] (render backward) */

@@ -26,19 +26,7 @@ namespace omr {
 
 namespace {
 
-// one wave: in [64][9] -> out[9] through the render backward's transposed wave reduction
-__global__ __launch_bounds__(64) void debug_wave_sum_kernel(const float* in, float* out)
-{
-    const uint32_t lane = threadIdx.x;
-    float v[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) v[c] = in[lane * 9 + c];
-    float t8;
-    const float tv = wave_sum8_transposed(v, in[lane * 9 + 8], lane, &t8);
-    if (lane < 9) out[transposed_slot_of_lane(lane)] = lane < 8 ? tv : t8;
-}
-
-// the same through wave_sum9_rows (the render backward's reduction before wave_sum9_lds)
+// one wave: in [64][9] -> out[9] through wave_sum9_rows (the row sums' long-Gaussian reduction)
 __global__ __launch_bounds__(64) void debug_wave_sum9_kernel(const float* in, float* out)
 {
     const uint32_t lane = threadIdx.x;
@@ -51,7 +39,7 @@ __global__ __launch_bounds__(64) void debug_wave_sum9_kernel(const float* in, fl
     if (lane == 1) out[8] = t8;
 }
 
-// the same through wave_sum9_lds (the render backward's default reduction, OMR_BWD_ROWS_RED 2)
+// the same through wave_sum9_lds (the render backward's unpaired reduction)
 __global__ __launch_bounds__(64) void debug_wave_sum9_lds_kernel(const float* in, float* out)
 {
     __shared__ __attribute__((aligned(16))) float s_red[8 * WS_LDS_STRIDE];
@@ -65,7 +53,7 @@ __global__ __launch_bounds__(64) void debug_wave_sum9_lds_kernel(const float* in
     if (lane == 1) out[8] = t8;
 }
 
-// two instances' rows through wave_sum9x2_stored (the render backward's paired reduction, OMR_BWD_PAIR): in is
+// two instances' rows through wave_sum9x2_stored (the render backward's paired reduction): in is
 // [2][64][9], out [2][9]
 __global__ __launch_bounds__(64) void debug_wave_sum9x2_kernel(const float* in, float* out)
 {
@@ -115,9 +103,6 @@ enum Stage { ST_PREPROCESS, ST_DEPTH_SORT, ST_SCAN, ST_EMIT, ST_TILE_SORT, ST_RA
 const char* kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "scan", "emit", "tile_sort", "tile_ranges",
                                      "render_forward", "render_backward", "gaussian_backward", "row_sums"};
 
-#ifndef OMR_EXT_STAGE_EVENTS
-#define OMR_EXT_STAGE_EVENTS 1
-#endif
 // Diagnostic (bench.py, tests): one process-wide profiler, guarded by a mutex; its events belong to the device that
 // was current when they were created, so profile one device per process.
 struct Profiler {
@@ -141,7 +126,7 @@ struct Profiler {
         }
         // timing only: no system-scope fence (an L2 writeback + invalidate, about 5 us of GPU idle per event)
         hipEvent_t e = nullptr;
-        if (hipEventCreateWithFlags(&e, OMR_EXT_STAGE_EVENTS ? hipEventDisableSystemFence : hipEventDefault) != hipSuccess)
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess)
             return nullptr;
         return e;
     }
@@ -158,7 +143,7 @@ struct StageScope {
     bool single;
     hipEvent_t a = nullptr, b = nullptr;
     StageScope(int st, hipStream_t stream, bool single_kernel = false)
-        : stage(st), s(stream), single(single_kernel && OMR_EXT_STAGE_EVENTS)
+        : stage(st), s(stream), single(single_kernel)
     {
         if (g_prof.on && (g_prof.mask >> st) & 1u) {
             std::lock_guard<std::mutex> lk(g_prof.mu);
@@ -195,13 +180,7 @@ struct StageScope {
 // with system-scope stores by the first wave of a kernel that runs anyway, followed by a sequence number the host
 // spins on (kernels.h: HostWords): no blit kernel and no event. Either of those costs a dispatch and ends in a
 // system-scope release that writes back the L2 — about 5 us of GPU idle each at config C (profiles/gaps.py).
-// OMR_HOST_WORDS_KERNEL=0: hipMemcpyAsync + event record + event wait.
-#ifndef OMR_TILE_KEYS16
-#define OMR_TILE_KEYS16 1
-#endif
-#ifndef OMR_HOST_WORDS_KERNEL
-#define OMR_HOST_WORDS_KERNEL 1
-#endif
+// (A hipMemcpyAsync + event record + event wait instead cost about 14 us of GPU idle per step at config C.)
 // one host read-back: data words + the sequence word the GPU writes after them
 struct HostRead {
     uint32_t* host;       // data, host address
@@ -209,20 +188,14 @@ struct HostRead {
     uint32_t* seq_host;   // sequence word
     uint32_t* seq_dev;
     uint32_t seq = 0;     // last value requested
-    hipEvent_t ev = nullptr;  // OMR_HOST_WORDS_KERNEL=0 only
 };
 
 // Requests src_dev[0..n) into r's words. Returns what the next launch that carries host words (emit_index,
-// backward_schedule) must write, or dst == NULL when the request is already queued (copy + event, or own kernel).
+// backward_schedule) must write, or dst == NULL when the request is already queued (own kernel).
 HostWords read_to_host(HostRead& r, const uint32_t* src_dev, int n, hipStream_t s, bool own_kernel, hipError_t* err)
 {
     HostWords h;
     *err = hipSuccess;
-    if (!OMR_HOST_WORDS_KERNEL) {
-        *err = hipMemcpyAsync(r.host, src_dev, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-        if (*err == hipSuccess) *err = hipEventRecord(r.ev, s);
-        return h;
-    }
     h.dst = r.dev;
     h.src = src_dev;
     h.n = n;
@@ -241,7 +214,6 @@ HostWords read_to_host(HostRead& r, const uint32_t* src_dev, int n, hipStream_t 
 // reports an error or has drained without the words.
 hipError_t wait_host_read(const HostRead& r, hipStream_t s)
 {
-    if (!OMR_HOST_WORDS_KERNEL) return hipEventSynchronize(r.ev);
     const auto t0 = std::chrono::steady_clock::now();
     uint32_t polls = 0;
     while (__atomic_load_n(r.seq_host, __ATOMIC_ACQUIRE) != r.seq) {
@@ -286,9 +258,7 @@ HostSlots* host_slots(hipStream_t s)
     h.device = dev;
     const bool ok = hipHostMalloc(reinterpret_cast<void**>(&h.words), 8 * sizeof(uint32_t),
                                   hipHostMallocPortable | hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess &&
-                    hipHostGetDevicePointer(reinterpret_cast<void**>(&h.words_dev), h.words, 0) == hipSuccess &&
-                    hipEventCreateWithFlags(&h.fwd.ev, hipEventDisableTiming) == hipSuccess &&
-                    hipEventCreateWithFlags(&h.bwd.ev, hipEventDisableTiming) == hipSuccess;
+                    hipHostGetDevicePointer(reinterpret_cast<void**>(&h.words_dev), h.words, 0) == hipSuccess;
     if (ok) {
         std::memset(h.words, 0, 8 * sizeof(uint32_t));
         h.fwd.host = h.words;
@@ -536,7 +506,7 @@ int forward_impl(const ForwardIn& in)
 
     const int tile_passes = tile_sort_passes(d.T);
     // tile ids below 2^16: the tile sort moves 16-bit keys (emit, both passes and the ranges read 2 B less per key)
-    const bool keys16 = OMR_TILE_KEYS16 && d.T <= 65536u;
+    const bool keys16 = d.T <= 65536u;
     size_t& hint = capacity_hint(in.width, in.height, in.camera_type);
     bool known = false;
     size_t L = 0;
@@ -603,6 +573,9 @@ int forward_impl(const ForwardIn& in)
     if (L > cap) {  // the hint was too small: redo the back half at the exact size (outputs are overwritten)
         cap = L;
         rerun = true;
+        // the count words were read already: the re-run's emit must not write the pinned slot again (a later
+        // forward of this thread on another stream could be reading it by the time this write lands)
+        count_words.dst = nullptr;
         rt_add(RS_BACK_HALF_RERUNS, 1);
         if (int e = back_half(cap)) return e;
     }
@@ -1025,6 +998,21 @@ int omr_ply_save(const char* path, int P, int Mr, const float* const params[6], 
     return hip_check("ply_save");
 }
 
+int omr_forward_status(char* geom_buffer, int P, void* stream)
+{
+    g_last_error.clear();
+    if (!geom_buffer || P < 0) return fail(OMR_ERR_INVALID_ARGUMENT, "forward_status: bad geometry buffer");
+    GeomState g;
+    GeomState::carve(geom_buffer, (size_t)P, &g);
+    uint32_t err = 0;
+    const hipStream_t s = (hipStream_t)stream;
+    OMR_HIP(hipMemcpyAsync(&err, g.counters + 3, sizeof(err), hipMemcpyDeviceToHost, s));
+    OMR_HIP(hipStreamSynchronize(s));
+    // not counted in RS_LOOKBACK_ERRORS: a backward on the same buffers reports (and counts) the same word
+    if (err != 0) return fail(OMR_ERR_HIP, "forward binning: a decoupled look-back gave up waiting for a predecessor");
+    return OMR_OK;
+}
+
 size_t omr_geometry_bytes(int P) { return GeomState::carve(nullptr, (size_t)std::max(P, 0), nullptr); }
 
 size_t omr_image_bytes(int width, int height)
@@ -1060,12 +1048,6 @@ int omr_debug_wave_sum9x2(const float* in, float* out, void* stream)
     return hip_check("debug_wave_sum9x2");
 }
 
-int omr_debug_wave_sum(const float* in, float* out, void* stream)
-{
-    g_last_error.clear();
-    debug_wave_sum_kernel<<<1, 64, 0, (hipStream_t)stream>>>(in, out);
-    return hip_check("debug_wave_sum");
-}
 
 void omr_profile_enable(int on) { g_prof.on = on != 0; }
 void omr_profile_set_mask(uint32_t mask) { g_prof.mask = mask; }

@@ -197,7 +197,7 @@ __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const
             }
             out4[q] = make_float4(v[0], v[1], v[2], v[3]);
         }
-    } else {
+    } else if (dL_dsh) {  // NULL: the caller skips the SH gradient (omr_backward's skip_dsh), any M
         float* out = dL_dsh + (size_t)idx * Mr * 3;
         const int nk = (deg + 1) * (deg + 1);
         for (int k = 0; k < Mr; ++k)
@@ -312,10 +312,6 @@ __device__ __forceinline__ void huge_row_sums(const RowSumArgs& a, uint32_t hb, 
     }
 }
 
-#ifndef OMR_RS_COMPACT
-#define OMR_RS_COMPACT 1
-#endif
-#if OMR_RS_COMPACT
 #ifndef OMR_RS_WIN
 #define OMR_RS_WIN 512
 #endif
@@ -323,7 +319,6 @@ constexpr uint32_t RS_WIN = OMR_RS_WIN;  // rows whose marks a wave compacts at 
                                          // 512: C 0.056 / E 0.37 ms, 1024: 0.060 / 0.40)
 constexpr uint32_t RS_RPL = RS_WIN / 64;
 static_assert(RS_RPL == 8 || RS_RPL == 16, "8-B or 16-B mark loads");
-#endif
 
 __device__ __forceinline__ uint32_t wave_exclusive_scan_u32(uint32_t x, uint32_t lane, uint32_t* total)
 {
@@ -351,9 +346,7 @@ __device__ __forceinline__ uint32_t lds_lower_bound(const uint32_t* list, uint32
 __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
 {
     __shared__ float s_rows_all[4][RS_ROWS * GRAD_ROW];  // row-major, 9 floats per row (odd stride: no conflicts)
-#if OMR_RS_COMPACT
     __shared__ uint32_t s_list_all[4][RS_WIN];
-#endif
     if (blockIdx.x < a.huge_blocks) {  // dispatched first: the huge Gaussians overlap the rest of the grid
         huge_row_sums(a, blockIdx.x, &s_rows_all[0][0]);
         return;
@@ -378,7 +371,6 @@ __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
 #pragma unroll
     for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
 
-#if OMR_RS_COMPACT
     // Sparse rows (config C: 24 % of the rows are marked, config E: 4 %): the wave compacts the marked rows of
     // each 512-row window of its span into an LDS list (one 8-B load of marks per lane, a wave scan), then
     // streams the list in chunks of RS_ROWS marked rows: one HBM round trip per 128 marked rows instead of one
@@ -480,85 +472,9 @@ __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
         }
         wave_sync();  // the next window overwrites the list
     }
-#else
-    const bool is_long = n > RS_LONG;
-    // row_valid bytes of the first chunk; each iteration requests the next chunk's with its rows
-    uint32_t flag[RS_Q];
-#pragma unroll
-    for (int q = 0; q < RS_Q; ++q) {
-        const uint32_t r = lo + (uint32_t)q * 64u + lane;
-        flag[q] = lo < hi && r < hi ? a.row_valid[r] : 0u;
-    }
-    for (uint32_t c0 = lo; c0 < hi; c0 += RS_ROWS) {  // lo > hi when the wave owns no rows
-        const uint32_t c1 = c0 + RS_ROWS;
-        bool ok[RS_Q];
-#pragma unroll
-        for (int q = 0; q < RS_Q; ++q) ok[q] = flag[q] != 0;
-        // chunks inside a skipped huge Gaussian's rows: nothing to stage
-        if (!__ballot(n != 0 && s < c1 && e > c0)) {
-#pragma unroll
-            for (int q = 0; q < RS_Q; ++q) {
-                const uint32_t r = c1 + (uint32_t)q * 64u + lane;
-                flag[q] = r < hi ? a.row_valid[r] : 0u;
-            }
-            continue;
-        }
-        float x[RS_Q][GRAD_ROW];
-#pragma unroll
-        for (int q = 0; q < RS_Q; ++q) {
-#pragma unroll
-            for (int c = 0; c < GRAD_ROW; ++c) x[q][c] = 0.f;
-            add_marked_row(x[q], a.inst_grad, c0 + (uint32_t)q * 64u + lane, ok[q]);
-        }
-#pragma unroll
-        for (int q = 0; q < RS_Q; ++q) {
-            const uint32_t r = c1 + (uint32_t)q * 64u + lane;
-            flag[q] = r < hi ? a.row_valid[r] : 0u;
-        }
-#pragma unroll
-        for (int q = 0; q < RS_Q; ++q)
-#pragma unroll
-            for (int c = 0; c < GRAD_ROW; ++c) s_rows[(q * 64 + lane) * GRAD_ROW + c] = x[q][c];
-        wave_sync();
-        // short segments: the owner adds its rows of this chunk in order
-        if (n != 0 && !is_long && s < c1 && e > c0) {
-            const uint32_t j1 = min(e, c1) - c0;
-            for (uint32_t j = max(s, c0) - c0; j < j1; ++j)
-#pragma unroll
-                for (int c = 0; c < GRAD_ROW; ++c) acc[c] += s_rows[j * GRAD_ROW + c];
-        }
-        // long segments overlapping this chunk: the whole wave, one Gaussian at a time
-        uint64_t longs = __ballot(is_long && s < c1 && e > c0);
-        while (longs) {
-            const int jl = __builtin_ctzll(longs);
-            longs &= longs - 1;
-            const uint32_t sj = max(__builtin_amdgcn_readlane(s, jl), c0) - c0;
-            const uint32_t ej = min(__builtin_amdgcn_readlane(e, jl), c1) - c0;
-            float v[GRAD_ROW];
-#pragma unroll
-            for (int c = 0; c < GRAD_ROW; ++c) v[c] = 0.f;
-#pragma unroll
-            for (int q = 0; q < RS_Q; ++q) {
-                const uint32_t pos = (uint32_t)q * 64u + lane;
-                if (pos >= sj && pos < ej)
-#pragma unroll
-                    for (int c = 0; c < GRAD_ROW; ++c) v[c] += x[q][c];
-            }
-            float t8;
-            const float tv = wave_sum9_rows(v, v[8], lane, &t8);  // lane l: total of value (l >> 3) & 7
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const float tc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tv), 8 * c));
-                if ((int)lane == jl) acc[c] += tc;
-            }
-            if ((int)lane == jl) acc[8] += t8;
-        }
-        wave_sync();  // the next chunk overwrites the staging rows
-    }
-#endif
     if (idx < a.g_end && !huge) {
         // a Gaussian without instances (culled: radii 0) has no sums to keep; gaussian_bwd does not read them
-        if (!OMR_SKIP_CULLED_SUMS || n_all != 0) {
+        if (n_all != 0) {
             float* out = a.row_sums + (size_t)idx * GRAD_ROW;
 #pragma unroll
             for (int c = 0; c < GRAD_ROW; ++c) out[c] = acc[c];
@@ -574,9 +490,6 @@ __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
 #define OMR_GBWD_MINW 1
 #endif
 
-#ifndef OMR_GBWD_STAGE
-#define OMR_GBWD_STAGE 1
-#endif
 
 // Everything after the row sums for one visible Gaussian idx (radii > 0). dsh4: where the MC == 16 dL_dsh row goes.
 template <int CAM, int MC>
@@ -788,7 +701,7 @@ template <int CAM, int MC>
 __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussBwdArgs a)
 {
     constexpr int SH_F4 = 12;
-    constexpr bool STAGED = MC == 16 && OMR_GBWD_STAGE;
+    constexpr bool STAGED = MC == 16;
     __shared__ float4 s_stage[4][STAGED ? stage_f4<SH_F4>() : 1];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const int wave_first = a.g_begin + (int)(blockIdx.x * 256u + wv * 64u);
@@ -800,15 +713,15 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
     const bool vis = valid && a.radii[idx] > 0;
     // sums and conic are read for visible Gaussians only (radii > 0 implies instances, preprocess.hip, so
     // row_sum_kernel wrote the row): at config E pinhole 88 % of the Gaussians are culled
-    if (OMR_SKIP_CULLED_SUMS ? vis : valid) {
+    if (vis) {
 #pragma unroll
         for (int c = 0; c < GRAD_ROW; ++c) g[c] = a.row_sums[(size_t)idx * GRAD_ROW + c];
-        if (OMR_BWD_RAW_MOMENTS) co = a.conic_op[idx];
+        co = a.conic_op[idx];
     }
     float4* stage = s_stage[wv];
-    // MC == 16 only (the MC == 0 path reads and writes the rows itself)
-    float4* dsh4 = STAGED ? stage + lane * stage_stride<SH_F4>() : reinterpret_cast<float4*>(a.dL_dsh) + (size_t)idx * SH_F4;
-    const float4* sh4 = STAGED ? stage + lane * stage_stride<SH_F4>() : reinterpret_cast<const float4*>(a.shs) + (size_t)idx * SH_F4;
+    // MC == 16 only (the MC == 0 path reads and writes the rows itself, and skips the write for dL_dsh == NULL)
+    float4* dsh4 = STAGED ? stage + lane * stage_stride<SH_F4>() : nullptr;
+    const float4* sh4 = dsh4;
     if constexpr (STAGED) {
         if (a.shs) {
             const int nf4 = (3 * (a.D + 1) * (a.D + 1) + 3) >> 2;
@@ -818,7 +731,7 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
         }
     }
     if (vis) {
-        if (OMR_BWD_RAW_MOMENTS) raw_row_to_grads(g, co, a.W, a.H);
+        raw_row_to_grads(g, co, a.W, a.H);
         gaussian_bwd_point<CAM, MC>(a, idx, g, sh4, dsh4);
     }
     else if (valid) gaussian_bwd_culled<MC>(a, idx, dsh4);

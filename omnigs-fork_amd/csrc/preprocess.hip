@@ -79,10 +79,6 @@ __device__ __forceinline__ float3 cov2d_from_J(const float* v, const float J0[3]
     return {c00, c01, c11};
 }
 
-#ifndef OMR_PRE_STAGE
-#define OMR_PRE_STAGE 1
-#endif
-
 // What one Gaussian's preprocess produces (forward.cu:693-702); rec = the 64-B render record (raster_common.h)
 struct PreOut {
     float4 rec[SPLAT_F4];
@@ -211,7 +207,7 @@ __device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, int id
     return true;
 }
 
-// One wave per 64 consecutive Gaussians. With OMR_PRE_STAGE the wave reads its 64 SH rows (12 KiB) and writes its
+// One wave per 64 consecutive Gaussians. The wave reads its 64 SH rows (12 KiB) and writes its
 // 64 render records (4 KiB) as contiguous spans through LDS (wave_rows.h). The SH rows are requested before the
 // projection math so their latency overlaps it; pinhole views, which frustum-cull most of a scene, request only
 // the rows of points in front of the camera.
@@ -241,21 +237,15 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     float shv[48];
     if (sh16) {
         float4 shq[SH_F4];
-        if (OMR_PRE_STAGE) {
-            const bool want = CAM == CAM_LONLAT ? valid : valid && transformPoint4x3(p_orig, a.viewmatrix).z > 0.2f;
-            const uint64_t rows = __ballot(want);
-            wave_rows_load<SH_F4>(reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4, rows, nf4,
-                                  stage, lane);
-            wave_sync();
+        const bool want = CAM == CAM_LONLAT ? valid : valid && transformPoint4x3(p_orig, a.viewmatrix).z > 0.2f;
+        const uint64_t rows = __ballot(want);
+        wave_rows_load<SH_F4>(reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4, rows, nf4, stage,
+                              lane);
+        wave_sync();
 #pragma unroll
-            for (int q = 0; q < SH_F4; ++q)
-                shq[q] = q < nf4 ? stage[lane * stage_stride<SH_F4>() + q] : make_float4(0.f, 0.f, 0.f, 0.f);
-            wave_sync();  // the image is reused for the records below
-        } else {
-            const float4* row4 = reinterpret_cast<const float4*>(a.shs + (size_t)idx * 48);
-#pragma unroll
-            for (int q = 0; q < SH_F4; ++q) shq[q] = valid && q < nf4 ? row4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        for (int q = 0; q < SH_F4; ++q)
+            shq[q] = q < nf4 ? stage[lane * stage_stride<SH_F4>() + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        wave_sync();  // the image is reused for the records below
 #pragma unroll
         for (int q = 0; q < SH_F4; ++q) {
             shv[4 * q] = shq[q].x;
@@ -274,23 +264,17 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
         g.val_a[idx] = (uint32_t)idx;
         if (vis) {
             g.clamped[idx] = o.clamp_bits;
-            if (OMR_BWD_RAW_MOMENTS) g.conic_op[idx] = o.rec[1];  // the backward's per-Gaussian factors
+            g.conic_op[idx] = o.rec[1];  // the backward's per-Gaussian factors (raw_row_to_grads)
         }
     }
     // the render record of a visible Gaussian (culled records are never read)
-    if (OMR_PRE_STAGE) {
-        const uint64_t rows = __ballot(vis);
-        if (vis) {
+    const uint64_t rec_rows = __ballot(vis);
+    if (vis) {
 #pragma unroll
-            for (int j = 0; j < SPLAT_F4; ++j) stage[lane * stage_stride<SPLAT_F4>() + j] = o.rec[j];
-        }
-        wave_sync();
-        wave_rows_store<SPLAT_F4>(g.splat + (size_t)wave_first * SPLAT_F4, rows, stage, lane);
-    } else if (vis) {
-        float4* rec = g.splat + (size_t)idx * SPLAT_F4;
-#pragma unroll
-        for (int j = 0; j < SPLAT_F4; ++j) rec[j] = o.rec[j];
+        for (int j = 0; j < SPLAT_F4; ++j) stage[lane * stage_stride<SPLAT_F4>() + j] = o.rec[j];
     }
+    wave_sync();
+    wave_rows_store<SPLAT_F4>(g.splat + (size_t)wave_first * SPLAT_F4, rec_rows, stage, lane);
 }
 
 __global__ void mark_frustum_kernel(int P, const float* means3D, const float* viewmatrix, bool* present)

@@ -39,19 +39,12 @@ constexpr int SCAN_TILE = 4096;
 constexpr int SCAN_ITEMS = SCAN_TILE / SCAN_THREADS;
 
 // per-instance gradient row written by the render backward (render_bwd.hip) and reduced per Gaussian
-// (gaussian_bwd.hip). With OMR_BWD_RAW_MOMENTS (default) the row holds the instance's raw pixel-weight moments
-// S_u dx, S_u dy, S_u dx^2, S_u dx dy, S_u dy^2, S_u, then dcolor.rgb: every factor of backward.cu:805-840 that is
-// the same for all of a Gaussian's instances (conic, opacity, W/2, H/2) is applied once to the Gaussian's sums by
-// gaussian_bwd (raw_row_to_grads), not once per instance. Without it: dmean2D.x, dmean2D.y, dconic.x, dconic.y,
-// dconic.w, dopacity, dcolor.rgb.
+// (gaussian_bwd.hip). The row holds the instance's raw pixel-weight moments S_u dx, S_u dy, S_u dx^2, S_u dx dy,
+// S_u dy^2, S_u, then dcolor.rgb: every factor of backward.cu:805-840 that is the same for all of a Gaussian's
+// instances (conic, opacity, W/2, H/2) is applied once to the Gaussian's sums by gaussian_bwd (raw_row_to_grads),
+// not once per instance. Row sums of Gaussians without instances are neither written (row_sum_kernel) nor read
+// (gaussian_bwd_kernel).
 constexpr int GRAD_ROW = 9;
-#ifndef OMR_BWD_RAW_MOMENTS
-#define OMR_BWD_RAW_MOMENTS 1
-#endif
-// row sums of Gaussians without instances are neither written (row_sum_kernel) nor read (gaussian_bwd_kernel)
-#ifndef OMR_SKIP_CULLED_SUMS
-#define OMR_SKIP_CULLED_SUMS 1
-#endif
 // a Gaussian touching more tiles than this gets a whole workgroup for its row sums (gaussian_bwd.hip); the
 // forward's scan lists these Gaussians (sort.hip: scan2_downsweep_kernel)
 constexpr uint32_t ROW_SUM_HUGE = 256;
@@ -113,7 +106,7 @@ struct GeomState {
     uint32_t* row_first;      // first gradient row of each Gaussian (index-order exclusive scan, launch_forward_scans)
     float* row_sums;          // backward: [P][GRAD_ROW] each Gaussian's instance rows summed (launch_row_sums)
     float4* conic_op;         // [P] conic + opacity (= splat record slot 1), contiguous for gaussian_bwd's coalesced
-                              // read (raw-moment rows: raster_common.h OMR_BWD_RAW_MOMENTS)
+                              // read (raw-moment rows, GRAD_ROW above)
     uint32_t* huge_list;      // Gaussians with more than ROW_SUM_HUGE tiles, any order; count in counters[2]
     int* internal_radii;      // used when the caller passes radii == NULL (rasterizer_impl.cu:284-287)
 

@@ -16,9 +16,9 @@
 // their dx-multiples)
 // The per-Gaussian constants of the reference's expressions (conic, opacity, 0.5 W, 0.5 H, -1/2) are linear
 // factors that every instance of the Gaussian shares, so they are applied neither per pixel nor per instance but
-// once to the Gaussian's summed rows (raster_common.h: OMR_BWD_RAW_MOMENTS); the nine values of an instance are
+// once to the Gaussian's summed rows (raster_common.h: GRAD_ROW); the nine values of an instance are
 // summed over the wave: eight transposed through LDS, the ninth by v_permlane{16,32}_swap + DPP (wave_ops.h).
-// Contributing instances are summed in pairs (OMR_BWD_PAIR): the first one's eight values wait in LDS rows 0-7
+// Contributing instances are summed in pairs: the first one's eight values wait in LDS rows 0-7
 // until the second's fill rows 8-15, then one pass sums both (wave_sum9x2_stored).
 // Lanes 0..8 store the instance's 36-B gradient row, indexed by its row slot (Gaussian-index-major: row_first), with
 // plain stores, and lane 0 marks the slot in row_valid (zeroed before the launch); an instance no pixel takes a contribution from writes
@@ -53,37 +53,14 @@ __device__ unsigned long long g_bwd_counts[5];
 #define BWD_COUNT(k, v)
 #endif
 
-#ifndef OMR_BWD_MINW
-#define OMR_BWD_MINW 1
-#endif
-// wave reduction of the per-instance sums: wave_sum9_rows (1), wave_sum9_lds (2) or the transposed DPP butterfly (0),
-// wave_ops.h
-#ifndef OMR_BWD_ROWS_RED
-#define OMR_BWD_ROWS_RED 2
-#endif
-// with the LDS reduction: reduce the rows of two contributing instances together (wave_sum9x2_lds), the first one
-// held in registers until the second arrives or the unit ends
-#ifndef OMR_BWD_PAIR
-#define OMR_BWD_PAIR 1
-#endif
-#if OMR_BWD_PAIR && OMR_BWD_ROWS_RED != 2
-#error "OMR_BWD_PAIR needs the LDS reduction (OMR_BWD_ROWS_RED 2)"
-#endif
-
-#ifdef OMR_BWD_WPE
-#define OMR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(OMR_BWD_WPE)))
-#else
-#define OMR_BWD_ATTR
-#endif
-__global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) OMR_BWD_ATTR void render_bwd_kernel(RenderBwdArgs a)
+__global__ __launch_bounds__(64 * TW_WAVES) void render_bwd_kernel(RenderBwdArgs a)
 {
     OMR_STAMP_BEGIN
     __shared__ float4 s_geo_all[TW_WAVES][TW_BATCH];   // x, y, position in range (u32 bits), band mask (u32 bits)
     __shared__ float4 s_quad_all[TW_WAVES][TW_BATCH];  // qa, qb, qc, opacity
     __shared__ float4 s_rgb_all[TW_WAVES][TW_BATCH];   // colour, gradient row slot (u32 bits)
-#if OMR_BWD_ROWS_RED == 2
-    __shared__ __attribute__((aligned(16))) float s_red_all[TW_WAVES][(OMR_BWD_PAIR ? 16 : 8) * WS_LDS_STRIDE];
-#endif
+    // rows 0-7: the held instance's eight values, rows 8-15: its partner's (wave_sum9x2_stored)
+    __shared__ __attribute__((aligned(16))) float s_red_all[TW_WAVES][16 * WS_LDS_STRIDE];
     __shared__ float s_floor_all[TW_WAVES][TW_BATCH];  // p2_floor(opacity)
 
     static_assert(TW_WAVES == 1, "one (tile, segment) unit per workgroup");
@@ -168,20 +145,11 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) OMR_BWD_ATTR void rend
 
     // instances behind every pixel's last contributor get no row (row_valid stays 0 for them)
 
-#if !OMR_BWD_RAW_MOMENTS
-    // ddelx_dx, ddely_dy (backward.cu:700-701) = W/2, H/2, with the 2 / log2(e) of the staged conic folded in
-    const float kx = (float)a.W / LOG2E, ky = (float)a.H / LOG2E;
-#endif
-#if !OMR_BWD_ROWS_RED
-    const uint32_t slot_of_lane = transposed_slot_of_lane(lane);
-#endif
 #ifdef OMR_BWD_COUNT
     uint32_t cnt_[5] = {0, 0, 0, 0, 0};
 #endif
-#if OMR_BWD_PAIR
     float pv8 = 0.f;        // the held instance's 9th value (its first eight wait in rows 0-7 of s_red)
     uint32_t pslot = ~0u;   // its gradient row slot (wave-uniform: an SGPR); ~0: nothing held
-#endif
 
     // positions seg_hi-1 .. seg_lo, 64 per batch, back to front: batch entry `lane` <-> position hi-1-lane
     for (int hi = (int)seg_hi; hi > (int)seg_lo; hi -= TW_BATCH) {
@@ -270,38 +238,21 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) OMR_BWD_ATTR void rend
                 sc2 = __builtin_fmaf(wc, dp2b, sc2);
             }
             const uint32_t slot_j = __builtin_bit_cast(uint32_t, f.w);
-#if !OMR_BWD_PAIR
-            float* row = a.inst_grad + (size_t)slot_j * GRAD_ROW;
-#endif
             if (!any) continue;  // no pixel took a contribution: no row
             BWD_COUNT(3, 1);
-#if !OMR_BWD_PAIR
-            if (lane == 0) a.row_valid[slot_j] = 1;  // paired: marked with the pair's row stores
-#endif
             const float su = s_uy.x, suy = s_uy.y;
             const float sux = su * dx, suxx = sux * dx, suxy = suy * dx;
             float v[8];
-#if OMR_BWD_RAW_MOMENTS
             // the raw moments: their per-Gaussian factors are applied once to the Gaussian's sums (raw_row_to_grads)
             v[0] = sux;
             v[1] = suy;
             v[2] = suxx;
             v[3] = suxy;
             v[4] = suyy;
-#else
-            const float o = qo.w;
-            const float hb = 0.5f * q.qb, mo = -0.5f * o;
-            v[0] = (o * kx) * __builtin_fmaf(q.qa, sux, hb * suy);  // dL/dmean2D.x
-            v[1] = (o * ky) * __builtin_fmaf(q.qc, suy, hb * sux);  // dL/dmean2D.y
-            v[2] = mo * suxx;                                        // dL/dconic.x
-            v[3] = mo * suxy;                                        // dL/dconic.y (the reference's half-weight slot)
-            v[4] = mo * suyy;                                        // dL/dconic.w
-#endif
             v[5] = su;                                         // dL/dopacity
             v[6] = sc01.x;                                     // dL/dcolour
             v[7] = sc01.y;
             float t8;
-#if OMR_BWD_PAIR
             float* s_red = s_red_all[wv];
             const uint32_t slot_u = uniform(slot_j);
             const bool held = pslot != ~0u;  // scalar
@@ -323,23 +274,9 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) OMR_BWD_ATTR void rend
                 if ((lane & 31) == 0) a.row_valid[dslot] = 1;
                 pslot = ~0u;
             }
-#elif OMR_BWD_ROWS_RED
-#if OMR_BWD_ROWS_RED == 2
-            const float tv = wave_sum9_lds(v, sc2, lane, s_red_all[wv], &t8);
-#else
-            const float tv = wave_sum9_rows(v, sc2, lane, &t8);
-#endif
-            // lane 8k holds value k (k < 8), every lane the 9th: lanes 0, 8, ..., 56 and 1 store the 36-B row
-            const bool lead = (lane & 7) == 0;
-            if (lead || lane == 1) row[lead ? (lane >> 3) : 8u] = lead ? tv : t8;
-#else
-            const float tv = wave_sum8_transposed(v, sc2, lane, &t8);
-            if (lane < GRAD_ROW) row[slot_of_lane] = lane < 8 ? tv : t8;
-#endif
         }
         wave_sync();  // the next batch overwrites the staging arrays
     }
-#if OMR_BWD_PAIR
     if (pslot != ~0u) {  // the unit's last contributing instance had no partner: sum its rows 0-7 alone
         float v[8], t8;
         const float* r8 = s_red_all[wv];
@@ -350,7 +287,6 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) OMR_BWD_ATTR void rend
         if (lead || lane == 1) a.inst_grad[(size_t)pslot * GRAD_ROW + (lead ? (lane >> 3) : 8u)] = lead ? tv : t8;
         if (lane == 0) a.row_valid[pslot] = 1;
     }
-#endif
     OMR_STAMP_END(g_stamps_bwd, blockIdx.x);
 #ifdef OMR_BWD_COUNT
     if (lane == 0)

@@ -30,12 +30,6 @@ namespace {
 #ifndef OMR_FWD_MINW
 #define OMR_FWD_MINW 8
 #endif
-#ifndef OMR_FWD_PREFETCH
-#define OMR_FWD_PREFETCH 0
-#endif
-#ifndef OMR_FWD_LESS_SALU
-#define OMR_FWD_LESS_SALU 1
-#endif
 
 OMR_STAMP_DECL(g_stamps_fwd)
 
@@ -55,11 +49,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
     float4* s_quad = s_quad_all[wv];
     float4* s_rgb = s_rgb_all[wv];
     float* s_floor = s_floor_all[wv];
-#ifdef OMR_NO_TILE_ORDER
-    const uint32_t tile = unit / FWD_GROUPS;
-#else
     const uint32_t tile = a.tile_order[unit / FWD_GROUPS];
-#endif
     const uint32_t grp = unit % FWD_GROUPS;
     const uint32_t band0 = grp * FWD_BANDS;  // this wave's bands: band0 .. band0 + FWD_BANDS - 1
     const TileLane tl(tile, a.gx);
@@ -153,17 +143,8 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
         }
         wave_sync();  // orders this wave's LDS stores before its reads below
         const uint32_t cnt = (uint32_t)__popcll(useful);
-        float4 g = s_geo[0], qo = s_quad[0], f = s_rgb[0];
         for (uint32_t j = 0; j < cnt; ++j) {
-#if OMR_FWD_PREFETCH
-            // prefetch the next entry (index 63 at most; an entry past cnt is read but never used)
-            const uint32_t jn = min(j + 1, (uint32_t)TW_BATCH - 1);
-            const float4 gn = s_geo[jn], qn = s_quad[jn], fn = s_rgb[jn];
-#else
-            g = s_geo[j];
-            qo = s_quad[j];
-            f = s_rgb[j];
-#endif
+            const float4 g = s_geo[j], qo = s_quad[j], f = s_rgb[j];
             const float pfloor = s_floor[j];
             const uint32_t mb = uniform(__builtin_bit_cast(uint32_t, g.w)) & active;
             const uint32_t contributor = __builtin_bit_cast(uint32_t, g.z) + 1u;
@@ -178,13 +159,9 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
                 const float dy = dy0 - (float)(4 * b);
                 const float p2 = falloff_p2(kq, dy);
                 const bool live = T[b] > 0.0f;
-#if OMR_FWD_LESS_SALU
                 // a done pixel (T < 0) may evaluate: its test_T is negative, so sat holds, wgt = 0, T keeps -|T| and
                 // `last` stays (wgt > 0 below) — the same results with one scalar AND less per band
-                bool ok = p2_in_band(p2, pfloor);  // alpha >= 1/255 (tile_wave.h: p2_floor)
-#else
-                bool ok = live && p2_in_band(p2, pfloor);  // alpha >= 1/255 (tile_wave.h: p2_floor)
-#endif
+                const bool ok = p2_in_band(p2, pfloor);  // alpha >= 1/255 (tile_wave.h: p2_floor)
                 // a lane that is not ok gets alpha = 0: test_T = T, wgt = 0
                 const float alpha = fminf(0.99f, qo.w * __builtin_amdgcn_exp2f(ok ? p2 : -__builtin_inff()));
                 const float test_T = T[b] * (1.0f - alpha);
@@ -199,13 +176,8 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
                 C1[b] = __builtin_fmaf(f.y, wgt, C1[b]);
                 C2[b] = __builtin_fmaf(f.z, wgt, C2[b]);
                 T[b] = sat ? -fabsf(T[b]) : test_T;  // done: keeps the last live T, negated
-#if OMR_FWD_LESS_SALU
                 // blended iff wgt > 0: alpha >= 1/255 and T >= 1e-4 make wgt >= 3.9e-7 on every contributing lane
                 last[b] = wgt > 0.0f ? contributor : last[b];
-#else
-                ok = ok && !sat;
-                last[b] = ok ? contributor : last[b];
-#endif
             }
             if (sat_any) {  // some pixel saturated: drop bands with no live pixel left
 #pragma unroll
@@ -213,11 +185,6 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
                     if (!__ballot(T[b] > 0.0f)) active &= ~(1u << b);
                 if (!active) break;
             }
-#if OMR_FWD_PREFETCH
-            g = gn;
-            qo = qn;
-            f = fn;
-#endif
         }
         wave_sync();  // the next batch overwrites the staging arrays
         start = next_start;

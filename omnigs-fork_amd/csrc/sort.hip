@@ -294,9 +294,6 @@ __device__ __forceinline__ size_t live_count(size_t n, const uint32_t* count)
     return count ? binning_count(count, n) : n;
 }
 
-#ifndef OMR_UPSWEEP_V4
-#define OMR_UPSWEEP_V4 2
-#endif
 // BLOCK_MAJOR: hist[block][digit] (read back by the self-scanning downsweep of small sorts); else hist[digit][block].
 // Key arrays are 16-B aligned (Carver) for the 16-B loads.
 template <typename K, bool BLOCK_MAJOR, int ITEMS, int THREADS>
@@ -315,10 +312,8 @@ __global__ __launch_bounds__(THREADS) void radix_upsweep_kernel(const K* keys, s
     if (threadIdx.x < RADIX) s_hist[threadIdx.x] = 0;
     __syncthreads();
     const size_t base = (size_t)blockIdx.x * TILE_N;
-#if OMR_UPSWEEP_V4
-    // 16-B loads (4 per thread, each wave instruction one contiguous KiB), and one LDS add per distinct digit of
-    // each 64-key group (8-ballot match, as the downsweep ranks): same-address adds within one ds_add serialise,
-    // and neighbouring instances often share a digit
+    // 16-B loads (4 per thread, each wave instruction one contiguous KiB), one LDS atomic per key (one add per
+    // distinct digit of each 64-key group by an 8-ballot match measured slower: C tile sort 0.137 -> 0.164 ms)
     // keys per load: 16 B of them, or 8 B (4 16-bit keys) when ITEMS is not a multiple of 8
     constexpr int KPL = ITEMS % (16 / (int)sizeof(K)) == 0 ? 16 / (int)sizeof(K) : 4;
     static_assert(ITEMS % KPL == 0, "vector key loads");
@@ -349,26 +344,8 @@ __global__ __launch_bounds__(THREADS) void radix_upsweep_kernel(const K* keys, s
         const size_t i = base + KPL * ((size_t)(j / KPL) * THREADS + threadIdx.x) + (j % KPL);
         const bool valid = i < n;
         const uint32_t d = (kv[j] >> shift) & (RADIX - 1);
-        if (OMR_UPSWEEP_V4 == 2) {
-            if (valid) atomicAdd(&s_hist[d], 1u);
-            continue;
-        }
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < RADIX_BITS; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t m = __ballot(bit);
-            peers &= bit ? m : ~m;
-        }
-        if (valid && mask_rank(peers) == 0) atomicAdd(&s_hist[d], (uint32_t)__popcll(peers));
+        if (valid) atomicAdd(&s_hist[d], 1u);
     }
-#else
-#pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-        const size_t i = base + (size_t)k * THREADS + threadIdx.x;
-        if (i < n) atomicAdd(&s_hist[(keys[i] >> shift) & (RADIX - 1)], 1u);
-    }
-#endif
     __syncthreads();
     if (threadIdx.x < RADIX) {
         if (BLOCK_MAJOR) hist[(size_t)blockIdx.x * RADIX + threadIdx.x] = s_hist[threadIdx.x];
@@ -732,9 +709,6 @@ __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* offsets, uin
     return lo;
 }
 
-#ifndef OMR_EMIT_FAST_MASK
-#define OMR_EMIT_FAST_MASK 1
-#endif
 #ifndef OMR_EMIT_OWN_MAX
 #define OMR_EMIT_OWN_MAX 256
 #endif
@@ -826,14 +800,9 @@ __global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap,
             const float4* rec = splat + (size_t)gid * SPLAT_F4;
             const float4 pos = rec[0], co = rec[1], rect = rec[3];
             const BandConsts bc = band_consts(co);
-            if (OMR_EMIT_FAST_MASK) {
-                const BandSpan sp = band_span_consts(bc);
-                s_own_a[i] = make_float4(pos.x, pos.y, sp.kDt, sp.ak);
-                s_own_b[i] = make_float4(sp.adt, sp.At, sp.invA, 0.f);
-            } else {
-                s_own_a[i] = make_float4(pos.x, pos.y, bc.t, bc.k);
-                s_own_b[i] = make_float4(bc.dd, bc.a, 0.f, 0.f);
-            }
+            const BandSpan sp = band_span_consts(bc);
+            s_own_a[i] = make_float4(pos.x, pos.y, sp.kDt, sp.ak);
+            s_own_b[i] = make_float4(sp.adt, sp.At, sp.invA, 0.f);
             s_own_c[i] = make_uint4(__builtin_bit_cast(uint32_t, rect.x), __builtin_bit_cast(uint32_t, rect.y),
                                     __builtin_bit_cast(uint32_t, rect.z) - __builtin_bit_cast(uint32_t, rect.x), gid);
         }
@@ -879,13 +848,8 @@ __global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap,
             const uint32_t tx = oc.x + kx, ty = oc.y + ky;
             key[j] = ty * gx + tx;
             uint32_t m;
-            if (OMR_EMIT_FAST_MASK) {
-                const BandSpan sp = {oa.z, oa.w, ob.x, ob.y, ob.z};
-                m = band_mask_span<PL_BANDS>(sp, make_float2(oa.x, oa.y), tx, ty);
-            } else {
-                const BandConsts bc = {oa.z, oa.w, ob.x, ob.y};
-                m = band_mask_of<PL_BANDS>(bc, make_float2(oa.x, oa.y), tx, ty, 0);
-            }
+            const BandSpan sp = {oa.z, oa.w, ob.x, ob.y, ob.z};
+            m = band_mask_span<PL_BANDS>(sp, make_float2(oa.x, oa.y), tx, ty);
             val[j] = oc.w | (m << PL_GID_BITS);
         }
     } else {
@@ -1137,11 +1101,8 @@ void launch_forward_scans(const uint32_t* tiles_touched, const uint32_t* order, 
 
 size_t radix_hist_size(size_t n) { return (size_t)RADIX * div_up(n, SORT_TILE); }
 
-#ifndef OMR_ONESWEEP
-#define OMR_ONESWEEP 1
-#endif
 
-static bool use_onesweep(size_t n) { return OMR_ONESWEEP && div_up(n, os_tile(n)) <= OS_MAX_BLOCKS; }
+static bool use_onesweep(size_t n) { return div_up(n, os_tile(n)) <= OS_MAX_BLOCKS; }
 
 size_t radix_scratch_words(size_t n, int passes)
 {

@@ -177,14 +177,8 @@ __global__ __launch_bounds__(256) void l1_ssim_kernel(const float* img, const fl
 // row (x, y) and one row of partials. Per input row i: horizontal products of row i; moments, SSIM and partials
 // of row i - 5; the back-filtered gradient of output row i - 10. The taps are summed in the same order as the tiled
 // kernel above, so dL/dimg is bitwise the same; the loss sums differ only in their (fixed) blocking.
-#ifndef OMR_SSIM_STREAM
-#define OMR_SSIM_STREAM 1
-#endif
 #ifndef OMR_SSIM_ROWS
 #define OMR_SSIM_ROWS 48
-#endif
-#ifndef OMR_SSIM_PREFETCH
-#define OMR_SSIM_PREFETCH 0
 #endif
 constexpr int ST_OUT = 54;  // output columns per strip: lanes 0..53
 constexpr int ST_IN = 74;   // input columns x0-10 .. x0+63
@@ -217,17 +211,12 @@ __device__ __forceinline__ void ssim_stream_row(const StreamCtx& c, const float*
 {
     if (i > c.i1) return;  // wave-uniform
     const int lane = c.lane;
-    // A. input row i (prefetched into registers during row i - 1) to LDS; prefetch row i + 1; horizontal products
-    //    at product column x0 - 5 + lane
+    // A. input row i to LDS (a one-row register prefetch measured no faster); horizontal products at product
+    //    column x0 - 5 + lane
     float2* buf = s_in[i & 1];
-#if !OMR_SSIM_PREFETCH
     ssim_load_row(c, i, pre);
-#endif
     buf[lane] = pre[0];
     if (lane < ST_IN - 64) buf[64 + lane] = pre[1];
-#if OMR_SSIM_PREFETCH
-    ssim_load_row(c, i + 1, pre);
-#endif
     wave_sync();
     {
         float hx = 0.f, hy = 0.f, hxx = 0.f, hyy = 0.f, hxy = 0.f;
@@ -335,9 +324,6 @@ __global__ __launch_bounds__(64) void l1_ssim_stream_kernel(const float* img, co
     }
     float ssim_sum = 0.f, l1_sum = 0.f;
     float2 pre[2];
-#if OMR_SSIM_PREFETCH
-    ssim_load_row(c, c.y0 - 2 * SS_HALO, pre);
-#endif
     for (int base = c.y0 - 2 * SS_HALO; base <= c.i1; base += SS_WIN) {
         ssim_stream_row<0>(c, w, base + 0, s_in, s_p, hb, hd, pre, ssim_sum, l1_sum);
         ssim_stream_row<1>(c, w, base + 1, s_in, s_p, hb, hd, pre, ssim_sum, l1_sum);
@@ -425,7 +411,7 @@ void launch_l1_ssim(const float* img, const float* gt, int C, int H, int W, floa
     const double n = (double)C * H * W;
     // the streaming kernel walks its strip's rows in sequence: it needs enough strips to fill the chip
     // (>= ~2 waves per SIMD); smaller images take the tiled kernel (same dL/dimg bits)
-    const bool stream = OMR_SSIM_STREAM && (size_t)div_up(W, ST_OUT) * div_up(H, ST_ROWS) * C >= 2048;
+    const bool stream = (size_t)div_up(W, ST_OUT) * div_up(H, ST_ROWS) * C >= 2048;
     dim3 grid;
     if (stream) {
         grid = dim3(div_up(W, ST_OUT), div_up(H, ST_ROWS), C);

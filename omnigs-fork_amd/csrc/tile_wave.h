@@ -56,20 +56,13 @@ __device__ __forceinline__ float p2_floor(float opacity)
 // p2 <= 0 && p2 >= floor as ONE vector compare (floor <= 0): v_med3 returns one of its inputs, and p2 itself exactly
 // when it lies in [floor, 0]; a NaN p2 compares unequal. Two v_cmp and an s_and otherwise — the scalar unit is the
 // render forward's tighter issue port.
-#ifndef OMR_MED3_TEST
-#define OMR_MED3_TEST 1
-#endif
 __device__ __forceinline__ bool p2_in_band(float p2, float floor)
 {
-#if OMR_MED3_TEST
     return __builtin_amdgcn_fmed3f(p2, floor, 0.0f) == p2;
-#else
-    return p2 <= 0.0f && p2 >= floor;
-#endif
 }
 
 // The per-Gaussian factors of backward.cu:805-840 applied to a Gaussian's summed raw moments g[0..5] = S_u dx,
-// S_u dy, S_u dx^2, S_u dx dy, S_u dy^2, S_u (OMR_BWD_RAW_MOMENTS rows): dG/ddelx = -G (a dx + b dy), ... With the
+// S_u dy, S_u dx^2, S_u dx dy, S_u dy^2, S_u (raster_common.h: GRAD_ROW): dG/ddelx = -G (a dx + b dy), ... With the
 // staged quadratic form q = (-a/2, -b, -c/2) log2(e):  -(a S_ux + b S_uy) = (2 / log2 e) (qa S_ux + qb/2 S_uy), so
 // dL/dmean2D.x = o W/2 (2 / log2 e) (qa S_ux + qb/2 S_uy), likewise y with (qc, qb/2) and H/2; dL/dconic = -o/2 x
 // the second moments (the reference's half-weight dconic.y slot); dL/dopacity = S_u. In place.

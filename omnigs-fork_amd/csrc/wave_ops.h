@@ -34,36 +34,12 @@ __device__ __forceinline__ float cross_row_sum(float x)
     return a + b;
 }
 
-// Wave-sum of v[0..7] and v8. Returns, in lane l (l < 8), the wave total of value index bitrev3(l); v8 total
-// is returned in *t8 on every lane.
-__device__ __forceinline__ float wave_sum8_transposed(const float v[8], float v8, uint32_t lane, float* t8)
-{
-    const bool b0 = lane & 1, b1 = (lane >> 1) & 1, b2 = (lane >> 2) & 1;
-    float a[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = add_dpp<DPP_XOR1>(b0 ? v[i + 4] : v[i], b0 ? v[i] : v[i + 4]);
-    float b[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) b[i] = add_dpp<DPP_XOR2>(b1 ? a[i + 2] : a[i], b1 ? a[i] : a[i + 2]);
-    // lane i receives lane (i - 4) mod 16, whose bit 2 is flipped: each lane adds its partner's copy of the
-    // value index it keeps; after ror:8 every lane holds the row total of index 4*b0 + 2*b1 + b2
-    float c = add_dpp<DPP_ROR4>(b2 ? b[1] : b[0], b2 ? b[0] : b[1]);
-    c = add_dpp<DPP_ROR8>(c, c);
-    float w8 = add_dpp<DPP_XOR1>(v8, v8);
-    w8 = add_dpp<DPP_XOR2>(w8, w8);
-    w8 = add_dpp<DPP_ROR4>(w8, w8);
-    w8 = add_dpp<DPP_ROR8>(w8, w8);
-    *t8 = cross_row_sum(w8);
-    return cross_row_sum(c);
-}
-
-
 // Wave-sum of v[0..7] and v8 with the cross-row levels FIRST, where v_permlane32_swap / v_permlane16_swap move
 // whole halves / rows between two registers in one instruction (no per-lane select, unlike the DPP levels):
 //   level 1  permlane32_swap(v[i], v[i+4]) + add: lanes 0-31 hold v[i] summed with lane+32, lanes 32-63 v[i+4]
 //   level 2  permlane16_swap(a[i], a[i+2]) + add: row r of b[i] holds value index i + 2r, summed over 4 rows
 //   level 3  within the row (DPP row_ror:8, select by lane bit 3), then an 8-lane sum (xor1, xor2, half mirror)
-// 26 VALU (+2 s_nop) against 34 for wave_sum8_transposed. Returns, in every lane l, the wave total of value index
+// 26 VALU (+2 s_nop) against 34 for a transposed DPP butterfly. Returns, in every lane l, the wave total of value index
 // (l >> 3) & 7; *t8 = the total of v8 on every lane.
 __device__ __forceinline__ float wave_sum9_rows(const float v[8], float v8, uint32_t lane, float* t8)
 {
@@ -155,12 +131,6 @@ __device__ __forceinline__ float wave_sum9x2_stored(float va8, float vb8, uint32
               (((c.x + c.y) + (c.z + c.w)) + ((d.x + d.y) + (d.z + d.w)));
     s = add_dpp<DPP_XOR1>(s, s);
     return add_dpp<DPP_XOR2>(s, s);
-}
-
-// lane l < 8 holds value index bitrev3(l) after wave_sum8_transposed; lane 8 is used for the 9th value
-__device__ __forceinline__ uint32_t transposed_slot_of_lane(uint32_t lane)
-{
-    return lane < 8 ? (((lane & 1) << 2) | (lane & 2) | ((lane >> 2) & 1)) : 8u;
 }
 
 }  // namespace omr

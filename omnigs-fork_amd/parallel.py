@@ -135,18 +135,20 @@ def allreduce_compact_(buf: GradBuffer, info: DistInfo, dL_dcolors: torch.Tensor
 class CompactExchange:
     """allreduce_compact_ with the colour all-gather overlapped with the rest of the backward (module docstring).
 
-    Per step: call the backward with **backward_kwargs() (event + skip_dsh), then start() (queues the all-gather on a
-    side stream behind the event), then finish() (all-reduce of the 44 B/G prefix on the current stream once the
-    backward is done, then the SH rebuild behind both collectives). Over gloo (CPU rehearsals), or when `overlap` is
-    False (e.g. a host that cannot pass the event), it falls back to allreduce_compact_ inside finish()."""
+    Per step: call the backward with **backward_kwargs(campos) (event + skip_dsh; campos = this step's camera
+    position, copied into the gathered row P on the current stream BEFORE the backward is queued, so the all-gather
+    behind the event sees it), then start() (queues the all-gather on a side stream behind the event), then finish()
+    (all-reduce of the 44 B/G prefix on the current stream once the backward is done, then the SH rebuild behind both
+    collectives). Over gloo (CPU rehearsals), or when `overlap` is False (e.g. a host that cannot pass the event), it
+    falls back to allreduce_compact_ inside finish(). A trainer whose ranks change viewpoint every step must pass
+    each step's campos: the SH rebuild evaluates the view directions from it."""
 
     def __init__(self, buf: GradBuffer, info: DistInfo, campos: torch.Tensor, rebuild_packed, device,
                  overlap: bool = True, any_backend: bool = False):
         self.buf, self.info, self.rebuild_packed = buf, info, rebuild_packed
-        self.campos = campos
         P = buf.P
         buf.out_dict(device)  # creates colors_ext [P + 1, 3]
-        buf.colors_ext[P].copy_(campos.reshape(3).to(buf.colors_ext.dtype))
+        self.set_campos(campos)
         # any_backend: also overlap over gloo (ranks sharing one GPU in tests and `bench.py --rehearse`: the same
         # event / side-stream / collective sequence as over RCCL, with gloo's host copies)
         self.overlap = bool(overlap and info.enabled and (any_backend or dist.get_backend() == "nccl"))
@@ -155,7 +157,16 @@ class CompactExchange:
             self.comm = torch.cuda.Stream(device)
             self.packed_all = torch.empty((info.world_size, P + 1, 3), dtype=buf.colors_ext.dtype, device=device)
 
-    def backward_kwargs(self) -> dict:
+    def set_campos(self, campos: torch.Tensor):
+        """This step's camera position: stream-ordered copy into row P of the gathered tensor (current stream)."""
+        self.campos = campos
+        self.buf.colors_ext[self.buf.P].copy_(campos.reshape(3).to(self.buf.colors_ext.dtype))
+
+    def backward_kwargs(self, campos: torch.Tensor | None = None) -> dict:
+        """Keyword arguments of this step's RasterizeGaussiansBackwardCUDA call; campos: this step's camera position
+        (None = unchanged since the last step). Call before queueing the backward."""
+        if campos is not None:
+            self.set_campos(campos)
         return dict(colors_event=self.event, skip_dsh=True) if self.overlap else {}
 
     def start(self):

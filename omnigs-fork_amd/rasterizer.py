@@ -60,6 +60,7 @@ def lib() -> C.CDLL:
         L.omr_image_bytes.argtypes = [i, i]
         L.omr_binning_bytes.restype = sz
         L.omr_binning_bytes.argtypes = [i, i, i]
+        L.omr_forward_status.argtypes = [vp, i, vp]
         L.omr_backward_colors_event.argtypes = [vp]
         L.omr_backward_colors_event.restype = None
         L.omr_debug_point_list.argtypes = [vp, i, i, i, vp, vp]
@@ -67,7 +68,6 @@ def lib() -> C.CDLL:
         L.omr_debug_image_state.argtypes = [vp, i, i, vp, vp, vp]
         L.omr_debug_tile_cost.argtypes = [vp, i, i, vp, vp]
         L.omr_debug_geometry.argtypes = [vp, i, vp, vp, vp, vp, vp, vp]
-        L.omr_debug_wave_sum.argtypes = [vp, vp, vp]
         L.omr_debug_wave_sum9.argtypes = [vp, vp, vp]
         L.omr_debug_wave_sum9_lds.argtypes = [vp, vp, vp]
         L.omr_debug_wave_sum9x2.argtypes = [vp, vp, vp]
@@ -521,20 +521,26 @@ def runtime_stats_reset():
     lib().omr_runtime_stats_reset()
 
 
+def forward_status(geomBuffer: torch.Tensor, P: int) -> None:
+    """For forward-only callers: raises RasterizerError if the forward's device-side binning (emit, tile sort) failed
+    after RasterizeGaussiansCUDA returned (a decoupled look-back gave up: the view rendered background only). A
+    backward on the same buffers reports the same failure itself. Synchronises the current stream."""
+    _check(lib().omr_forward_status(geomBuffer.data_ptr(), int(P), _stream(geomBuffer.device)), "forward_status")
+
+
 def loaded_library() -> str:
     """Absolute path of the HIP library this process loaded (OMR_LIB_PATH or the in-tree build)."""
     lib()
     return os.path.realpath(LIB_PATH)
 
 
-def debug_wave_sum(x: torch.Tensor, rows: bool = False, lds: bool = False) -> torch.Tensor:
-    """Column sums of a [64, 9] float32 device tensor through a wave reduction of wave_ops.h: the transposed DPP
-    butterfly (default), the cross-row-first wave_sum9_rows (rows=True) or wave_sum9_lds (lds=True, the render
-    backward's)."""
+def debug_wave_sum(x: torch.Tensor, lds: bool = False) -> torch.Tensor:
+    """Column sums of a [64, 9] float32 device tensor through a wave reduction of wave_ops.h: the cross-row-first
+    wave_sum9_rows (default; the row sums') or wave_sum9_lds (lds=True, the render backward's unpaired one)."""
     x = _dev_f32(x, "x")
     assert tuple(x.shape) == (64, 9)
     out = torch.empty(9, dtype=torch.float32, device=x.device)
-    fn = lib().omr_debug_wave_sum9_lds if lds else (lib().omr_debug_wave_sum9 if rows else lib().omr_debug_wave_sum)
+    fn = lib().omr_debug_wave_sum9_lds if lds else lib().omr_debug_wave_sum9
     _check(fn(x.data_ptr(), out.data_ptr(), _stream(x.device)), "debug_wave_sum")
     return out
 

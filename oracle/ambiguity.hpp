@@ -1,21 +1,40 @@
 // ambiguity.hpp — how much of a result the missing reference run could still move (TEST INFRASTRUCTURE ONLY).
 //
-// The oracle is a restatement: no run of the CUDA reference pins it. Where the reference's own
-// arithmetic could decide differently from ours, a parity claim rests on the restatement alone. This counts those
-// places on a forward the oracle has just run (SURVEY.md §7 "Hard parts" 1, VERDICT r1 "quantify the unpinned
-// residual"):
+// The oracle is a restatement: no run of the CUDA reference pins it. Where the reference AS
+// COMPILED could decide differently from the restatement, a parity claim rests on the restatement alone. Two
+// effects separate them:
+//   1. transcendental implementations: libdevice atan2f / asinf / expf vs the shared omni_math.h and v_exp_f32;
+//   2. FMA contraction: nvcc's default --fmad=true (no -fmad flag in /root/reference/CMakeLists.txt:60-85) fuses
+//      mul+add pairs the oracle (-ffp-contract=off) rounds twice: transformPoint4x3 / 4x4 (auxiliary.h:85-104),
+//      too_close's rr (auxiliary.h:206), the cov2D products (forward.cu:86-228), det / mid / lambda
+//      (forward.cu:660-674), the falloff power (forward.cu:434, backward.cu:774). oracle/contraction.py measures
+//      the effect with two contracted builds of this oracle (GCC and LLVM fuse different multiplies).
+// This file bounds both from the restatement's own forward, per decision, with explicit error windows, and
+// returns the sets the parity tests excuse (tests/helpers.py: reference_allowance):
 //
-//  * rect-ambiguous Gaussians: lonlat pixel centres come from atan2f / asinf (auxiliary.h:236-248), which CUDA
-//    libdevice, ROCm OCML, glibc and our shared omni_math.h may round differently (<= 3 ulp measured against glibc,
-//    tests/test_math.py). A Gaussian whose getRect (auxiliary.h:56-66) changes when lon or lat moves by up to
-//    `ulps` ulp (every combination) could own other tiles -> other keys and point lists in the reference;
-//  * threshold pixels: a blend decision within `eps` (relative) of a threshold, alpha at 1/255
-//    (forward.cu:436-437) or T (1 - alpha) at 1e-4 (:440-444), where exp implementations (libdevice expf, v_exp_f32,
-//    glibc expf) may decide differently; such a pixel can differ by one Gaussian's contribution;
-//  * flip-affected Gaussians: the Gaussians whose own decision sits at a threshold somewhere. When it flips, that
-//    Gaussian gains or loses the whole pixel term of its gradient; every other Gaussian of the pixel changes by a
-//    term scaled by the flipped alpha (~1/255) or by the transmittance at saturation (~1e-4), inside the bar.
-// The parity tests use the last set to bound which gradient entries may fall outside the bar.
+//  * rect-ambiguous Gaussians: getRect (auxiliary.h:56-66) changes when the pixel centre moves by k_pos ulp (or, for
+//    lonlat, lon / lat by atan_ulps ulp), or when the radius ceil(3 sqrt(lambda_max)) (forward.cu:672) sits within
+//    its rounding window of an integer and radius +-1 moves the rect. Such a Gaussian may own other tiles in the
+//    reference: pixels of the tiles it gains or loses where it reaches alpha >= 1/255 are marked (PX_RECT);
+//  * order-ambiguous pairs: same-tile neighbours of the sorted list whose depths (the sort key's low 32 bits,
+//    rasterizer_impl.cu:133) differ by less than the sum of their depth rounding windows may sort the other way;
+//    a pixel where two members of such a run both blend is marked (PX_ORDER);
+//  * threshold pixels: a blend decision inside its window — alpha at 1/255 (forward.cu:436-437), power at 0
+//    (:434-435), T (1 - alpha) at 1e-4 (:440-444). The window of power is the rounding bound of its evaluation from
+//    rounded conic and centre: (kappa_g + k_eval eps) S + u G, S = a dx^2 / 2 + c dy^2 / 2 + |b dx dy|,
+//    G = |a dx + b dy| + |b dx + c dy|, u = k_pos ulp of the centre, kappa_g = k_eval eps (|ac| + b^2) / |ac - b^2|
+//    (the conic's condition); plus eps_exp for the exp implementations. T's window accumulates alpha x the power
+//    window of every blended Gaussian in front;
+//  * per flagged pixel, a bound on the colour change the flagged decisions can make (Allowance::bound, any channel):
+//    each flipped term moves the pixel by at most its blend weight alpha T times the colour span 2 cmax (cmax = the
+//    largest |colour| of the scene and background): alpha ~1/255 for an alpha flip, the opacity for a power-0 flip,
+//    alpha_a alpha_b for an order swap, the transmittance ~1e-4 at saturation, the Gaussian's reach for a rect;
+//  * flip Gaussians: the Gaussians owning any such decision. When one flips, that Gaussian gains or loses a whole
+//    pixel term (or swaps its order with its pair) and its gradient may leave the bar;
+//  * exposed Gaussians (G_EXPOSED): the ones blending behind such a decision (alpha, power 0, order, rect). Their
+//    pixel term there scales by the flipped alpha (~1/255 for a threshold flip) — small against the Gaussian's total,
+//    unless its pixel terms cancel; the parity tests give them a wider bar (tests/helpers.py). A saturation flip only
+//    moves terms of transmittance ~1e-4 and exposes no one.
 #pragma once
 
 #include <cmath>
@@ -26,13 +45,36 @@
 
 namespace oracle {
 
-struct Ambiguity {
-    int64_t rect_gaussians = 0;   // lonlat Gaussians whose tile rect moves under +-ulps of atan2 / asin
-    int64_t alpha_pixels = 0;     // pixels with an alpha decision within eps of 1/255
-    int64_t sat_pixels = 0;       // pixels with a T(1 - alpha) decision within eps of 1e-4
-    int64_t flip_gaussians = 0;   // Gaussians whose own blend decision sits at a threshold
-    std::vector<uint8_t> flip;    // [P] 1 = flip-affected
+// pixel flags (Allowance::pixel)
+enum : uint8_t { PX_ALPHA = 1, PX_SAT = 2, PX_ZERO = 4, PX_ORDER = 8, PX_RECT = 16 };
+// Gaussian flags (Allowance::flip)
+// G_RUN: member of an order-ambiguous run of some tile's list (its position may change; its result only where two
+// members blend at one pixel, G_ORDER)
+// G_RADIUS: the radius output (forward.cu:672) may differ by one in the reference (with or without a rect change)
+enum : uint8_t { G_THRESHOLD = 1, G_ORDER = 2, G_RECT = 4, G_EXPOSED = 8, G_RUN = 16, G_RADIUS = 32 };
+
+struct AllowanceParams {
+    double eps_exp = 1e-5;  // relative window of alpha and T for the exp implementations
+    int atan_ulps = 3;      // lonlat: ulps of atan2f / asinf (tests/test_math.py: <= 3 against glibc)
+    double k_eval = 8.0;    // ulps (of the evaluated terms) for a contracted vs uncontracted expression
+    double k_pos = 4.0;     // ulps of the pixel centre coordinates
+    double k_depth = 8.0;   // ulps of the largest term of the view transform, for the depth key
 };
+
+struct Allowance {
+    int64_t rect_gaussians = 0;    // flip & G_RECT
+    int64_t radius_gaussians = 0;  // radius within its rounding window of an integer (a subset may move the rect)
+    int64_t alpha_pixels = 0, sat_pixels = 0, zero_pixels = 0, order_pixels = 0, rect_pixels = 0;
+    int64_t order_pairs = 0;       // adjacent same-tile instances whose order the reference may swap
+    int64_t flip_gaussians = 0;    // Gaussians with any flag
+    int64_t threshold_gaussians = 0, order_gaussians = 0, exposed_gaussians = 0;
+    int64_t any_pixels = 0;
+    std::vector<uint8_t> flip;     // [P] G_* flags
+    std::vector<uint8_t> pixel;    // [H*W] PX_* flags
+    std::vector<float> bound;      // [H*W] largest colour change the flagged decisions can make (per channel)
+};
+
+constexpr double EPS32 = 5.9604644775390625e-08;  // 2^-24
 
 inline float step_ulps(float v, int k)
 {
@@ -40,89 +82,270 @@ inline float step_ulps(float v, int k)
     for (; k < 0; ++k) v = std::nextafter(v, -INFINITY);
     return v;
 }
+inline double ulp_of(float v) { return (double)std::nextafter(std::fabs(v), INFINITY) - std::fabs(v); }
 
 // getRect of a lonlat Gaussian for lon / lat moved by (dl, db) ulp (forward.cu:630-640 order of operations)
-inline Rect lonlat_rect_perturbed(const State<float>& s, int idx, int dl, int db)
+inline Rect lonlat_rect_perturbed(const State<float>& s, int idx, int dl, int db, int radius)
 {
     const Args<float>& a = s.a;
     V3<float> p_orig = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
-    V4<float> pv;
+    V4<float> pv = {0.f, 0.f, 0.f, 0.f};
     too_close(p_orig, a.viewmatrix, pv);
     const float inv_r = 1.0f / (pv.w + 0.0000001f);
     const float lon = step_ulps(Math<float>::atan2(pv.x, pv.z), dl);
     const float lat = step_ulps(Math<float>::asin(pv.y * inv_r), db);
     const V2<float> p_proj = {lon * R_1_PI<float>, lat * R_2_PI<float>};
     const V2<float> pix = {ndc2Pix(p_proj.x, a.width), ndc2Pix(p_proj.y, a.height)};
-    return getRect(pix, s.radii[idx], s.gx, s.gy);
+    return getRect(pix, radius, s.gx, s.gy);
 }
 
-inline Ambiguity ambiguity_scan(const State<float>& s, double eps, int ulps)
+inline bool same_rect(const Rect& p, const Rect& q)
 {
-    Ambiguity out;
+    return p.minx == q.minx && p.maxx == q.maxx && p.miny == q.miny && p.maxy == q.maxy;
+}
+
+// rounding window of the depth key of a visible Gaussian: the view transform's components carry an absolute error
+// of ~k_depth eps x their largest term (auxiliary.h:85-93); lonlat depth = |p_view| (auxiliary.h:206-213)
+inline double depth_window(const State<float>& s, int idx, const AllowanceParams& prm)
+{
+    const Args<float>& a = s.a;
+    const float* m = a.viewmatrix;
+    const double p[3] = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
+    double tmax = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        if (a.camera_type != 3 && i != 2) continue;  // pinhole depth = p_view.z
+        const double t = std::fabs(m[i] * p[0]) + std::fabs(m[4 + i] * p[1]) + std::fabs(m[8 + i] * p[2]) +
+                         std::fabs((double)m[12 + i]);
+        tmax = std::fmax(tmax, t);
+    }
+    return prm.k_depth * EPS32 * tmax + 2.0 * EPS32 * std::fabs((double)s.depths[idx]);
+}
+
+// x = 3 sqrt(lambda_max) (forward.cu:663-672) and its rounding window, from the conic (the inverse of cov2D)
+inline void radius_window(const V4<float>& co, const AllowanceParams& prm, double& x, double& dx)
+{
+    const double dc = (double)co.x * co.z - (double)co.y * co.y;
+    const double a = co.z / dc, b = -co.y / dc, c = co.x / dc;  // cov2D
+    const double det = a * c - b * b, mid = 0.5 * (a + c);
+    const double arg = mid * mid - det;
+    const double sq = std::sqrt(std::fmax(0.1, arg));
+    const double lam = mid + sq;
+    x = 3.0 * std::sqrt(std::fmax(lam, mid - sq));
+    double dlam = prm.k_eval * EPS32 * mid;
+    if (arg > 0.1) dlam += prm.k_eval * EPS32 * (mid * mid + std::fabs(det)) / (2.0 * sq);
+    dx = 3.0 * dlam / (2.0 * std::sqrt(std::fmax(lam, 1e-30))) + prm.k_eval * EPS32 * x;
+}
+
+inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& prm)
+{
+    Allowance out;
     const Args<float>& a = s.a;
     const int P = a.P, W = a.width, H = a.height;
     out.flip.assign(P, 0);
+    out.pixel.assign((size_t)W * H, 0);
+    out.bound.assign((size_t)W * H, 0.f);
     if (P == 0) return out;
-    if (a.camera_type == 3) {
-        int64_t n = 0;
-#pragma omp parallel for schedule(dynamic, 4096) reduction(+ : n)
-        for (int i = 0; i < P; ++i) {
-            if (s.radii[i] <= 0) continue;
-            const Rect base = lonlat_rect_perturbed(s, i, 0, 0);
-            bool moved = false;
-            for (int dl = -ulps; dl <= ulps && !moved; ++dl)
-                for (int db = -ulps; db <= ulps && !moved; ++db) {
-                    const Rect r = lonlat_rect_perturbed(s, i, dl, db);
-                    moved = r.minx != base.minx || r.maxx != base.maxx || r.miny != base.miny || r.maxy != base.maxy;
-                }
-            n += moved ? 1 : 0;
-        }
-        out.rect_gaussians = n;
-    }
-    // blend decisions, walked exactly as render_tile (forward.cu:346-467), in double so the window is not itself
-    // blurred by float rounding
     const uint32_t T = s.gx * s.gy;
-    int64_t na = 0, ns = 0;
-    std::vector<std::vector<uint32_t>> marked(T);
-#pragma omp parallel for schedule(dynamic, 4) reduction(+ : na, ns)
+    const float* features = a.colors_precomp != nullptr ? a.colors_precomp : s.rgb.data();
+    double cmax = 0.0;
+    for (int ch = 0; ch < 3; ++ch) cmax = std::fmax(cmax, std::fabs((double)a.background[ch]));
+    for (int i = 0; i < P; ++i)
+        if (s.radii[i] > 0)
+            for (int ch = 0; ch < 3; ++ch) cmax = std::fmax(cmax, std::fabs((double)features[3 * i + ch]));
+    const double span = 2.0 * cmax;
+
+    // per Gaussian: depth window, conic condition, centre window; rect / radius ambiguity
+    std::vector<double> dwin(P, 0.0), kappa(P, 0.0), upos(P, 0.0);
+    std::vector<Rect> alt_rect(P);  // the union of the rects the reference could use (rect-ambiguous ones)
+    int64_t n_rect = 0, n_rad = 0;
+#pragma omp parallel for schedule(dynamic, 4096) reduction(+ : n_rect, n_rad)
+    for (int i = 0; i < P; ++i) {
+        if (s.radii[i] <= 0) continue;
+        dwin[i] = depth_window(s, i, prm);
+        const V4<float> co = s.conic_opacity[i];
+        const double ac = (double)co.x * co.z, bb = (double)co.y * co.y;
+        kappa[i] = prm.k_eval * EPS32 * (std::fabs(ac) + bb) / std::fmax(std::fabs(ac - bb), 1e-300);
+        const V2<float> m2 = s.means2D[i];
+        upos[i] = prm.k_pos * std::fmax(ulp_of(m2.x), ulp_of(m2.y));
+        // radius window
+        double x, dx;
+        radius_window(co, prm, x, dx);
+        const int r0 = s.radii[i];
+        int rlo = r0, rhi = r0;
+        if ((int)std::ceil(x - dx) != r0 || (int)std::ceil(x + dx) != r0) {
+            n_rad += 1;
+            out.flip[i] |= G_RADIUS;
+            rlo = std::min(r0, (int)std::ceil(x - dx));
+            rhi = std::max(r0, (int)std::ceil(x + dx));
+        }
+        const Rect base = getRect(m2, r0, s.gx, s.gy);
+        Rect un = base;
+        bool moved = false;  // some candidate rect differs (grown or shrunk)
+        auto widen = [&](const Rect& r) {
+            moved = moved || !same_rect(r, base);
+            un.minx = std::min(un.minx, r.minx); un.miny = std::min(un.miny, r.miny);
+            un.maxx = std::max(un.maxx, r.maxx); un.maxy = std::max(un.maxy, r.maxy);
+        };
+        for (int rad = rlo; rad <= rhi; ++rad)
+            for (int sx = -1; sx <= 1; ++sx)
+                for (int sy = -1; sy <= 1; ++sy) {
+                    const V2<float> p = {(float)(m2.x + sx * upos[i]), (float)(m2.y + sy * upos[i])};
+                    widen(getRect(p, rad, s.gx, s.gy));
+                }
+        if (a.camera_type == 3)
+            for (int dl = -prm.atan_ulps; dl <= prm.atan_ulps; ++dl)
+                for (int db = -prm.atan_ulps; db <= prm.atan_ulps; ++db)
+                    for (int rad = rlo; rad <= rhi; ++rad) widen(lonlat_rect_perturbed(s, i, dl, db, rad));
+        alt_rect[i] = un;
+        if (moved) {
+            out.flip[i] = (uint8_t)(out.flip[i] | G_RECT);
+            n_rect += 1;
+        }
+    }
+    out.rect_gaussians = n_rect;
+    out.radius_gaussians = n_rad;
+
+    // per tile: order runs of the sorted list (consecutive instances whose depths are within the summed windows)
+    // and the rect-ambiguous Gaussians that may join the tile; then every pixel is walked as render_tile
+    // (forward.cu:346-467) in double, decisions tested against their windows
+    std::vector<std::vector<int>> gx_extra(T);  // rect-ambiguous Gaussians that may reach tile t but are not listed
+    for (int i = 0; i < P; ++i) {
+        if (!(out.flip[i] & G_RECT)) continue;
+        const Rect base = getRect(s.means2D[i], s.radii[i], s.gx, s.gy), un = alt_rect[i];
+        for (uint32_t ty = un.miny; ty < un.maxy; ++ty)
+            for (uint32_t tx = un.minx; tx < un.maxx; ++tx) {
+                const bool in_base = tx >= base.minx && tx < base.maxx && ty >= base.miny && ty < base.maxy;
+                if (!in_base) gx_extra[ty * s.gx + tx].push_back(i);
+            }
+    }
+    int64_t na = 0, ns = 0, nz = 0, no = 0, nr = 0, npairs = 0, nany = 0;
+    std::vector<std::vector<std::pair<uint32_t, uint8_t>>> marked(T);
+#pragma omp parallel for schedule(dynamic, 4) reduction(+ : na, ns, nz, no, nr, npairs, nany)
     for (int t = 0; t < (int)T; ++t) {
         const uint32_t tx = t % s.gx, ty = t / s.gx;
         const uint32_t rx = s.ranges[2 * t], ry = s.ranges[2 * t + 1];
+        const uint32_t n = ry - rx;
+        std::vector<uint32_t> run(n);  // run id of each position: consecutive positions in one run may swap
+        uint32_t rid = 0;
+        for (uint32_t k = 0; k < n; ++k) {
+            if (k > 0) {
+                const uint32_t i0 = s.point_list[rx + k - 1], i1 = s.point_list[rx + k];
+                const double gap = std::fabs((double)s.depths[i1] - (double)s.depths[i0]);
+                if (gap <= dwin[i0] + dwin[i1]) {
+                    npairs += 1;
+                    marked[t].push_back({i0, G_RUN});
+                    marked[t].push_back({i1, G_RUN});
+                } else {
+                    rid += 1;
+                }
+            }
+            run[k] = rid;
+        }
         for (int ly = 0; ly < BLOCK_Y; ++ly)
             for (int lx = 0; lx < BLOCK_X; ++lx) {
                 const uint32_t px = tx * BLOCK_X + lx, py = ty * BLOCK_Y + ly;
                 if (!(px < (uint32_t)W && py < (uint32_t)H)) continue;
-                double Tr = 1.0;
-                bool amb_a = false, amb_s = false;
-                for (uint32_t k = rx; k < ry; ++k) {
-                    const uint32_t id = s.point_list[k];
+                uint8_t pf = 0;
+                double Tr = 1.0, errT = 0.0, bnd = 0.0, last_alpha = 0.0;
+                uint32_t last_run = ~0u, last_run_id = 0;
+                bool behind = false;  // a decision in front of this position is ambiguous (alpha, power 0, order, rect)
+                auto eval = [&](uint32_t id, double& power, double& dp) {
                     const double dx = (double)s.means2D[id].x - px, dy = (double)s.means2D[id].y - py;
                     const V4<float> co = s.conic_opacity[id];
-                    const double power = -0.5 * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                    if (power > 0) continue;
-                    const double alpha = std::fmin(0.99, co.w * std::exp(power));
-                    if (std::fabs(alpha - 1.0 / 255.0) < eps / 255.0) {
-                        amb_a = true;
-                        marked[t].push_back(id);
+                    power = -0.5 * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                    const double S = 0.5 * std::fabs(co.x) * dx * dx + 0.5 * std::fabs(co.z) * dy * dy +
+                                     std::fabs(co.y * dx * dy);
+                    const double G = std::fabs(co.x * dx + co.y * dy) + std::fabs(co.y * dx + co.z * dy);
+                    dp = (kappa[id] + prm.k_eval * EPS32) * S + upos[id] * G;
+                };
+                for (uint32_t k = 0; k < n; ++k) {
+                    const uint32_t id = s.point_list[rx + k];
+                    double power, dp;
+                    eval(id, power, dp);
+                    const V4<float> co = s.conic_opacity[id];
+                    if (std::fabs(power) <= dp && power + dp > 0.0) {  // power > 0 skip (forward.cu:434-435)
+                        pf |= PX_ZERO;
+                        marked[t].push_back({id, G_THRESHOLD});
+                        bnd += span * Tr * std::fmin(0.99, (double)co.w);
                     }
-                    if (alpha < 1.0 / 255.0) continue;
+                    if (power > 0) continue;
+                    const double thr = -std::log(255.0 * co.w);  // alpha = o exp(power) = 1/255
+                    if (std::fabs(power - thr) <= dp + prm.eps_exp) {
+                        pf |= PX_ALPHA;
+                        marked[t].push_back({id, G_THRESHOLD});
+                        bnd += span * Tr * (1.0 / 255.0) * std::exp(dp + prm.eps_exp);
+                    }
+                    const double alpha = std::fmin(0.99, co.w * std::exp(power));
+                    if (alpha < 1.0 / 255.0) {
+                        behind = behind || (pf & (PX_ALPHA | PX_ZERO));
+                        continue;
+                    }
+                    if (behind) marked[t].push_back({id, G_EXPOSED});
+                    if (out.flip[id] & G_RECT) {  // a rect-ambiguous Gaussian may leave a tile on its rect's edge
+                        const Rect b = getRect(s.means2D[id], s.radii[id], s.gx, s.gy);
+                        if (tx == b.minx || tx + 1 == b.maxx || ty == b.miny || ty + 1 == b.maxy) {
+                            pf |= PX_RECT;
+                            bnd += span * Tr * alpha;
+                        }
+                    }
+                    behind = behind || (pf & (PX_ALPHA | PX_ZERO | PX_ORDER | PX_RECT));
+                    // order: a second blended member of the same run
+                    if (last_run == run[k]) {
+                        pf |= PX_ORDER;
+                        marked[t].push_back({id, G_ORDER});
+                        marked[t].push_back({last_run_id, G_ORDER});
+                        // swapping a, b moves (alpha_a alpha_b T_a)(c_a - c_b); T after both is unchanged
+                        bnd += span * (Tr / std::fmax(1.0 - last_alpha, 1e-2)) * last_alpha * alpha;
+                    }
+                    last_run = run[k];
+                    last_run_id = id;
+                    last_alpha = alpha;
                     const double test_T = Tr * (1.0 - alpha);
-                    if (std::fabs(test_T - 1e-4) < eps * 1e-4) {
-                        amb_s = true;
-                        marked[t].push_back(id);
+                    const double errk = errT + alpha * dp;
+                    if (std::fabs(test_T - 1e-4) <= (prm.eps_exp + errk) * 1e-4) {
+                        pf |= PX_SAT;
+                        marked[t].push_back({id, G_THRESHOLD});
+                        bnd += span * Tr;  // this term and everything behind carry transmittance <= Tr
                     }
                     if (test_T < 1e-4) break;
                     Tr = test_T;
+                    errT = errk;
                 }
-                na += amb_a ? 1 : 0;
-                ns += amb_s ? 1 : 0;
+                // a rect-ambiguous Gaussian that may join this tile in the reference and reaches the pixel
+                for (int id : gx_extra[t]) {
+                    double power, dp;
+                    eval((uint32_t)id, power, dp);
+                    const float o = s.conic_opacity[id].w;
+                    if (power - dp <= 0.0 && power + dp >= -std::log(255.0 * o) - prm.eps_exp) {
+                        pf |= PX_RECT;
+                        bnd += span * std::fmin(0.99, o * std::exp(std::fmin(0.0, power + dp)));
+                    }
+                }
+                na += (pf & PX_ALPHA) ? 1 : 0;
+                ns += (pf & PX_SAT) ? 1 : 0;
+                nz += (pf & PX_ZERO) ? 1 : 0;
+                no += (pf & PX_ORDER) ? 1 : 0;
+                nr += (pf & PX_RECT) ? 1 : 0;
+                nany += pf ? 1 : 0;
+                out.pixel[(size_t)py * W + px] = pf;
+                out.bound[(size_t)py * W + px] = (float)bnd;
             }
     }
     out.alpha_pixels = na;
     out.sat_pixels = ns;
+    out.zero_pixels = nz;
+    out.order_pixels = no;
+    out.rect_pixels = nr;
+    out.order_pairs = npairs;
+    out.any_pixels = nany;
     for (const auto& v : marked)
-        for (uint32_t id : v) out.flip[id] = 1;
-    for (int i = 0; i < P; ++i) out.flip_gaussians += out.flip[i];
+        for (const auto& e : v) out.flip[e.first] |= e.second;
+    for (int i = 0; i < P; ++i) {
+        out.flip_gaussians += (out.flip[i] & (G_THRESHOLD | G_ORDER | G_RECT)) != 0;
+        out.threshold_gaussians += (out.flip[i] & G_THRESHOLD) != 0;
+        out.order_gaussians += (out.flip[i] & G_ORDER) != 0;
+        out.exposed_gaussians += (out.flip[i] & (G_THRESHOLD | G_ORDER | G_RECT | G_EXPOSED)) == G_EXPOSED;
+    }
     return out;
 }
 

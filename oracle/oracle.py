@@ -13,7 +13,12 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
-_lib = None
+# builds of the same sources (oracle/Makefile): "base" is the parity checker (no FMA contraction); "fma_gcc" /
+# "fma_clang" contract mul+add into FMA as nvcc compiles the reference (oracle/contraction.py); "fast" is the
+# -O3 timing build of bench.py's cpu_baseline
+VARIANTS = {"base": "liboracle.so", "fma_gcc": "liboracle_fma_gcc.so", "fma_clang": "liboracle_fma_clang.so",
+            "fast": "liboracle_fast.so"}
+_libs = {}
 
 _F32 = {"out_color", "depths", "cov3D", "rgb", "final_T", "means2D", "conic_opacity", "dmean2D", "dconic",
         "dopacity", "dcolor", "dmean3D", "dcov3D", "dsh", "dscale", "drot"}
@@ -27,12 +32,12 @@ def build() -> str:
     return _LIB_PATH
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(_LIB_PATH):
+def lib(variant: str = "base"):
+    if variant not in _libs:
+        path = os.path.join(_HERE, "_build", VARIANTS[variant])
+        if not os.path.exists(path):
             build()
-        L = C.CDLL(_LIB_PATH)
+        L = C.CDLL(path)
         vp, i, f, d = C.c_void_p, C.c_int, C.c_float, C.c_double
         L.oracle_new.restype = vp
         L.oracle_new.argtypes = [i]
@@ -53,9 +58,9 @@ def lib():
         L.oracle_asinf.restype = f
         L.oracle_asinf.argtypes = [f]
         L.oracle_mark_visible.argtypes = [i, vp, vp, vp, i, vp]
-        L.oracle_ambiguity.argtypes = [vp, d, i, vp, C.POINTER(C.c_int64)]
-        _lib = L
-    return _lib
+        L.oracle_allowance.argtypes = [vp, C.POINTER(C.c_double), vp, vp, vp, C.POINTER(C.c_int64)]
+        _libs[variant] = L
+    return _libs[variant]
 
 
 def _ptr(a):
@@ -65,16 +70,18 @@ def _ptr(a):
 class Oracle:
     """One rasterizer instance (geometry/binning/image state kept between forward and backward)."""
 
-    def __init__(self, double: bool = False):
+    def __init__(self, double: bool = False, variant: str = "base"):
         self.double = double
+        self.variant = variant
         self.dtype = np.float64 if double else np.float32
-        self.h = lib().oracle_new(1 if double else 0)
+        self.L = lib(variant)
+        self.h = self.L.oracle_new(1 if double else 0)
         self._keep = []
 
     def __del__(self):
         try:
             if self.h:
-                lib().oracle_free(self.h)
+                self.L.oracle_free(self.h)
         except Exception:
             pass
 
@@ -89,12 +96,13 @@ class Oracle:
                 cov3D_precomp=None, viewmatrix, projmatrix, campos, width, height, sh_degree=3,
                 scale_modifier=1.0, tanfovx=0.0, tanfovy=0.0, prefiltered=False, camera_type=3, render_depth=False):
         self._keep = []
+        self.background = np.asarray(background, dtype=np.float64).reshape(3)
         P = int(means3D.shape[0])
         M = 0 if shs is None or shs.shape[0] == 0 else int(shs.shape[1])
         args = [self._arr(x) for x in (background, means3D, shs, colors_precomp, opacity, scales)]
         rest = [self._arr(x) for x in (rotations, cov3D_precomp, viewmatrix, projmatrix, campos)]
         err = C.create_string_buffer(512)
-        fn = lib().oracle_forward_f64 if self.double else lib().oracle_forward_f32
+        fn = self.L.oracle_forward_f64 if self.double else self.L.oracle_forward_f32
         L = fn(self.h, P, int(sh_degree), M, _ptr(args[0]), int(width), int(height), _ptr(args[1]), _ptr(args[2]),
                _ptr(args[3]), _ptr(args[4]), _ptr(args[5]), scale_modifier, _ptr(rest[0]), _ptr(rest[1]),
                _ptr(rest[2]), _ptr(rest[3]), _ptr(rest[4]), tanfovx, tanfovy, int(prefiltered), int(camera_type),
@@ -106,18 +114,18 @@ class Oracle:
 
     def get(self, name: str) -> np.ndarray:
         es = C.c_int(0)
-        n = lib().oracle_size(self.h, name.encode(), C.byref(es))
+        n = self.L.oracle_size(self.h, name.encode(), C.byref(es))
         if n < 0:
             raise KeyError(name)
         dt = _DT.get(name, self.dtype)
         out = np.empty(n, dtype=dt)
         if n:
-            lib().oracle_get(self.h, name.encode(), _ptr(out))
+            self.L.oracle_get(self.h, name.encode(), _ptr(out))
         return out
 
     def backward(self, dL_dout: np.ndarray, nthreads: int = 1):
         d = np.ascontiguousarray(dL_dout, dtype=self.dtype)
-        lib().oracle_backward(self.h, _ptr(d), int(nthreads))
+        self.L.oracle_backward(self.h, _ptr(d), int(nthreads))
         P, M = self.P, self.M
         return dict(dmean2D=self.get("dmean2D").reshape(P, 3), dconic=self.get("dconic").reshape(P, 4),
                     dopacity=self.get("dopacity").reshape(P, 1), dcolor=self.get("dcolor").reshape(P, 3),
@@ -125,27 +133,52 @@ class Oracle:
                     dsh=self.get("dsh").reshape(P, M, 3), dscale=self.get("dscale").reshape(P, 3),
                     drot=self.get("drot").reshape(P, 4))
 
-    def ambiguity(self, eps: float = 1e-5, ulps: int = 3):
-        """ambiguity.hpp on the last (float) forward: dict of counts and the [P] flip-affected mask."""
-        counts = (C.c_int64 * 4)()
+    # what the reference as compiled may decide differently (oracle/ambiguity.hpp); the parity tests excuse
+    # exactly these pixels and Gaussians (tests/helpers.py: reference_allowance)
+    ALLOWANCE_DEFAULTS = dict(eps_exp=1e-5, atan_ulps=3, k_eval=8.0, k_pos=4.0, k_depth=8.0)
+    ALLOWANCE_COUNTS = ("rect_gaussians", "radius_gaussians", "alpha_pixels", "saturation_pixels", "zero_power_pixels",
+                        "order_pixels", "rect_pixels", "order_pairs", "flip_gaussians", "threshold_gaussians",
+                        "order_gaussians", "allowed_pixels", "exposed_gaussians")
+    PX = dict(alpha=1, saturation=2, zero_power=4, order=8, rect=16)
+    G = dict(threshold=1, order=2, rect=4, exposed=8, run=16, radius=32)
+
+    def allowance(self, **kw):
+        """ambiguity.hpp's allowance_scan on the last (float) forward. Returns (counts dict, flip [P] uint8 of G flags,
+        pixel [H, W] uint8 of PX flags, bound [H, W] float32: the largest colour change those decisions can make)."""
+        if self.double:
+            raise RuntimeError("allowance needs a float forward")
+        prm = dict(self.ALLOWANCE_DEFAULTS, **kw)
+        pv = (C.c_double * 5)(prm["eps_exp"], prm["atan_ulps"], prm["k_eval"], prm["k_pos"], prm["k_depth"])
         flip = np.zeros(self.P, dtype=np.uint8)
-        if lib().oracle_ambiguity(self.h, float(eps), int(ulps), _ptr(flip), counts) != 0:
-            raise RuntimeError("ambiguity needs a float forward")
-        return dict(rect_gaussians=int(counts[0]), alpha_pixels=int(counts[1]), saturation_pixels=int(counts[2]),
-                    flip_gaussians=int(counts[3]), eps=eps, ulps=ulps), flip.astype(bool)
+        pix = np.zeros(self.W * self.H, dtype=np.uint8)
+        bound = np.zeros(self.W * self.H, dtype=np.float32)
+        counts = (C.c_int64 * 13)()
+        if self.L.oracle_allowance(self.h, pv, _ptr(flip), _ptr(pix), _ptr(bound), counts) != 0:
+            raise RuntimeError("allowance failed")
+        out = {k: int(counts[i]) for i, k in enumerate(self.ALLOWANCE_COUNTS)}
+        out.update(prm)
+        return out, flip, pix.reshape(self.H, self.W), bound.reshape(self.H, self.W)
+
+    def ambiguity(self, **kw):
+        """allowance() as (counts, boolean [P] mask of the Gaussians owning an ambiguous decision)."""
+        counts, flip, _, _ = self.allowance(**kw)
+        return counts, (flip & 7) != 0
 
     @property
     def num_rendered(self) -> int:
-        return lib().oracle_num_rendered(self.h)
+        return self.L.oracle_num_rendered(self.h)
 
 
 def set_threads(n: int):
-    lib().oracle_set_threads(int(n))
+    """OpenMP threads of every loaded build (each links its own OpenMP runtime)."""
+    lib()
+    for L in _libs.values():
+        L.oracle_set_threads(int(n))
 
 
-def run_scene(g, cam, dL=None, bg=(0.0, 0.0, 0.0), double=False, nthreads=1, **kw):
+def run_scene(g, cam, dL=None, bg=(0.0, 0.0, 0.0), double=False, nthreads=1, variant="base", **kw):
     """Convenience: forward (+ backward if dL given) on a scene.Gaussians / scene.Camera pair."""
-    o = Oracle(double)
+    o = Oracle(double, variant)
     L = o.forward(background=np.asarray(bg, dtype=np.float64), means3D=g.means3D, opacity=g.opacity,
                   scales=kw.pop("scales", g.scales), rotations=kw.pop("rotations", g.rotations),
                   shs=kw.pop("shs", g.shs), viewmatrix=cam.viewmatrix, projmatrix=cam.projmatrix, campos=cam.campos,

@@ -178,18 +178,29 @@ void oracle_mark_visible(int P, const float* means3D, const float* viewmatrix, c
     oracle::markVisible<float>(P, means3D, viewmatrix, projmatrix, camera_type, present);
 }
 
-// ambiguity.hpp on the last float forward: counts[0] rect-ambiguous Gaussians, [1] alpha-threshold pixels,
-// [2] saturation-threshold pixels, [3] flip-affected Gaussians; flip_out [P] (may be NULL) marks the latter
-int oracle_ambiguity(void* hv, double eps, int ulps, uint8_t* flip_out, int64_t* counts)
+// ambiguity.hpp (allowance_scan) on the last float forward. prm: eps_exp, atan_ulps, k_eval, k_pos, k_depth.
+// counts (13): rect_gaussians, radius_gaussians, alpha_pixels, sat_pixels, zero_pixels, order_pixels, rect_pixels,
+// order_pairs, flip_gaussians, threshold_gaussians, order_gaussians, any_pixels, exposed_gaussians. flip_out [P] G_* flags,
+// pixel_out [H*W] PX_* flags, bound_out [H*W] the largest colour change of those decisions (any may be NULL).
+int oracle_allowance(void* hv, const double* prm, uint8_t* flip_out, uint8_t* pixel_out, float* bound_out,
+                     int64_t* counts)
 {
     Handle* h = static_cast<Handle*>(hv);
     if (h->dbl) return -1;
-    const oracle::Ambiguity a = oracle::ambiguity_scan(h->sf, eps, ulps);
-    counts[0] = a.rect_gaussians;
-    counts[1] = a.alpha_pixels;
-    counts[2] = a.sat_pixels;
-    counts[3] = a.flip_gaussians;
+    oracle::AllowanceParams p;
+    p.eps_exp = prm[0];
+    p.atan_ulps = (int)prm[1];
+    p.k_eval = prm[2];
+    p.k_pos = prm[3];
+    p.k_depth = prm[4];
+    const oracle::Allowance a = oracle::allowance_scan(h->sf, p);
+    const int64_t c[13] = {a.rect_gaussians, a.radius_gaussians, a.alpha_pixels, a.sat_pixels, a.zero_pixels,
+                           a.order_pixels, a.rect_pixels, a.order_pairs, a.flip_gaussians, a.threshold_gaussians,
+                           a.order_gaussians, a.any_pixels, a.exposed_gaussians};
+    std::memcpy(counts, c, sizeof(c));
     if (flip_out && !a.flip.empty()) std::memcpy(flip_out, a.flip.data(), a.flip.size());
+    if (pixel_out && !a.pixel.empty()) std::memcpy(pixel_out, a.pixel.data(), a.pixel.size());
+    if (bound_out && !a.bound.empty()) std::memcpy(bound_out, a.bound.data(), a.bound.size() * sizeof(float));
     return 0;
 }
 

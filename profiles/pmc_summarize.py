@@ -60,8 +60,14 @@ def per_kernel(counter_dir, counter):
 def main():
     tag = sys.argv[1]
     stats = glob.glob(os.path.join(OUT, f"prof_{tag}", "**", "*kernel_stats.csv"), recursive=True)
+    rocprof_avg = {}  # stage -> rocprofv3 --stats average duration (ms) of its kernel, same build as the PMC passes
     if stats:
         shutil.copy(stats[0], os.path.join(HERE, f"{tag}_kernel_stats.csv"))
+        with open(stats[0]) as f:
+            for row in csv.DictReader(f):
+                for frag, stage in STAGES.items():
+                    if frag in row["Name"]:
+                        rocprof_avg[stage] = (float(row["AverageNs"]) * 1e-6, int(row["Calls"]))
     fetch = per_kernel(os.path.join(OUT, f"pmc_fetch_{tag}"), "FETCH_SIZE")
     write = per_kernel(os.path.join(OUT, f"pmc_write_{tag}"), "WRITE_SIZE")
     with open(os.path.join(OUT, f"bench_pmc_fetch_{tag}.json")) as f:
@@ -80,13 +86,16 @@ def main():
                 kernels[stage] = {"kernel": name, "fetch_kib_raw": round(fk, 1), "write_kib": round(wk, 1),
                                   "hbm_bytes_per_launch": int(hbm), "hbm_bytes_lower": int((fk + wk) * 1024),
                                   "dispatches": n}
+                if stage in rocprof_avg:
+                    kernels[stage]["rocprof_avg_ms"] = round(rocprof_avg[stage][0], 5)
+                    kernels[stage]["rocprof_calls"] = rocprof_avg[stage][1]
     with open(os.path.join(HERE, f"{tag}_pmc.csv"), "w", newline="") as f:
         w = csv.writer(f)
         w.writerow(["kernel", "dispatches", "FETCH_SIZE_KiB_avg", "WRITE_SIZE_KiB_avg", "hbm_bytes_per_launch"])
         w.writerows(rows)
     latest = {"tag": tag, "config": cfg, "P": bench["config"]["P"], "L": bench["config"]["L"],
               "method": "(2*FETCH_SIZE + WRITE_SIZE) KiB * 1024, separate --pmc passes, gfx950 FETCH x2 correction",
-              "kernels": kernels}
+              "kernel_stats_file": f"profiles/{tag}_kernel_stats.csv" if stats else None, "kernels": kernels}
     with open(os.path.join(HERE, "pmc_latest.json"), "w") as f:
         json.dump(latest, f, indent=1)
     print(json.dumps(latest, indent=1))

@@ -40,11 +40,22 @@ def oracle_run(g, cam, dL=None, bg=(0.0, 0.0, 0.0), double=False, colors_precomp
 
 
 def hip_run(g, cam, dL=None, bg=(0.0, 0.0, 0.0), colors_precomp=None, cov3D_precomp=None, render_depth=False,
-            prefiltered=False, device="cuda"):
+            prefiltered=False, device="cuda", sh_misalign=False, skip_dsh=False):
+    """The HIP path on one view. sh_misalign: the SH tensor starts 4 B past a 16-B boundary (a view into a larger
+    buffer), so the kernels take their unaligned-row paths; skip_dsh: the backward does not write dL_dsh."""
     import torch
 
     R = omr.rasterizer
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(device)
+
+    def t_sh(a):
+        if not sh_misalign:
+            return t(a)
+        flat = torch.zeros(a.size + 1, dtype=torch.float32, device=device)
+        v = flat[1:].view(a.shape)
+        v.copy_(torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)))
+        assert v.data_ptr() % 16 != 0
+        return v
     use_cov = cov3D_precomp is not None
     use_col = colors_precomp is not None
     empty = torch.empty(0, device=device)
@@ -54,7 +65,7 @@ def hip_run(g, cam, dL=None, bg=(0.0, 0.0, 0.0), colors_precomp=None, cov3D_prec
                 rotations=empty if use_cov else t(g.rotations), scale_modifier=1.0,
                 cov3D_precomp=t(cov3D_precomp) if use_cov else empty, viewmatrix=t(cam.viewmatrix),
                 projmatrix=t(cam.projmatrix), tan_fovx=cam.tanfovx, tan_fovy=cam.tanfovy, image_height=cam.height,
-                image_width=cam.width, sh=empty if use_col else t(g.shs), degree=g.sh_degree, campos=t(cam.campos),
+                image_width=cam.width, sh=empty if use_col else t_sh(g.shs), degree=g.sh_degree, campos=t(cam.campos),
                 prefiltered=prefiltered, camera_type=cam.camera_type, render_depth=render_depth)
     num_rendered, color, radii, geomB, binB, imgB = R.RasterizeGaussiansCUDA(**args)
     out = dict(L=num_rendered, color=color, radii=radii, geom=geomB, binning=binB, img=imgB)
@@ -63,7 +74,7 @@ def hip_run(g, cam, dL=None, bg=(0.0, 0.0, 0.0), colors_precomp=None, cov3D_prec
         grads = R.RasterizeGaussiansBackwardCUDA(
             bg_t, args["means3D"], radii, args["colors"], args["scales"], args["rotations"], 1.0, args["cov3D_precomp"],
             args["viewmatrix"], args["projmatrix"], cam.tanfovx, cam.tanfovy, t(dL), args["sh"], g.sh_degree,
-            args["campos"], geomB, num_rendered, binB, imgB, cam.camera_type)
+            args["campos"], geomB, num_rendered, binB, imgB, cam.camera_type, skip_dsh=skip_dsh)
         names = ["dmean2D", "dcolor", "dopacity", "dmean3D", "dcov3D", "dsh", "dscale", "drot"]
         out["grads"] = dict(zip(names, grads))
     import torch as _t
@@ -72,37 +83,57 @@ def hip_run(g, cam, dL=None, bg=(0.0, 0.0, 0.0), colors_precomp=None, cov3D_prec
     return out
 
 
-def blend_threshold_flip(o, width, P, x, y, rel=1e-5):
-    """True when pixel (x, y)'s float64 re-blend of its tile list (oracle geometry, which the parity tests check
-    bit-exact) has a decision within `rel` of a threshold: alpha at 1/255 (skip, forward.cu:436-437) or T(1-alpha)
-    at 1e-4 (saturation, :440-444). There the GPU's v_exp and the oracle's expf may decide differently by one ulp,
-    and the pixel then differs by one Gaussian's contribution (up to |c|/255 T)."""
-    pl = o.get("point_list")
-    rg = o.get("ranges").reshape(-1, 2)
-    gx = (width + 15) // 16
-    t = (y // 16) * gx + x // 16
-    ids = pl[rg[t, 0]:rg[t, 1]]
-    m2 = o.get("means2D").reshape(P, 2)[ids].astype(np.float64)
-    co = o.get("conic_opacity").reshape(P, 4)[ids].astype(np.float64)
-    dx, dy = m2[:, 0] - x, m2[:, 1] - y
-    power = -0.5 * (co[:, 0] * dx * dx + co[:, 2] * dy * dy) - co[:, 1] * dx * dy
-    alpha = np.minimum(0.99, co[:, 3] * np.exp(power))
-    T = 1.0
-    for k in range(len(ids)):
-        if power[k] > 0:
-            continue
-        a = alpha[k]
-        if abs(a - 1 / 255) < rel / 255:
-            return True
-        if a < 1 / 255:
-            continue
-        tt = T * (1 - a)
-        if abs(tt - 1e-4) < rel * 1e-4:
-            return True
-        if tt < 1e-4:
-            break
-        T = tt
-    return False
+# ---- parity bars against the reference AS COMPILED -------------------------------------------
+# The oracle restates the reference without FMA contraction and with the shared omni_math.h transcendentals; the
+# reference binary contracts mul+add (nvcc --fmad=true) and uses libdevice. oracle/ambiguity.hpp bounds, from the
+# oracle's own forward, every decision the two could take differently (tile rects, depth order of near-equal keys,
+# alpha / power / saturation thresholds) and the colour change each can make. The bars below excuse exactly that,
+# and tests/test_contraction_allowance.py checks on CPU that two FMA-contracted builds of the oracle (GCC, LLVM)
+# stay inside them; the HIP path (bit-exact integers, v_exp in the blend loops) is held to the same bars.
+WIDE_RTOL, WIDE_ATOL_FRAC = 1e-2, 1e-3  # gradients of Gaussians blending behind a flagged decision
+
+
+def reference_allowance(o):
+    """oracle/ambiguity.hpp on o's (float) forward: dict(counts, pixel flags [H,W], bound [H,W] (largest colour
+    change of the flagged decisions), flags [P] (G_* bits), owners [P] (Gaussians owning a flagged decision: their gradients are excused),
+    exposed [P] (Gaussians blending behind one: the wide gradient bar), t_bound [H,W] (the same for final_T))."""
+    counts, flip, pix, bound = o.allowance()
+    P = o.P
+    vis = o.get("radii") > 0
+    rgb = o.get("rgb").reshape(P, 3)[vis] if vis.any() else np.zeros((1, 3), np.float32)
+    cmax = max(float(np.abs(rgb).max()) if rgb.size else 0.0, float(np.abs(o.background).max()), 1e-6)
+    return dict(counts=counts, pixel=pix, bound=bound, t_bound=bound / (2.0 * cmax), flags=flip,
+                owners=(flip & 7) != 0, exposed=(flip & 8) != 0)
+
+
+def check_image(test_img, ref_img, allow, what="out_color", bound_key="bound"):
+    """|test - ref| <= 1e-4 (north_star) everywhere, plus the flagged pixels' own bound where the reference as
+    compiled may decide differently. test_img / ref_img: [..., H, W] (channels reduced by max)."""
+    err = np.abs(np.asarray(test_img, np.float64) - np.asarray(ref_img, np.float64))
+    if err.ndim == 3:
+        err = err.max(0)
+    bad = err > 1e-4 + allow[bound_key]
+    if bad.any():
+        ys, xs = np.nonzero(bad)
+        raise AssertionError(f"{what}: {int(bad.sum())} pixels over 1e-4 + allowance (first ({xs[0]},{ys[0]}): err "
+                             f"{err[ys[0], xs[0]]:.3g}, flags {int(allow['pixel'][ys[0], xs[0]])}, allowance "
+                             f"{float(allow[bound_key][ys[0], xs[0]]):.3g})")
+    return int((err > 1e-4).sum())
+
+
+def check_grads(test, ref, allow, P, names=None):
+    """grad_close per element, except on the Gaussians owning a flagged decision (excused) and the wide bar
+    (WIDE_RTOL, WIDE_ATOL_FRAC) on the ones blending behind one."""
+    names = names or list(ref)
+    for name in names:
+        a, b = np.asarray(test[name]), np.asarray(ref[name])
+        ok = grad_close(a, b, elementwise=True).reshape(P, -1).all(axis=1)
+        wide = grad_close(a, b, rtol=WIDE_RTOL, atol_frac=WIDE_ATOL_FRAC, elementwise=True).reshape(P, -1).all(axis=1)
+        bad = ~ok & ~allow["owners"] & ~(allow["exposed"] & wide)
+        if bad.any():
+            i = int(np.nonzero(bad)[0][0])
+            raise AssertionError(f"{name}: {int(bad.sum())} Gaussians outside the bar (first {i}: "
+                                 f"{a.reshape(P, -1)[i]} vs {b.reshape(P, -1)[i]}, exposed {bool(allow['exposed'][i])})")
 
 
 def oracle_threads() -> int:

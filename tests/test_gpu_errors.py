@@ -32,6 +32,16 @@ e = torch.empty(0, device="cuda")
 args = (t(np.zeros(3)), t(g.means3D), e, t(g.opacity), t(g.scales), t(g.rotations), 1.0, e, t(cam.viewmatrix),
         t(cam.projmatrix), 0.0, 0.0, cam.height, cam.width, t(g.shs), 3, t(cam.campos), False, 3)
 out = []
+fwd_only = []
+for it in range(4):  # forward only, checked by forward_status (ADVICE r02: no silent background-only image)
+    try:
+        nr, color, radii, gb, bb, ib = R.RasterizeGaussiansCUDA(*args)  # raises for depth sort / scan give-ups
+        R.forward_status(gb, g.P)  # raises for emit / tile sort give-ups
+        fwd_only.append(["ok", float(color.abs().sum())])
+    except R.RasterizerError as ex:
+        fwd_only.append(["error", str(ex)])
+torch.cuda.synchronize()
+R.runtime_stats_reset()  # the counts below are the fwd+bwd loop's
 for it in range(4):
     try:
         nr, color, radii, gb, bb, ib = R.RasterizeGaussiansCUDA(*args)
@@ -42,7 +52,7 @@ for it in range(4):
     except R.RasterizerError as ex:
         torch.cuda.synchronize()
         out.append(["error", str(ex)])
-print(json.dumps(dict(lib=R.loaded_library(), runs=out, stats=R.runtime_stats())))
+print(json.dumps(dict(lib=R.loaded_library(), runs=out, fwd_only=fwd_only, stats=R.runtime_stats())))
 """
 
 
@@ -72,3 +82,11 @@ def test_lookback_give_up_is_reported_not_silent():
     # a good call after a failed one: the variant's ok runs (if any) render the same instance count
     n_ok = {n for kind, n in res["runs"] if kind == "ok"}
     assert n_ok <= {ok["runs"][0][1]}
+    # forward-only: a forward whose binning gave up is reported by forward_status, never a silent background image
+    assert all(kind == "ok" for kind, _ in ok["fwd_only"]), ok["fwd_only"]
+    good = ok["fwd_only"][0][1]
+    for kind, v in res["fwd_only"]:
+        if kind == "ok":
+            assert v == good, (v, good)  # a forward reported good renders the good image
+        else:
+            assert "look-back" in v, v

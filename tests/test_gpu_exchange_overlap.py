@@ -22,7 +22,7 @@ def _case(view):
     return make_case(6000, 256, 128, scene.CAMERA_LONLAT, 23, view_index=view, spread=2.0)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, move_view=False):
     import torch
     import torch.distributed as dist
 
@@ -47,14 +47,17 @@ def _worker(rank, world, port, q):
                                  lambda pk, out: R.sh_grad_from_colors_packed(m, sh, g.sh_degree, pk, out=out), dev,
                                  any_backend=True)
         assert cx.overlap
-        for _ in range(2):  # twice: the event and the buffers are reused across steps
+        for step in range(2):  # twice: the event and the buffers are reused across steps
+            if move_view and step == 1:  # the second step renders another viewpoint (rank + 2): campos changes
+                g, cam, dL = _case(rank + 2)
+                vm, pm, cp = t(cam.viewmatrix), t(cam.projmatrix), t(cam.campos)
             nr, color, radii, gb, bb, ib = R.RasterizeGaussiansCUDA(bg, m, e, t(g.opacity), t(g.scales),
                                                                     t(g.rotations), 1.0, e, vm, pm, cam.tanfovx,
                                                                     cam.tanfovy, cam.height, cam.width, sh,
                                                                     g.sh_degree, cp, False, cam.camera_type, False)
             R.RasterizeGaussiansBackwardCUDA(bg, m, radii, e, t(g.scales), t(g.rotations), 1.0, e, vm, pm,
                                              cam.tanfovx, cam.tanfovy, t(dL), sh, g.sh_degree, cp, gb, nr, bb, ib,
-                                             cam.camera_type, out=out, **cx.backward_kwargs())
+                                             cam.camera_type, out=out, **cx.backward_kwargs(cp))
             cx.start()
             cx.finish()
         torch.cuda.synchronize()
@@ -63,13 +66,13 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_overlapped_compact_exchange_sums_views_bitwise():
+def _run(move_view):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, move_view)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in procs)
@@ -83,10 +86,21 @@ def test_overlapped_compact_exchange_sums_views_bitwise():
     sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
     from helpers import hip_run, to_np
 
-    h = [hip_run(*_case(v)) for v in (0, 1)]
+    views = (2, 3) if move_view else (0, 1)  # the last step's views
+    h = [hip_run(*_case(v)) for v in views]
     names = {"dL_dmeans3D": "dmean3D", "dL_dopacity": "dopacity", "dL_dscales": "dscale", "dL_drotations": "drot",
              "dL_dsh": "dsh"}
     for k, n in names.items():
         ref = (h[0]["grads"][n] + h[1]["grads"][n]).reshape(res[0][k].shape)
         torch.cuda.synchronize()
         np.testing.assert_array_equal(res[0][k], to_np(ref), err_msg=k)
+
+
+def test_overlapped_compact_exchange_sums_views_bitwise():
+    _run(move_view=False)
+
+
+def test_overlapped_exchange_follows_a_moving_camera():
+    """the gathered camera position must be each step's (the SH rebuild evaluates view directions from
+    it); the second step renders other viewpoints and must equal the per-view sums of THAT step bitwise."""
+    _run(move_view=True)

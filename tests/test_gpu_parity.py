@@ -3,24 +3,23 @@
 Bars (written here, checked per case):
   * bit-exact: radii, tiles_touched, pixel centres (means2D), conic+opacity, depths, sorted instance list
     (point_list) and per-tile ranges, num_rendered;
-  * forward colour: |gpu - oracle| <= 1e-4 absolute (north_star); final_T <= 1e-4 absolute;
-    n_contrib equal on >= 99.99 % of pixels (exp() is the hardware v_exp on the GPU, glibc expf in the oracle,
-    so a pixel whose alpha sits within an ulp of 1/255 or whose T lands within an ulp of 1e-4 may differ by one);
-    a pixel over 1e-4 is accepted only when a float64 re-blend of its tile list finds such a threshold decision
-    (helpers.blend_threshold_flip) and at most 1 in 1e5 pixels (at least 1) is one: config C (2 M pixels) has
-    one, |err| 3.6e-4 from a Gaussian with alpha = 1/255 (1 + 3e-6);
-  * gradients: per element |gpu - oracle| <= 1e-3 |oracle| + 1e-4 max|oracle| (helpers.grad_close), except on
-    Gaussians whose own blend decision sits within 1e-5 of a threshold (alpha at 1/255, T(1-alpha) at 1e-4) at some
-    pixel (oracle/ambiguity.hpp: 886 of 1 M at config C); there the two exp implementations may decide differently
-    and the Gaussian gains or loses a whole pixel term (config C: one dscale entry, 1.4e-4 off).
+  * forward colour and final_T: |gpu - oracle| <= 1e-4 absolute (north_star), plus, on the pixels where the
+    reference as compiled may take another blend decision than the oracle (oracle/ambiguity.hpp: alpha at 1/255,
+    power at 0, T(1-alpha) at 1e-4 inside their rounding windows, near-equal depths that may sort the other way,
+    ambiguous tile rects), the largest colour change those decisions can make (helpers.check_image).
+    n_contrib equal on >= 99.99 % of pixels (the GPU's v_exp vs glibc expf at such a decision);
+  * gradients: per element |gpu - oracle| <= 1e-3 |oracle| + 1e-4 max|oracle| (helpers.grad_close), except the
+    Gaussians owning such a decision (excused: they may gain or lose a whole pixel term) and the wider bar 1e-2 /
+    1e-3 max for the Gaussians blending behind one (helpers.check_grads). The same bars hold for two FMA-contracted
+    builds of the oracle, the proxy of the reference binary (tests/test_contraction_allowance.py).
 """
 import os
 
 import numpy as np
 import pytest
 
-from helpers import (blend_threshold_flip, grad_close, hip_run, make_case, omr, oracle_run, oracle_threads, scene,
-                     to_np)
+from helpers import (check_grads, check_image, grad_close, hip_run, make_case, omr, oracle_run, oracle_threads,
+                     reference_allowance, scene, to_np)
 
 pytestmark = pytest.mark.gpu
 
@@ -42,7 +41,7 @@ CASES = [
 
 
 def _compare(g, cam, dL, nthreads=1, **kw):
-    o, L, og = oracle_run(g, cam, dL, nthreads=nthreads, **kw)
+    o, L, og = oracle_run(g, cam, dL, nthreads=nthreads, **{k: v for k, v in kw.items() if k != "sh_misalign"})
     h = hip_run(g, cam, dL, **kw)
     st = {k: to_np(v) for k, v in h["state"].items()}
     P = g.P
@@ -59,39 +58,23 @@ def _compare(g, cam, dL, nthreads=1, **kw):
         np.testing.assert_allclose(st["rgb"][vis], o.get("rgb").reshape(P, 3)[vis], rtol=0, atol=1e-6)
     np.testing.assert_array_equal(st["point_list"].astype(np.uint32), o.get("point_list"))
     np.testing.assert_array_equal(st["ranges"].astype(np.uint32).reshape(-1), o.get("ranges"))
-    # forward image
-    img_o = o.get("out_color").reshape(3, cam.height, cam.width)
-    err = np.abs(to_np(h["color"]) - img_o).max(0)
-    over = np.argwhere(err > 1e-4)
-    assert len(over) <= max(1, 1e-5 * err.size), f"out_color: {len(over)} pixels over 1e-4 (max {err.max()})"
-    for y, x in over:  # allowed only where a blend decision sits at a threshold (bar in the module docstring)
-        assert blend_threshold_flip(o, cam.width, P, int(x), int(y)), f"pixel ({x},{y}) err {err[y, x]} unexplained"
-    # final_T: the same bar and the same allowance as the image (a pixel over 1e-4 only at a threshold decision)
-    err_t = np.abs(st["final_T"] - o.get("final_T")).reshape(cam.height, cam.width)
-    over_t = np.argwhere(err_t > 1e-4)
-    assert len(over_t) <= max(1, 1e-5 * err_t.size), f"final_T: {len(over_t)} pixels over 1e-4 (max {err_t.max()})"
-    for y, x in over_t:
-        assert blend_threshold_flip(o, cam.width, P, int(x), int(y)), f"final_T ({x},{y}) err {err_t[y, x]} unexplained"
-    same = (st["n_contrib"].astype(np.uint32) == o.get("n_contrib")).mean()
-    assert same >= 0.9999, f"n_contrib agreement {same}"
+    # forward image and final_T: 1e-4, plus each flagged pixel's allowance (helpers.reference_allowance, computed
+    # only when some pixel is over 1e-4)
+    allow = None
+    img_h, img_o = to_np(h["color"]), o.get("out_color").reshape(3, cam.height, cam.width)
+    t_h, t_o = st["final_T"].reshape(cam.height, cam.width), o.get("final_T").reshape(cam.height, cam.width)
+    if np.abs(img_h - img_o).max(initial=0.0) > 1e-4 or np.abs(t_h - t_o).max(initial=0.0) > 1e-4:
+        allow = reference_allowance(o)
+        check_image(img_h, img_o, allow)
+        check_image(t_h, t_o, allow, "final_T", "t_bound")
+    n_same = st["n_contrib"].astype(np.uint32) == o.get("n_contrib")
+    assert n_same.mean() >= 0.9999, f"n_contrib agreement {n_same.mean()}"
     if dL is None:
         return
     hg = {k: to_np(v) for k, v in h["grads"].items()}
-    pairs = [("dmean2D", og["dmean2D"]), ("dcolor", og["dcolor"]), ("dopacity", og["dopacity"]),
-             ("dmean3D", og["dmean3D"]), ("dcov3D", og["dcov3D"]), ("dsh", og["dsh"]), ("dscale", og["dscale"]),
-             ("drot", og["drot"])]
-    flip = None
-    for name, ref in pairs:
-        ok, emax, nbad = grad_close(hg[name], ref)
-        if ok:
-            continue
-        # outside the bar only where the Gaussian's own blend decision sits at a threshold (oracle/ambiguity.hpp):
-        # there v_exp and expf may decide differently and the Gaussian gains or loses a whole pixel term
-        if flip is None:
-            counts, flip = o.ambiguity()
-        bad = ~grad_close(hg[name], ref, elementwise=True).reshape(P, -1).all(axis=1)
-        assert not (bad & ~flip).any(), (f"{name}: max abs err {emax}, {nbad} elements outside tolerance, "
-                                         f"{int((bad & ~flip).sum())} of them on Gaussians without a threshold decision")
+    names = ["dmean2D", "dcolor", "dopacity", "dmean3D", "dcov3D", "dsh", "dscale", "drot"]
+    if not all(grad_close(hg[n], og[n])[0] for n in names):
+        check_grads(hg, og, allow or reference_allowance(o), P, names)
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
@@ -99,6 +82,46 @@ def test_parity(case):
     _, P, W, H, cam_t, seed, view, deg, mult = case
     g, cam, dL = make_case(P, W, H, cam_t, seed, view_index=view, sh_degree=deg, spread=mult)
     _compare(g, cam, dL)
+
+
+@pytest.mark.parametrize("M,deg,cam_t", [(4, 1, LON), (9, 2, LON), (9, 1, PIN), (1, 0, LON), (25, 3, LON)],
+                         ids=["M4_deg1", "M9_deg2", "M9_deg1_pinhole", "M1_deg0", "M25_deg3"])
+def test_generic_sh_layout(M, deg, cam_t):
+    """sh tensors with M != 16 coefficients (the reference takes any max_coeffs M = sh.size(1): forward.cu:30-83,
+    backward.cu:30-151, rasterize_points.cu:94): preprocess's generic SH path and gaussian_bwd_kernel<CAM, 0>.
+    M = 25 > 16: coefficients past 16 are never read and get zero gradients, as in the reference."""
+    g, cam, dL = make_case(2000, 128, 64, cam_t, 60 + M, view_index=1, sh_degree=deg, spread=3.0)
+    sh = np.zeros((g.P, M, 3), np.float32)
+    k = min(M, 16)
+    sh[:, :k] = g.shs[:, :k]
+    g.shs = sh
+    _compare(g, cam, dL)
+
+
+@pytest.mark.parametrize("cam_t", [LON, PIN], ids=["lonlat", "pinhole"])
+def test_unaligned_sh_rows(cam_t):
+    """M = 16 but the SH tensor 4 B off a 16-B boundary: the kernels' 16-B staged row loads do not apply
+    (preprocess.hip: sh16, gaussian_bwd.hip: m16) and the generic paths run on the reference's layout."""
+    g, cam, dL = make_case(2000, 128, 64, cam_t, 70, view_index=2, spread=3.0)
+    _compare(g, cam, dL, sh_misalign=True)
+
+
+@pytest.mark.parametrize("M,misalign", [(1, False), (4, False), (9, False), (16, True), (16, False)],
+                         ids=["M1", "M4", "M9", "M16_unaligned", "M16"])
+def test_skip_dsh_any_layout(M, misalign):
+    """skip_dsh (dL_dsh = NULL, the view-parallel exchange's per-view call) for every SH layout (the
+    generic-M path wrote through the null pointer): the other seven gradients equal the full call's bitwise."""
+    import torch
+
+    g, cam, dL = make_case(2000, 128, 64, LON, 80 + M, view_index=3, sh_degree={1: 0, 4: 1, 9: 2}.get(M, 3),
+                           spread=3.0)
+    g.shs = np.ascontiguousarray(g.shs[:, :M])
+    full = hip_run(g, cam, dL, sh_misalign=misalign)
+    skip = hip_run(g, cam, dL, sh_misalign=misalign, skip_dsh=True)
+    assert skip["grads"]["dsh"] is None
+    for name, v in full["grads"].items():
+        if name != "dsh":
+            torch.testing.assert_close(skip["grads"][name], v, rtol=0, atol=0, msg=name)
 
 
 def test_long_and_huge_row_segments():

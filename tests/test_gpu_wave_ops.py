@@ -1,5 +1,5 @@
-"""GPU unit test of the wave64 gradient reductions of wave_ops.h (DPP transposed butterfly, cross-row-first
-v_permlane16/32_swap, and the LDS-transposed one the render backward uses). Column sums of a [64, 9] block must
+"""GPU unit test of the wave64 gradient reductions of wave_ops.h (cross-row-first v_permlane16/32_swap, and the
+LDS-transposed ones the render backward uses). Column sums of a [64, 9] block must
 match a float64 reference to f32 rounding."""
 import numpy as np
 import pytest
@@ -7,10 +7,10 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-MODES = [dict(), dict(rows=True), dict(lds=True)]
+MODES = [dict(), dict(lds=True)]
 
 
-@pytest.mark.parametrize("mode", MODES, ids=["transposed", "rows", "lds"])
+@pytest.mark.parametrize("mode", MODES, ids=["rows", "lds"])
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_wave_sum_matches_column_sums(seed, mode, omr):
     import torch
@@ -24,7 +24,7 @@ def test_wave_sum_matches_column_sums(seed, mode, omr):
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("mode", MODES, ids=["transposed", "rows", "lds"])
+@pytest.mark.parametrize("mode", MODES, ids=["rows", "lds"])
 def test_wave_sum_lane_identity(mode, omr):
     import torch
 
@@ -37,7 +37,7 @@ def test_wave_sum_lane_identity(mode, omr):
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_wave_sum_pair_matches_column_sums(seed, omr):
-    """wave_sum9x2_stored (render_bwd.hip, OMR_BWD_PAIR): two instances' rows summed in one pass."""
+    """wave_sum9x2_stored (render_bwd.hip): two instances' rows summed in one pass."""
     import torch
 
     rng = np.random.default_rng(10 + seed)
