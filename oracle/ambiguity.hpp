@@ -246,7 +246,7 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
                 const uint32_t px = tx * BLOCK_X + lx, py = ty * BLOCK_Y + ly;
                 if (!(px < (uint32_t)W && py < (uint32_t)H)) continue;
                 uint8_t pf = 0;
-                double Tr = 1.0, errT = 0.0, bnd = 0.0, last_alpha = 0.0;
+                double Tr = 1.0, errT = 0.0, bnd = 0.0, last_alpha = 0.0, T_before_last = 1.0;
                 uint32_t last_run = ~0u, last_run_id = 0;
                 bool behind = false;  // a decision in front of this position is ambiguous (alpha, power 0, order, rect)
                 auto eval = [&](uint32_t id, double& power, double& dp) {
@@ -290,7 +290,8 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
                     }
                     behind = behind || (pf & (PX_ALPHA | PX_ZERO | PX_ORDER | PX_RECT));
                     // order: a second blended member of the same run
-                    if (last_run == run[k]) {
+                    const bool pair_prev = last_run == run[k];
+                    if (pair_prev) {
                         pf |= PX_ORDER;
                         marked[t].push_back({id, G_ORDER});
                         marked[t].push_back({last_run_id, G_ORDER});
@@ -307,7 +308,16 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
                         marked[t].push_back({id, G_THRESHOLD});
                         bnd += span * Tr;  // this term and everything behind carry transmittance <= Tr
                     }
-                    if (test_T < 1e-4) break;
+                    if (test_T < 1e-4) {
+                        // the run's previous member blended and this one saturates: swapped, the other one may
+                        // end the pixel, which moves T and the colour by up to the transmittance before the pair
+                        if (pair_prev) {
+                            pf |= PX_ORDER;
+                            bnd += span * T_before_last;
+                        }
+                        break;
+                    }
+                    T_before_last = Tr;
                     Tr = test_T;
                     errT = errk;
                 }
