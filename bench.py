@@ -120,17 +120,32 @@ def dist_check(args) -> int:
     return 0
 
 
-def stage_bytes(stage, P, V, L, N, T, M=16, D=3):
-    """Algorithmic HBM bytes of one launch of each stage (SURVEY.md §8(d) accounting)."""
+def stage_bytes(stage, P, V, L, N, T, M=16, D=3, rows=None):
+    """Algorithmic HBM bytes of one launch of each stage (SURVEY.md §8(d) accounting). rows = the row
+    binning's row-slot count M_r (bin.hip; None: sort.hip's emit + tile sort + ranges)."""
     sh = 12 * (D + 1) ** 2
     kb = 2 if T <= 65536 else 4  # tile-id bytes: 16-bit keys up to 65536 tiles (capi.hip: keys16)
+    if rows is not None:
+        # bin.hip, all timed as tile_sort: the rows pass reads each visible rank's row offset and depth-ordered rect
+        # word twice (hist, scatter) and its Gaussian index once (28 B) and writes M_r row entries (Gaussian, width |
+        # x0, first instance slot: 12 B); the columns pass reads the entries' slot and width (hist, 8 B) and the whole
+        # entry plus its Gaussian's 32-B bin record (scatter, 44 B), writes the point list and row_valid (5 B per
+        # instance) and the ranges (8 B per tile)
+        binning = 28 * V + 64 * rows + 5 * L + 8 * T
+        emit, tile_sort, tile_ranges = 0, binning, 16 * T  # tile_ranges: the render schedule (tile_order) only
+    else:
+        emit = 8 * P + 12 * V + (kb + 4) * L
+        tile_sort = 2 * 2 * (kb + 4) * L           # 2 passes x (tile id + point-list entry, read + write)
+        tile_ranges = kb * L + 16 * T
     return {
-        "preprocess": 28 * P + (40 + sh + 45) * V,
+        "preprocess": 32 * P + (40 + sh + 45 + 40) * V,  # + the 8-B rect word and the 32-B bin record
         "depth_sort": 4 * 2 * 8 * P,               # 4 passes x (key+value read + write)
-        "scan": 16 * P,                            # tiles_touched read in depth and index order; two scans written
-        "emit": 8 * P + 12 * V + (kb + 4) * L,
-        "tile_sort": 2 * 2 * (kb + 4) * L,         # 2 passes x (tile id + point-list entry, read + write)
-        "tile_ranges": kb * L + 16 * T,
+        # order, tiles_touched (index order) and row_first; sort path: tiles_touched in depth order and offsets; row
+        # path: the 8-B rect words in depth order (read and written) and row_offsets
+        "scan": 12 * P + (8 * P if rows is None else 20 * P),
+        "emit": emit,
+        "tile_sort": tile_sort,
+        "tile_ranges": tile_ranges,
         "render_forward": 40 * L + 20 * N + 8 * T,
         "render_backward": 40 * L + 20 * N + 8 * T + 88 * V,
         # tiles_touched + row_first + row_valid bytes + one 36-B sum row written per Gaussian; the marked 36-B
@@ -306,7 +321,7 @@ def main():
             for name, idx in (("dL_dmeans3D", 3), ("dL_dsh", 5), ("dL_dopacity", 2), ("dL_dscales", 6),
                               ("dL_drotations", 7), ("dL_dcolors", 1)):
                 (out if name == "dL_dcolors" else grads.views)[name].copy_(gr[idx])
-        return nr, radii, ib
+        return nr, radii, gb, ib
 
     # compact exchange: the colour all-gather overlaps the backward's per-Gaussian stage (parallel.CompactExchange);
     # the LibTorch boundary has no event hook, so it exchanges after the backward
@@ -333,7 +348,7 @@ def main():
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record(stream)
         if LT is not None:
-            nr, radii, ib = step_libtorch()
+            nr, radii, gb, ib = step_libtorch()
         else:
             nr, color, radii, gb, bb, ib = R.RasterizeGaussiansCUDA(
                 bg, means3D, empty, opacity, scales, rots, 1.0, empty, view, proj, cam.tanfovx, cam.tanfovy, H, W,
@@ -348,6 +363,7 @@ def main():
         stats["L"] = nr
         stats["radii"] = radii
         stats["img"] = ib
+        stats["geom"] = gb
 
     for _ in range(args.warmup):
         step()
@@ -436,8 +452,12 @@ def main():
     except (OSError, ValueError):
         pass
 
+    # the row binning (bin.hip) runs for views of at most 1024 tiles a side; its algorithmic bytes need its row slots
+    gxy = ((W + 15) // 16, (H + 15) // 16)
+    rows_slots = R.debug_counters(P, stats["geom"])["row_slots"] if max(gxy) <= 1024 else None
+
     def stage_entry(k, live_ok=True):
-        b = stage_bytes(k, P, V, L, N, T, M, g.sh_degree)
+        b = stage_bytes(k, P, V, L, N, T, M, g.sh_degree, rows_slots)
         ms_l, cnt_l = live.get(k, (0.0, 0))
         ms_k = ms_l / cnt_l if (cnt_l and live_ok) else stage_avg[k]
         ach = b / (ms_k * 1e-3) / 1e9 if ms_k > 0 else 0.0
@@ -458,7 +478,7 @@ def main():
                 "rocprof_file": pmc_file if rp else None}
 
     d = stage_entry(dom)
-    algo_total = sum(stage_bytes(s, P, V, L, N, T, M, g.sh_degree) for s in stage_avg)
+    algo_total = sum(stage_bytes(s, P, V, L, N, T, M, g.sh_degree, rows_slots) for s in stage_avg)
     # VALU secondary: pixel-instance evaluations = the forward's (instance, 16x4 band) pairs x 64,
     # at nominal 20 flop (forward) / 60 flop (backward) each, against the f32 vector peak; the backward evaluates at
     # most the forward's pairs (it stops at each band's last contributor), so its figure is an upper bound
@@ -499,7 +519,8 @@ def main():
         "data": "synthetic (SplitMix64 scene, SURVEY.md §8(d)); random-init Gaussians, fixed dL/dout",
         "config": {"workload": workload_text(cfg_name, args.config, world, P, W, H, cam.camera_type, g.sh_degree,
                                                args.exchange),
-                   "P": P, "V": V, "L": L, "N": N, "T": T, "width": W, "height": H,
+                   "P": P, "V": V, "L": L, "N": N, "T": T, "width": W, "height": H, "row_slots": rows_slots,
+                   "binning": "rows then columns (bin.hip)" if rows_slots is not None else "emit + radix tile sort",
                    "parallelism": f"view-parallel dp{world}", "boundary": args.boundary,
                    "exchange": args.exchange if world > 1 else None, "ambiguous": ambiguous},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": d["achieved_GBps"], "peak": HBM_PEAK_GBS,

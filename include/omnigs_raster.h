@@ -243,6 +243,9 @@ int omr_debug_ranges(char* image_buffer, int width, int height, uint32_t* dst, v
 int omr_debug_image_state(char* image_buffer, int width, int height, float* final_T, uint32_t* n_contrib, void* stream);
 /* the forward's per-tile count of (instance, 16x4 band) evaluations [T] (the backward's schedule key) */
 int omr_debug_tile_cost(char* image_buffer, int width, int height, uint32_t* dst, void* stream);
+/* the forward's count words: [0] num_rendered, [1] prefiltered flag, [2] huge-Gaussian count, [3] look-back error,
+ * [4] row slots M of the row binning (bin.hip; 0 on sort.hip's path); dst: 8 device words */
+int omr_debug_counters(char* geom_buffer, int P, uint32_t* dst, void* stream);
 /* per-Gaussian pixel centre [P,2], conic+opacity [P,4], rgb [P,3], depth [P], tiles_touched [P] */
 /* one wave64 through the render backward's gradient reduction: in [64][9] -> out [9] (column sums) */
 int omr_debug_wave_sum9(const float* in, float* out, void* stream); /* wave_sum9_rows */

@@ -13,6 +13,7 @@
 #include <mutex>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -332,12 +333,17 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s)
     g.scan_partials = c.take<uint32_t>(radix_partials_words(P));
     g.scan2_status = c.take<uint32_t>(scan2_status_words(P));
     g.offsets = c.take<uint32_t>(P);
-    g.counters = c.take<uint32_t>(4);
+    g.counters = c.take<uint32_t>(8);
     g.row_first = c.take<uint32_t>(P);
     g.row_sums = c.take<float>(P * GRAD_ROW);
     g.conic_op = c.take<float4>(P);
     g.huge_list = c.take<uint32_t>(P);
     g.internal_radii = c.take<int>(P);
+    g.rect = c.take<uint2>(P);
+    g.drect = c.take<uint2>(P);
+    g.row_offsets = c.take<uint32_t>(P);
+    g.desc_r = c.take<uint2>(P / 2 + 2);  // M <= BIN_MAX_GRID P slots: at most P / 2 + 1 chunks
+    g.bin_rec = c.take<float4>(2 * P);
     g.order = g.val_a;  // the depth sort runs DEPTH_SORT_PASSES (even) passes, so its result lands in val_a
     if (s) *s = g;
     return c.size();
@@ -365,9 +371,25 @@ size_t ImageState::carve(char* base, size_t N, size_t T, ImageState* s)
     return c.size();
 }
 
-size_t BinningState::carve(char* base, size_t cap, uint32_t T, BinningState* s)
+// OMR_BINNING=sort (read once) forces the emit + radix sort binning on every view: an A/B switch for measurements
+static bool sort_binning_forced()
 {
+    static const bool forced = [] {
+        const char* v = std::getenv("OMR_BINNING");
+        return v && std::strcmp(v, "sort") == 0;
+    }();
+    return forced;
+}
+static bool row_binning(uint32_t gx, uint32_t gy)
+{
+    return gx <= BIN_MAX_GRID && gy <= BIN_MAX_GRID && !sort_binning_forced();
+}
+
+size_t BinningState::carve(char* base, size_t cap, uint32_t gx, uint32_t gy, BinningState* s)
+{
+    const uint32_t T = gx * gy;
     const int tile_passes = tile_sort_passes(T);
+    const bool rows = row_binning(gx, gy);
     Carver c(base);
     BinningState b;
     b.inst_grad = c.take<float>(cap * GRAD_ROW);
@@ -379,11 +401,17 @@ size_t BinningState::carve(char* base, size_t cap, uint32_t T, BinningState* s)
     b.key_a = c.take<uint32_t>(cap);
     b.key_b = c.take<uint32_t>(cap);
     b.val_a = c.take<uint32_t>(cap);
-    b.val_b = c.take<uint32_t>(cap);
-    b.hist = c.take<uint32_t>(radix_scratch_words(cap, tile_passes));
-    b.scan_partials = c.take<uint32_t>(radix_partials_words(cap));  // look-back words of the histogram scan
-    b.block_owner = c.take<uint32_t>(emit_index_size(cap));
+    b.val_b = c.take<uint32_t>(rows ? 0 : cap);
+    b.hist = c.take<uint32_t>(rows ? 0 : radix_scratch_words(cap, tile_passes));
+    b.scan_partials = c.take<uint32_t>(rows ? 0 : radix_partials_words(cap));  // look-back words of the histogram scan
+    b.block_owner = c.take<uint32_t>(rows ? 0 : emit_index_size(cap));
     b.point_keys = (tile_passes & 1) != 0 ? b.key_b : b.key_a;  // result buffer of the key ping-pong
+    b.bin_hist_r = c.take<uint32_t>(rows ? 2 * (size_t)gy * bin_chunks_r(cap) : 0);
+    b.bin_hist_b = c.take<uint32_t>(rows ? bin_chunks_b(cap, gy) * gx : 0);
+    b.bin_desc_b = c.take<uint4>(rows ? 2 * bin_chunks_b(cap, gy) : 0);
+    b.bin_rowinfo = c.take<uint4>(rows ? gy + 1 : 0);
+    b.bin_words = c.take<uint32_t>(rows ? 4 : 0);
+    b.bin_zero = c.take<uint32_t>(rows ? bin_zero_words(cap, gx, gy) : 0);
     if (s) *s = b;
     return c.size();
 }
@@ -484,7 +512,8 @@ int forward_impl(const ForwardIn& in)
     uint32_t* const err_dev = g.counters + 3;  // every decoupled look-back of the forward reports a give-up here
     int which; { StageScope st_(ST_DEPTH_SORT, s); which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr, nullptr, 0, DEPTH_SORT_PASSES, s, true, err_dev); }
     g.order = which ? g.val_b : g.val_a;
-    { StageScope st_(ST_SCAN, s); launch_forward_scans(g.tiles_touched, g.order, g.offsets, g.row_first, g.huge_list, g.counters + 2, g.scan2_status, g.counters, err_dev, P, s); }
+    const bool rows_path = row_binning(d.gx, d.gy);  // bin.hip; sort.hip's emit + tile sort for larger views
+    { StageScope st_(ST_SCAN, s); launch_forward_scans(g.tiles_touched, rows_path ? g.rect : nullptr, g.order, g.offsets, g.row_first, g.row_offsets, g.drect, g.desc_r, g.huge_list, g.counters + 2, g.scan2_status, g.counters, err_dev, P, s); }
 
     // num_rendered = offsets[P-1] (+ the prefiltered error flag) to pinned host memory, without waiting for it:
     // the binning buffer is sized from a capacity hint and everything after the scan reads the count on the device,
@@ -534,27 +563,40 @@ int forward_impl(const ForwardIn& in)
         if (ckpt_bytes(capacity) >= 0x80000000ull)  // 32-bit buffer offsets of the checkpoints (raster_common.h)
             return fail(OMR_ERR_INVALID_ARGUMENT, "more than 2^28 Gaussian x tile instances in one view");
         char* bin_base = static_cast<char*>(
-            alloc_counted(in.binning_alloc, in.binning_ctx, BinningState::carve(nullptr, capacity, d.T, nullptr)));
+            alloc_counted(in.binning_alloc, in.binning_ctx, BinningState::carve(nullptr, capacity, d.gx, d.gy, nullptr)));
         if (!bin_base) return fail(OMR_ERR_ALLOCATION, "binning allocation failed");
         BinningState b;
-        BinningState::carve(bin_base, capacity, d.T, &b);
-        { StageScope st_(ST_EMIT, s); launch_emit_instances(count_words, in.P, capacity, count_dev, g, d.gx, b.block_owner, b.key_a, keys16, b.val_a, bin_base, s); }
-        {
-            StageScope st_(ST_TILE_SORT, s);
-            if (keys16)
-                radix_sort_pairs(reinterpret_cast<uint16_t*>(b.key_a), reinterpret_cast<uint16_t*>(b.key_b), b.val_a,
-                                 b.val_b, b.hist, b.scan_partials, capacity, count_dev, bin_base, 0, tile_passes, s,
-                                 false, err_dev);
-            else
-                radix_sort_pairs(b.key_a, b.key_b, b.val_a, b.val_b, b.hist, b.scan_partials, capacity, count_dev,
-                                 bin_base, 0, tile_passes, s, false, err_dev);
-        }
+        BinningState::carve(bin_base, capacity, d.gx, d.gy, &b);
         if (rerun) OMR_HIP(hipMemsetAsync(im.ranges, 0, d.T * sizeof(uint2), s));
-        {
+        if (rows_path) {
+            // the binning as two counting passes (bin.hip): the whole of it is timed as the tile_sort stage
+            BinArgs ba;
+            ba.hw = count_words; ba.P = in.P; ba.gx = d.gx; ba.gy = d.gy; ba.cap = capacity;
+            ba.counters = g.counters; ba.err = err_dev; ba.order = g.order; ba.row_offsets = g.row_offsets;
+            ba.splat = g.splat; ba.bin_rec = g.bin_rec;
+            ba.ent_gid = b.key_a; ba.ent_w = b.key_b; ba.ent_ex = b.val_a;
+            ba.hist_r = b.bin_hist_r; ba.chunks_r = bin_chunks_r(capacity); ba.desc_r = g.desc_r; ba.drect = g.drect;
+            ba.hist_b = b.bin_hist_b; ba.chunks_b = bin_chunks_b(capacity, d.gy); ba.desc_b = b.bin_desc_b;
+            ba.rowinfo = b.bin_rowinfo; ba.words = b.bin_words; ba.zero = b.bin_zero; ba.nzero = 0;
+            ba.ranges = im.ranges; ba.binning = bin_base;
+            StageScope st_(ST_TILE_SORT, s);
+            launch_row_binning(ba, s);
+        } else {
+            { StageScope st_(ST_EMIT, s); launch_emit_instances(count_words, in.P, capacity, count_dev, g, d.gx, b.block_owner, b.key_a, keys16, b.val_a, bin_base, s); }
+            {
+                StageScope st_(ST_TILE_SORT, s);
+                if (keys16)
+                    radix_sort_pairs(reinterpret_cast<uint16_t*>(b.key_a), reinterpret_cast<uint16_t*>(b.key_b), b.val_a,
+                                     b.val_b, b.hist, b.scan_partials, capacity, count_dev, bin_base, 0, tile_passes, s,
+                                     false, err_dev);
+                else
+                    radix_sort_pairs(b.key_a, b.key_b, b.val_a, b.val_b, b.hist, b.scan_partials, capacity, count_dev,
+                                     bin_base, 0, tile_passes, s, false, err_dev);
+            }
             StageScope st_(ST_RANGES, s);
             launch_tile_ranges(capacity, count_dev, b.point_keys, keys16, im.ranges, s);
-            launch_tile_order(im.ranges, nullptr, d.T, im.tile_order, s);
         }
+        { StageScope st_(ST_RANGES, s); launch_tile_order(im.ranges, nullptr, d.T, im.tile_order, s); }
         if (rerun) OMR_HIP(hipMemsetAsync(im.tile_cost, 0, d.T * sizeof(uint32_t), s));
         RenderFwdArgs ra;
         ra.W = in.width; ra.H = in.height; ra.gx = d.gx; ra.gy = d.gy;
@@ -623,7 +665,7 @@ int backward_impl(const BackwardIn& in)
     GeomState g;
     GeomState::carve(in.geom_buffer, P, &g);
     BinningState b;
-    BinningState::carve(in.binning_buffer, (size_t)in.R, d.T, &b);
+    BinningState::carve(in.binning_buffer, (size_t)in.R, d.gx, d.gy, &b);
     ImageState im;
     ImageState::carve(in.image_buffer, d.N, d.T, &im);
     const int* radii = in.radii ? in.radii : geom_internal_radii(in.geom_buffer, P);
@@ -1024,7 +1066,7 @@ size_t omr_image_bytes(int width, int height)
 size_t omr_binning_bytes(int num_rendered, int width, int height)
 {
     const Dims d = dims(width, height);
-    return BinningState::carve(nullptr, (size_t)std::max(num_rendered, 0), d.T, nullptr);
+    return BinningState::carve(nullptr, (size_t)std::max(num_rendered, 0), d.gx, d.gy, nullptr);
 }
 
 int omr_debug_wave_sum9(const float* in, float* out, void* stream)
@@ -1111,7 +1153,7 @@ int omr_debug_point_list(char* binning_buffer, int R, int width, int height, uin
     if (R <= 0) return OMR_OK;
     const Dims d = dims(width, height);
     BinningState b;
-    BinningState::carve(binning_buffer, (size_t)R, d.T, &b);
+    BinningState::carve(binning_buffer, (size_t)R, d.gx, d.gy, &b);
     // the Gaussian indices alone (entries carry the instance's band mask in their top bits, raster_common.h)
     debug_point_ids_kernel<<<div_up((size_t)R, 256), 256, 0, (hipStream_t)stream>>>(b.point_list, (size_t)R, dst);
     return hip_check("debug_point_list");
@@ -1145,6 +1187,15 @@ int omr_debug_tile_cost(char* image_buffer, int width, int height, uint32_t* dst
     ImageState im;
     ImageState::carve(image_buffer, d.N, d.T, &im);
     OMR_HIP(hipMemcpyAsync(dst, im.tile_cost, d.T * sizeof(uint32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return OMR_OK;
+}
+
+int omr_debug_counters(char* geom_buffer, int P, uint32_t* dst, void* stream)
+{
+    g_last_error.clear();
+    GeomState g;
+    GeomState::carve(geom_buffer, (size_t)std::max(P, 0), &g);
+    OMR_HIP(hipMemcpyAsync(dst, g.counters, 8 * sizeof(uint32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
     return OMR_OK;
 }
 

@@ -50,15 +50,18 @@ size_t radix_hist_size(size_t n);
 // words of the `hist` and `scan_partials` scratch radix_sort_pairs needs for n items over `passes` passes
 size_t radix_scratch_words(size_t n, int passes);
 size_t radix_partials_words(size_t n);
-// the forward's scans of tiles_touched (sort.hip): offsets = inclusive scan in depth order (gather by order),
-// row_first = exclusive scan in index order (gradient row numbering); huge_list / *huge_count (zeroed by the
-// caller) = the Gaussians with more than ROW_SUM_HUGE tiles; status: scan2_status_words(n) words, zeroed before
-// the launch (one look-back kernel); *count_out = offsets[n-1] (num_rendered); err (device word, zeroed by the
-// caller; NULL = a private word) is OR-ed with 1 if a look-back gave up (sort.hip: LB_SPIN_MAX)
+// the forward's scans of tiles_touched (sort.hip): row_first = exclusive scan in index order (gradient row
+// numbering), *count_out = its total (num_rendered); huge_list / *huge_count (zeroed by the caller) = the Gaussians
+// with more than ROW_SUM_HUGE tiles; status: scan2_status_words(n) words, zeroed before the launch (one look-back
+// kernel); err (device word, zeroed by the caller; NULL = a private word) is OR-ed with 1 if a look-back gave up
+// (sort.hip: LB_SPIN_MAX). rects == NULL (sort path): offsets = inclusive scan in depth order (gather by order).
+// rects != NULL (row path): drect = rects in depth order, row_offsets = inclusive scan of their rows in depth order,
+// count_out[4] = its total M, desc_r = each BIN_CHUNK-slot chunk's first and last owner rank.
 size_t scan2_status_words(size_t n);
-void launch_forward_scans(const uint32_t* tiles_touched, const uint32_t* order, uint32_t* offsets, uint32_t* row_first,
-                          uint32_t* huge_list, uint32_t* huge_count, uint32_t* status, uint32_t* count_out,
-                          uint32_t* err, size_t n, hipStream_t s);
+void launch_forward_scans(const uint32_t* tiles_touched, const uint2* rects, const uint32_t* order, uint32_t* offsets,
+                          uint32_t* row_first, uint32_t* row_offsets, uint2* drect, uint2* desc_r, uint32_t* huge_list,
+                          uint32_t* huge_count, uint32_t* status, uint32_t* count_out, uint32_t* err, size_t n,
+                          hipStream_t s);
 // stable LSD radix sort of (key, value) over bits [0, 8*passes); returns which buffer holds the result (0: a, 1: b).
 // n = capacity; count (device, may be NULL) = live element count <= n. canon != NULL: the last pass writes the
 // values to the canonical point list of the binning buffer at canon (raster_common.h) instead of val_a / val_b.
@@ -72,6 +75,13 @@ int radix_sort_pairs(K* key_a, K* key_b, uint32_t* val_a, uint32_t* val_b, uint3
                      bool scratch_zeroed = false, uint32_t* err = nullptr);
 // the words of `hist` a sort of n items over `passes` passes needs zeroed before it starts (possibly none)
 ZeroSpan radix_zero_span(uint32_t* hist, size_t n, int passes);
+// one-launch exclusive scan of n u32 (in may equal out) of in[i] & mask; n_dev (device word, may be NULL) = live
+// length <= n; status: scan_status_words(n) words zeroed before the launch; err: the look-back error word (NULL: a
+// private one)
+size_t scan_status_words(size_t n);
+void launch_exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, const uint32_t* n_dev, uint32_t* status,
+                           uint32_t* err, hipStream_t s, uint32_t mask = 0xFFFFFFFFu);
+
 // duplicateWithKeys; L_cap = capacity, *count (device) = num_rendered; block_owner: emit_index_size(L_cap) words
 #ifndef OMR_EMIT_THREADS
 #define OMR_EMIT_THREADS 256
@@ -86,7 +96,7 @@ size_t emit_index_size(size_t L_cap);
 // also zeroes the backward's row_valid bytes at binning + row_valid_offset(L)
 // Words the host reads back (capi.hip: HostRead): src[0..n) into pinned fine-grained memory at dst, then seq into
 // seq_dst once they are acknowledged, with system-scope vector stores. Written by the first wave of a kernel that runs
-// anyway (emit_index, backward_schedule), or by host_words_kernel; dst == NULL: nothing to write.
+// anyway (emit_index or the row binning's first kernel, backward_schedule), or by host_words_kernel; dst == NULL: nothing to write.
 struct HostWords {
     uint32_t* dst = nullptr;
     const uint32_t* src = nullptr;
@@ -104,6 +114,45 @@ __device__ __forceinline__ void write_host_words(const HostWords& h, uint32_t la
 }
 #endif
 void launch_host_words(const HostWords& h, hipStream_t s);
+
+// bin.hip: tile binning by rows, then columns (the point list, its band masks and the tile ranges) for views of at most
+// BIN_MAX_GRID tiles a side; sort.hip's emit + tile sort + ranges otherwise
+constexpr uint32_t BIN_MAX_GRID = 1024;
+struct BinArgs {
+    HostWords hw;               // the forward's count words, written by the first kernel
+    int P;
+    uint32_t gx, gy;
+    size_t cap;                 // binning capacity (instances)
+    const uint32_t* counters;   // GeomState::counters: [0] L, [3] error word, [4] M (row slots)
+    uint32_t* err;              // look-back error word (counters + 3)
+    const uint32_t* order;      // depth order
+    const uint32_t* row_offsets;  // inclusive scan of the rect rows in depth order
+    const uint2* drect;         // rect words in depth order (launch_forward_scans)
+    const float4* splat;        // render records (rect in slot 3)
+    const float4* bin_rec;      // [P][2] band-mask constants, x0 | width << 16 (preprocess)
+    uint32_t *ent_gid, *ent_w, *ent_ex;  // row entries [cap]: Gaussian, rect width | x0 << 16, first instance slot
+    uint32_t* hist_r;           // [2][gy][live row chunks] entry counts, width sums; scanned in place
+    size_t chunks_r;            // row chunks of the capacity (grid size; the live count is div_up(M, chunk))
+    const uint2* desc_r;        // owners of each row chunk: first, last (depth ranks; launch_forward_scans)
+    uint32_t* hist_b;           // [tile][chunk] counts (row-major chunk blocks), scanned in place; chunks_b * gx words
+    size_t chunks_b;
+    uint4* desc_b;              // [chunks_b][2] column chunks: {y, chunk of the row, row chunks, row's first chunk},
+                                // {first slot, end slot, first owner entry, owners}
+    uint4* rowinfo;             // [gy + 1]
+    uint32_t* words;            // [0] live M, [1] column chunks, [2] live hist_r length, [3] live hist_b length
+    uint32_t* zero;             // look-back words of the two scans (bin_zero_words)
+    size_t nzero;
+    uint2* ranges;              // [T] tile ranges
+    char* binning;              // the binning buffer (canonical point list, row_valid at L-only offsets)
+};
+size_t bin_chunks_r(size_t cap);
+size_t bin_chunks_b(size_t cap, uint32_t gy);
+inline size_t bin_zero_words(size_t cap, uint32_t gx, uint32_t gy)
+{
+    return scan_status_words(2 * (size_t)gy * bin_chunks_r(cap)) + scan_status_words(bin_chunks_b(cap, gy) * gx);
+}
+void launch_row_binning(const BinArgs& a, hipStream_t s);
+
 
 // tile_keys: uint16_t[L_cap] when keys16 (at most 65536 tiles), else uint32_t[L_cap]
 void launch_emit_instances(const HostWords& hw, int P, size_t L_cap, const uint32_t* count, const GeomState& g,

@@ -260,6 +260,18 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     if (valid) {
         a.radii[idx] = vis ? o.rad : 0;
         g.tiles_touched[idx] = vis ? o.area : 0u;
+        const uint32_t x0 = __builtin_bit_cast(uint32_t, o.rec[3].x), y0 = __builtin_bit_cast(uint32_t, o.rec[3].y);
+        const uint32_t wd = __builtin_bit_cast(uint32_t, o.rec[3].z) - x0;
+        // the row binning's rect word (fields sized for BIN_MAX_GRID tiles a side; unused past that)
+        g.rect[idx] = vis ? make_uint2((__builtin_bit_cast(uint32_t, o.rec[3].w) - y0) | (y0 << RECT_ROWS_BITS) |
+                                           (wd << 21),
+                                       x0)
+                          : make_uint2(0u, 0u);
+        if (vis) {  // the binning's band-mask constants (bin.hip: the columns pass reads them per (Gaussian, row))
+            const BandSpan sp = band_span_consts(band_consts(o.rec[1]));
+            g.bin_rec[2 * (size_t)idx] = make_float4(o.rec[0].x, o.rec[0].y, sp.kDt, sp.ak);
+            g.bin_rec[2 * (size_t)idx + 1] = make_float4(sp.adt, sp.At, sp.invA, __builtin_bit_cast(float, x0 | (wd << 16)));
+        }
         g.key_a[idx] = vis ? __float_as_uint(o.depth) : 0xFFFFFFFFu;  // culled Gaussians sort last, emit nothing
         g.val_a[idx] = (uint32_t)idx;
         if (vis) {

@@ -37,6 +37,10 @@ constexpr int DEPTH_SORT_PASSES = 4;  // the depth sort's 32-bit keys (float bit
 constexpr int SCAN_THREADS = OMR_SCAN_THREADS;
 constexpr int SCAN_TILE = 4096;
 constexpr int SCAN_ITEMS = SCAN_TILE / SCAN_THREADS;
+constexpr uint32_t SCAN_GRID_MAX = 512;  // blocks of the persistent look-back scan (two 16-wave blocks per CU, 256 CUs)
+// row binning (bin.hip): slots per chunk of both passes, and the rect word's row-count field (rows <= BIN_MAX_GRID)
+constexpr uint32_t BIN_CHUNK = 2048;
+constexpr int RECT_ROWS_BITS = 11;
 
 // per-instance gradient row written by the render backward (render_bwd.hip) and reduced per Gaussian
 // (gaussian_bwd.hip). The row holds the instance's raw pixel-weight moments S_u dx, S_u dy, S_u dx^2, S_u dx dy,
@@ -101,13 +105,20 @@ struct GeomState {
     uint32_t* scan_partials;  // scan block sums
     uint32_t* scan2_status;   // look-back words of the forward scans (launch_forward_scans), zeroed by preprocess
     uint32_t* offsets;        // inclusive scan of tiles_touched in depth order
-    uint32_t* counters;       // [0] num_rendered, [1] prefiltered-cull flag, [2] huge_list count, [3] look-back error
+    uint32_t* counters;       // [0] num_rendered, [1] prefiltered-cull flag, [2] huge_list count, [3] look-back error,
+                              // [4] M = row slots of the row binning (sum of rect heights)
     uint32_t* order;          // depth order (points at val_a or val_b after the sort)
     uint32_t* row_first;      // first gradient row of each Gaussian (index-order exclusive scan, launch_forward_scans)
     float* row_sums;          // backward: [P][GRAD_ROW] each Gaussian's instance rows summed (launch_row_sums)
     float4* conic_op;         // [P] conic + opacity (= splat record slot 1), contiguous for gaussian_bwd's coalesced
                               // read (raw-moment rows, GRAD_ROW above)
     uint32_t* huge_list;      // Gaussians with more than ROW_SUM_HUGE tiles, any order; count in counters[2]
+    uint2* rect;              // rect word: rows | y0 << 11 | width << 21, x0 (0 if culled), for the row binning (bin.hip)
+    uint2* drect;             // the rect words in depth order (launch_forward_scans, row path)
+    uint32_t* row_offsets;    // inclusive scan of the rect rows in depth order (launch_forward_scans, row path)
+    uint2* desc_r;            // [P / 2 + 2] first / last owner rank of each row-binning chunk (launch_forward_scans)
+    float4* bin_rec;          // [P][2] {x, y, kDt, ak}, {adt, At, invA, x0 | rect width << 16}: the band-mask
+                              // constants (band_span_consts) the binning's columns pass needs per (Gaussian, row)
     int* internal_radii;      // used when the caller passes radii == NULL (rasterizer_impl.cu:284-287)
 
     static size_t carve(char* base, size_t P, GeomState* s);
@@ -192,10 +203,17 @@ struct BinningState {
     uint32_t* hist;        // radix histograms
     uint32_t* scan_partials;
     uint32_t* block_owner;  // emit index: owner rank of every EMIT_SLOTS-th slot
+    // the row binning (bin.hip; views of at most BIN_MAX_GRID tiles a side): row entries reuse key_a / key_b / val_a
+    uint32_t* bin_hist_r;   // [2][gy][bin_chunks_r]
+    uint32_t* bin_hist_b;   // [bin_chunks_b][gx]
+    uint4* bin_desc_b;      // [bin_chunks_b][2]
+    uint4* bin_rowinfo;     // [gy + 1]
+    uint32_t* bin_words;    // [4]
+    uint32_t* bin_zero;     // bin_zero_words look-back words
     uint8_t* row_valid;     // backward: 1 where inst_grad holds a row (at row_valid_offset(L); zeroed by emit)
     uint32_t* point_keys;  // sorted tile ids (points at key_a or key_b)
     // carve for capacity cap; point_list is set for L = cap (exact sizing: backward, debug, omr_binning_bytes)
-    static size_t carve(char* base, size_t cap, uint32_t T, BinningState* s);
+    static size_t carve(char* base, size_t cap, uint32_t gx, uint32_t gy, BinningState* s);
 };
 
 // number of 8-bit passes needed for tile ids < T (rasterizer_impl.cu:651: sort end bit = 32 + getHigherMsb(T))

@@ -117,28 +117,37 @@ __device__ uint64_t wave_lookback(uint64_t* status, uint32_t vb, uint32_t total,
     return excl;
 }
 
-// ---- the forward's two scans of tiles_touched, in one launch ---------------------------------------------------
-// offsets   = inclusive scan in depth order (gather by `order`): the emission slots, num_rendered = offsets[P-1];
+// ---- the forward's scans of tiles_touched (and the rect rows), in one launch -------------------------------------
 // row_first = exclusive scan in Gaussian INDEX order: the first gradient row of each Gaussian. The backward numbers
 //             its per-instance gradient rows this way (render_bwd.hip), so the 64 Gaussians of a wave own one
-//             contiguous span of rows when their sums are taken (gaussian_bwd.hip: row_sum_kernel).
-// Both sequences have the same tile structure: each 4096-item tile scans both in LDS, and its wave 0 / wave 1 find
-// the two exclusive prefixes by decoupled look-back at the same time (status_d / status_i, ticket, error word:
-// scan2_status_words(n), zeroed by preprocess). The kernel also lists the Gaussians with more than ROW_SUM_HUGE
-// tiles (huge_list, in no particular order), whose row sums take a whole workgroup.
-__global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint32_t* in, const uint32_t* order, size_t n,
-                                                                      uint64_t* status_d, uint64_t* status_i,
+//             contiguous span of rows when their sums are taken (gaussian_bwd.hip: row_sum_kernel); its total is
+//             num_rendered;
+// sort path (rects == NULL): offsets = inclusive scan of tiles_touched in depth order (gather by `order`): the
+//             emission slots (emit_kernel);
+// row path (rects != NULL; bin.hip): drect = the rect words in depth order, row_offsets = inclusive scan of their row
+//             counts in depth order: the row binning's slots, their total M in count_out[4]; and desc_r, the owners of
+//             every BIN_CHUNK-slot chunk: the rank holding the chunk's first slot (x) and its last (y) — each rank
+//             covers at most one chunk start (rows <= BIN_MAX_GRID < BIN_CHUNK) and writes the words it decides.
+// The sequences have the same tile structure: each 4096-item tile scans them in LDS, and its waves 0 / 1 find the
+// exclusive prefixes by decoupled look-back at the same time (status_a: depth order, status_i: index order; ticket,
+// error word: scan2_status_words(n), zeroed by preprocess). The kernel also lists the Gaussians with more than
+// ROW_SUM_HUGE tiles (huge_list, in no particular order), whose row sums take a whole workgroup.
+__global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint32_t* in, const uint2* rects,
+                                                                      const uint32_t* order, size_t n,
+                                                                      uint64_t* status_a, uint64_t* status_i,
                                                                       uint32_t* ticket, uint32_t* err,
                                                                       uint32_t* offsets, uint32_t* row_first,
-                                                                      uint32_t* huge_list, uint32_t* huge_count,
-                                                                      uint32_t* count_out)
+                                                                      uint32_t* row_offsets, uint2* drect,
+                                                                      uint32_t* desc_r, uint32_t* huge_list,
+                                                                      uint32_t* huge_count, uint32_t* count_out)
 {
-    __shared__ uint32_t s_d[SCAN_TILE + SCAN_TILE / 32];  // +1 pad per 32 to break the 16-stride conflicts
-    __shared__ uint32_t s_i[SCAN_TILE + SCAN_TILE / 32];
+    __shared__ uint32_t s_a[SCAN_TILE + SCAN_TILE / 32];  // depth order: tiles (sort path) or rows (row path)
+    __shared__ uint32_t s_i[SCAN_TILE + SCAN_TILE / 32];  // +1 pad per 32 to break the 16-stride conflicts
     __shared__ uint32_t s_wave[SCAN_THREADS / 64];
     __shared__ uint32_t s_vb, s_huge, s_huge_base;
     __shared__ uint32_t s_excl[2];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const bool rows = rects != nullptr;  // launch-uniform
     if (tid == 0) {
         s_vb = atomicAdd(ticket, 1u);
         s_huge = 0;
@@ -147,32 +156,40 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint
     const uint32_t vb = s_vb;
     const size_t base = (size_t)vb * SCAN_TILE;
     auto pad = [](uint32_t i) { return i + (i >> 5); };
+    constexpr uint32_t ROWS_MASK = (1u << RECT_ROWS_BITS) - 1u;
     // a depth sort whose look-back gave up may leave `order` partly unwritten: never gather through it then
     const bool order_ok = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; ++k) {
         const uint32_t li = k * SCAN_THREADS + tid;
         const size_t i = base + li;
-        s_d[pad(li)] = i < n && order_ok ? in[order[i]] : 0u;
+        const uint32_t o = i < n && order_ok ? order[i] : 0u;
+        if (rows) {
+            const uint2 rw = i < n && order_ok ? rects[o] : make_uint2(0u, 0u);
+            if (i < n) drect[i] = rw;
+            s_a[pad(li)] = rw.x & ROWS_MASK;
+        } else {
+            s_a[pad(li)] = i < n && order_ok ? in[o] : 0u;
+        }
         s_i[pad(li)] = i < n ? in[i] : 0u;
     }
     __syncthreads();
-    uint32_t vd[SCAN_ITEMS], vi[SCAN_ITEMS];
-    uint32_t sum_d = 0, sum_i = 0;
+    uint32_t va[SCAN_ITEMS], vi[SCAN_ITEMS];
+    uint32_t sum_a = 0, sum_i = 0;
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; ++k) {
-        vd[k] = s_d[pad(tid * SCAN_ITEMS + k)];
+        va[k] = s_a[pad(tid * SCAN_ITEMS + k)];
         vi[k] = s_i[pad(tid * SCAN_ITEMS + k)];
-        sum_d += vd[k];
+        sum_a += va[k];
         sum_i += vi[k];
     }
-    uint32_t total_d, total_i;
-    uint32_t run_d = block_exclusive_scan(sum_d, s_wave, &total_d);
+    uint32_t total_a, total_i;
+    uint32_t run_a = block_exclusive_scan(sum_a, s_wave, &total_a);
     uint32_t run_i = block_exclusive_scan(sum_i, s_wave, &total_i);
-    if (tid < 128) {  // wave 0: depth order, wave 1: index order
-        const bool dep = tid < 64;
-        const uint64_t excl = wave_lookback(dep ? status_d : status_i, vb, dep ? total_d : total_i, lane, err);
-        if (lane == 0) s_excl[dep ? 0 : 1] = (uint32_t)excl;
+    if (tid < 128u) {  // wave 0: depth order, wave 1: index order
+        const uint32_t wv = tid >> 6;
+        const uint64_t excl = wave_lookback(wv == 0 ? status_a : status_i, vb, wv == 0 ? total_a : total_i, lane, err);
+        if (lane == 0) s_excl[wv] = (uint32_t)excl;
     }
     // the tile's huge Gaussians get consecutive list slots: LDS ranks, one global reservation per tile
     uint32_t hrank[SCAN_ITEMS];
@@ -183,12 +200,12 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint
     }
     __syncthreads();
     if (tid == 0) s_huge_base = s_huge ? atomicAdd(huge_count, s_huge) : 0u;
-    run_d += s_excl[0];
+    run_a += s_excl[0];
     run_i += s_excl[1];
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; ++k) {
-        run_d += vd[k];  // inclusive
-        s_d[pad(tid * SCAN_ITEMS + k)] = run_d;
+        run_a += va[k];  // inclusive
+        s_a[pad(tid * SCAN_ITEMS + k)] = run_a;
         s_i[pad(tid * SCAN_ITEMS + k)] = run_i;  // exclusive
         run_i += vi[k];
     }
@@ -197,63 +214,98 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint
     for (int k = 0; k < SCAN_ITEMS; ++k) {
         const uint32_t li = k * SCAN_THREADS + tid;
         const size_t i = base + li;
-        if (i < n) {
-            offsets[i] = s_d[pad(li)];
-            if (i == n - 1) *count_out = s_d[pad(li)];  // num_rendered next to the flag words the host reads
-            row_first[i] = s_i[pad(li)];
-            if (hrank[k] != 0xFFFFFFFFu) huge_list[s_huge_base + hrank[k]] = (uint32_t)i;
+        if (i >= n) continue;
+        const uint32_t ex_i = s_i[pad(li)];
+        row_first[i] = ex_i;
+        if (i == n - 1) count_out[0] = ex_i + in[i];  // num_rendered next to the flag words the host reads
+        if (hrank[k] != 0xFFFFFFFFu) huge_list[s_huge_base + hrank[k]] = (uint32_t)i;
+        const uint32_t incl = s_a[pad(li)];
+        if (!rows) {
+            offsets[i] = incl;
+            if (i == n - 1) count_out[4] = 0u;  // no row slots on this path
+            continue;
         }
+        row_offsets[i] = incl;
+        if (i == n - 1) count_out[4] = incl;  // M, the row binning's slot count
+        const uint32_t start = li == 0 ? incl - (order_ok ? rects[order[i]].x & ROWS_MASK : 0u)
+                                       : s_a[pad(li - 1)];
+        if (incl == start) continue;  // no rows (culled: ranked last)
+        const uint32_t r = (uint32_t)i;
+        const uint32_t kk = (start + BIN_CHUNK - 1) / BIN_CHUNK;  // the first chunk start at or after `start`
+        if (kk * BIN_CHUNK < incl) {
+            desc_r[2 * kk] = r;  // first owner of chunk kk
+            if (kk > 0) desc_r[2 * (kk - 1) + 1] = start < kk * BIN_CHUNK ? r : r - 1;  // last owner of chunk kk - 1
+        }
+        // the last rank with rows owns the last slot (culled ranks, all rowless, come after every visible one)
+        uint32_t next_rows;
+        if (i + 1 >= n) next_rows = 0;
+        else if (li + 1 < SCAN_TILE) next_rows = s_a[pad(li + 1)] - incl;
+        else next_rows = order_ok ? rects[order[i + 1]].x & ROWS_MASK : 0u;
+        if (next_rows == 0) desc_r[2 * ((incl - 1) / BIN_CHUNK) + 1] = r;
     }
 }
 
 // Exclusive scan of a u32 array in ONE launch, for the [digit][block] histograms of the large sorts (the 3-launch
-// reduce / partials / downsweep scan before); status / ticket zeroed by radix_upsweep_kernel.
+// reduce / partials / downsweep scan before) and the row binning (bin.hip); status / ticket zeroed by the kernel
+// before. Persistent: each block takes tickets (tile numbers, in dispatch order) until they run past the live tiles, so
+// a grid capped at SCAN_GRID_MAX blocks serves any length and a capacity-sized scan costs no dispatch of dead blocks
+// (a tile looks back only at lower tickets, held by blocks already running: no block waits on one not yet resident).
+// n_dev (may be NULL): a device word with the live length (<= n). mask: applied to every input word.
 __global__ __launch_bounds__(SCAN_THREADS) void scan_lookback_kernel(const uint32_t* in, uint32_t* out, size_t n,
-                                                                     uint64_t* status, uint32_t* ticket, uint32_t* err)
+                                                                     const uint32_t* n_dev, uint64_t* status,
+                                                                     uint32_t* ticket, uint32_t* err,
+                                                                     uint32_t mask = 0xFFFFFFFFu)
 {
     __shared__ uint32_t s_data[SCAN_TILE + SCAN_TILE / 32];
     __shared__ uint32_t s_wave[SCAN_THREADS / 64];
     __shared__ uint32_t s_vb;
     __shared__ uint64_t s_excl;
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    if (tid == 0) s_vb = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const uint32_t vb = s_vb;
-    const size_t base = (size_t)vb * SCAN_TILE;
+    if (n_dev) n = min(n, (size_t)*n_dev);
+    const uint32_t ntiles = max(1u, (uint32_t)((n + SCAN_TILE - 1) / SCAN_TILE));  // tile 0 runs for n = 0 (publishes 0)
+    if (blockIdx.x >= ntiles) return;
     auto pad = [](uint32_t i) { return i + (i >> 5); };
+    while (true) {
+        if (tid == 0) s_vb = atomicAdd(ticket, 1u);
+        __syncthreads();
+        const uint32_t vb = s_vb;
+        if (vb >= ntiles) return;  // block-uniform
+        const size_t base = (size_t)vb * SCAN_TILE;
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        const uint32_t li = k * SCAN_THREADS + tid;
-        const size_t i = base + li;
-        s_data[pad(li)] = i < n ? in[i] : 0u;
-    }
-    __syncthreads();
-    uint32_t v[SCAN_ITEMS];
-    uint32_t sum = 0;
+        for (int k = 0; k < SCAN_ITEMS; ++k) {
+            const uint32_t li = k * SCAN_THREADS + tid;
+            const size_t i = base + li;
+            s_data[pad(li)] = i < n ? in[i] & mask : 0u;
+        }
+        __syncthreads();
+        uint32_t v[SCAN_ITEMS];
+        uint32_t sum = 0;
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        v[k] = s_data[pad(tid * SCAN_ITEMS + k)];
-        sum += v[k];
-    }
-    uint32_t total;
-    const uint32_t run0 = block_exclusive_scan(sum, s_wave, &total);
-    if (tid < 64) {  // wave 0: publish, look back, publish the inclusive prefix
-        const uint64_t excl = wave_lookback(status, vb, total, lane, err);
-        if (tid == 0) s_excl = excl;
-    }
-    __syncthreads();
-    uint32_t run = (uint32_t)s_excl + run0;
+        for (int k = 0; k < SCAN_ITEMS; ++k) {
+            v[k] = s_data[pad(tid * SCAN_ITEMS + k)];
+            sum += v[k];
+        }
+        uint32_t total;
+        const uint32_t run0 = block_exclusive_scan(sum, s_wave, &total);
+        if (tid < 64) {  // wave 0: publish, look back, publish the inclusive prefix
+            const uint64_t excl = wave_lookback(status, vb, total, lane, err);
+            if (tid == 0) s_excl = excl;
+        }
+        __syncthreads();
+        uint32_t run = (uint32_t)s_excl + run0;
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        s_data[pad(tid * SCAN_ITEMS + k)] = run;
-        run += v[k];
-    }
-    __syncthreads();
+        for (int k = 0; k < SCAN_ITEMS; ++k) {
+            s_data[pad(tid * SCAN_ITEMS + k)] = run;
+            run += v[k];
+        }
+        __syncthreads();
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        const uint32_t li = k * SCAN_THREADS + tid;
-        const size_t i = base + li;
-        if (i < n) out[i] = s_data[pad(li)];
+        for (int k = 0; k < SCAN_ITEMS; ++k) {
+            const uint32_t li = k * SCAN_THREADS + tid;
+            const size_t i = base + li;
+            if (i < n) out[i] = s_data[pad(li)];
+        }
+        __syncthreads();  // s_data and s_vb are rewritten by the next tile
     }
 }
 
@@ -1086,16 +1138,18 @@ size_t radix_partials_words(size_t n) { return 2 * scan_partials_size(radix_hist
 
 size_t scan2_status_words(size_t n) { return 4 * div_up(n, SCAN_TILE) + 2; }
 
-void launch_forward_scans(const uint32_t* tiles_touched, const uint32_t* order, uint32_t* offsets, uint32_t* row_first,
-                          uint32_t* huge_list, uint32_t* huge_count, uint32_t* status, uint32_t* count_out,
-                          uint32_t* err, size_t n, hipStream_t s)
+void launch_forward_scans(const uint32_t* tiles_touched, const uint2* rects, const uint32_t* order, uint32_t* offsets,
+                          uint32_t* row_first, uint32_t* row_offsets, uint2* drect, uint2* desc_r, uint32_t* huge_list,
+                          uint32_t* huge_count, uint32_t* status, uint32_t* count_out, uint32_t* err, size_t n,
+                          hipStream_t s)
 {
     if (n == 0) return;
     const uint32_t nb = div_up(n, SCAN_TILE);
     uint64_t* st = reinterpret_cast<uint64_t*>(status);  // [2][nb] 64-bit | ticket | own error word
     uint32_t* ticket = status + 4 * (size_t)nb;
-    scan2_lookback_kernel<<<nb, SCAN_THREADS, 0, s>>>(tiles_touched, order, n, st, st + nb, ticket,
-                                                      err ? err : ticket + 1, offsets, row_first, huge_list, huge_count,
+    scan2_lookback_kernel<<<nb, SCAN_THREADS, 0, s>>>(tiles_touched, rects, order, n, st, st + nb, ticket,
+                                                      err ? err : ticket + 1, offsets, row_first, row_offsets, drect,
+                                                      reinterpret_cast<uint32_t*>(desc_r), huge_list, huge_count,
                                                       count_out);
 }
 
@@ -1181,8 +1235,8 @@ int radix_sort_pairs(K* key_a, K* key_b, uint32_t* val_a, uint32_t* val_b, uint3
             else
                 radix_upsweep_kernel<K, false, SORT_ITEMS_S, SORT_THREADS_S><<<nb, SORT_THREADS_S, 0, s>>>(ki, n, count, shift, hist, nb,
                                                                                    scan_partials, 2 * nbs + 2);
-            scan_lookback_kernel<<<nbs, SCAN_THREADS, 0, s>>>(hist, hist, (size_t)RADIX * nb, lb, lb_ticket,
-                                                             err_out ? err_out : lb_ticket + 1);
+            scan_lookback_kernel<<<std::min(nbs, SCAN_GRID_MAX), SCAN_THREADS, 0, s>>>(
+                hist, hist, (size_t)RADIX * nb, nullptr, lb, lb_ticket, err_out ? err_out : lb_ticket + 1);
             if (large)
                 radix_downsweep_kernel<K, false, SORT_ITEMS_LARGE, SORT_THREADS_LARGE><<<nb, SORT_THREADS_LARGE, 0, s>>>(
                     ki, vi, ko, vo, n, count, last ? canon : nullptr, shift, hist, nb);
@@ -1203,6 +1257,18 @@ template int radix_sort_pairs<uint16_t>(uint16_t*, uint16_t*, uint32_t*, uint32_
                                         const uint32_t*, char*, int, int, hipStream_t, bool, uint32_t*);
 
 size_t emit_index_size(size_t L_cap) { return div_up(L_cap, EMIT_SLOTS) + 1; }
+
+size_t scan_status_words(size_t n) { return 2 * (size_t)div_up(n, SCAN_TILE) + 2; }
+
+void launch_exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, const uint32_t* n_dev, uint32_t* status,
+                           uint32_t* err, hipStream_t s, uint32_t mask)
+{
+    if (n == 0) return;
+    const uint32_t nbs = div_up(n, SCAN_TILE);
+    uint32_t* ticket = status + 2 * (size_t)nbs;
+    scan_lookback_kernel<<<std::min(nbs, SCAN_GRID_MAX), SCAN_THREADS, 0, s>>>(
+        in, out, n, n_dev, reinterpret_cast<uint64_t*>(status), ticket, err ? err : ticket + 1, mask);
+}
 
 void launch_emit_instances(const HostWords& hw, int P, size_t L_cap, const uint32_t* count, const GeomState& g,
                            uint32_t gx, uint32_t* block_owner, void* tile_keys, bool keys16, uint32_t* gauss_vals,

@@ -67,6 +67,7 @@ def lib() -> C.CDLL:
         L.omr_debug_ranges.argtypes = [vp, i, i, vp, vp]
         L.omr_debug_image_state.argtypes = [vp, i, i, vp, vp, vp]
         L.omr_debug_tile_cost.argtypes = [vp, i, i, vp, vp]
+        L.omr_debug_counters.argtypes = [vp, i, vp, vp]
         L.omr_debug_geometry.argtypes = [vp, i, vp, vp, vp, vp, vp, vp]
         L.omr_debug_wave_sum9.argtypes = [vp, vp, vp]
         L.omr_debug_wave_sum9_lds.argtypes = [vp, vp, vp]
@@ -470,6 +471,15 @@ def debug_tile_cost(width, height, imgBuffer) -> torch.Tensor:
     _check(lib().omr_debug_tile_cost(imgBuffer.data_ptr(), width, height, out.data_ptr(), _stream(imgBuffer.device)),
            "debug_tile_cost")
     return out
+
+
+def debug_counters(P, geomBuffer) -> dict:
+    """The forward's count words (omr_debug_counters): num_rendered, the row binning's row slots M, ..."""
+    out = torch.zeros((8,), dtype=torch.int32, device=geomBuffer.device)
+    _check(lib().omr_debug_counters(geomBuffer.data_ptr(), int(P), out.data_ptr(), _stream(geomBuffer.device)),
+           "debug_counters")
+    c = [int(v) for v in out.cpu().tolist()]
+    return {"num_rendered": c[0], "prefiltered_flag": c[1], "huge": c[2], "error": c[3], "row_slots": c[4]}
 
 
 # --------------------------------------------------------------------------------------------------------------

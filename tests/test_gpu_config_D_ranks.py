@@ -1,0 +1,116 @@
+"""Config D (1 M Gaussians, eight equirect views, one per GPU; BASELINE.json) through the real exchange code: eight
+ranks over gloo, all on cuda:0 (the one-GPU box's stand-in for the 8-GPU node the driver's scaling run uses). Each
+rank renders its view of the config-C scene, runs the HIP backward into its GradBuffer and calls
+parallel.allreduce_compact_ (the exchange bench.py runs at N > 1: all-reduce of the 44 B/G xyz / opacity / scale /
+rotation gradients, all-gather of every view's colour gradient and camera position, SH gradient rebuilt on every
+rank). Checked against the eight per-view HIP gradients computed one after another in this process:
+  * every rank holds the same buffer, bit for bit;
+  * the 44 B/G part equals the per-view sum to float32 summation-order error (gloo's ring adds the eight views in
+    another order than a sequential loop: |diff| <= 8 ulp of the sum of magnitudes);
+  * the SH part equals, bit for bit, the rebuild from the eight gathered colour gradients in view order, and that
+    rebuild equals the sequential sum of the per-view SH gradients bit for bit (same arithmetic, same order).
+"""
+import hashlib
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORLD = 8
+NAMES = {"dL_dmeans3D": "dmean3D", "dL_dopacity": "dopacity", "dL_dscales": "dscale", "dL_drotations": "drot"}
+
+
+def _worker(rank, world, port, q, tmpdir):
+    import torch
+    import torch.distributed as dist
+
+    sys.path[:0] = [ROOT]
+    import _omnigs
+
+    omr = _omnigs.load()
+    R, par = omr.rasterizer, omr.parallel
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        g, cam, dL = omr.scene.config_scene("D", view_index=rank)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)  # noqa: E731
+        m, sh = t(g.means3D), t(g.shs)
+        vm, pm, cp, bg, e = t(cam.viewmatrix), t(cam.projmatrix), t(cam.campos), torch.zeros(3, device=dev), \
+            torch.empty(0, device=dev)
+        buf = par.GradBuffer(g.P, g.shs.shape[1], dev)
+        out = buf.out_dict(dev)
+        nr, color, radii, gb, bb, ib = R.RasterizeGaussiansCUDA(bg, m, e, t(g.opacity), t(g.scales), t(g.rotations),
+                                                                1.0, e, vm, pm, cam.tanfovx, cam.tanfovy, cam.height,
+                                                                cam.width, sh, g.sh_degree, cp, False, cam.camera_type,
+                                                                False)
+        R.RasterizeGaussiansBackwardCUDA(bg, m, radii, e, t(g.scales), t(g.rotations), 1.0, e, vm, pm, cam.tanfovx,
+                                         cam.tanfovy, t(dL), sh, g.sh_degree, cp, gb, nr, bb, ib, cam.camera_type,
+                                         out=out)
+        torch.cuda.synchronize()
+        par.allreduce_compact_(buf, par.DistInfo(rank, world, 0), out["dL_dcolors"], cp, None,
+                               rebuild_packed=lambda pk, out: R.sh_grad_from_colors_packed(m, sh, g.sh_degree, pk,
+                                                                                           out=out))
+        torch.cuda.synchronize()
+        flat = buf.flat.cpu().numpy()
+        if rank == 0:
+            np.save(os.path.join(tmpdir, "flat0.npy"), flat)
+        q.put((rank, hashlib.sha1(flat.tobytes()).hexdigest()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_config_D_eight_ranks_compact_exchange(tmp_path):
+    import torch
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q, str(tmp_path))) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    digests = dict(q.get(timeout=420) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(set(digests.values())) == 1, digests  # identical replicas, bit for bit
+    flat0 = np.load(os.path.join(str(tmp_path), "flat0.npy"))
+
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+    from helpers import hip_run, omr, to_np
+
+    R, par = omr.rasterizer, omr.parallel
+    sums, mags, dsh_seq, dcolors, campos = None, None, None, [], []
+    for v in range(WORLD):
+        g, cam, dL = omr.scene.config_scene("D", view_index=v)
+        h = hip_run(g, cam, dL)
+        gr = h["grads"]
+        part = np.concatenate([to_np(gr[NAMES[k]]).reshape(g.P, -1) for k in NAMES], axis=1).astype(np.float64)
+        sums = part if sums is None else sums + part
+        mags = np.abs(part) if mags is None else mags + np.abs(part)
+        dsh_seq = gr["dsh"].clone() if dsh_seq is None else dsh_seq + gr["dsh"]
+        dcolors.append(gr["dcolor"].clone())
+        campos.append(torch.from_numpy(cam.campos).cuda())
+        del h, gr
+    P = g.P
+    buf = par.GradBuffer(P, g.shs.shape[1], torch.device("cpu"))
+    buf.flat.copy_(torch.from_numpy(flat0))
+    got = np.concatenate([buf.views[k].numpy().reshape(P, -1) for k in NAMES], axis=1).astype(np.float64)
+    tol = 8 * np.finfo(np.float32).eps * mags + np.finfo(np.float32).tiny
+    bad = np.abs(got - sums) > tol
+    assert not bad.any(), f"{int(bad.sum())} entries of the 44 B/G sum off by more than 8 ulp of their magnitude sum"
+    dev = dsh_seq.device
+    packed = torch.cat([torch.stack(dcolors), torch.stack(campos)[:, None, :]], dim=1).contiguous()
+    rebuilt = R.sh_grad_from_colors_packed(torch.from_numpy(g.means3D).to(dev), torch.from_numpy(g.shs).to(dev),
+                                           g.sh_degree, packed)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(buf.views["dL_dsh"].numpy(), to_np(rebuilt))
+    np.testing.assert_array_equal(to_np(rebuilt), to_np(dsh_seq))

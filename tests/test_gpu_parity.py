@@ -188,12 +188,37 @@ def test_more_than_65536_tiles_sorts_32_bit_tile_keys(oracle_mt):
     _compare(g, cam, None, nthreads=oracle_mt)
 
 
+def test_views_past_1024_tiles_a_side_take_the_radix_binning(oracle_mt):
+    """The row binning (bin.hip) covers views of at most 1024 tiles a side (16384 px); a wider view takes sort.hip's
+    emit + radix tile sort + tile_ranges: 16400 x 48 equirect = 1025 x 3 tiles, forward and backward."""
+    g, cam, dL = make_case(6000, 16400, 48, LON, 52, view_index=2, spread=2.0)
+    assert (cam.width + 15) // 16 > 1024
+    _compare(g, cam, dL, nthreads=oracle_mt)
+    h = hip_run(g, cam, None)
+    assert omr.rasterizer.debug_counters(g.P, h["geom"])["row_slots"] == 0  # the rows scan did not run
+
+
+def test_row_binning_reports_its_row_slots():
+    """bin.hip's rows pass: M = the sum of the visible Gaussians' rect heights (counters[4])."""
+    g, cam, _ = make_case(3000, 512, 256, LON, 53, view_index=1, spread=1.5)
+    o, _, _ = oracle_run(g, cam)
+    h = hip_run(g, cam, None)
+    P = g.P
+    r = o.get("radii").astype(np.float64)
+    m = o.get("means2D").reshape(P, 2).astype(np.float32)
+    vis = r > 0
+    rad = r.astype(np.float32)
+    y0 = np.clip(((m[:, 1] - rad) / np.float32(16)).astype(np.int64), 0, 16)
+    # getRect's ((y + r) + 16) - 1, left to right in float (auxiliary.h:56-66)
+    y1 = np.clip(((((m[:, 1] + rad) + np.float32(16)) - np.float32(1)) / np.float32(16)).astype(np.int64), 0, 16)
+    assert omr.rasterizer.debug_counters(P, h["geom"])["row_slots"] == int((y1 - y0)[vis].sum())
+
+
 def test_config_D_standin_eight_views(oracle_mt):
-    """Config D (1 M Gaussians, 8 views one per GPU, BASELINE.json) on one GPU: the eight views of the §8(d) ring run
-    one after another. The compact exchange's result (parallel.allreduce_compact_: sum of the 44 B/G xyz / opacity /
-    scale / rotation gradients + the SH gradient rebuilt from the gathered colour gradients) must equal the sum of
-    the per-view HIP gradients (the SH part bit for bit: same arithmetic, same view order), and two of the views
-    match the oracle."""
+    """Config D's eight views of the §8(d) ring (1 M Gaussians each) one after another on one GPU: views 0 and 5
+    against the oracle, and the SH gradient the compact exchange rebuilds from the eight colour gradients equal, bit
+    for bit, to the sum of the per-view SH gradients (same arithmetic, same view order). The exchange itself — eight
+    ranks calling parallel.allreduce_compact_ — is tests/test_gpu_config_D_ranks.py."""
     import torch
 
     R = omr.rasterizer
