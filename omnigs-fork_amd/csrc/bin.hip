@@ -75,6 +75,21 @@ __device__ __forceinline__ uint32_t live_M(const uint32_t* counters, size_t cap)
     return binning_count(counters, cap) ? counters[4] : 0u;
 }
 
+// Chunk order of the grid-stride kernels: the dispatcher deals blocks to the 8 XCDs round-robin (block b on XCD
+// b % 8), so XCD x takes the x-th eighth of the chunks and its blocks stride over that range: blocks running together
+// on one XCD work on neighbouring chunks, whose count words and point-list runs share cache lines in that XCD's L2
+// (rather than partial lines written back from eight L2s). Grids that are not a multiple of 8 stride plainly.
+struct ChunkRange {
+    uint32_t first, end, step;
+};
+__device__ __forceinline__ ChunkRange xcd_chunks(uint32_t C)
+{
+    const uint32_t G = gridDim.x, b = blockIdx.x;
+    if (G % 8u != 0u) return {b, C, G};
+    const uint32_t x = b % 8u;
+    return {(uint32_t)((uint64_t)C * x / 8u) + b / 8u, (uint32_t)((uint64_t)C * (x + 1u) / 8u), G / 8u};
+}
+
 // block-wide exclusive scan (THREADS threads, one value each)
 template <int THREADS>
 __device__ __forceinline__ uint32_t bin_block_scan(uint32_t x, uint32_t* s_wave, uint32_t* total)
@@ -174,13 +189,7 @@ __device__ __forceinline__ void rank_items(const uint32_t (&d)[RB_ROUNDS], const
     uint32_t lr[RB_ROUNDS];
 #pragma unroll
     for (int r = 0; r < RB_ROUNDS; ++r) {
-        uint64_t peers = __ballot(valid[r]);
-#pragma unroll
-        for (int b = 0; b < BITS; ++b) {
-            const bool bit = (d[r] >> b) & 1u;
-            const uint64_t m = __ballot(bit);
-            peers &= bit ? m : ~m;
-        }
+        const uint64_t peers = wave_match_digit<BITS>(d[r], valid[r]);
         const uint32_t rank = mask_rank(peers);
         const uint32_t prev = valid[r] ? s_whist[w][d[r]] : 0u;
         lr[r] = prev + rank;
@@ -263,7 +272,8 @@ __global__ __launch_bounds__(RB_THREADS) void rows_hist_kernel(BinArgs a)
         a.words[2] = 2u * gy * C;
     }
     const size_t half = (size_t)gy * C;
-    for (uint32_t c = blockIdx.x; c < C; c += gridDim.x) {
+    const ChunkRange cr = xcd_chunks(C);
+    for (uint32_t c = cr.first; c < cr.end; c += cr.step) {
         for (uint32_t y = tid; y <= gy; y += RB_THREADS) {
             s_cnt[y] = 0;
             s_wsum[y] = 0;
@@ -351,26 +361,66 @@ __global__ __launch_bounds__(RB_THREADS) void rows_scatter_kernel(BinArgs a)
     const uint32_t M = live_M(a.counters, a.cap), C = row_chunks(M), gy = a.gy;
     const size_t half = (size_t)gy * C;
     uint32_t* desc_w = reinterpret_cast<uint32_t*>(a.desc_b);
-    for (uint32_t c = blockIdx.x; c < C; c += gridDim.x) {
-        const RowChunk k = row_chunk(a, c, M);
+    // software pipeline: the next chunk's owners (first RP x 256) and count bases are loaded into registers while the
+    // current chunk is ranked and written
+    constexpr int RP = 3, GBP = (1 << BITS) / RB_THREADS;
+    uint32_t p_end[RP], p_rx[RP], p_ry[RP], p_gid[RP], p_gb[GBP], p_wb[GBP];
+    auto load_owners = [&](const RowChunk& q, uint32_t cq) {
+#pragma unroll
+        for (int j = 0; j < RP; ++j) {
+            const uint32_t i = tid + j * RB_THREADS;
+            if (i < q.nr) {
+                const uint32_t r = q.r_lo + i;
+                p_end[j] = a.row_offsets[r];
+                const uint2 rw = a.drect[r];
+                p_rx[j] = rw.x;
+                p_ry[j] = rw.y;
+                p_gid[j] = a.order[r];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < GBP; ++j) {
+            const uint32_t y = tid + j * RB_THREADS;
+            if (y < gy) {
+                p_gb[j] = a.hist_r[(size_t)y * C + cq];
+                p_wb[j] = a.hist_r[half + (size_t)y * C + cq];
+            }
+        }
+    };
+    const ChunkRange cr = xcd_chunks(C);
+    RowChunk k = row_chunk(a, min(cr.first, C - 1u), M);  // (C = 0: no iteration reads it)
+    if (cr.first < cr.end) load_owners(k, cr.first);
+    for (uint32_t c = cr.first; c < cr.end; c += cr.step) {
+        const uint32_t cn = c + cr.step;
+        const RowChunk kn = row_chunk(a, min(cn, C - 1u), M);
         uint32_t* s_yoff = s_yoff_sorted;
         reinterpret_cast<uint4*>(s_own)[tid] = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
-        for (uint32_t i = tid; i < k.nr; i += RB_THREADS) {
-            const uint32_t r = k.r_lo + i;
-            const uint32_t end = a.row_offsets[r];
-            const uint2 rw = a.drect[r];
-            const uint32_t start = end - (rw.x & ((1u << RECT_ROWS_BITS) - 1u));
-            s_yoff[i] = rect_y0(rw) - start;  // modular: s + (y0 - start) = y0 + (s - start)
-            s_gid[i] = a.order[r];
-            s_xw[i] = rect_w(rw) | (rw.y << 16);
+        auto stage = [&](uint32_t i, uint32_t end, uint32_t rx, uint32_t ry, uint32_t gid) {
+            const uint32_t start = end - (rx & ((1u << RECT_ROWS_BITS) - 1u));
+            s_yoff[i] = rect_y0(make_uint2(rx, ry)) - start;  // modular: s + (y0 - start) = y0 + (s - start)
+            s_gid[i] = gid;
+            s_xw[i] = rect_w(make_uint2(rx, ry)) | (ry << 16);
             if (start >= k.s0 && start < end) s_own[start - k.s0] = (uint16_t)i;
+        };
+#pragma unroll
+        for (int j = 0; j < RP; ++j)
+            if (tid + j * RB_THREADS < k.nr) stage(tid + j * RB_THREADS, p_end[j], p_rx[j], p_ry[j], p_gid[j]);
+        for (uint32_t i = tid + RP * RB_THREADS; i < k.nr; i += RB_THREADS) {
+            const uint32_t r = k.r_lo + i;
+            const uint2 rw = a.drect[r];
+            stage(i, a.row_offsets[r], rw.x, rw.y, a.order[r]);
         }
-        for (uint32_t y = tid; y < gy; y += RB_THREADS) {
-            s_gbase[y] = a.hist_r[(size_t)y * C + c];
-            s_wbase[y] = a.hist_r[half + (size_t)y * C + c] - M;
+#pragma unroll
+        for (int j = 0; j < GBP; ++j) {
+            const uint32_t y = tid + j * RB_THREADS;
+            if (y < gy) {
+                s_gbase[y] = p_gb[j];
+                s_wbase[y] = p_wb[j] - M;
+            }
         }
         __syncthreads();
+        if (cn < cr.end) load_owners(kn, cn);
         owner_fill(s_own, s_wave);
         uint32_t d[RB_ROUNDS], own[RB_ROUNDS], lp[RB_ROUNDS];
         bool valid[RB_ROUNDS];
@@ -453,6 +503,7 @@ __global__ __launch_bounds__(RB_THREADS) void rows_scatter_kernel(BinArgs a)
                 if (kk > 0) desc_w[8 * (size_t)(cc - 1) + 7] = ex < s0 ? dst + 1 : dst;  // owner end of the chunk before
             }
         }
+        k = kn;
         __syncthreads();  // the next chunk rewrites the staging arrays
     }
 }
@@ -475,27 +526,44 @@ __device__ __forceinline__ size_t col_index(const ColChunk& k, uint32_t gx, uint
     return (size_t)k.cb * gx + (size_t)x * k.nch + k.kk;
 }
 
-// Per column chunk (grid-stride): the instance counts per tile column from a difference array.
+// Per column chunk (grid-stride): the instance counts per tile column from a difference array. Latency-bound, so
+// every load of a chunk is issued before any is used: the owners' words for the first HP x 256 owners at once, and
+// the next chunk's descriptor while this one is counted.
 __global__ __launch_bounds__(RB_THREADS) void cols_hist_kernel(BinArgs a)
 {
+    constexpr int HP = 4;
     __shared__ int s_diff[BIN_MAX_GRID + 1];
     __shared__ uint32_t s_wave[RB_WAVES];
     const uint32_t tid = threadIdx.x, gx = a.gx, C = a.words[1];
-    for (uint32_t c = blockIdx.x; c < C; c += gridDim.x) {
+    const ChunkRange cr = xcd_chunks(C);
+    ColChunk k = col_chunk(a, min(cr.first, C - 1u));  // (C = 0: no iteration reads it)
+    for (uint32_t c = cr.first; c < cr.end; c += cr.step) {
+        const ColChunk kn = col_chunk(a, min(c + cr.step, C - 1u));
+        uint32_t ex[HP], ew[HP];
+#pragma unroll
+        for (int j = 0; j < HP; ++j) {
+            const uint32_t i = tid + j * RB_THREADS;
+            if (i < k.nr) {
+                ex[j] = a.ent_ex[k.e_lo + i];
+                ew[j] = a.ent_w[k.e_lo + i];
+            }
+        }
         for (uint32_t x = tid; x <= gx; x += RB_THREADS) s_diff[x] = 0;
-        const ColChunk k = col_chunk(a, c);
         __syncthreads();
-        for (uint32_t i = tid; i < k.nr; i += RB_THREADS) {
-            const uint32_t e = k.e_lo + i;
-            const uint32_t ex = a.ent_ex[e], ew = a.ent_w[e];
-            const uint32_t wd = ew & 0xFFFFu, x0 = ew >> 16;
-            const uint32_t ja = max(k.s0, ex) - ex, jb = min(k.s1, ex + wd) - ex;
+        auto add = [&](uint32_t e_x, uint32_t e_w) {
+            const uint32_t wd = e_w & 0xFFFFu, x0 = e_w >> 16;
+            const uint32_t ja = max(k.s0, e_x) - e_x, jb = min(k.s1, e_x + wd) - e_x;
             atomicAdd(&s_diff[x0 + ja], 1);
             atomicAdd(&s_diff[x0 + jb], -1);
-        }
+        };
+#pragma unroll
+        for (int j = 0; j < HP; ++j)
+            if (tid + j * RB_THREADS < k.nr) add(ex[j], ew[j]);
+        for (uint32_t i = tid + HP * RB_THREADS; i < k.nr; i += RB_THREADS) add(a.ent_ex[k.e_lo + i], a.ent_w[k.e_lo + i]);
         __syncthreads();
         diff_to_counts<RB_THREADS>(s_diff, gx, s_wave);
         for (uint32_t x = tid; x < gx; x += RB_THREADS) a.hist_b[col_index(k, gx, x)] = (uint32_t)s_diff[x];
+        k = kn;
         __syncthreads();
     }
 }
@@ -558,12 +626,13 @@ __global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
     const uint32_t L = live_L(a.counters, a.cap);
     uint8_t* row_valid = reinterpret_cast<uint8_t*>(a.binning + row_valid_offset(L));  // the backward's row map
     uint32_t* point_list = reinterpret_cast<uint32_t*>(a.binning + canonical_list_offset(L));
-    // software pipeline: the next chunk's descriptor, staged owners' entries and band constants are loaded into
-    // registers while the current chunk is expanded and ranked (PF owners per thread)
+    // software pipeline: the next chunk's descriptor, count bases, staged owners' entries and band constants are
+    // loaded into registers while the current chunk is expanded and ranked (PF owners per thread)
     constexpr int PF = CB_OWN_CONST / RB_THREADS;
     static_assert(PF * RB_THREADS == CB_OWN_CONST, "staged owners: whole rounds of the block");
     typedef float f4v __attribute__((ext_vector_type(4)));  // native vectors: the prefetch stays in registers
-    uint32_t p_ex[PF], p_ew[PF], p_gid[PF];
+    constexpr int GBP = (1 << BITS) / RB_THREADS;  // the chunk's per-column count bases, per thread
+    uint32_t p_ex[PF], p_ew[PF], p_gid[PF], p_gb[GBP];
     f4v p_ba[PF], p_bb[PF];
     const f4v* bin_rec_v = reinterpret_cast<const f4v*>(a.bin_rec);
 #define OMR_CS_LOAD_ENTRIES(q)                                                 \
@@ -575,6 +644,11 @@ __global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
             p_ew[j] = a.ent_w[(q).e_lo + i_];                                  \
             p_gid[j] = a.ent_gid[(q).e_lo + i_];                               \
         }                                                                      \
+    }                                                                          \
+    _Pragma("unroll") for (int j = 0; j < GBP; ++j)                            \
+    {                                                                          \
+        const uint32_t x_ = tid + j * RB_THREADS;                              \
+        if (x_ < gx) p_gb[j] = a.hist_b[col_index((q), gx, x_)];               \
     }
 #define OMR_CS_LOAD_CONSTS(q)                                                  \
     _Pragma("unroll") for (int j = 0; j < PF; ++j)                             \
@@ -585,15 +659,16 @@ __global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
             p_bb[j] = bin_rec_v[2 * (size_t)p_gid[j] + 1];                     \
         }                                                                      \
     }
-    uint32_t c = blockIdx.x, it = 0;
+    const ChunkRange cr = xcd_chunks(C);
+    uint32_t c = cr.first, it = 0;
     ColChunk k = col_chunk(a, min(c, C - 1u));  // (C = 0: no iteration reads it)
-    if (c < C) {
+    if (c < cr.end) {
         OMR_CS_LOAD_ENTRIES(k)
         OMR_CS_LOAD_CONSTS(k)
     }
-    for (; c < C; c += gridDim.x, ++it) {
+    for (; c < cr.end; c += cr.step, ++it) {
         BSTAMP(it, 0);
-        const uint32_t cn = c + gridDim.x;
+        const uint32_t cn = c + cr.step;
         const ColChunk kn = col_chunk(a, min(cn, C - 1u));  // the next chunk's descriptor, in flight meanwhile
         const bool staged = k.nr <= CB_OWN_CONST;  // chunk-uniform
         reinterpret_cast<uint4*>(s_own)[tid] = make_uint4(0u, 0u, 0u, 0u);
@@ -619,9 +694,11 @@ __global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
                 if (ex >= k.s0) s_own[ex - k.s0] = (uint16_t)i;
             }
         }
-        for (uint32_t x = tid; x < gx; x += RB_THREADS) s_gbase[x] = a.hist_b[col_index(k, gx, x)];
+#pragma unroll
+        for (int j = 0; j < GBP; ++j)
+            if (tid + j * RB_THREADS < gx) s_gbase[tid + j * RB_THREADS] = p_gb[j];
         __syncthreads();
-        if (cn < C) {
+        if (cn < cr.end) {
             OMR_CS_LOAD_ENTRIES(kn)
         }
         BSTAMP(it, 1);
@@ -631,7 +708,7 @@ __global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
         bool valid[RB_ROUNDS];
         if (staged) col_expand<true>(a, k, s_own, s_xoff, s_bc, row_valid, d, val, valid);
         else col_expand<false>(a, k, s_own, s_xoff, s_bc, row_valid, d, val, valid);
-        if (cn < C) {
+        if (cn < cr.end) {
             OMR_CS_LOAD_CONSTS(kn)
         }
         BSTAMP(it, 3);

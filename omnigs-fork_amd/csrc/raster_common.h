@@ -363,6 +363,25 @@ __device__ __forceinline__ uint32_t mask_rank(uint64_t mask)
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// The lanes of this wave whose BITS-bit digit equals this lane's (and that are valid): one ballot per bit, each
+// folded in as peers &= ~(m ^ s) with s = the bit sign-extended (0 or ~0) — 6 VALU per bit on two 32-bit halves,
+// against 11 for the `bit ? m : ~m` select the compiler builds through 64-bit masks (the ranks of the binning
+// scatters and the radix downsweeps, sort.hip / bin.hip).
+template <int BITS>
+__device__ __forceinline__ uint64_t wave_match_digit(uint32_t d, bool valid)
+{
+    const uint64_t v = __ballot(valid);
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#pragma unroll
+    for (int b = 0; b < BITS; ++b) {
+        const uint32_t sx = (uint32_t)((int32_t)(d << (31 - b)) >> 31);  // v_bfe_i32
+        const uint64_t m = __ballot(sx != 0u);
+        lo &= ~((uint32_t)m ^ sx);
+        hi &= ~((uint32_t)(m >> 32) ^ sx);
+    }
+    return ((uint64_t)hi << 32) | lo;
+}
+
 #endif  // __HIPCC__
 
 }  // namespace omr

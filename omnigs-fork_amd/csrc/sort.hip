@@ -478,13 +478,7 @@ __global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const K* keys_
     for (int r = 0; r < ROUNDS; ++r) {
         const bool valid = base + 64 * r < n;
         const uint32_t d = (k[r] >> shift) & (RADIX - 1);
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < RADIX_BITS; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t m = __ballot(bit);
-            peers &= bit ? m : ~m;
-        }
+        const uint64_t peers = wave_match_digit<RADIX_BITS>(d, valid);
         const uint32_t rank = mask_rank(peers);
         const uint32_t prev = valid ? s_whist[w][d] : 0u;
         lr[r] = prev + rank;
@@ -661,13 +655,7 @@ __global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, 
     for (int r = 0; r < ROUNDS; ++r) {
         const bool valid = base + 64 * r < n;
         const uint32_t d = (k[r] >> shift) & (RADIX - 1);
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < RADIX_BITS; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t m = __ballot(bit);
-            peers &= bit ? m : ~m;
-        }
+        const uint64_t peers = wave_match_digit<RADIX_BITS>(d, valid);
         const uint32_t rank = mask_rank(peers);
         const uint32_t prev = valid ? s_whist[w][d] : 0u;
         lr[r] = prev + rank;

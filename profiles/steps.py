@@ -16,7 +16,8 @@ def timeline(d):
     t0 = int(rows[i0]["Start_Timestamp"])
     for r in rows[i0:i1]:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        name = re.sub(r"\(.*", "", r["Kernel_Name"]).split("::")[-1][:44]
+        m = re.findall(r"(\w+)(?:<[^<>]*>)?\(", r["Kernel_Name"])
+        name = (m[-1] if m else r["Kernel_Name"])[:44]
         print(f'{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f}  {name:44s} grid={r["Grid_Size_X"]} lds={r["LDS_Block_Size"]} '
               f'vgpr={r["VGPR_Count"]}')
 
