@@ -49,6 +49,9 @@ def parse():
                    help="N > 1 gradient exchange: compact = all-reduce of the 44 B/G non-SH gradients + all-gather of "
                         "12 B/G colour gradients and an SH rebuild (parallel.allreduce_compact_); flat = one "
                         "all-reduce of all 236 B/G")
+    p.add_argument("--ar-chunks", type=int, default=1,
+                   help="compact exchange: all-reduce the 44 B/G gradients per Gaussian range, each as soon as the "
+                        "backward finishes it (1 = one all-reduce after the backward; DESIGN.md §6)")
     p.add_argument("--boundary", choices=["ctypes", "libtorch"], default="ctypes",
                    help="ctypes: Python host on the C ABI (writes grads into the flat all-reduce buffer); libtorch: "
                         "the rasterize_points.h drop-in (librasterize_points.so) through its pybind module")
@@ -329,7 +332,7 @@ def main():
     if world > 1 and args.exchange == "compact":
         cx = par.CompactExchange(grads, info, campos,
                                  lambda pk, out: R.sh_grad_from_colors_packed(means3D, shs, g.sh_degree, pk, out=out),
-                                 dev, overlap=LT is None, any_backend=args.rehearse)
+                                 dev, overlap=LT is None, any_backend=args.rehearse, ar_chunks=args.ar_chunks)
     bwd_kwargs = cx.backward_kwargs() if cx is not None else {}
 
     def exchange():
@@ -522,7 +525,9 @@ def main():
                    "P": P, "V": V, "L": L, "N": N, "T": T, "width": W, "height": H, "row_slots": rows_slots,
                    "binning": "rows then columns (bin.hip)" if rows_slots is not None else "emit + radix tile sort",
                    "parallelism": f"view-parallel dp{world}", "boundary": args.boundary,
-                   "exchange": args.exchange if world > 1 else None, "ambiguous": ambiguous},
+                   "exchange": args.exchange if world > 1 else None,
+                   "ar_chunks": args.ar_chunks if world > 1 and args.exchange == "compact" else None,
+                   "ambiguous": ambiguous},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": d["achieved_GBps"], "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": d["frac"], "traffic": d["traffic"],
                      "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],

@@ -120,6 +120,13 @@ int omr_forward_status(char* geom_buffer, int P, void* stream);
  * view-parallel host starts the all-gather of the colour gradients on another stream waiting on that event, so the
  * collective overlaps the rest of the backward. NULL clears a pending event. */
 void omr_backward_colors_event(void* event);
+/* The next omr_*_backward call on this thread runs the per-Gaussian backward (gaussian_bwd) as n launches over the
+ * Gaussian ranges [omr_backward_chunk_begin(P, n, k), omr_backward_chunk_begin(P, n, k + 1)) and records events[k]
+ * (hipEvent_t) on its stream after range k, then forgets them: a view-parallel host all-reduces each range's xyz /
+ * opacity / scale / rotation gradients as soon as they are final. n = 0 or events = NULL clears. */
+void omr_backward_chunk_events(int n, void* const* events);
+/* First Gaussian of range k of n (a multiple of 256; 0 for k <= 0, P for k >= n). */
+int omr_backward_chunk_begin(int P, int n, int k);
 /* dL_dsh [P,M,3] = sum over nviews views of the SH gradient the backward computes for each, rebuilt from each
  * view's dL_dcolors ([nviews][P][3], RasterizeGaussiansBackwardCUDA's second output) and camera position
  * (campos [nviews][3]) with the backward's own SH arithmetic. Lets view-parallel ranks exchange 12 B per

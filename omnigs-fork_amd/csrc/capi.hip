@@ -78,6 +78,9 @@ __global__ __launch_bounds__(256) void debug_point_ids_kernel(const uint32_t* li
 thread_local std::string g_last_error;
 // omr_backward_colors_event: recorded by this thread's next backward once dL_dcolor is final, then cleared
 thread_local hipEvent_t t_colors_event = nullptr;
+// omr_backward_chunk_events: the next backward on this thread runs gaussian_bwd over that many Gaussian ranges and
+// records one event after each (omr_backward_chunk_begin gives the ranges), then forgets them
+thread_local std::vector<hipEvent_t> t_chunk_events;
 
 int fail(int code, const std::string& msg)
 {
@@ -648,6 +651,8 @@ int backward_impl(const BackwardIn& in)
 {
     const hipEvent_t colors_event = t_colors_event;  // omr_backward_colors_event applies to this call only
     t_colors_event = nullptr;
+    std::vector<hipEvent_t> chunk_events;  // omr_backward_chunk_events: likewise
+    chunk_events.swap(t_chunk_events);
     g_last_error.clear();
     if (in.camera_type != CAM_PINHOLE && in.camera_type != CAM_LONLAT)
         return fail(OMR_ERR_CAMERA_TYPE, "[CudaRasterizer]Invalid camera_type");
@@ -725,9 +730,21 @@ int backward_impl(const BackwardIn& in)
                         b.row_valid, (uint32_t)in.R, g.row_sums, in.dL_dcolor, s);
     }
     if (colors_event) OMR_HIP(hipEventRecord(colors_event, s));  // dL_dcolor is final from here on
-    ga.g_begin = 0;
-    ga.g_end = in.P;
-    { StageScope st_(ST_GAUSS_BWD, s, true); launch_gaussian_backward(in.camera_type, ga, s, st_.start(), st_.stop()); }
+    if (chunk_events.empty()) {
+        ga.g_begin = 0;
+        ga.g_end = in.P;
+        StageScope st_(ST_GAUSS_BWD, s, true);
+        launch_gaussian_backward(in.camera_type, ga, s, st_.start(), st_.stop());
+    } else {  // Gaussian ranges, an event after each: a view-parallel host reduces each range as soon as it is final
+        const int nch = (int)chunk_events.size();
+        StageScope st_(ST_GAUSS_BWD, s);
+        for (int k = 0; k < nch; ++k) {
+            ga.g_begin = omr_backward_chunk_begin(in.P, nch, k);
+            ga.g_end = omr_backward_chunk_begin(in.P, nch, k + 1);
+            launch_gaussian_backward(in.camera_type, ga, s, nullptr, nullptr);
+            OMR_HIP(hipEventRecord(chunk_events[k], s));
+        }
+    }
     if (int e = hip_check("backward")) return e;
     OMR_HIP(timed_wait(hs->bwd, s, RS_BWD_WAIT_NS));
     if (hs->words[4] != 0) {
@@ -746,6 +763,17 @@ extern "C" {
 
 int omr_abi_version(void) { return OMR_ABI_VERSION; }
 void omr_backward_colors_event(void* event) { t_colors_event = static_cast<hipEvent_t>(event); }
+void omr_backward_chunk_events(int n, void* const* events)
+{
+    t_chunk_events.clear();
+    for (int k = 0; k < n && events; ++k) t_chunk_events.push_back(static_cast<hipEvent_t>(events[k]));
+}
+int omr_backward_chunk_begin(int P, int n, int k)
+{
+    if (n <= 0 || k <= 0) return 0;
+    if (k >= n) return std::max(P, 0);
+    return (int)((int64_t)std::max(P, 0) * k / n / 256 * 256);  // multiples of 256 (gaussian_bwd's wave layout)
+}
 const char* omr_last_error(void) { return g_last_error.c_str(); }
 
 int omr_rasterizer_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -26,6 +26,9 @@ Two exchanges give the same summed gradients (up to the order of the float addit
                         dL_dcolors before the per-Gaussian backward runs, the backward records an event there
                         (omr_backward_colors_event), and the colour all-gather starts on a side stream as soon as it
                         fires; the per-view dL_dsh is not written at all (skip_dsh), since the rebuild replaces it.
+                        ar_chunks = k > 1 also pipelines the 44 B/G all-reduce: the per-Gaussian backward runs over k
+                        Gaussian ranges with an event after each (omr_backward_chunk_events) and each range is
+                        reduced on the side stream once final.
 """
 from __future__ import annotations
 
@@ -144,7 +147,7 @@ class CompactExchange:
     each step's campos: the SH rebuild evaluates the view directions from it."""
 
     def __init__(self, buf: GradBuffer, info: DistInfo, campos: torch.Tensor, rebuild_packed, device,
-                 overlap: bool = True, any_backend: bool = False):
+                 overlap: bool = True, any_backend: bool = False, ar_chunks: int = 1):
         self.buf, self.info, self.rebuild_packed = buf, info, rebuild_packed
         P = buf.P
         buf.out_dict(device)  # creates colors_ext [P + 1, 3]
@@ -156,6 +159,16 @@ class CompactExchange:
             self.event = torch.cuda.Event()
             self.comm = torch.cuda.Stream(device)
             self.packed_all = torch.empty((info.world_size, P + 1, 3), dtype=buf.colors_ext.dtype, device=device)
+        # ar_chunks > 1: the 44 B/G all-reduce runs per Gaussian range on the side stream behind the colour all-gather,
+        # each range as soon as the backward's per-Gaussian kernel has finished it (chunk events; DESIGN.md §6 on
+        # when that can pay)
+        self.ar_chunks = int(ar_chunks) if self.overlap else 1
+        self.chunk_events, self.ranges = [], []
+        if self.ar_chunks > 1:
+            from . import rasterizer as _R  # the ranges the library uses (omr_backward_chunk_begin)
+
+            self.chunk_events = [torch.cuda.Event() for _ in range(self.ar_chunks)]
+            self.ranges = _R.backward_chunk_ranges(P, self.ar_chunks)
 
     def set_campos(self, campos: torch.Tensor):
         """This step's camera position: stream-ordered copy into row P of the gathered tensor (current stream)."""
@@ -167,7 +180,12 @@ class CompactExchange:
         (None = unchanged since the last step). Call before queueing the backward."""
         if campos is not None:
             self.set_campos(campos)
-        return dict(colors_event=self.event, skip_dsh=True) if self.overlap else {}
+        if not self.overlap:
+            return {}
+        kw = dict(colors_event=self.event, skip_dsh=True)
+        if self.chunk_events:
+            kw["chunk_events"] = self.chunk_events
+        return kw
 
     def start(self):
         if not self.overlap:
@@ -178,6 +196,11 @@ class CompactExchange:
                 dist.all_gather_into_tensor(self.packed_all, self.buf.colors_ext)
             else:  # gloo: list form
                 dist.all_gather(list(self.packed_all.unbind(0)), self.buf.colors_ext)
+            for ev, (b, e) in zip(self.chunk_events, self.ranges):  # ar_chunks > 1: each range once it is final
+                self.comm.wait_event(ev)
+                if e > b:
+                    for name in SEGMENTS[:4]:
+                        dist.all_reduce(self.buf.views[name][b:e], op=dist.ReduceOp.SUM)
 
     def finish(self):
         if not self.info.enabled:
@@ -186,6 +209,7 @@ class CompactExchange:
             allreduce_compact_(self.buf, self.info, self.buf.colors_ext[:self.buf.P], self.campos, None,
                                rebuild_packed=self.rebuild_packed)
             return
-        dist.all_reduce(self.buf.flat[:REDUCED_FLOATS * self.buf.P], op=dist.ReduceOp.SUM)
+        if not self.chunk_events:
+            dist.all_reduce(self.buf.flat[:REDUCED_FLOATS * self.buf.P], op=dist.ReduceOp.SUM)
         torch.cuda.current_stream().wait_stream(self.comm)
         self.rebuild_packed(self.packed_all, out=self.buf.views["dL_dsh"])

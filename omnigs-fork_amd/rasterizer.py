@@ -63,6 +63,10 @@ def lib() -> C.CDLL:
         L.omr_forward_status.argtypes = [vp, i, vp]
         L.omr_backward_colors_event.argtypes = [vp]
         L.omr_backward_colors_event.restype = None
+        L.omr_backward_chunk_events.argtypes = [i, vp]
+        L.omr_backward_chunk_events.restype = None
+        L.omr_backward_chunk_begin.argtypes = [i, i, i]
+        L.omr_backward_chunk_begin.restype = i
         L.omr_debug_point_list.argtypes = [vp, i, i, i, vp, vp]
         L.omr_debug_ranges.argtypes = [vp, i, i, vp, vp]
         L.omr_debug_image_state.argtypes = [vp, i, i, vp, vp, vp]
@@ -219,10 +223,17 @@ def RasterizeGaussiansCUDA(background, means3D, colors, opacity, scales, rotatio
     return int(nr.value), out_color, radii, geom.tensor, binning.tensor, img.tensor
 
 
+def backward_chunk_ranges(P, n):
+    """The Gaussian ranges [begin, end) of a backward run with n chunk events (omr_backward_chunk_begin)."""
+    L = lib()
+    b = [int(L.omr_backward_chunk_begin(int(P), int(n), k)) for k in range(int(n) + 1)]
+    return [(b[k], b[k + 1]) for k in range(int(n))]
+
+
 def RasterizeGaussiansBackwardCUDA(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp,
                                    viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos,
                                    geomBuffer, R, binningBuffer, imageBuffer, camera_type=CAMERA_PINHOLE, out=None,
-                                   colors_event=None, skip_dsh=False):
+                                   colors_event=None, skip_dsh=False, chunk_events=None):
     """rasterize_points.cu:166-285. Returns (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh,
     dL_dscales, dL_drotations).
 
@@ -232,7 +243,9 @@ def RasterizeGaussiansBackwardCUDA(background, means3D, radii, colors, scales, r
       `colors_event` a torch.cuda.Event recorded on the stream as soon as dL_dcolors is final (after the row sums,
                      before the per-Gaussian backward): the colour all-gather can wait on it and overlap the rest;
       `skip_dsh`     dL_dsh is not written (returned as None): the compact exchange rebuilds the summed SH gradient
-                     from the gathered colour gradients, so the per-view one would be overwritten unread."""
+                     from the gathered colour gradients, so the per-view one would be overwritten unread;
+      `chunk_events` a list of n torch.cuda.Events: the per-Gaussian backward runs over the n Gaussian ranges of
+                     backward_chunk_ranges(P, n) and event k is recorded once range k's gradients are final."""
     if camera_type not in (CAMERA_PINHOLE, CAMERA_LONLAT):
         raise RasterizerError("[CudaRasterizer]Invalid camera_type")
     dev = means3D.device
@@ -266,6 +279,12 @@ def RasterizeGaussiansBackwardCUDA(background, means3D, radii, colors, scales, r
             if colors_event.cuda_event == 0:  # torch creates the HIP event at its first record
                 colors_event.record(torch.cuda.current_stream(dev))
             L.omr_backward_colors_event(C.c_void_p(colors_event.cuda_event))
+        if chunk_events:
+            for ev in chunk_events:
+                if ev.cuda_event == 0:
+                    ev.record(torch.cuda.current_stream(dev))
+            arr = (C.c_void_p * len(chunk_events))(*[ev.cuda_event for ev in chunk_events])
+            L.omr_backward_chunk_events(len(chunk_events), arr)
         if camera_type == CAMERA_PINHOLE:
             pm = _dev_f32(projmatrix, "projmatrix")
             rc = L.omr_rasterizer_backward(P, int(degree), M, int(R), _ptr(a["bg"]), W, H, _ptr(a["m"]), _ptr(a["shc"]),

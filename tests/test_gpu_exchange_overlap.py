@@ -22,7 +22,7 @@ def _case(view):
     return make_case(6000, 256, 128, scene.CAMERA_LONLAT, 23, view_index=view, spread=2.0)
 
 
-def _worker(rank, world, port, q, move_view=False):
+def _worker(rank, world, port, q, move_view=False, ar_chunks=1):
     import torch
     import torch.distributed as dist
 
@@ -45,8 +45,8 @@ def _worker(rank, world, port, q, move_view=False):
         out = buf.out_dict(dev)
         cx = par.CompactExchange(buf, par.DistInfo(rank, world, 0), cp,
                                  lambda pk, out: R.sh_grad_from_colors_packed(m, sh, g.sh_degree, pk, out=out), dev,
-                                 any_backend=True)
-        assert cx.overlap
+                                 any_backend=True, ar_chunks=ar_chunks)
+        assert cx.overlap and cx.ar_chunks == ar_chunks
         for step in range(2):  # twice: the event and the buffers are reused across steps
             if move_view and step == 1:  # the second step renders another viewpoint (rank + 2): campos changes
                 g, cam, dL = _case(rank + 2)
@@ -66,13 +66,13 @@ def _worker(rank, world, port, q, move_view=False):
         dist.destroy_process_group()
 
 
-def _run(move_view):
+def _run(move_view, ar_chunks=1):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, move_view)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, move_view, ar_chunks)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in procs)
@@ -104,3 +104,14 @@ def test_overlapped_exchange_follows_a_moving_camera():
     """the gathered camera position must be each step's (the SH rebuild evaluates view directions from
     it); the second step renders other viewpoints and must equal the per-view sums of THAT step bitwise."""
     _run(move_view=True)
+
+
+def test_pipelined_all_reduce_over_gaussian_ranges_sums_views_bitwise():
+    """ar_chunks = 3 runs the per-Gaussian backward over three Gaussian ranges (omr_backward_chunk_
+    events) and all-reduces each range's 44 B/G on the side stream as soon as its event fires; the replicas must
+    equal the per-view sums bit for bit, as with one all-reduce."""
+    import _omnigs
+
+    ranges = _omnigs.load().rasterizer.backward_chunk_ranges(6000, 3)
+    assert ranges == [(0, 1792), (1792, 3840), (3840, 6000)]  # multiples of 256, covering [0, P)
+    _run(move_view=True, ar_chunks=3)
