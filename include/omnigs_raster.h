@@ -245,6 +245,9 @@ void omr_runtime_stats_reset(void);
 /* --- introspection for tests / tools (read from the private scratch layout) ---------------------- */
 /* copies the sorted per-instance Gaussian indices (R entries) and tile ranges ([T] uint2) to device dst */
 int omr_debug_point_list(char* binning_buffer, int R, int width, int height, uint32_t* dst, void* stream);
+/* The point list's raw entries [R]: Gaussian index in the low 28 bits, the instance's band mask (the 16x4 bands of its
+ * tile the alpha >= 1/255 ellipse can reach) in the top 4. Diagnostic (tests/test_gpu_parity.py checks the masks). */
+int omr_debug_point_list_raw(char* binning_buffer, int R, int width, int height, uint32_t* dst, void* stream);
 int omr_debug_ranges(char* image_buffer, int width, int height, uint32_t* dst, void* stream);
 /* per-pixel final transmittance [N] f32 and contributor count [N] u32 */
 int omr_debug_image_state(char* image_buffer, int width, int height, float* final_T, uint32_t* n_contrib, void* stream);

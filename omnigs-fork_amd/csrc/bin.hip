@@ -46,7 +46,7 @@ static_assert(RB_N == BIN_CHUNK, "launch_forward_scans cuts the rows pass's chun
 constexpr int RB_WAVES = RB_THREADS / 64;
 constexpr int RB_PER_WAVE = RB_N / RB_WAVES;
 constexpr int RB_ROUNDS = RB_PER_WAVE / 64;
-// columns pass: owners whose band constants are staged in LDS (1024: config C's chunks, ~600 owners, all staged;
+// columns pass: owners whose band intervals are staged in LDS (1024: config C's chunks, ~600 owners, all staged;
 // 512 measured 0.26 ms slower at config E)
 constexpr uint32_t CB_OWN_CONST = 1024;
 // grid caps of the grid-stride chunk kernels (256 CUs: 8 resident hist blocks, 4 scatter blocks of <= 40 KiB LDS each)
@@ -569,11 +569,12 @@ __global__ __launch_bounds__(RB_THREADS) void cols_hist_kernel(BinArgs a)
 }
 
 // the slots of one round: column, point-list word (Gaussian | band mask << PL_GID_BITS); STAGED: every owner's band
-// constants are in LDS (a chunk-uniform choice, so the loads stay plain LDS reads)
+// intervals and Gaussian are in LDS (a chunk-uniform choice, so the loads stay plain LDS reads), else each slot derives
+// its owner's intervals from bin_rec itself
 template <bool STAGED>
 __device__ __forceinline__ void col_expand(const BinArgs& a, const ColChunk& k, const uint16_t* s_own,
-                                           const uint32_t* s_xoff, const float4* s_bc, uint8_t* row_valid,
-                                           uint32_t (&d)[RB_ROUNDS], uint32_t (&val)[RB_ROUNDS],
+                                           const uint32_t* s_xoff, const uint4* s_iv, const uint32_t* s_gid,
+                                           uint8_t* row_valid, uint32_t (&d)[RB_ROUNDS], uint32_t (&val)[RB_ROUNDS],
                                            bool (&valid)[RB_ROUNDS])
 {
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
@@ -586,21 +587,17 @@ __device__ __forceinline__ void col_expand(const BinArgs& a, const ColChunk& k, 
         if (valid[r]) {
             const uint32_t o = s_own[j];
             const uint32_t x = s + s_xoff[o];
-            float4 ba, bb;
+            uint4 iv;
             uint32_t gid;
             if (STAGED) {
-                ba = s_bc[2 * o];
-                bb = s_bc[2 * o + 1];
-                gid = __builtin_bit_cast(uint32_t, bb.w);
+                iv = s_iv[o];
+                gid = s_gid[o];
             } else {
                 gid = a.ent_gid[k.e_lo + o];
-                ba = a.bin_rec[2 * (size_t)gid];
-                bb = a.bin_rec[2 * (size_t)gid + 1];
+                iv = band_row_intervals(a.bin_rec[2 * (size_t)gid], a.bin_rec[2 * (size_t)gid + 1], k.y, 0u, a.gx);
             }
-            const BandSpan sp = {ba.z, ba.w, bb.x, bb.y, bb.z};
-            const uint32_t m = band_mask_span<PL_BANDS>(sp, make_float2(ba.x, ba.y), x, k.y);
             d[r] = x;
-            val[r] = gid | (m << PL_GID_BITS);
+            val[r] = gid | (band_mask_of_intervals(iv, x) << PL_GID_BITS);
             row_valid[s] = 0;
         }
     }
@@ -609,14 +606,16 @@ __device__ __forceinline__ void col_expand(const BinArgs& a, const ColChunk& k, 
 template <int BITS>
 __global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
 {
-    // phase 1 (expansion): per owner, x0 minus its first instance slot (slot s is column s + s_xoff), and the band
-    // constants of the owners when they fit (bin_rec, the Gaussian in the second record's .w); phase 2 (write-out):
-    // the slots' point-list words and columns in column order, in the same storage
-    constexpr size_t PH1 = RB_N * sizeof(uint32_t) + 2 * CB_OWN_CONST * sizeof(float4);
+    // phase 1 (expansion): per owner, x0 minus its first instance slot (slot s is column s + s_xoff), and, when the
+    // owners fit, each one's reachable columns per band of this row (band_row_intervals: computed once per row entry,
+    // not once per instance) and its Gaussian; phase 2 (write-out): the slots' point-list words and columns in column
+    // order, in the same storage
+    constexpr size_t PH1 = RB_N * sizeof(uint32_t) + CB_OWN_CONST * (sizeof(uint4) + sizeof(uint32_t));
     constexpr size_t PH2 = RB_N * (sizeof(uint32_t) + sizeof(uint16_t));
-    __shared__ float4 s_raw[(PH1 > PH2 ? PH1 : PH2) / sizeof(float4)];
-    float4* s_bc = s_raw;
-    uint32_t* s_xoff = reinterpret_cast<uint32_t*>(s_raw + 2 * CB_OWN_CONST);
+    __shared__ uint4 s_raw[(PH1 > PH2 ? PH1 : PH2) / sizeof(uint4)];
+    uint4* s_iv = s_raw;
+    uint32_t* s_gid = reinterpret_cast<uint32_t*>(s_raw + CB_OWN_CONST);
+    uint32_t* s_xoff = s_gid + CB_OWN_CONST;
     __shared__ __attribute__((aligned(16))) uint16_t s_own[RB_N];
     __shared__ uint32_t s_whist[RB_WAVES][1 << BITS];
     __shared__ uint32_t s_dstart[1 << BITS];
@@ -626,10 +625,11 @@ __global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
     const uint32_t L = live_L(a.counters, a.cap);
     uint8_t* row_valid = reinterpret_cast<uint8_t*>(a.binning + row_valid_offset(L));  // the backward's row map
     uint32_t* point_list = reinterpret_cast<uint32_t*>(a.binning + canonical_list_offset(L));
-    // software pipeline: the next chunk's descriptor, count bases, staged owners' entries and band constants are
-    // loaded into registers while the current chunk is expanded and ranked (PF owners per thread)
-    constexpr int PF = CB_OWN_CONST / RB_THREADS;
-    static_assert(PF * RB_THREADS == CB_OWN_CONST, "staged owners: whole rounds of the block");
+    // software pipeline: the next chunk's descriptor, count bases and its first PF x 256 owners' entries and band
+    // constants are loaded into registers while the current chunk is expanded and ranked (more would cost the VGPRs
+    // of a fourth block per CU); staged owners past those are loaded when staged
+    constexpr int PF = 2;
+    static_assert(PF * RB_THREADS <= CB_OWN_CONST, "prefetched owners are staged owners");
     typedef float f4v __attribute__((ext_vector_type(4)));  // native vectors: the prefetch stays in registers
     constexpr int GBP = (1 << BITS) / RB_THREADS;  // the chunk's per-column count bases, per thread
     uint32_t p_ex[PF], p_ew[PF], p_gid[PF], p_gb[GBP];
@@ -680,11 +680,18 @@ __global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
                 if (i < k.nr) {
                     s_xoff[i] = (p_ew[j] >> 16) - p_ex[j];  // modular
                     if (p_ex[j] >= k.s0) s_own[p_ex[j] - k.s0] = (uint16_t)i;  // distinct first slots (width >= 1)
-                    f4v bb = p_bb[j];
-                    bb.w = __builtin_bit_cast(float, p_gid[j]);
-                    reinterpret_cast<f4v*>(s_bc)[2 * i] = p_ba[j];
-                    reinterpret_cast<f4v*>(s_bc)[2 * i + 1] = bb;
+                    const f4v ba = p_ba[j], bb = p_bb[j];
+                    s_iv[i] = band_row_intervals(make_float4(ba.x, ba.y, ba.z, ba.w), make_float4(bb.x, bb.y, bb.z, bb.w),
+                                                 k.y, 0u, gx);
+                    s_gid[i] = p_gid[j];
                 }
+            }
+            for (uint32_t i = tid + PF * RB_THREADS; i < k.nr; i += RB_THREADS) {
+                const uint32_t e = k.e_lo + i, ex = a.ent_ex[e], gid = a.ent_gid[e];
+                s_xoff[i] = (a.ent_w[e] >> 16) - ex;
+                if (ex >= k.s0) s_own[ex - k.s0] = (uint16_t)i;
+                s_iv[i] = band_row_intervals(a.bin_rec[2 * (size_t)gid], a.bin_rec[2 * (size_t)gid + 1], k.y, 0u, gx);
+                s_gid[i] = gid;
             }
         } else {
             for (uint32_t i = tid; i < k.nr; i += RB_THREADS) {
@@ -706,8 +713,8 @@ __global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
         BSTAMP(it, 2);
         uint32_t d[RB_ROUNDS], val[RB_ROUNDS], lp[RB_ROUNDS];
         bool valid[RB_ROUNDS];
-        if (staged) col_expand<true>(a, k, s_own, s_xoff, s_bc, row_valid, d, val, valid);
-        else col_expand<false>(a, k, s_own, s_xoff, s_bc, row_valid, d, val, valid);
+        if (staged) col_expand<true>(a, k, s_own, s_xoff, s_iv, s_gid, row_valid, d, val, valid);
+        else col_expand<false>(a, k, s_own, s_xoff, s_iv, s_gid, row_valid, d, val, valid);
         if (cn < cr.end) {
             OMR_CS_LOAD_CONSTS(kn)
         }

@@ -1187,6 +1187,18 @@ int omr_debug_point_list(char* binning_buffer, int R, int width, int height, uin
     return hip_check("debug_point_list");
 }
 
+int omr_debug_point_list_raw(char* binning_buffer, int R, int width, int height, uint32_t* dst, void* stream)
+{
+    g_last_error.clear();
+    if (R <= 0) return OMR_OK;
+    const Dims d = dims(width, height);
+    BinningState b;
+    BinningState::carve(binning_buffer, (size_t)R, d.gx, d.gy, &b);
+    OMR_HIP(hipMemcpyAsync(dst, b.point_list, (size_t)R * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                           (hipStream_t)stream));
+    return hip_check("debug_point_list_raw");
+}
+
 int omr_debug_ranges(char* image_buffer, int width, int height, uint32_t* dst, void* stream)
 {
     g_last_error.clear();

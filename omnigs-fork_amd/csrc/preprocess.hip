@@ -268,9 +268,10 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
                                        x0)
                           : make_uint2(0u, 0u);
         if (vis) {  // the binning's band-mask constants (bin.hip: the columns pass reads them per (Gaussian, row))
-            const BandSpan sp = band_span_consts(band_consts(o.rec[1]));
-            g.bin_rec[2 * (size_t)idx] = make_float4(o.rec[0].x, o.rec[0].y, sp.kDt, sp.ak);
-            g.bin_rec[2 * (size_t)idx + 1] = make_float4(sp.adt, sp.At, sp.invA, __builtin_bit_cast(float, x0 | (wd << 16)));
+            float4 r0, r1;
+            band_row_consts(band_consts(o.rec[1]), make_float2(o.rec[0].x, o.rec[0].y), r0, r1);
+            g.bin_rec[2 * (size_t)idx] = r0;
+            g.bin_rec[2 * (size_t)idx + 1] = r1;
         }
         g.key_a[idx] = vis ? __float_as_uint(o.depth) : 0xFFFFFFFFu;  // culled Gaussians sort last, emit nothing
         g.val_a[idx] = (uint32_t)idx;

@@ -117,8 +117,8 @@ struct GeomState {
     uint2* drect;             // the rect words in depth order (launch_forward_scans, row path)
     uint32_t* row_offsets;    // inclusive scan of the rect rows in depth order (launch_forward_scans, row path)
     uint2* desc_r;            // [P / 2 + 2] first / last owner rank of each row-binning chunk (launch_forward_scans)
-    float4* bin_rec;          // [P][2] {x, y, kDt, ak}, {adt, At, invA, x0 | rect width << 16}: the band-mask
-                              // constants (band_span_consts) the binning's columns pass needs per (Gaussian, row)
+    float4* bin_rec;          // [P][2] {x, y, k, dd}, {1/a, t, dyR, Dt} (band_row_consts): the constants the binning's
+                              // columns pass turns into each (Gaussian, row)'s reachable columns per band
     int* internal_radii;      // used when the caller passes radii == NULL (rasterizer_impl.cu:284-287)
 
     static size_t carve(char* base, size_t P, GeomState* s);
@@ -340,6 +340,59 @@ __device__ __forceinline__ uint32_t band_mask_span(const BandSpan& sp, float2 xy
     for (int b = 0; b < NB; ++b)
         if (dy0 - (float)(4 * b + 3) <= y2 && dy0 - (float)(4 * b) >= y1) m |= 1u << b;
     return m;
+}
+
+// The same question posed per (Gaussian, tile row) for the row binning's columns pass (bin.hip): for each band b of
+// tile row ty, the tile columns x whose strip [16x, 16x + 15] meets the ellipse {q <= t} inside the band's slab of
+// pixel rows, as an interval. Restricted to the slab dy in S = [dy0 - 4b - 3, dy0 - 4b] ∩ [-Dt, Dt] (Dt = sqrt(t /
+// dd)), the ellipse a (dx - k dy)^2 + dd dy^2 <= t spans dx from the minimum over S of k dy - sqrt((t - dd dy^2) /
+// a) to the maximum of k dy + sqrt(...): the right edge is concave with its top at dyR = k sqrt(a t / (dd A)), A =
+// a k^2 + dd, so its maximum over S is at dyR clamped to S; the left edge is the mirror image (-dyR). "The ellipse
+// meets strip x slab" is band_mask_span's question answered per slab instead of per strip, so it is likewise a
+// superset of band_mask_of's per-row test; the extent is widened by 0.02 px + 2e-6 |X| against rounding, so a
+// render kernel never skips a pixel it would blend (tests/test_gpu_parity.py checks the masks against every pixel).
+// Per-Gaussian constants (preprocess -> bin_rec): {x, y, k, dd}, {1/a, t, dyR, Dt}; t = -inf: no band, +inf: every.
+__device__ __forceinline__ void band_row_consts(const BandConsts& bc, float2 xy, float4& r0, float4& r1)
+{
+    if (!(bc.t > -__builtin_inff() && bc.t < __builtin_inff())) {
+        r0 = make_float4(xy.x, xy.y, 0.f, 0.f);
+        r1 = make_float4(0.f, bc.t, 0.f, 0.f);
+        return;
+    }
+    const float A = __builtin_fmaf(bc.a * bc.k, bc.k, bc.dd);
+    r0 = make_float4(xy.x, xy.y, bc.k, bc.dd);
+    r1 = make_float4(1.0f / bc.a, bc.t, bc.k * sqrtf(bc.a * bc.t / (bc.dd * A)), sqrtf(bc.t / bc.dd));
+}
+// per band b: the reachable tile columns of tile row ty as xa | count << 16 (count 0: none), clipped to [x_lo, x_hi)
+__device__ __forceinline__ uint4 band_row_intervals(float4 r0, float4 r1, uint32_t ty, uint32_t x_lo, uint32_t x_hi)
+{
+    const float mx = r0.x, my = r0.y, k = r0.z, dd = r0.w, inv_a = r1.x, t = r1.y, dyR = r1.z, Dt = r1.w;
+    uint32_t out[4];
+    const uint32_t full = x_lo | ((x_hi - x_lo) << 16);
+    const float dy0 = my - (float)(ty * BLOCK_Y);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const float s_hi = fminf(dy0 - (float)(4 * b), Dt), s_lo = fmaxf(dy0 - (float)(4 * b + 3), -Dt);
+        const float da = __builtin_amdgcn_fmed3f(dyR, s_lo, s_hi), db = __builtin_amdgcn_fmed3f(-dyR, s_lo, s_hi);
+        const float ra = __builtin_amdgcn_sqrtf(fmaxf(t - dd * da * da, 0.0f) * inv_a);
+        const float rb = __builtin_amdgcn_sqrtf(fmaxf(t - dd * db * db, 0.0f) * inv_a);
+        float xmax = k * da + ra, xmin = k * db - rb;
+        xmax += 0.02f + 2e-6f * fabsf(xmax);
+        xmin -= 0.02f + 2e-6f * fabsf(xmin);
+        // strip x reaches [xmin, xmax] in dx = mx - px:  16 x + 15 >= mx - xmax  and  16 x <= mx - xmin
+        const float fa = ceilf((mx - xmax - 15.0f) * (1.0f / BLOCK_X)), fb = floorf((mx - xmin) * (1.0f / BLOCK_X));
+        const int xa = (int)fmaxf(fa, (float)x_lo), xb = (int)fminf(fb, (float)x_hi - 1.0f);
+        out[b] = (s_lo <= s_hi && xa <= xb) ? (uint32_t)xa | ((uint32_t)(xb - xa + 1) << 16) : 0u;
+    }
+    if (t == __builtin_inff()) out[0] = out[1] = out[2] = out[3] = full;  // degenerate conic: every band
+    if (t == -__builtin_inff()) out[0] = out[1] = out[2] = out[3] = 0u;   // 255 o < 1: no band
+    return make_uint4(out[0], out[1], out[2], out[3]);
+}
+// the band mask of tile column x from band_row_intervals' words
+__device__ __forceinline__ uint32_t band_mask_of_intervals(uint4 iv, uint32_t x)
+{
+    auto in = [&](uint32_t w) { return (x - (w & 0xFFFFu)) < (w >> 16) ? 1u : 0u; };
+    return in(iv.x) | (in(iv.y) << 1) | (in(iv.z) << 2) | (in(iv.w) << 3);
 }
 
 // Which of the bands band0 .. band0 + NB - 1 of tile (tx, ty) (band b = pixel rows 4b..4b+3 of the tile, 16

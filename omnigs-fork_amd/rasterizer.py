@@ -68,6 +68,7 @@ def lib() -> C.CDLL:
         L.omr_backward_chunk_begin.argtypes = [i, i, i]
         L.omr_backward_chunk_begin.restype = i
         L.omr_debug_point_list.argtypes = [vp, i, i, i, vp, vp]
+        L.omr_debug_point_list_raw.argtypes = [vp, i, i, i, vp, vp]
         L.omr_debug_ranges.argtypes = [vp, i, i, vp, vp]
         L.omr_debug_image_state.argtypes = [vp, i, i, vp, vp, vp]
         L.omr_debug_tile_cost.argtypes = [vp, i, i, vp, vp]
@@ -481,6 +482,15 @@ def debug_state(P, R, width, height, geomBuffer, binningBuffer, imgBuffer):
         _check(L.omr_debug_image_state(imgBuffer.data_ptr(), width, height, out["final_T"].data_ptr(),
                                        out["n_contrib"].data_ptr(), st), "debug_image_state")
     return out
+
+
+def debug_point_masks(R, width, height, binningBuffer) -> torch.Tensor:
+    """Each point-list entry's band mask (top 4 bits: the tile's 16x4 bands the instance can reach), int32 [R]."""
+    out = torch.empty((max(R, 0),), dtype=torch.int32, device=binningBuffer.device)
+    if R > 0:
+        _check(lib().omr_debug_point_list_raw(binningBuffer.data_ptr(), R, width, height, out.data_ptr(),
+                                              _stream(binningBuffer.device)), "debug_point_list_raw")
+    return (out >> 28) & 15
 
 
 def debug_tile_cost(width, height, imgBuffer) -> torch.Tensor:

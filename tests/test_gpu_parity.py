@@ -333,3 +333,49 @@ def test_tile_cost_bounds():
     assert (cost >= 0).all() and (cost[n == 0] == 0).all()
     assert (cost <= 4 * n).all()
     assert cost.sum() > 0
+
+
+def _band_mask_misses(h, g, cam):
+    """(instance, band) pairs whose point-list band mask is 0 although a pixel of that 16x4 band has alpha >= 1/255
+    (float64, the reference's formula: forward.cu:431-437), and the fraction of mask bits set."""
+    import torch
+
+    st = {k: to_np(v) for k, v in h["state"].items()}
+    masks = to_np(omr.rasterizer.debug_point_masks(h["L"], cam.width, cam.height, h["binning"]))
+    ids = st["point_list"].astype(np.int64)
+    ranges = st["ranges"].reshape(-1, 2).astype(np.int64)
+    gx = (cam.width + 15) // 16
+    xy = st["means2D"].astype(np.float64)
+    co = st["conic_opacity"].astype(np.float64)
+    tile = np.repeat(np.arange(len(ranges)), ranges[:, 1] - ranges[:, 0])
+    pos = np.concatenate([np.arange(a, b) for a, b in ranges if b > a]) if len(tile) else np.zeros(0, np.int64)
+    gid, msk = ids[pos], masks[pos]
+    tx, ty = (tile % gx) * 16, (tile // gx) * 16
+    misses = 0
+    lane = np.arange(64)
+    for b in range(4):
+        px = tx[:, None] + (lane % 16)[None, :]
+        py = ty[:, None] + 4 * b + (lane // 16)[None, :]
+        inside = (px < cam.width) & (py < cam.height)
+        dx = xy[gid, 0][:, None] - px
+        dy = xy[gid, 1][:, None] - py
+        a, bb, c, o = (co[gid, k][:, None] for k in range(4))
+        power = -0.5 * (a * dx * dx + c * dy * dy) - bb * dx * dy
+        alpha = np.minimum(0.99, o * np.exp(power))
+        reach = ((power <= 0) & (alpha >= (1.0 / 255.0) * (1 + 1e-5)) & inside).any(axis=1)
+        misses += int((reach & ((msk >> b) & 1 == 0)).sum())
+    torch.cuda.synchronize()
+    return misses, float(np.mean([(msk >> b) & 1 for b in range(4)])) if len(msk) else 0.0
+
+
+@pytest.mark.parametrize("cam_t,n,w,hgt,seed", [(LON, 20000, 512, 256, 61), (PIN, 20000, 480, 270, 62),
+                                                (LON, 3000, 256, 128, 63)], ids=["lonlat", "pinhole", "lonlat_small"])
+def test_band_masks_cover_every_contributing_pixel(cam_t, n, w, hgt, seed):
+    """The row binning's band masks (bin.hip: band_row_intervals, one x-interval per (Gaussian, row, band)) may only
+    drop a 16x4 band of a tile in which no pixel reaches alpha >= 1/255 — checked by brute force over every pixel of
+    every instance's tile (the render kernels skip masked-out bands, so a miss would change images)."""
+    g, cam, _ = make_case(n, w, hgt, cam_t, seed, view_index=1, spread=1.5)
+    h = hip_run(g, cam, None)
+    misses, frac = _band_mask_misses(h, g, cam)
+    assert misses == 0, f"{misses} contributing (instance, band) pairs masked out"
+    assert frac < 0.95  # the masks do cull bands
