@@ -39,17 +39,30 @@ namespace omr {
 
 namespace {
 
-constexpr int RB_THREADS = 256;
-constexpr int RB_ITEMS = 8;
-constexpr uint32_t RB_N = RB_THREADS * RB_ITEMS;  // slots per chunk, both passes
+// chunk geometry: THREADS threads, ITEMS slots each; slots are laid out in rounds (slot = wave * PER_WAVE + 64 r +
+// lane), so a round of a wave is 64 consecutive slots
+template <int THREADS_, int ITEMS_>
+struct Geo {
+    static constexpr int THREADS = THREADS_, ITEMS = ITEMS_, WAVES = THREADS / 64;
+    static constexpr uint32_t N = (uint32_t)THREADS * ITEMS;
+    static constexpr int PER_WAVE = (int)N / WAVES, ROUNDS = PER_WAVE / 64;
+};
+using RowGeo = Geo<256, 8>;  // rows pass: 2048-slot chunks
+// columns pass: 2048-slot chunks, or 4096 for large views (BinArgs::cb_shift; half the chunks: fewer counts to scan
+// and fewer descriptors and barriers per instance, at the same 16 waves per CU — config E tile sort 1.27 -> 1.17 ms,
+// while config C, whose 2048-slot chunks are only ~7 per block, lost 7 us to the coarser tail)
+using ColGeoS = Geo<256, 8>;
+using ColGeoL = Geo<512, 8>;
+constexpr int RB_THREADS = RowGeo::THREADS;
+constexpr int RB_ITEMS = RowGeo::ITEMS;
+constexpr uint32_t RB_N = RowGeo::N;  // slots per rows-pass chunk
 static_assert(RB_N == BIN_CHUNK, "launch_forward_scans cuts the rows pass's chunks at BIN_CHUNK slots");
-constexpr int RB_WAVES = RB_THREADS / 64;
-constexpr int RB_PER_WAVE = RB_N / RB_WAVES;
-constexpr int RB_ROUNDS = RB_PER_WAVE / 64;
-// columns pass: owners whose band intervals are staged in LDS (1024: config C's chunks, ~600 owners, all staged;
-// 512 measured 0.26 ms slower at config E)
-constexpr uint32_t CB_OWN_CONST = 1024;
-// grid caps of the grid-stride chunk kernels (256 CUs: 8 resident hist blocks, 4 scatter blocks of <= 40 KiB LDS each)
+constexpr int RB_WAVES = RowGeo::WAVES;
+constexpr int RB_PER_WAVE = RowGeo::PER_WAVE;
+constexpr int RB_ROUNDS = RowGeo::ROUNDS;
+static_assert(ColGeoS::N == 1u << 11 && ColGeoL::N == 1u << 12, "cb_shift 11 / 12");
+// grid caps of the grid-stride chunk kernels (256 CUs: 8 resident hist blocks of 256 threads, 4 scatter blocks of
+// 256 threads and <= 40 KiB LDS, or 2 of 512 threads and <= 80 KiB)
 constexpr uint32_t BIN_GRID_HIST = 2048, BIN_GRID_SCATTER = 1024;
 
 #ifdef OMR_BIN_STAMPS  // diagnostic: per-phase s_memrealtime stamps of cols_scatter_kernel (profiles/bin_stamps.py)
@@ -143,9 +156,10 @@ __device__ __forceinline__ void diff_to_counts(int* s_diff, uint32_t nbuckets, u
 // Owner of every slot of a chunk, s_own[j] = the owner holding slot s0 + j: the caller zeroes s_own, marks each owner
 // at its first slot in the chunk (owners have distinct first slots; the first owner, which may start before s0, is 0),
 // and this fills the runs by an inclusive max-scan — one LDS read per slot afterwards instead of walking owner ends.
+template <class G>
 __device__ __forceinline__ void owner_fill(uint16_t* s_own, uint32_t* s_wave)
 {
-    static_assert(RB_ITEMS == 8, "one 16-byte LDS word of 8 owners per thread");
+    static_assert(G::ITEMS == 8, "one 16-byte LDS word of 8 owners per thread");
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     uint4 q = reinterpret_cast<const uint4*>(s_own)[threadIdx.x];
     uint32_t v[8] = {q.x & 0xFFFFu, q.x >> 16, q.y & 0xFFFFu, q.y >> 16, q.z & 0xFFFFu, q.z >> 16, q.w & 0xFFFFu, q.w >> 16};
@@ -162,7 +176,7 @@ __device__ __forceinline__ void owner_fill(uint16_t* s_own, uint32_t* s_wave)
     if (lane == 0) prev = 0;
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < RB_WAVES; ++k)
+    for (int k = 0; k < G::WAVES; ++k)
         if ((uint32_t)k < w) prev = max(prev, s_wave[k]);
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = max(v[i], prev);
@@ -171,24 +185,24 @@ __device__ __forceinline__ void owner_fill(uint16_t* s_own, uint32_t* s_wave)
     __syncthreads();
 }
 
-// Ranks RB_ITEMS items per lane in round layout (item = wave * RB_PER_WAVE + 64 r + lane, i.e. slot order) by digit
+// Ranks G::ITEMS items per lane in round layout (item = wave * PER_WAVE + 64 r + lane, i.e. slot order) by digit
 // d[r] < 2^BITS, stably: on return lp[r] = the item's position in the block's digit-sorted order and s_dstart[d] =
-// the block-local start of digit d. s_whist: [RB_WAVES][2^BITS] scratch. Matches radix_downsweep_kernel (sort.hip).
-template <int BITS>
-__device__ __forceinline__ void rank_items(const uint32_t (&d)[RB_ROUNDS], const bool (&valid)[RB_ROUNDS],
-                                           uint32_t (&lp)[RB_ROUNDS], uint32_t (*s_whist)[1 << BITS],
+// the block-local start of digit d. s_whist: [WAVES][2^BITS] scratch. Matches radix_downsweep_kernel (sort.hip).
+template <int BITS, class G>
+__device__ __forceinline__ void rank_items(const uint32_t (&d)[G::ROUNDS], const bool (&valid)[G::ROUNDS],
+                                           uint32_t (&lp)[G::ROUNDS], uint32_t (*s_whist)[1 << BITS],
                                            uint32_t* s_dstart, uint32_t* s_wave)
 {
     constexpr uint32_t NB = 1u << BITS;
     const uint32_t tid = threadIdx.x, w = tid >> 6;
-    for (uint32_t i = tid; i < RB_WAVES * NB; i += RB_THREADS) (&s_whist[0][0])[i] = 0;
+    for (uint32_t i = tid; i < G::WAVES * NB; i += G::THREADS) (&s_whist[0][0])[i] = 0;
     __syncthreads();
     // per round: the lanes with this lane's digit (a match by BITS ballots); the group's lowest lane advances the wave's
     // running count of the digit after every lane of the wave has read it (a read-then-write per round measured faster
     // than a ds_add_rtn per group plus a broadcast: config E tile sort 1.78 vs 2.14 ms)
-    uint32_t lr[RB_ROUNDS];
+    uint32_t lr[G::ROUNDS];
 #pragma unroll
-    for (int r = 0; r < RB_ROUNDS; ++r) {
+    for (int r = 0; r < G::ROUNDS; ++r) {
         const uint64_t peers = wave_match_digit<BITS>(d[r], valid[r]);
         const uint32_t rank = mask_rank(peers);
         const uint32_t prev = valid[r] ? s_whist[w][d[r]] : 0u;
@@ -199,7 +213,7 @@ __device__ __forceinline__ void rank_items(const uint32_t (&d)[RB_ROUNDS], const
     }
     __syncthreads();
     // per digit: per-wave exclusive offsets, then the block-wide exclusive scan of the digit totals
-    constexpr uint32_t DPT = (NB + RB_THREADS - 1) / RB_THREADS;  // digits per thread
+    constexpr uint32_t DPT = (NB + G::THREADS - 1) / G::THREADS;  // digits per thread
     uint32_t run[DPT], tsum = 0;
 #pragma unroll
     for (uint32_t q = 0; q < DPT; ++q) {
@@ -207,7 +221,7 @@ __device__ __forceinline__ void rank_items(const uint32_t (&d)[RB_ROUNDS], const
         run[q] = 0;
         if (dg < NB) {
 #pragma unroll
-            for (int ww = 0; ww < RB_WAVES; ++ww) {
+            for (int ww = 0; ww < G::WAVES; ++ww) {
                 const uint32_t c = s_whist[ww][dg];
                 s_whist[ww][dg] = run[q];
                 run[q] += c;
@@ -216,7 +230,7 @@ __device__ __forceinline__ void rank_items(const uint32_t (&d)[RB_ROUNDS], const
         tsum += run[q];
     }
     uint32_t total;
-    uint32_t ex = bin_block_scan<RB_THREADS>(tsum, s_wave, &total);
+    uint32_t ex = bin_block_scan<G::THREADS>(tsum, s_wave, &total);
 #pragma unroll
     for (uint32_t q = 0; q < DPT; ++q) {
         const uint32_t dg = tid * DPT + q;
@@ -225,7 +239,7 @@ __device__ __forceinline__ void rank_items(const uint32_t (&d)[RB_ROUNDS], const
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < RB_ROUNDS; ++r) lp[r] = valid[r] ? s_dstart[d[r]] + s_whist[w][d[r]] + lr[r] : 0u;
+    for (int r = 0; r < G::ROUNDS; ++r) lp[r] = valid[r] ? s_dstart[d[r]] + s_whist[w][d[r]] + lr[r] : 0u;
 }
 
 // ---- rows pass -------------------------------------------------------------------------------------------------
@@ -321,7 +335,7 @@ __global__ __launch_bounds__(BIN_MAX_GRID) void rows_info_kernel(BinArgs a)
     if (y < gy && L) {
         e0 = entry(y);
         sl0 = slot(y);
-        n = (slot(y + 1) - sl0 + RB_N - 1) / RB_N;
+        n = (slot(y + 1) - sl0 + (1u << a.cb_shift) - 1u) >> a.cb_shift;
     }
     uint32_t total;
     const uint32_t cb = bin_block_scan<BIN_MAX_GRID>(n, s_wave, &total);
@@ -361,6 +375,7 @@ __global__ __launch_bounds__(RB_THREADS) void rows_scatter_kernel(BinArgs a)
     const uint32_t M = live_M(a.counters, a.cap), C = row_chunks(M), gy = a.gy;
     const size_t half = (size_t)gy * C;
     uint32_t* desc_w = reinterpret_cast<uint32_t*>(a.desc_b);
+    const uint32_t cbn = 1u << a.cb_shift;  // columns-pass chunk size
     // software pipeline: the next chunk's owners (first RP x 256) and count bases are loaded into registers while the
     // current chunk is ranked and written
     constexpr int RP = 3, GBP = (1 << BITS) / RB_THREADS;
@@ -421,7 +436,7 @@ __global__ __launch_bounds__(RB_THREADS) void rows_scatter_kernel(BinArgs a)
         }
         __syncthreads();
         if (cn < cr.end) load_owners(kn, cn);
-        owner_fill(s_own, s_wave);
+        owner_fill<RowGeo>(s_own, s_wave);
         uint32_t d[RB_ROUNDS], own[RB_ROUNDS], lp[RB_ROUNDS];
         bool valid[RB_ROUNDS];
 #pragma unroll
@@ -432,7 +447,7 @@ __global__ __launch_bounds__(RB_THREADS) void rows_scatter_kernel(BinArgs a)
             d[r] = valid[r] ? s + s_yoff[o] : 0u;
             own[r] = o;
         }
-        rank_items<BITS>(d, valid, lp, s_whist, s_dstart, s_wave);  // its barriers end the expansion's reads of s_yoff
+        rank_items<BITS, RowGeo>(d, valid, lp, s_whist, s_dstart, s_wave);  // its barriers end the expansion's reads of s_yoff
         uint32_t* s_sorted = s_yoff_sorted;
 #pragma unroll
         for (int r = 0; r < RB_ROUNDS; ++r)
@@ -490,12 +505,12 @@ __global__ __launch_bounds__(RB_THREADS) void rows_scatter_kernel(BinArgs a)
             a.ent_gid[dst] = s_gid[oi];
             a.ent_w[dst] = xw;
             a.ent_ex[dst] = ex;
-            // the columns chunk whose first slot this entry holds (widths <= BIN_MAX_GRID < N: at most one)
+            // the columns chunk whose first slot this entry holds (widths <= BIN_MAX_GRID < 2048: at most one)
             const uint4 ri = a.rowinfo[y];
-            const uint32_t rel = ex - ri.y, kk = (rel + RB_N - 1) / RB_N;
-            if (kk < ri.w && kk * RB_N < rel + (xw & 0xFFFFu)) {
-                const uint32_t cc = ri.z + kk, s0 = ri.y + kk * RB_N;
-                const uint32_t s1 = min(a.rowinfo[y + 1].y, s0 + RB_N);
+            const uint32_t rel = ex - ri.y, kk = (rel + cbn - 1u) >> a.cb_shift;
+            if (kk < ri.w && (kk << a.cb_shift) < rel + (xw & 0xFFFFu)) {
+                const uint32_t cc = ri.z + kk, s0 = ri.y + (kk << a.cb_shift);
+                const uint32_t s1 = min(a.rowinfo[y + 1].y, s0 + cbn);
                 reinterpret_cast<uint4*>(desc_w)[2 * (size_t)cc] = make_uint4(y, kk, ri.w, ri.z);
                 desc_w[8 * (size_t)cc + 4] = s0;
                 desc_w[8 * (size_t)cc + 5] = s1;
@@ -571,16 +586,16 @@ __global__ __launch_bounds__(RB_THREADS) void cols_hist_kernel(BinArgs a)
 // the slots of one round: column, point-list word (Gaussian | band mask << PL_GID_BITS); STAGED: every owner's band
 // intervals and Gaussian are in LDS (a chunk-uniform choice, so the loads stay plain LDS reads), else each slot derives
 // its owner's intervals from bin_rec itself
-template <bool STAGED>
+template <bool STAGED, class G>
 __device__ __forceinline__ void col_expand(const BinArgs& a, const ColChunk& k, const uint16_t* s_own,
                                            const uint32_t* s_xoff, const uint4* s_iv, const uint32_t* s_gid,
-                                           uint8_t* row_valid, uint32_t (&d)[RB_ROUNDS], uint32_t (&val)[RB_ROUNDS],
-                                           bool (&valid)[RB_ROUNDS])
+                                           uint8_t* row_valid, uint32_t (&d)[G::ROUNDS],
+                                           uint32_t (&val)[G::ROUNDS], bool (&valid)[G::ROUNDS])
 {
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
 #pragma unroll
-    for (int r = 0; r < RB_ROUNDS; ++r) {
-        const uint32_t j = w * RB_PER_WAVE + 64u * r + lane, s = k.s0 + j;
+    for (int r = 0; r < G::ROUNDS; ++r) {
+        const uint32_t j = w * G::PER_WAVE + 64u * r + lane, s = k.s0 + j;
         valid[r] = s < k.s1;
         d[r] = 0;
         val[r] = 0;
@@ -603,24 +618,25 @@ __device__ __forceinline__ void col_expand(const BinArgs& a, const ColChunk& k, 
     }
 }
 
-template <int BITS>
-__global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
+template <int BITS, class G>
+__global__ __launch_bounds__(G::THREADS) void cols_scatter_kernel(BinArgs a)
 {
     // phase 1 (expansion): per owner, x0 minus its first instance slot (slot s is column s + s_xoff), and, when the
     // owners fit, each one's reachable columns per band of this row (band_row_intervals: computed once per row entry,
     // not once per instance) and its Gaussian; phase 2 (write-out): the slots' point-list words and columns in column
     // order, in the same storage
-    constexpr size_t PH1 = RB_N * sizeof(uint32_t) + CB_OWN_CONST * (sizeof(uint4) + sizeof(uint32_t));
-    constexpr size_t PH2 = RB_N * (sizeof(uint32_t) + sizeof(uint16_t));
+    constexpr uint32_t CB_OWN = G::N / 2;  // owners staged in LDS (C's 2048-slot chunks have ~600, E's 4096 ~650)
+    constexpr size_t PH1 = G::N * sizeof(uint32_t) + CB_OWN * (sizeof(uint4) + sizeof(uint32_t));
+    constexpr size_t PH2 = G::N * (sizeof(uint32_t) + sizeof(uint16_t));
     __shared__ uint4 s_raw[(PH1 > PH2 ? PH1 : PH2) / sizeof(uint4)];
     uint4* s_iv = s_raw;
-    uint32_t* s_gid = reinterpret_cast<uint32_t*>(s_raw + CB_OWN_CONST);
-    uint32_t* s_xoff = s_gid + CB_OWN_CONST;
-    __shared__ __attribute__((aligned(16))) uint16_t s_own[RB_N];
-    __shared__ uint32_t s_whist[RB_WAVES][1 << BITS];
+    uint32_t* s_gid = reinterpret_cast<uint32_t*>(s_raw + CB_OWN);
+    uint32_t* s_xoff = s_gid + CB_OWN;
+    __shared__ __attribute__((aligned(16))) uint16_t s_own[G::N];
+    __shared__ uint32_t s_whist[G::WAVES][1 << BITS];
     __shared__ uint32_t s_dstart[1 << BITS];
     __shared__ uint32_t s_gbase[1 << BITS];
-    __shared__ uint32_t s_wave[RB_WAVES];
+    __shared__ uint32_t s_wave[G::WAVES];
     const uint32_t tid = threadIdx.x, gx = a.gx, C = a.words[1];
     const uint32_t L = live_L(a.counters, a.cap);
     uint8_t* row_valid = reinterpret_cast<uint8_t*>(a.binning + row_valid_offset(L));  // the backward's row map
@@ -629,17 +645,17 @@ __global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
     // constants are loaded into registers while the current chunk is expanded and ranked (more would cost the VGPRs
     // of a fourth block per CU); staged owners past those are loaded when staged
     constexpr int PF = 2;
-    static_assert(PF * RB_THREADS <= CB_OWN_CONST, "prefetched owners are staged owners");
+    static_assert(PF * G::THREADS <= CB_OWN, "prefetched owners are staged owners");
     typedef float f4v __attribute__((ext_vector_type(4)));  // native vectors: the prefetch stays in registers
-    constexpr int GBP = (1 << BITS) / RB_THREADS;  // the chunk's per-column count bases, per thread
+    constexpr int GBP = ((1 << BITS) + G::THREADS - 1) / G::THREADS;  // per-column count bases per thread
     uint32_t p_ex[PF], p_ew[PF], p_gid[PF], p_gb[GBP];
     f4v p_ba[PF], p_bb[PF];
     const f4v* bin_rec_v = reinterpret_cast<const f4v*>(a.bin_rec);
 #define OMR_CS_LOAD_ENTRIES(q)                                                 \
     _Pragma("unroll") for (int j = 0; j < PF; ++j)                             \
     {                                                                          \
-        const uint32_t i_ = tid + j * RB_THREADS;                              \
-        if ((q).nr <= CB_OWN_CONST && i_ < (q).nr) {                           \
+        const uint32_t i_ = tid + j * G::THREADS;                              \
+        if ((q).nr <= CB_OWN && i_ < (q).nr) {                           \
             p_ex[j] = a.ent_ex[(q).e_lo + i_];                                 \
             p_ew[j] = a.ent_w[(q).e_lo + i_];                                  \
             p_gid[j] = a.ent_gid[(q).e_lo + i_];                               \
@@ -647,14 +663,14 @@ __global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
     }                                                                          \
     _Pragma("unroll") for (int j = 0; j < GBP; ++j)                            \
     {                                                                          \
-        const uint32_t x_ = tid + j * RB_THREADS;                              \
+        const uint32_t x_ = tid + j * G::THREADS;                              \
         if (x_ < gx) p_gb[j] = a.hist_b[col_index((q), gx, x_)];               \
     }
 #define OMR_CS_LOAD_CONSTS(q)                                                  \
     _Pragma("unroll") for (int j = 0; j < PF; ++j)                             \
     {                                                                          \
-        const uint32_t i_ = tid + j * RB_THREADS;                              \
-        if ((q).nr <= CB_OWN_CONST && i_ < (q).nr) {                           \
+        const uint32_t i_ = tid + j * G::THREADS;                              \
+        if ((q).nr <= CB_OWN && i_ < (q).nr) {                           \
             p_ba[j] = bin_rec_v[2 * (size_t)p_gid[j]];                         \
             p_bb[j] = bin_rec_v[2 * (size_t)p_gid[j] + 1];                     \
         }                                                                      \
@@ -670,13 +686,13 @@ __global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
         BSTAMP(it, 0);
         const uint32_t cn = c + cr.step;
         const ColChunk kn = col_chunk(a, min(cn, C - 1u));  // the next chunk's descriptor, in flight meanwhile
-        const bool staged = k.nr <= CB_OWN_CONST;  // chunk-uniform
+        const bool staged = k.nr <= CB_OWN;  // chunk-uniform
         reinterpret_cast<uint4*>(s_own)[tid] = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
         if (staged) {
 #pragma unroll
             for (int j = 0; j < PF; ++j) {
-                const uint32_t i = tid + j * RB_THREADS;
+                const uint32_t i = tid + j * G::THREADS;
                 if (i < k.nr) {
                     s_xoff[i] = (p_ew[j] >> 16) - p_ex[j];  // modular
                     if (p_ex[j] >= k.s0) s_own[p_ex[j] - k.s0] = (uint16_t)i;  // distinct first slots (width >= 1)
@@ -686,7 +702,7 @@ __global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
                     s_gid[i] = p_gid[j];
                 }
             }
-            for (uint32_t i = tid + PF * RB_THREADS; i < k.nr; i += RB_THREADS) {
+            for (uint32_t i = tid + PF * G::THREADS; i < k.nr; i += G::THREADS) {
                 const uint32_t e = k.e_lo + i, ex = a.ent_ex[e], gid = a.ent_gid[e];
                 s_xoff[i] = (a.ent_w[e] >> 16) - ex;
                 if (ex >= k.s0) s_own[ex - k.s0] = (uint16_t)i;
@@ -694,7 +710,7 @@ __global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
                 s_gid[i] = gid;
             }
         } else {
-            for (uint32_t i = tid; i < k.nr; i += RB_THREADS) {
+            for (uint32_t i = tid; i < k.nr; i += G::THREADS) {
                 const uint32_t e = k.e_lo + i;
                 const uint32_t ex = a.ent_ex[e];
                 s_xoff[i] = (a.ent_w[e] >> 16) - ex;
@@ -703,28 +719,28 @@ __global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
         }
 #pragma unroll
         for (int j = 0; j < GBP; ++j)
-            if (tid + j * RB_THREADS < gx) s_gbase[tid + j * RB_THREADS] = p_gb[j];
+            if (tid + j * G::THREADS < gx) s_gbase[tid + j * G::THREADS] = p_gb[j];
         __syncthreads();
         if (cn < cr.end) {
             OMR_CS_LOAD_ENTRIES(kn)
         }
         BSTAMP(it, 1);
-        owner_fill(s_own, s_wave);
+        owner_fill<G>(s_own, s_wave);
         BSTAMP(it, 2);
-        uint32_t d[RB_ROUNDS], val[RB_ROUNDS], lp[RB_ROUNDS];
-        bool valid[RB_ROUNDS];
-        if (staged) col_expand<true>(a, k, s_own, s_xoff, s_iv, s_gid, row_valid, d, val, valid);
-        else col_expand<false>(a, k, s_own, s_xoff, s_iv, s_gid, row_valid, d, val, valid);
+        uint32_t d[G::ROUNDS], val[G::ROUNDS], lp[G::ROUNDS];
+        bool valid[G::ROUNDS];
+        if (staged) col_expand<true, G>(a, k, s_own, s_xoff, s_iv, s_gid, row_valid, d, val, valid);
+        else col_expand<false, G>(a, k, s_own, s_xoff, s_iv, s_gid, row_valid, d, val, valid);
         if (cn < cr.end) {
             OMR_CS_LOAD_CONSTS(kn)
         }
         BSTAMP(it, 3);
-        rank_items<BITS>(d, valid, lp, s_whist, s_dstart, s_wave);  // its barriers end the expansion's reads of s_raw
+        rank_items<BITS, G>(d, valid, lp, s_whist, s_dstart, s_wave);  // its barriers end the expansion's reads of s_raw
         BSTAMP(it, 4);
         uint32_t* s_v = reinterpret_cast<uint32_t*>(s_raw);
-        uint16_t* s_x = reinterpret_cast<uint16_t*>(s_v + RB_N);
+        uint16_t* s_x = reinterpret_cast<uint16_t*>(s_v + G::N);
 #pragma unroll
-        for (int r = 0; r < RB_ROUNDS; ++r)
+        for (int r = 0; r < G::ROUNDS; ++r)
             if (valid[r]) {
                 s_v[lp[r]] = val[r];
                 s_x[lp[r]] = (uint16_t)d[r];
@@ -732,14 +748,14 @@ __global__ __launch_bounds__(RB_THREADS) void cols_scatter_kernel(BinArgs a)
         __syncthreads();
         BSTAMP(it, 5);
         const uint32_t nvalid = k.s1 - k.s0;
-        for (uint32_t j = tid; j < nvalid; j += RB_THREADS) {
+        for (uint32_t j = tid; j < nvalid; j += G::THREADS) {
             const uint32_t x = s_x[j];
             point_list[s_gbase[x] + (j - s_dstart[x])] = s_v[j];
         }
         // identifyTileRanges from the counts: the row's first chunk writes its tiles' ranges; empty tiles keep the
         // {0, 0} preprocess wrote, as the reference leaves them (rasterizer_impl.cu:145-167 writes boundaries only)
         if (k.kk == 0)
-            for (uint32_t x = tid; x < gx; x += RB_THREADS) {
+            for (uint32_t x = tid; x < gx; x += G::THREADS) {
                 const size_t i = col_index(k, gx, x);
                 const uint32_t b0 = a.hist_b[i], b1 = a.hist_b[i + k.nch];
                 if (b1 != b0) a.ranges[(size_t)k.y * gx + x] = make_uint2(b0, b1);
@@ -764,11 +780,13 @@ extern "C" int omr_debug_bin_stamps(uint64_t* dst, size_t bytes)
 
 // scratch of the row binning for a binning capacity of `cap` instances (BinningState::carve)
 size_t bin_chunks_r(size_t cap) { return div_up(cap, RB_N) + 1; }
-size_t bin_chunks_b(size_t cap, uint32_t gy) { return div_up(cap, RB_N) + gy + 1; }
+uint32_t bin_cols_shift(size_t cap) { return cap >= ((size_t)1 << 25) ? 12u : 11u; }
+size_t bin_chunks_b(size_t cap, uint32_t gy) { return (div_up(cap, (size_t)1 << bin_cols_shift(cap))) + gy + 1; }
 
 void launch_row_binning(const BinArgs& a_in, hipStream_t s)
 {
     BinArgs a = a_in;
+    a.cb_shift = bin_cols_shift(a.cap);
     const uint32_t cr = (uint32_t)a.chunks_r, cbk = (uint32_t)a.chunks_b;
     // look-back words of the two scans, zeroed by rows_hist_kernel; grids and scans are sized for the capacity (capped
     // grid-stride kernels and persistent scans), the kernels stop at the live lengths (words[])
@@ -778,7 +796,7 @@ void launch_row_binning(const BinArgs& a_in, hipStream_t s)
     uint32_t* st_b = st_r + zr;
     a.nzero = zr + zb;
     const uint32_t gh_r = std::min(cr, BIN_GRID_HIST), gs_r = std::min(cr, BIN_GRID_SCATTER);
-    const uint32_t gh_b = std::min(cbk, BIN_GRID_HIST), gs_b = std::min(cbk, BIN_GRID_SCATTER);
+    const uint32_t gh_b = std::min(cbk, BIN_GRID_HIST);
     rows_hist_kernel<<<gh_r, RB_THREADS, 0, s>>>(a);
     launch_exclusive_scan(a.hist_r, a.hist_r, nr_hist, a.words + 2, st_r, a.err, s);
     rows_info_kernel<<<1, BIN_MAX_GRID, 0, s>>>(a);
@@ -786,8 +804,15 @@ void launch_row_binning(const BinArgs& a_in, hipStream_t s)
     else rows_scatter_kernel<10><<<gs_r, RB_THREADS, 0, s>>>(a);
     cols_hist_kernel<<<gh_b, RB_THREADS, 0, s>>>(a);
     launch_exclusive_scan(a.hist_b, a.hist_b, nb_hist, a.words + 3, st_b, a.err, s);
-    if (a.gx <= 256) cols_scatter_kernel<8><<<gs_b, RB_THREADS, 0, s>>>(a);
-    else cols_scatter_kernel<10><<<gs_b, RB_THREADS, 0, s>>>(a);
+    if (a.cb_shift == 12) {
+        const uint32_t g = std::min(cbk, BIN_GRID_SCATTER / 2);
+        if (a.gx <= 256) cols_scatter_kernel<8, ColGeoL><<<g, ColGeoL::THREADS, 0, s>>>(a);
+        else cols_scatter_kernel<10, ColGeoL><<<g, ColGeoL::THREADS, 0, s>>>(a);
+    } else {
+        const uint32_t g = std::min(cbk, BIN_GRID_SCATTER);
+        if (a.gx <= 256) cols_scatter_kernel<8, ColGeoS><<<g, ColGeoS::THREADS, 0, s>>>(a);
+        else cols_scatter_kernel<10, ColGeoS><<<g, ColGeoS::THREADS, 0, s>>>(a);
+    }
 }
 
 }  // namespace omr

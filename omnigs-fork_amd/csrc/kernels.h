@@ -136,6 +136,7 @@ struct BinArgs {
     const uint2* desc_r;        // owners of each row chunk: first, last (depth ranks; launch_forward_scans)
     uint32_t* hist_b;           // [tile][chunk] counts (row-major chunk blocks), scanned in place; chunks_b * gx words
     size_t chunks_b;
+    uint32_t cb_shift;          // columns-pass chunk = 1 << cb_shift slots (bin_cols_shift; set by launch_row_binning)
     uint4* desc_b;              // [chunks_b][2] column chunks: {y, chunk of the row, row chunks, row's first chunk},
                                 // {first slot, end slot, first owner entry, owners}
     uint4* rowinfo;             // [gy + 1]
@@ -146,6 +147,7 @@ struct BinArgs {
     char* binning;              // the binning buffer (canonical point list, row_valid at L-only offsets)
 };
 size_t bin_chunks_r(size_t cap);
+uint32_t bin_cols_shift(size_t cap);
 size_t bin_chunks_b(size_t cap, uint32_t gy);
 inline size_t bin_zero_words(size_t cap, uint32_t gx, uint32_t gy)
 {
