@@ -165,6 +165,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint
         const size_t i = base + li;
         const uint32_t o = i < n && order_ok ? order[i] : 0u;
         if (rows) {
+            // the one random gather of the forward scans: a second one measured +79 us at config E (139 -> 218 us)
             const uint2 rw = i < n && order_ok ? rects[o] : make_uint2(0u, 0u);
             if (i < n) drect[i] = rw;
             s_a[pad(li)] = rw.x & ROWS_MASK;
@@ -1057,19 +1058,27 @@ __global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(HostWo
     uint32_t* cc = in_lds ? s_cost : cost_tmp;
     const uint32_t ub = in_lds ? lo : 0u;  // index of unit u = u - ub
     if (first0 < hi && first0 + mine > lo) {
+        // tiles in groups of SG whose loads are all issued before the group's stores (the stores may alias the
+        // loads as far as the compiler knows: one tile at a time, each load waited for a global round trip)
+        constexpr uint32_t SG = 8;
         uint32_t first = first0;
-        for (uint32_t t = t0; t < t1 && first < hi; ++t) {
-            uint32_t rx, mc;
-            const uint32_t c = tile_units(ranges, max_contrib, t, &rx, &mc);
-            for (uint32_t k = 0; k < c; ++k) {
-                const uint32_t u = first + k;
-                if (u < lo || u >= hi) continue;
-                const uint32_t chunk = rx / CKPT + k;
-                uu[u - ub] = make_uint2(t, chunk);
-                // cost: the segment's positions below the tile's last contributor
-                cc[u - ub] = min(rx + mc, (chunk + 1) * CKPT) - max(rx, chunk * CKPT);
+        for (uint32_t tg = t0; tg < t1 && first < hi; tg += SG) {
+            uint32_t rxs[SG], mcs[SG], cs[SG];
+#pragma unroll
+            for (uint32_t j = 0; j < SG; ++j) cs[j] = tg + j < t1 ? tile_units(ranges, max_contrib, tg + j, &rxs[j], &mcs[j]) : 0u;
+#pragma unroll
+            for (uint32_t j = 0; j < SG; ++j) {
+                const uint32_t t = tg + j, c = cs[j], rx = rxs[j], mc = mcs[j];
+                for (uint32_t k = 0; k < c; ++k) {
+                    const uint32_t u = first + k;
+                    if (u < lo || u >= hi) continue;
+                    const uint32_t chunk = rx / CKPT + k;
+                    uu[u - ub] = make_uint2(t, chunk);
+                    // cost: the segment's positions below the tile's last contributor
+                    cc[u - ub] = min(rx + mc, (chunk + 1) * CKPT) - max(rx, chunk * CKPT);
+                }
+                first += c;
             }
-            first += c;
         }
     }
     if (tid < RADIX) s_hist[tid] = 0;
@@ -1084,7 +1093,13 @@ __global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(HostWo
     auto bucket = [&](uint32_t u) {  // 0 = costliest
         return (uint32_t)(RADIX - 1) - (uint32_t)(((uint64_t)cc[u - ub] * RADIX) / scale);
     };
-    for (uint32_t u = lo + tid; u < hi; u += SCHED_THREADS) atomicAdd(&s_hist[bucket(u)], 1u);
+    // wave-aggregated LDS atomics: most units of a large view are full segments of one cost, so per-unit adds would
+    // serialise on one bucket (config E: ~16 k per block)
+    for (uint32_t u = lo + tid; u < hi; u += SCHED_THREADS) {
+        const uint32_t b = bucket(u);
+        const uint64_t peers = wave_match_digit<RADIX_BITS>(b, true);
+        if (mask_rank(peers) == 0) atomicAdd(&s_hist[b], (uint32_t)__popcll(peers));
+    }
     __syncthreads();
     {
         const uint32_t cnt = tid < RADIX ? s_hist[tid] : 0u;
@@ -1093,7 +1108,14 @@ __global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(HostWo
         if (tid < RADIX) s_hist[tid] = lo + ex;
     }
     __syncthreads();
-    for (uint32_t u = lo + tid; u < hi; u += SCHED_THREADS) units[atomicAdd(&s_hist[bucket(u)], 1u)] = uu[u - ub];
+    for (uint32_t u = lo + tid; u < hi; u += SCHED_THREADS) {  // slots per bucket, one LDS atomic per bucket and wave
+        const uint32_t b = bucket(u);
+        const uint64_t peers = wave_match_digit<RADIX_BITS>(b, true);
+        const uint32_t rank = mask_rank(peers);
+        const uint32_t leader = (uint32_t)__builtin_ctzll(peers);
+        const uint32_t base0 = rank == 0 ? atomicAdd(&s_hist[b], (uint32_t)__popcll(peers)) : 0u;
+        units[(uint32_t)__shfl((int)base0, (int)leader, 64) + rank] = uu[u - ub];
+    }
     if (x == 0 && tid == 0) *unit_count = total;
 }
 
