@@ -226,11 +226,11 @@ __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const
 //  * a Gaussian with at most RS_LONG rows adds its rows of the chunk itself, in row order, from LDS;
 //  * a longer one is summed by the whole wave: each lane adds the chunk rows it holds, then one wave reduction
 //    (wave_ops.h) per (long Gaussian, chunk), in chunk order.
-// The row_valid bytes of the next chunk are requested with the rows of the current one: one HBM round trip per
-// chunk for the whole wave. Gaussians with more than ROW_SUM_HUGE rows (polar Gaussians reach every tile of the
+// The row_valid bytes of the next window are requested with the rows of the current one: one HBM round trip per
+// window for the whole wave. Gaussians with more than ROW_SUM_HUGE rows (polar Gaussians reach every tile of the
 // image; 0.1 % of them at config C, 13 % of the rows) would make their wave the kernel's tail: the wave skips them
 // (and the chunks only they own), and RS_HUGE_BLOCKS extra workgroups at the start of the grid take them from the
-// forward's huge_list, 256 threads per Gaussian. The order of every sum is fixed: the result is deterministic.
+// forward's huge_list, one wave per Gaussian. The order of every sum is fixed: the result is deterministic.
 #ifndef OMR_RS_ROWS
 #define OMR_RS_ROWS 128
 #endif
@@ -240,8 +240,6 @@ constexpr int RS_Q = RS_ROWS / 64;    // rows per lane per chunk
 #define OMR_RS_LONG 32
 #endif
 constexpr uint32_t RS_LONG = OMR_RS_LONG;
-constexpr uint32_t RS_HUGE_BLOCKS = 512;
-constexpr int RS_HUGE_STEP = 8;  // rows in flight per thread of a huge-Gaussian workgroup
 
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
 {
@@ -273,52 +271,92 @@ struct RowSumArgs {
     float* dL_dcolor;  // [P][3] = row_sums[:, 6:9], written here so that it is final before gaussian_bwd runs
 };
 
-// one workgroup per huge Gaussian (the first RS_HUGE_BLOCKS blocks of the grid): thread t adds rows t, t + 256, ... (RS_HUGE_STEP in flight), then
-// the four waves' sums are combined in a fixed order
-__device__ __forceinline__ void huge_row_sums(const RowSumArgs& a, uint32_t hb, float* s_red)
+// The huge Gaussians, one per wave of the first RS_HUGE_BLOCKS workgroups of the grid. A pass covers 64 x
+// RS_HUGE_GROUPS 16-row mark groups (4096 rows: one 16-B mark load per group, all in flight at once), then loads the
+// lane's marked rows four at a time; each lane adds its rows in row order, then one wave reduction in a fixed order. (One workgroup per Gaussian with byte marks took 345 us at config E: its many huge Gaussians, mostly a few
+// hundred rows each, paid two barriers and a 256-thread reduction apiece.)
+#ifndef OMR_RS_HUGE_BLOCKS
+#define OMR_RS_HUGE_BLOCKS 512
+#endif
+constexpr uint32_t RS_HUGE_BLOCKS = OMR_RS_HUGE_BLOCKS;
+constexpr int RS_HUGE_GROUPS = 4;
+__device__ __forceinline__ void huge_row_sums(const RowSumArgs& a, uint32_t hb)
 {
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
     const uint32_t count = *a.huge_count;
-    for (uint32_t t = hb; t < count; t += RS_HUGE_BLOCKS) {
+    for (uint32_t t = hb * 4u + (threadIdx.x >> 6); t < count; t += RS_HUGE_BLOCKS * 4u) {
         const uint32_t idx = a.huge_list[t];
         const uint32_t s = a.row_first[idx];
         uint32_t n = a.tiles_touched[idx];
         if (s >= a.R || n > a.R - s) n = 0;  // never true for a consistent forward
+        const uint32_t e = s + n;
         float acc[GRAD_ROW];
 #pragma unroll
         for (int c = 0; c < GRAD_ROW; ++c) acc[c] = 0.f;
-        for (uint32_t k0 = 0; k0 < n; k0 += 256u * RS_HUGE_STEP) {
-            bool ok[RS_HUGE_STEP];
+        // row_valid is 256-B aligned and its region holds R bytes rounded up to 256: a 16-row group starting
+        // below e <= R is readable whole
+        for (uint32_t g0 = s & ~15u; g0 < e; g0 += 64u * 16u * RS_HUGE_GROUPS) {
+            uint4 f[RS_HUGE_GROUPS];
 #pragma unroll
-            for (int q = 0; q < RS_HUGE_STEP; ++q) {
-                const uint32_t k = k0 + (uint32_t)q * 256u + tid;
-                ok[q] = k < n && a.row_valid[s + k] != 0;
+            for (int q = 0; q < RS_HUGE_GROUPS; ++q) {
+                const uint32_t r = g0 + ((uint32_t)q * 64u + lane) * 16u;
+                f[q] = r < e ? *reinterpret_cast<const uint4*>(a.row_valid + r) : make_uint4(0u, 0u, 0u, 0u);
             }
+            uint64_t mk = 0;  // bit 16 q + j: row g0 + (64 q + lane) * 16 + j is marked and Gaussian idx's
 #pragma unroll
-            for (int q = 0; q < RS_HUGE_STEP; ++q) add_marked_row(acc, a.inst_grad, s + k0 + (uint32_t)q * 256u + tid, ok[q]);
+            for (int q = 0; q < RS_HUGE_GROUPS; ++q) {
+                const uint32_t w[4] = {f[q].x, f[q].y, f[q].z, f[q].w};
+                const uint32_t r = g0 + ((uint32_t)q * 64u + lane) * 16u;
+#pragma unroll
+                for (uint32_t j = 0; j < 16; ++j)
+                    if (((w[j >> 2] >> (8u * (j & 3u))) & 0xFFu) != 0u && r + j >= s && r + j < e)
+                        mk |= 1ull << (16 * q + j);
+            }
+            while (mk) {  // four marked rows in flight, added in row order
+                uint32_t rr[4];
+                bool ok[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    ok[u] = mk != 0;
+                    const uint32_t b = ok[u] ? (uint32_t)__builtin_ctzll(mk) : 0u;
+                    rr[u] = g0 + ((b >> 4) * 64u + lane) * 16u + (b & 15u);
+                    mk &= mk - 1;
+                }
+                float x[4][GRAD_ROW];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                    for (int c = 0; c < GRAD_ROW; ++c) x[u][c] = 0.f;
+                    add_marked_row(x[u], a.inst_grad, rr[u], ok[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (ok[u])
+#pragma unroll
+                        for (int c = 0; c < GRAD_ROW; ++c) acc[c] += x[u][c];
+            }
         }
         float t8;
         const float tv = wave_sum9_rows(acc, acc[8], lane, &t8);  // lane l: total of value (l >> 3) & 7
-        if ((lane & 7) == 0) s_red[wv * GRAD_ROW + (lane >> 3)] = tv;
-        if (lane == 1) s_red[wv * GRAD_ROW + 8] = t8;
-        __syncthreads();
-        if (tid < GRAD_ROW) {
-            const float tot =
-                ((s_red[tid] + s_red[GRAD_ROW + tid]) + s_red[2 * GRAD_ROW + tid]) + s_red[3 * GRAD_ROW + tid];
-            a.row_sums[(size_t)idx * GRAD_ROW + tid] = tot;
-            if (tid >= 6) a.dL_dcolor[(size_t)idx * 3 + (tid - 6)] = tot;
+        if ((lane & 7) == 0) {
+            const uint32_t c = lane >> 3;
+            a.row_sums[(size_t)idx * GRAD_ROW + c] = tv;
+            if (c >= 6) a.dL_dcolor[(size_t)idx * 3 + (c - 6)] = tv;
         }
-        __syncthreads();
+        if (lane == 1) {
+            a.row_sums[(size_t)idx * GRAD_ROW + 8] = t8;
+            a.dL_dcolor[(size_t)idx * 3 + 2] = t8;
+        }
     }
 }
 
 #ifndef OMR_RS_WIN
 #define OMR_RS_WIN 512
 #endif
-constexpr uint32_t RS_WIN = OMR_RS_WIN;  // rows whose marks a wave compacts at once (8 or 16 per lane, one load;
-                                         // 512: C 0.056 / E 0.37 ms, 1024: 0.060 / 0.40)
+constexpr uint32_t RS_WIN = OMR_RS_WIN;  // rows whose marks a wave compacts at once (8 per lane, one load; 1024
+                                         // rows, 16 per lane: C 0.060 vs 0.056 ms, E 0.40 vs 0.37 ms, round 2)
 constexpr uint32_t RS_RPL = RS_WIN / 64;
-static_assert(RS_RPL == 8 || RS_RPL == 16, "8-B or 16-B mark loads");
+static_assert(RS_RPL == 8, "8-B mark loads");
 
 __device__ __forceinline__ uint32_t wave_exclusive_scan_u32(uint32_t x, uint32_t lane, uint32_t* total)
 {
@@ -332,23 +370,12 @@ __device__ __forceinline__ uint32_t wave_exclusive_scan_u32(uint32_t x, uint32_t
     return inc - x;
 }
 
-// first position p in [lo, hi) of the sorted list with list[p] >= v
-__device__ __forceinline__ uint32_t lds_lower_bound(const uint32_t* list, uint32_t lo, uint32_t hi, uint32_t v)
-{
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (list[mid] < v) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
-
 __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
 {
     __shared__ float s_rows_all[4][RS_ROWS * GRAD_ROW];  // row-major, 9 floats per row (odd stride: no conflicts)
     __shared__ uint32_t s_list_all[4][RS_WIN];
     if (blockIdx.x < a.huge_blocks) {  // dispatched first: the huge Gaussians overlap the rest of the grid
-        huge_row_sums(a, blockIdx.x, &s_rows_all[0][0]);
+        huge_row_sums(a, blockIdx.x);
         return;
     }
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -377,27 +404,26 @@ __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
     // per 128 rows. Each Gaussian's marked rows are a contiguous run of the sorted list; the sums keep row order.
     uint32_t* s_list = s_list_all[wv];
     const uint64_t huges = __ballot(huge && idx < a.g_end && s < a.R);
-    for (uint32_t w0 = lo & ~(RS_RPL - 1u); w0 < hi; w0 += RS_WIN) {  // lo > hi when the wave owns no rows
+    // the marks of window W, 8 rows per lane (row_valid is 256-B aligned and padded to a multiple of 256 B). W is
+    // 0xFFFFFFF8 past the last window: the first test keeps W + 8 lane from wrapping into [0, hi).
+#define RS_MARKS(W)                                                                                                    \
+    ((W) < hi && (W) + RS_RPL * lane < hi                                                                             \
+         ? *reinterpret_cast<const uint2*>(a.row_valid + (size_t)((W) + RS_RPL * lane))                               \
+         : make_uint2(0u, 0u))
+    uint32_t w0 = lo & ~(RS_RPL - 1u);  // lo > hi when the wave owns no rows
+    uint2 f_cur = RS_MARKS(w0);
+    while (w0 < hi) {
+        // the next window starts at the first row of the wave's own Gaussians past this one: the spans of huge
+        // Gaussians between them (summed by huge_row_sums; tens of thousands of rows at config E) are skipped. Its
+        // marks are requested now, with this window's rows.
+        const uint32_t nx = w0 + RS_WIN;
+        const uint32_t w1 =
+            __builtin_amdgcn_readfirstlane(wave_min_u32(n != 0 && e > nx ? max(s, nx) : 0xFFFFFFFFu)) & ~(RS_RPL - 1u);
+        const uint2 f_next = RS_MARKS(w1);
         const uint32_t r0 = w0 + RS_RPL * lane;
         uint32_t m = 0;  // bit j: row r0 + j is marked, inside [lo, hi) and not a huge Gaussian's
         if (r0 < hi) {
-            uint32_t fw[RS_RPL / 4] = {};
-            if (r0 + RS_RPL <= a.R) {  // row_valid is 256-B aligned
-                if constexpr (RS_RPL == 8) {
-                    const uint2 f = *reinterpret_cast<const uint2*>(a.row_valid + r0);
-                    fw[0] = f.x;
-                    fw[1] = f.y;
-                } else {
-                    const uint4 f = *reinterpret_cast<const uint4*>(a.row_valid + r0);
-                    fw[0] = f.x;
-                    fw[1] = f.y;
-                    fw[2] = f.z;
-                    fw[3] = f.w;
-                }
-            } else {
-                for (uint32_t j = 0; j < RS_RPL && r0 + j < a.R; ++j)
-                    fw[j >> 2] |= (uint32_t)a.row_valid[r0 + j] << (8u * (j & 3u));
-            }
+            const uint32_t fw[2] = {f_cur.x, f_cur.y};
 #pragma unroll
             for (uint32_t j = 0; j < RS_RPL; ++j) {
                 const uint32_t r = r0 + j;
@@ -413,8 +439,18 @@ __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
             }
         }
         uint32_t total;
-        uint32_t k = wave_exclusive_scan_u32((uint32_t)__popc(m), lane, &total);
+        const uint32_t k0 = wave_exclusive_scan_u32((uint32_t)__popc(m), lane, &total);
+        uint32_t k = k0;
         for (uint32_t mm = m; mm; mm &= mm - 1) s_list[k++] = r0 + (uint32_t)__builtin_ctz(mm);
+        // this lane's Gaussian's marked rows in the window: list positions [PA, PB), the marked rows before s and
+        // before e, counted from the scan (the lane holding window row d has k0 before its rows and m over them)
+        const uint32_t ds = s > w0 ? min(s - w0, RS_WIN) : 0u, de = e > w0 ? min(e - w0, RS_WIN) : 0u;
+        const uint32_t la = min(ds / RS_RPL, 63u), lb = min(de / RS_RPL, 63u);
+        const uint32_t ba = ds - la * RS_RPL, bb = de - lb * RS_RPL;  // 0 .. 8
+        const uint32_t ka = (uint32_t)__shfl((int)k0, (int)la, 64), ma = (uint32_t)__shfl((int)m, (int)la, 64);
+        const uint32_t kb = (uint32_t)__shfl((int)k0, (int)lb, 64), mb = (uint32_t)__shfl((int)m, (int)lb, 64);
+        const uint32_t PA = n != 0 ? ka + (uint32_t)__popc(ma & ((1u << ba) - 1u)) : 0u;
+        const uint32_t PB = n != 0 ? kb + (uint32_t)__popc(mb & ((1u << bb) - 1u)) : 0u;
         wave_sync();
         for (uint32_t c0 = 0; c0 < total; c0 += RS_ROWS) {
             const uint32_t c1 = min(total, c0 + RS_ROWS);
@@ -431,12 +467,7 @@ __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
 #pragma unroll
                 for (int c = 0; c < GRAD_ROW; ++c) s_rows[(q * 64 + lane) * GRAD_ROW + c] = x[q][c];
             // this lane's Gaussian's marked rows in the chunk: list positions [pa, pb)
-            const uint32_t first = s_list[c0], last = s_list[c1 - 1];
-            uint32_t pa = c0, pb = c0;
-            if (n != 0 && s <= last && e > first) {
-                pa = lds_lower_bound(s_list, c0, c1, s);
-                pb = lds_lower_bound(s_list, pa, c1, e);
-            }
+            const uint32_t pa = min(max(PA, c0), c1), pb = min(max(PB, c0), c1);
             wave_sync();
             const bool is_long = pb - pa > RS_LONG;
             if (!is_long)
@@ -471,7 +502,10 @@ __global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
             wave_sync();  // the next chunk overwrites the staging rows
         }
         wave_sync();  // the next window overwrites the list
+        w0 = w1;
+        f_cur = f_next;
     }
+#undef RS_MARKS
     if (idx < a.g_end && !huge) {
         // a Gaussian without instances (culled: radii 0) has no sums to keep; gaussian_bwd does not read them
         if (n_all != 0) {
