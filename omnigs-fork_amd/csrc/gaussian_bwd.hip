@@ -45,22 +45,19 @@ __device__ __forceinline__ void cov2d_backward(const float T0[3], const float T1
     const float b = B1[0] * T0[0] + B1[1] * T0[1] + B1[2] * T0[2];
     const float c = B1[0] * T1[0] + B1[1] * T1[1] + B1[2] * T1[2] + 0.3f;
     const float denom = a * c - b * b;
-    float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
     const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
-    if (denom2inv != 0.f) {
-        dL_da = denom2inv * (-c * c * dL_dconic.x + 2 * b * c * dL_dconic.y + (denom - a * c) * dL_dconic.z);
-        dL_dc = denom2inv * (-a * a * dL_dconic.z + 2 * a * b * dL_dconic.y + (denom - a * c) * dL_dconic.x);
-        dL_db = denom2inv * 2 * (b * c * dL_dconic.x - (denom + 2 * b * b) * dL_dconic.y + a * b * dL_dconic.z);
-        dcov[0] = (T0[0] * T0[0] * dL_da + T0[0] * T1[0] * dL_db + T1[0] * T1[0] * dL_dc);
-        dcov[3] = (T0[1] * T0[1] * dL_da + T0[1] * T1[1] * dL_db + T1[1] * T1[1] * dL_dc);
-        dcov[5] = (T0[2] * T0[2] * dL_da + T0[2] * T1[2] * dL_db + T1[2] * T1[2] * dL_dc);
-        dcov[1] = 2 * T0[0] * T0[1] * dL_da + (T0[0] * T1[1] + T0[1] * T1[0]) * dL_db + 2 * T1[0] * T1[1] * dL_dc;
-        dcov[2] = 2 * T0[0] * T0[2] * dL_da + (T0[0] * T1[2] + T0[2] * T1[0]) * dL_db + 2 * T1[0] * T1[2] * dL_dc;
-        dcov[4] = 2 * T0[2] * T0[1] * dL_da + (T0[1] * T1[2] + T0[2] * T1[1]) * dL_db + 2 * T1[1] * T1[2] * dL_dc;
-    } else {
-#pragma unroll
-        for (int i = 0; i < 6; ++i) dcov[i] = 0.f;
-    }
+    // denom2inv == 0: every gradient term is 0 (backward.cu's branch, as selects: a branch here kept part of dcov
+    // in scratch memory)
+    const bool ok = denom2inv != 0.f;
+    const float dL_da = ok ? denom2inv * (-c * c * dL_dconic.x + 2 * b * c * dL_dconic.y + (denom - a * c) * dL_dconic.z) : 0.f;
+    const float dL_dc = ok ? denom2inv * (-a * a * dL_dconic.z + 2 * a * b * dL_dconic.y + (denom - a * c) * dL_dconic.x) : 0.f;
+    const float dL_db = ok ? denom2inv * 2 * (b * c * dL_dconic.x - (denom + 2 * b * b) * dL_dconic.y + a * b * dL_dconic.z) : 0.f;
+    dcov[0] = ok ? (T0[0] * T0[0] * dL_da + T0[0] * T1[0] * dL_db + T1[0] * T1[0] * dL_dc) : 0.f;
+    dcov[3] = ok ? (T0[1] * T0[1] * dL_da + T0[1] * T1[1] * dL_db + T1[1] * T1[1] * dL_dc) : 0.f;
+    dcov[5] = ok ? (T0[2] * T0[2] * dL_da + T0[2] * T1[2] * dL_db + T1[2] * T1[2] * dL_dc) : 0.f;
+    dcov[1] = ok ? 2 * T0[0] * T0[1] * dL_da + (T0[0] * T1[1] + T0[1] * T1[0]) * dL_db + 2 * T1[0] * T1[1] * dL_dc : 0.f;
+    dcov[2] = ok ? 2 * T0[0] * T0[2] * dL_da + (T0[0] * T1[2] + T0[2] * T1[0]) * dL_db + 2 * T1[0] * T1[2] * dL_dc : 0.f;
+    dcov[4] = ok ? 2 * T0[2] * T0[1] * dL_da + (T0[1] * T1[2] + T0[2] * T1[1]) * dL_db + 2 * T1[1] * T1[2] * dL_dc : 0.f;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const float v0 = T0[0] * V[k][0] + T0[1] * V[k][1] + T0[2] * V[k][2];
