@@ -57,11 +57,10 @@ __global__ __launch_bounds__(64 * TW_WAVES) void render_bwd_kernel(RenderBwdArgs
 {
     OMR_STAMP_BEGIN
     __shared__ float4 s_geo_all[TW_WAVES][TW_BATCH];   // x, y, position in range (u32 bits), band mask (u32 bits)
-    __shared__ float4 s_quad_all[TW_WAVES][TW_BATCH];  // qa, qb, qc, opacity
+    __shared__ float4 s_quad_all[TW_WAVES][TW_BATCH];  // qa, qb, qc, log2(opacity) (tile_wave.h: column_quad)
     __shared__ float4 s_rgb_all[TW_WAVES][TW_BATCH];   // colour, gradient row slot (u32 bits)
     // rows 0-7: the held instance's eight values, rows 8-15: its partner's (wave_sum9x2_stored)
     __shared__ __attribute__((aligned(16))) float s_red_all[TW_WAVES][16 * WS_LDS_STRIDE];
-    __shared__ float s_floor_all[TW_WAVES][TW_BATCH];  // p2_floor(opacity)
 
     static_assert(TW_WAVES == 1, "one (tile, segment) unit per workgroup");
     const uint32_t wv = 0;
@@ -72,7 +71,6 @@ __global__ __launch_bounds__(64 * TW_WAVES) void render_bwd_kernel(RenderBwdArgs
     float4* s_geo = s_geo_all[wv];
     float4* s_quad = s_quad_all[wv];
     float4* s_rgb = s_rgb_all[wv];
-    float* s_floor = s_floor_all[wv];
     const TileLane tl(tile, a.gx);
     const uint32_t lane = tl.lane;
     const float pxf = (float)tl.px;
@@ -182,9 +180,8 @@ __global__ __launch_bounds__(64 * TW_WAVES) void render_bwd_kernel(RenderBwdArgs
             const uint32_t r = mask_rank(useful);
             const Quad q = quad_of_conic(co);
             s_geo[r] = make_float4(p.x, p.y, __builtin_bit_cast(float, pos), __builtin_bit_cast(float, m));
-            s_quad[r] = make_float4(q.qa, q.qb, q.qc, co.w);
+            s_quad[r] = make_float4(q.qa, q.qb, q.qc, p2_log2o(co.w));
             s_rgb[r] = make_float4(c.x, c.y, c.z, __builtin_bit_cast(float, slot));
-            s_floor[r] = p2_floor(co.w);
         }
         wave_sync();  // orders this wave's LDS stores before its reads below
         const uint32_t nuse = (uint32_t)__popcll(useful);
@@ -193,12 +190,12 @@ __global__ __launch_bounds__(64 * TW_WAVES) void render_bwd_kernel(RenderBwdArgs
             const float4 g = s_geo[j];
             const float4 qo = s_quad[j];
             const float4 f = s_rgb[j];
-            const float pfloor = s_floor[j];
             const uint32_t mb = uniform(__builtin_bit_cast(uint32_t, g.w));
             const uint32_t ipos = __builtin_bit_cast(uint32_t, g.z);
             const Quad q = {qo.x, qo.y, qo.z};
             const float dx = g.x - pxf;
-            const ColQuad kq = column_quad(q, dx);
+            const float lo = qo.w;
+            const ColQuad kq = column_quad(q, dx, lo);
             const float dy0 = g.y - (float)tl.py0;
             // dx is the same for all four of the lane's pixels (one column), so the x-moments are dx-multiples of
             // the band sums: S_u dx = dx S_u, S_u dx^2 = dx^2 S_u, S_u dx dy = dx S_u dy (applied after the bands)
@@ -214,15 +211,15 @@ __global__ __launch_bounds__(64 * TW_WAVES) void render_bwd_kernel(RenderBwdArgs
                 const float dy = dy0 - (float)(4 * b);
                 const float p2 = falloff_p2(kq, dy);
                 // backward.cu:770-781: skip positions at/after the pixel's last contributor, power > 0, alpha < 1/255
-                const bool contrib = ipos < lastb && p2_in_band(p2, pfloor);
+                const bool contrib = ipos < lastb && p2_in_band(p2, lo);
                 BWD_COUNT(1, 1);
                 if (!__ballot(contrib)) continue;
                 BWD_COUNT(2, 1);
                 BWD_COUNT(4, (uint32_t)__popcll(__ballot(contrib)));
                 any |= 1u << b;
-                // a lane that does not contribute gets G = alpha = 0: inv = 1, T and s unchanged, u = wc = 0
-                const float G = __builtin_amdgcn_exp2f(contrib ? p2 : -__builtin_inff());
-                const float alpha = fminf(0.99f, qo.w * G);
+                // a lane that does not contribute gets oG = alpha = 0: inv = 1, T and s unchanged, u = wc = 0
+                const float oG = __builtin_amdgcn_exp2f(contrib ? p2 : -__builtin_inff());  // o G (column_quad)
+                const float alpha = fminf(0.99f, oG);
                 const float inv = __builtin_amdgcn_rcpf(1.0f - alpha);
                 T[b] *= inv;
                 const float Ti = T[b];
@@ -230,7 +227,7 @@ __global__ __launch_bounds__(64 * TW_WAVES) void render_bwd_kernel(RenderBwdArgs
                 const float dL_dalpha = __builtin_fmaf(Ti, cdot, -s[b] * inv);
                 const float wc = alpha * Ti;  // dchannel/dcolour (backward.cu:800)
                 s[b] = __builtin_fmaf(cdot, wc, s[b]);
-                const float u = G * dL_dalpha;  // = dL/dopacity contribution; dL/dG * G = opacity * u
+                const float u = oG * dL_dalpha;  // dL/dG G; dL/dopacity gets u / o (raw_row_to_grads)
                 const float uy = u * dy;
                 s_uy += f2v{u, uy};
                 suyy = __builtin_fmaf(uy, dy, suyy);

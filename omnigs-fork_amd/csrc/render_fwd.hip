@@ -37,9 +37,8 @@ template <bool DEPTH>
 __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel(RenderFwdArgs a)
 {
     __shared__ float4 s_geo_all[TW_WAVES][TW_BATCH];  // x, y, position in range (u32 bits), band mask (u32 bits)
-    __shared__ float4 s_quad_all[TW_WAVES][TW_BATCH]; // qa, qb, qc, opacity
+    __shared__ float4 s_quad_all[TW_WAVES][TW_BATCH]; // qa, qb, qc, log2(opacity) (tile_wave.h: column_quad)
     __shared__ float4 s_rgb_all[TW_WAVES][TW_BATCH];  // feature (colour, or depth for DEPTH)
-    __shared__ float s_floor_all[TW_WAVES][TW_BATCH];  // p2_floor(opacity)
 
     OMR_STAMP_BEGIN
     const uint32_t wv = threadIdx.x >> 6;
@@ -48,7 +47,6 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
     float4* s_geo = s_geo_all[wv];
     float4* s_quad = s_quad_all[wv];
     float4* s_rgb = s_rgb_all[wv];
-    float* s_floor = s_floor_all[wv];
     const uint32_t tile = a.tile_order[unit / FWD_GROUPS];
     const uint32_t grp = unit % FWD_GROUPS;
     const uint32_t band0 = grp * FWD_BANDS;  // this wave's bands: band0 .. band0 + FWD_BANDS - 1
@@ -137,20 +135,19 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
             const uint32_t r = mask_rank(useful);
             const Quad q = quad_of_conic(co);
             s_geo[r] = make_float4(pos.x, pos.y, __builtin_bit_cast(float, k), __builtin_bit_cast(float, m));
-            s_quad[r] = make_float4(q.qa, q.qb, q.qc, co.w);
+            s_quad[r] = make_float4(q.qa, q.qb, q.qc, p2_log2o(co.w));
             s_rgb[r] = c;
-            s_floor[r] = p2_floor(co.w);
         }
         wave_sync();  // orders this wave's LDS stores before its reads below
         const uint32_t cnt = (uint32_t)__popcll(useful);
         for (uint32_t j = 0; j < cnt; ++j) {
             const float4 g = s_geo[j], qo = s_quad[j], f = s_rgb[j];
-            const float pfloor = s_floor[j];
             const uint32_t mb = uniform(__builtin_bit_cast(uint32_t, g.w)) & active;
             const uint32_t contributor = __builtin_bit_cast(uint32_t, g.z) + 1u;
             const Quad q = {qo.x, qo.y, qo.z};
+            const float lo = qo.w;
             const float dx = g.x - pxf;
-            const ColQuad kq = column_quad(q, dx);
+            const ColQuad kq = column_quad(q, dx, lo);
             const float dy0 = g.y - (float)tl.py(band0);
             uint64_t sat_any = 0;  // lanes that saturated at this instance (a wave mask: SALU only)
 #pragma unroll
@@ -161,9 +158,9 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
                 const bool live = T[b] > 0.0f;
                 // a done pixel (T < 0) may evaluate: its test_T is negative, so sat holds, wgt = 0, T keeps -|T| and
                 // `last` stays (wgt > 0 below) — the same results with one scalar AND less per band
-                const bool ok = p2_in_band(p2, pfloor);  // alpha >= 1/255 (tile_wave.h: p2_floor)
-                // a lane that is not ok gets alpha = 0: test_T = T, wgt = 0
-                const float alpha = fminf(0.99f, qo.w * __builtin_amdgcn_exp2f(ok ? p2 : -__builtin_inff()));
+                const bool ok = p2_in_band(p2, lo);  // power <= 0, alpha >= 1/255 (tile_wave.h)
+                // a lane that is not ok gets alpha = 0: test_T = T, wgt = 0; v_exp_f32 returns o G (column_quad)
+                const float alpha = fminf(0.99f, __builtin_amdgcn_exp2f(ok ? p2 : -__builtin_inff()));
                 const float test_T = T[b] * (1.0f - alpha);
                 // a live T is >= 1e-4 (T only takes values that passed this test) and a lane that is not ok has
                 // test_T = T, so `sat` holds for newly saturated and already done (negative) pixels alike

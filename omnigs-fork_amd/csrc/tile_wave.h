@@ -28,54 +28,63 @@ __device__ __forceinline__ Quad quad_of_conic(float4 co)
 {
     return {-0.5f * LOG2E * co.x, -LOG2E * co.y, -0.5f * LOG2E * co.z};
 }
-// A lane's pixels share one column (dx), so p2 is taken as a quadratic in dy whose dx-terms are formed once per
-// instance: p2 = A + dy (B + qc dy), A = qa dx^2, B = qb dx — two FMAs per pixel after the per-instance setup.
+// The opacity rides in the exponent: o 2^p = 2^(p + log2 o), so the staging lane adds lo = log2(o) to the constant
+// term and v_exp_f32 returns o G directly — one multiply less per (pixel, instance) in both render kernels.
+// A lane's pixels share one column (dx), so p2 = p + lo is taken as a quadratic in dy whose dx-terms are formed once
+// per instance: p2 = A + dy (B + qc dy), A = qa dx^2 + lo, B = qb dx — two FMAs per pixel after the per-instance
+// setup. Explicit FMAs: render_fwd.o and render_bwd.o are built with different contraction flags and must take the
+// same contribute / skip decisions.
 struct ColQuad {
     float A, B, C;
 };
-__device__ __forceinline__ ColQuad column_quad(const Quad& q, float dx)
+__device__ __forceinline__ ColQuad column_quad(const Quad& q, float dx, float lo)
 {
-    return {q.qa * dx * dx, q.qb * dx, q.qc};
+    return {__builtin_fmaf(q.qa * dx, dx, lo), q.qb * dx, q.qc};
 }
 __device__ __forceinline__ float falloff_p2(const ColQuad& k, float dy)
 {
     return __builtin_fmaf(dy, __builtin_fmaf(k.C, dy, k.B), k.A);
 }
 
-// The reference's skip test alpha = min(0.99, o 2^p2) < 1/255 (forward.cu:436-437, backward.cu:778-779) as a
-// bound on p2 formed once per instance: o 2^p2 >= 1/255  <=>  p2 >= -log2(255 o). Both render kernels test
-// p2 <= 0 && p2 >= p2_floor BEFORE v_exp_f32 and feed v_exp -inf for a pixel that does not contribute, so G, alpha
-// and every product built from them are exactly 0 there without per-result selects. v_log_f32 is within an ulp,
-// so the boundary moves by < 1e-6 relative in alpha (the same class as v_exp_f32 vs expf).
-// Clamped to <= 0: instances with 255 o < 1 are never staged (band_mask is 0 for them), and the clamp keeps the
-// in_band test below exact for every staged one.
-__device__ __forceinline__ float p2_floor(float opacity)
+// The reference's tests power > 0 and alpha = min(0.99, o 2^p) < 1/255 (forward.cu:434-437, backward.cu:774-779)
+// on p2 = p + log2 o: p <= 0  <=>  p2 <= lo, and o 2^p >= 1/255  <=>  p2 >= -log2(255). Both render kernels test
+// P2_FLOOR <= p2 <= lo BEFORE v_exp_f32 and feed v_exp -inf for a pixel that does not contribute, so o G, alpha and
+// every product built from them are exactly 0 there without per-result selects. v_log_f32 is within an ulp and p2
+// rounds at |p2| <= 8, so the boundary moves by ~1e-6 relative in alpha (the same class as v_exp_f32 vs expf; the
+// parity allowance's power window carries 1e-5 for the exp implementations).
+constexpr float P2_FLOOR = -7.99435343685885793769f;  // -log2(255)
+// lo of a staged instance; clamped to >= P2_FLOOR: instances with 255 o < 1 are never staged (band_mask is 0 for
+// them), and the clamp keeps the in-band test below exact for every staged one
+__device__ __forceinline__ float p2_log2o(float opacity)
 {
-    return fminf(-__builtin_amdgcn_logf(255.0f * opacity), 0.0f);
+    return fmaxf(__builtin_amdgcn_logf(opacity), P2_FLOOR);
 }
-// p2 <= 0 && p2 >= floor as ONE vector compare (floor <= 0): v_med3 returns one of its inputs, and p2 itself exactly
-// when it lies in [floor, 0]; a NaN p2 compares unequal. Two v_cmp and an s_and otherwise — the scalar unit is the
-// render forward's tighter issue port.
-__device__ __forceinline__ bool p2_in_band(float p2, float floor)
+// P2_FLOOR <= p2 <= lo as ONE vector compare: v_med3 returns one of its inputs, and p2 itself exactly when it lies in
+// [P2_FLOOR, lo]; a NaN p2 compares unequal. Two v_cmp and an s_and otherwise — the scalar unit is the render
+// forward's tighter issue port.
+__device__ __forceinline__ bool p2_in_band(float p2, float lo)
 {
-    return __builtin_amdgcn_fmed3f(p2, floor, 0.0f) == p2;
+    return __builtin_amdgcn_fmed3f(p2, P2_FLOOR, lo) == p2;
 }
 
 // The per-Gaussian factors of backward.cu:805-840 applied to a Gaussian's summed raw moments g[0..5] = S_u dx,
-// S_u dy, S_u dx^2, S_u dx dy, S_u dy^2, S_u (raster_common.h: GRAD_ROW): dG/ddelx = -G (a dx + b dy), ... With the
-// staged quadratic form q = (-a/2, -b, -c/2) log2(e):  -(a S_ux + b S_uy) = (2 / log2 e) (qa S_ux + qb/2 S_uy), so
-// dL/dmean2D.x = o W/2 (2 / log2 e) (qa S_ux + qb/2 S_uy), likewise y with (qc, qb/2) and H/2; dL/dconic = -o/2 x
-// the second moments (the reference's half-weight dconic.y slot); dL/dopacity = S_u. In place.
+// S_u dy, S_u dx^2, S_u dx dy, S_u dy^2, S_u (raster_common.h: GRAD_ROW), where u = o G dL/dalpha (the render backward's
+// v_exp_f32 returns o G, see column_quad) = dL/dG G, the weight of the mean and conic terms: dG/ddelx = -G (a dx +
+// b dy), ... With the staged quadratic form q = (-a/2, -b, -c/2) log2(e):  -(a S_ux + b S_uy) = (2 / log2 e) (qa S_ux +
+// qb/2 S_uy), so dL/dmean2D.x = W/2 (2 / log2 e) (qa S_ux + qb/2 S_uy), likewise y with (qc, qb/2) and H/2;
+// dL/dconic = -1/2 x the second moments (the reference's half-weight dconic.y slot); dL/dopacity = sum G dL/dalpha =
+// S_u / o (o >= 1/255 for every Gaussian with a row: band_mask stages none below). In place.
 __device__ __forceinline__ void raw_row_to_grads(float (&g)[9], float4 co, int W, int H)
 {
     const Quad q = quad_of_conic(co);
-    const float o = co.w, kx = (float)W / LOG2E, ky = (float)H / LOG2E;
-    const float sux = g[0], suy = g[1], hb = 0.5f * q.qb, mo = -0.5f * o;
-    g[0] = (o * kx) * __builtin_fmaf(q.qa, sux, hb * suy);
-    g[1] = (o * ky) * __builtin_fmaf(q.qc, suy, hb * sux);
-    g[2] = mo * g[2];
-    g[3] = mo * g[3];
-    g[4] = mo * g[4];
+    const float kx = (float)W / LOG2E, ky = (float)H / LOG2E;
+    const float sux = g[0], suy = g[1], hb = 0.5f * q.qb;
+    g[0] = kx * __builtin_fmaf(q.qa, sux, hb * suy);
+    g[1] = ky * __builtin_fmaf(q.qc, suy, hb * sux);
+    g[2] = -0.5f * g[2];
+    g[3] = -0.5f * g[3];
+    g[4] = -0.5f * g[4];
+    g[5] = g[5] != 0.0f ? g[5] / co.w : g[5];  // a Gaussian without rows keeps +0 (any opacity, 0 included)
 }
 
 // one lane's view of a tile: pixel coordinates of its band pixels; band b of the tile = rows 4b..4b+3
