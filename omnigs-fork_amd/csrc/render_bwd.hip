@@ -10,7 +10,8 @@
 // so the wave of a segment starts at its upper boundary from that state (or from the final state for a pixel whose
 // last contributor lies in front of it) and replays only its own positions. Units are ordered longest first by
 // the forward's per-segment work (sort.hip: backward_schedule_kernel): long tiles no longer form the launch's tail. For each instance the wave accumulates, per lane and over the bands the instance reaches,
-// nine moments of the pixel weights u = G * dL/dalpha and the colour weights alpha * T:
+// nine moments of the pixel weights u = o G * dL/dalpha (v_exp_f32 returns o G: tile_wave.h, column_quad) and the
+// colour weights alpha * T:
 //     S_u, S_u dx, S_u dy, S_u dx^2, S_u dx dy, S_u dy^2, S_aT dpix_{r,g,b}
 // (a lane's four pixels share one column, so only S_u, S_u dy, S_u dy^2 are summed per band; the x-moments are
 // their dx-multiples)
