@@ -61,6 +61,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
     float T[FWD_BANDS], C0[FWD_BANDS], C1[FWD_BANDS], C2[FWD_BANDS];
     uint32_t last[FWD_BANDS];
     uint32_t active = 0;  // local bands with at least one unsaturated in-image pixel (wave-uniform)
+    uint64_t done[FWD_BANDS];  // per band, the lanes whose pixel is done (saturated or outside the image): SGPR masks
     uint32_t work = 0;    // (instance, band) pairs staged for evaluation (omr_debug_tile_cost, bench.py's VALU secondary)
 #pragma unroll
     for (int b = 0; b < FWD_BANDS; ++b) {
@@ -68,7 +69,8 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
         T[b] = inside ? 1.0f : -1.0f;
         C0[b] = C1[b] = C2[b] = 0.f;
         last[b] = 0;
-        if (__ballot(inside)) active |= 1u << b;
+        done[b] = __ballot(!inside);
+        if (~done[b]) active |= 1u << b;
     }
 
     // a count past the capacity or a failed look-back: the binning kernels did nothing and the ranges stay empty
@@ -155,7 +157,6 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
                 if (!(mb & (1u << b))) continue;  // scalar branch
                 const float dy = dy0 - (float)(4 * b);
                 const float p2 = falloff_p2(kq, dy);
-                const bool live = T[b] > 0.0f;
                 // a done pixel (T < 0) may evaluate: its test_T is negative, so sat holds, wgt = 0, T keeps -|T| and
                 // `last` stays (wgt > 0 below) — the same results with one scalar AND less per band
                 const bool ok = p2_in_band(p2, lo);  // power <= 0, alpha >= 1/255 (tile_wave.h)
@@ -165,21 +166,24 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
                 // a live T is >= 1e-4 (T only takes values that passed this test) and a lane that is not ok has
                 // test_T = T, so `sat` holds for newly saturated and already done (negative) pixels alike
                 const bool sat = test_T < 0.0001f;
-                // newly saturated = live && sat (a live lane that is not ok keeps test_T = T >= 1e-4); two ballots of
-                // plain compares stay in SGPRs, a ballot of their conjunction goes through a VGPR
-                sat_any |= __ballot(live) & __ballot(sat);
+                // the done lanes are exactly the sat ones from here on: a mask OR on the scalar unit tracks them
+                // (a ballot of a plain compare stays in SGPRs), no per-band compare of T's sign
+                const uint64_t satm = __ballot(sat);
+                sat_any |= satm & ~done[b];  // newly saturated lanes
+                done[b] |= satm;
                 const float wgt = sat ? 0.0f : alpha * T[b];
                 C0[b] = __builtin_fmaf(f.x, wgt, C0[b]);
                 C1[b] = __builtin_fmaf(f.y, wgt, C1[b]);
                 C2[b] = __builtin_fmaf(f.z, wgt, C2[b]);
                 T[b] = sat ? -fabsf(T[b]) : test_T;  // done: keeps the last live T, negated
-                // blended iff wgt > 0: alpha >= 1/255 and T >= 1e-4 make wgt >= 3.9e-7 on every contributing lane
-                last[b] = wgt > 0.0f ? contributor : last[b];
+                // blended iff ok and not sat (alpha >= 1/255, T >= 1e-4: wgt > 0); a done lane is sat. Both are compare
+                // masks already, so this is a scalar and-not, not a third vector compare
+                last[b] = (ok && !sat) ? contributor : last[b];
             }
             if (sat_any) {  // some pixel saturated: drop bands with no live pixel left
 #pragma unroll
                 for (int b = 0; b < FWD_BANDS; ++b)
-                    if (!__ballot(T[b] > 0.0f)) active &= ~(1u << b);
+                    if (!~done[b]) active &= ~(1u << b);
                 if (!active) break;
             }
         }
