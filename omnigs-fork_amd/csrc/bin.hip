@@ -108,12 +108,7 @@ template <int THREADS>
 __device__ __forceinline__ uint32_t bin_block_scan(uint32_t x, uint32_t* s_wave, uint32_t* total)
 {
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    uint32_t inc = x;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
-        if (lane >= (uint32_t)o) inc += y;
-    }
+    const uint32_t inc = wave_incl_sum_u32(x);
     if (lane == 63) s_wave[w] = inc;
     __syncthreads();
     uint32_t off = 0, tot = 0;
@@ -165,12 +160,7 @@ __device__ __forceinline__ void owner_fill(uint16_t* s_own, uint32_t* s_wave)
     uint32_t v[8] = {q.x & 0xFFFFu, q.x >> 16, q.y & 0xFFFFu, q.y >> 16, q.z & 0xFFFFu, q.z >> 16, q.w & 0xFFFFu, q.w >> 16};
 #pragma unroll
     for (int i = 1; i < 8; ++i) v[i] = max(v[i], v[i - 1]);
-    uint32_t inc = v[7];
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
-        if (lane >= (uint32_t)o) inc = max(inc, y);
-    }
+    const uint32_t inc = wave_incl_max_u32(v[7]);
     if (lane == 63) s_wave[w] = inc;
     uint32_t prev = (uint32_t)__shfl_up((int)inc, 1, 64);
     if (lane == 0) prev = 0;
@@ -462,12 +452,7 @@ __global__ __launch_bounds__(RB_THREADS) void rows_scatter_kernel(BinArgs a)
             const uint32_t j = q * RB_THREADS + tid;
             e8[q] = j < nvalid ? s_sorted[j] : 0u;
             const uint32_t wd = j < nvalid ? (s_xw[e8[q] & 0xFFFFu] & 0xFFFFu) : 0u;
-            uint32_t inc = wd;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
-                if (lane >= (uint32_t)o) inc += y;
-            }
+            const uint32_t inc = wave_incl_sum_u32(wd);
             wp[q] = inc - wd;  // exclusive within the wave
             if (lane == 63) s_qtot[q][w] = inc;
         }

@@ -357,13 +357,9 @@ static_assert(RS_RPL == 8, "8-B mark loads");
 
 __device__ __forceinline__ uint32_t wave_exclusive_scan_u32(uint32_t x, uint32_t lane, uint32_t* total)
 {
-    uint32_t inc = x;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
-        if (lane >= (uint32_t)o) inc += y;
-    }
-    *total = (uint32_t)__shfl((int)inc, 63, 64);
+    (void)lane;
+    const uint32_t inc = wave_incl_sum_u32(x);
+    *total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
     return inc - x;
 }
 

@@ -410,6 +410,37 @@ __device__ __forceinline__ uint32_t band_mask(float2 xy, float4 co, uint32_t tx,
 }
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// Wave64 inclusive scans on DPP (gfx9 row_shr / row_bcast): four row_shr levels scan each 16-lane row, then
+// row_bcast:15 carries rows 0 / 2 into rows 1 / 3 and row_bcast:31 carries row 1 into rows 2 and 3. Six VALU ops with
+// no LDS round trip, where the __shfl_up ladder issues six dependent ds_bpermute. All 64 lanes must be active.
+// dpp_ctrl: row_shr:n = 0x110 + n, row_bcast:15 = 0x142, row_bcast:31 = 0x143.
+template <int CTRL, int ROW_MASK, bool BOUND_ZERO>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW_MASK, 0xf, BOUND_ZERO);
+}
+__device__ __forceinline__ uint32_t wave_incl_sum_u32(uint32_t x)
+{
+    x += dpp_u32<0x111, 0xf, true>(x);  // lanes without a source read 0 (bound_ctrl)
+    x += dpp_u32<0x112, 0xf, true>(x);
+    x += dpp_u32<0x114, 0xf, true>(x);
+    x += dpp_u32<0x118, 0xf, true>(x);
+    x += dpp_u32<0x142, 0xa, false>(x);  // rows 1, 3 += lane 15 / 47; rows 0, 2 add the old value 0
+    x += dpp_u32<0x143, 0xc, false>(x);  // rows 2, 3 += lane 31
+    return x;
+}
+// the same for max (values >= 0: the zero fill is the identity)
+__device__ __forceinline__ uint32_t wave_incl_max_u32(uint32_t x)
+{
+    x = max(x, dpp_u32<0x111, 0xf, true>(x));
+    x = max(x, dpp_u32<0x112, 0xf, true>(x));
+    x = max(x, dpp_u32<0x114, 0xf, true>(x));
+    x = max(x, dpp_u32<0x118, 0xf, true>(x));
+    x = max(x, dpp_u32<0x142, 0xa, false>(x));
+    x = max(x, dpp_u32<0x143, 0xc, false>(x));
+    return x;
+}
 // number of set bits of `mask` below this lane
 __device__ __forceinline__ uint32_t mask_rank(uint64_t mask)
 {

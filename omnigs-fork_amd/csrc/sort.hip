@@ -27,16 +27,7 @@ namespace omr {
 
 namespace {
 
-__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x)
-{
-    const uint32_t lane = lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
-    }
-    return x;
-}
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) { return wave_incl_sum_u32(x); }
 
 // block-wide exclusive scan of one value per thread (THREADS threads); returns the block total via *total
 template <int THREADS = SCAN_THREADS>
