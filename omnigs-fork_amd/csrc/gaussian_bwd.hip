@@ -238,12 +238,7 @@ constexpr int RS_Q = RS_ROWS / 64;    // rows per lane per chunk
 #endif
 constexpr uint32_t RS_LONG = OMR_RS_LONG;
 
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
-{
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return v;
-}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) { return ~wave_max_u32(~v); }  // DPP (tile_wave.h)
 
 __device__ __forceinline__ void add_marked_row(float* acc, const float* __restrict__ inst_grad, uint32_t row, bool ok)
 {

@@ -61,20 +61,36 @@ constexpr uint32_t LB_SPIN_MAX = OMR_LB_SPIN_MAX;  // polls of one status word b
                                                    // error word (capi.hip reports it as OMR_ERR_HIP; a test build shrinks it)
 constexpr uint64_t SLB_AGG = 1ull << 62, SLB_PRE = 2ull << 62, SLB_VAL = SLB_AGG - 1;
 
-__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src)
+// lane `src` (wave-uniform) of a 64-bit value: two v_readlane, no LDS crossbar
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, uint32_t src)
 {
-    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)src);
     return ((uint64_t)hi << 32) | lo;
+}
+// Sum over the wave on every lane, by DPP inside each 16-lane row (quad_perm xor1 / xor2, row_ror 4 / 8) and
+// v_permlane16/32_swap across rows (as tile_wave.h: wave_max_u32): no ds_bpermute round trips on the look-back's path
+template <int CTRL>
+__device__ __forceinline__ uint64_t add_dpp_u64(uint64_t v)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xf, 0xf, true);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), CTRL, 0xf, 0xf, true);
+    return v + (((uint64_t)hi << 32) | lo);
 }
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o, 64);
-        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o, 64);
-        v += ((uint64_t)hi << 32) | lo;
-    }
-    return v;
+    v = add_dpp_u64<0xb1>(v);   // quad_perm [1,0,3,2]
+    v = add_dpp_u64<0x4e>(v);   // quad_perm [2,3,0,1]
+    v = add_dpp_u64<0x124>(v);  // row_ror:4
+    v = add_dpp_u64<0x128>(v);  // row_ror:8
+    uint32_t alo = (uint32_t)v, blo = alo, ahi = (uint32_t)(v >> 32), bhi = ahi;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(alo), "+v"(blo));
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(ahi), "+v"(bhi));
+    v = (((uint64_t)ahi << 32) | alo) + (((uint64_t)bhi << 32) | blo);
+    alo = (uint32_t)v, blo = alo, ahi = (uint32_t)(v >> 32), bhi = ahi;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(alo), "+v"(blo));
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(ahi), "+v"(bhi));
+    return (((uint64_t)ahi << 32) | alo) + (((uint64_t)bhi << 32) | blo);
 }
 
 // Called by all 64 lanes of one wave of tile vb: publishes `total`, returns the exclusive prefix of the tile (on every
@@ -96,7 +112,7 @@ __device__ uint64_t wave_lookback(uint64_t* status, uint32_t vb, uint32_t total,
         const uint64_t stop = __ballot((st & ~SLB_VAL) != SLB_AGG);  // PRE or not yet published
         const uint32_t k = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
         excl += wave_sum_u64(lane < k || (lane == k && (st & SLB_PRE)) ? (st & SLB_VAL) : 0ull);
-        if (k < 64u && (shfl_u64(st, (int)k) & SLB_PRE)) break;
+        if (k < 64u && (readlane_u64(st, k) & SLB_PRE)) break;
         if (k == 0 && ++spins > LB_SPIN_MAX) {
             if (lane == 0) atomicOr(err, 1u);
             break;
