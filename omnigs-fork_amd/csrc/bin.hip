@@ -195,10 +195,11 @@ __device__ __forceinline__ void rank_items(const uint32_t (&d)[G::ROUNDS], const
     for (int r = 0; r < G::ROUNDS; ++r) {
         const uint64_t peers = wave_match_digit<BITS>(d[r], valid[r]);
         const uint32_t rank = mask_rank(peers);
-        const uint32_t prev = valid[r] ? s_whist[w][d[r]] : 0u;
-        lr[r] = prev + rank;
-        __builtin_amdgcn_wave_barrier();  // every lane has read the count (LDS ops of a wave complete in order)
-        if (valid[r] && rank == 0) s_whist[w][d[r]] = prev + (uint32_t)__popcll(peers);
+        // LDS ops of a wave complete in issue order: every lane reads the count before the leader's add lands, and
+        // the next round's read sees it; the add returns nothing, so no round waits for the previous one's read
+        lr[r] = (valid[r] ? s_whist[w][d[r]] : 0u) + rank;
+        __builtin_amdgcn_wave_barrier();
+        if (valid[r] && rank == 0) atomicAdd(&s_whist[w][d[r]], (uint32_t)__popcll(peers));
         __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();

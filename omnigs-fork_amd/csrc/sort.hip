@@ -488,11 +488,11 @@ __global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const K* keys_
         const uint32_t d = (k[r] >> shift) & (RADIX - 1);
         const uint64_t peers = wave_match_digit<RADIX_BITS>(d, valid);
         const uint32_t rank = mask_rank(peers);
-        const uint32_t prev = valid ? s_whist[w][d] : 0u;
-        lr[r] = prev + rank;
-        // every lane of the wave has read the count (LDS ops of a wave complete in order) before the leader stores
+        // LDS ops of a wave complete in issue order: every lane reads the count before the leader's add lands, and
+        // the next round's read sees it. The add needs no value back, so no round waits for the previous one
+        lr[r] = (valid ? s_whist[w][d] : 0u) + rank;
         __builtin_amdgcn_wave_barrier();
-        if (valid && rank == 0) s_whist[w][d] = prev + (uint32_t)__popcll(peers);
+        if (valid && rank == 0) atomicAdd(&s_whist[w][d], (uint32_t)__popcll(peers));
         __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
@@ -665,10 +665,9 @@ __global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, 
         const uint32_t d = (k[r] >> shift) & (RADIX - 1);
         const uint64_t peers = wave_match_digit<RADIX_BITS>(d, valid);
         const uint32_t rank = mask_rank(peers);
-        const uint32_t prev = valid ? s_whist[w][d] : 0u;
-        lr[r] = prev + rank;
+        lr[r] = (valid ? s_whist[w][d] : 0u) + rank;  // in-order LDS: read, then the leader's add (as above)
         __builtin_amdgcn_wave_barrier();
-        if (valid && rank == 0) s_whist[w][d] = prev + (uint32_t)__popcll(peers);
+        if (valid && rank == 0) atomicAdd(&s_whist[w][d], (uint32_t)__popcll(peers));
         __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
