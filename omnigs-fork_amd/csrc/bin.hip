@@ -188,8 +188,8 @@ __device__ __forceinline__ void rank_items(const uint32_t (&d)[G::ROUNDS], const
     for (uint32_t i = tid; i < G::WAVES * NB; i += G::THREADS) (&s_whist[0][0])[i] = 0;
     __syncthreads();
     // per round: the lanes with this lane's digit (a match by BITS ballots); the group's lowest lane advances the wave's
-    // running count of the digit after every lane of the wave has read it (a read-then-write per round measured faster
-    // than a ds_add_rtn per group plus a broadcast: config E tile sort 1.78 vs 2.14 ms)
+    // running count of the digit after every lane of the wave has read it, with an add that returns nothing (a
+    // ds_add_rtn per group plus a broadcast measured slower: config E tile sort 1.78 vs 2.14 ms)
     uint32_t lr[G::ROUNDS];
 #pragma unroll
     for (int r = 0; r < G::ROUNDS; ++r) {
