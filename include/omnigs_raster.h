@@ -261,6 +261,7 @@ int omr_debug_counters(char* geom_buffer, int P, uint32_t* dst, void* stream);
 int omr_debug_wave_sum9(const float* in, float* out, void* stream); /* wave_sum9_rows */
 int omr_debug_wave_sum9_lds(const float* in, float* out, void* stream); /* wave_sum9_lds (render backward, unpaired) */
 int omr_debug_wave_sum9x2(const float* in, float* out, void* stream); /* wave_sum9x2_stored: [2][64][9] -> [2][9] (render backward) */
+int omr_debug_wave_scans(const uint32_t* in, uint32_t* out, void* stream); /* DPP wave scans: [2][64] -> [3][64] (incl. sum, incl. max, wave max) */
 int omr_debug_geometry(char* geom_buffer, int P, float* means2D, float* conic_opacity, float* rgb, float* depths,
                        uint32_t* tiles_touched, void* stream);
 

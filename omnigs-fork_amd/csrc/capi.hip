@@ -21,6 +21,7 @@
 
 #include "../../include/omnigs_raster.h"
 #include "kernels.h"
+#include "tile_wave.h"
 #include "wave_ops.h"
 
 namespace omr {
@@ -67,6 +68,16 @@ __global__ __launch_bounds__(64) void debug_wave_sum9x2_kernel(const float* in, 
     const uint32_t k = lane >> 2;
     if ((lane & 3) == 0) out[(k >> 3) * 9 + (k & 7)] = tv;
     if ((lane & 31) == 1) out[(lane >> 5) * 9 + 8] = t8;
+}
+
+// the DPP wave scans of raster_common.h (every block scan of the sorts and the binning): in [2][64] u32, out [3][64] =
+// inclusive sum of in[0], inclusive max of in[1], the wave max of in[1] on every lane (tile_wave.h)
+__global__ __launch_bounds__(64) void debug_wave_scans_kernel(const uint32_t* in, uint32_t* out)
+{
+    const uint32_t lane = threadIdx.x;
+    out[lane] = wave_incl_sum_u32(in[lane]);
+    out[64 + lane] = wave_incl_max_u32(in[64 + lane]);
+    out[128 + lane] = wave_max_u32(in[64 + lane]);
 }
 
 __global__ __launch_bounds__(256) void debug_point_ids_kernel(const uint32_t* list, size_t n, uint32_t* out)
@@ -1116,6 +1127,13 @@ int omr_debug_wave_sum9x2(const float* in, float* out, void* stream)
     g_last_error.clear();
     debug_wave_sum9x2_kernel<<<1, 64, 0, (hipStream_t)stream>>>(in, out);
     return hip_check("debug_wave_sum9x2");
+}
+
+int omr_debug_wave_scans(const uint32_t* in, uint32_t* out, void* stream)
+{
+    g_last_error.clear();
+    debug_wave_scans_kernel<<<1, 64, 0, (hipStream_t)stream>>>(in, out);
+    return hip_check("debug_wave_scans");
 }
 
 

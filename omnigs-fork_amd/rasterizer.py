@@ -77,6 +77,7 @@ def lib() -> C.CDLL:
         L.omr_debug_wave_sum9.argtypes = [vp, vp, vp]
         L.omr_debug_wave_sum9_lds.argtypes = [vp, vp, vp]
         L.omr_debug_wave_sum9x2.argtypes = [vp, vp, vp]
+        L.omr_debug_wave_scans.argtypes = [vp, vp, vp]
         L.omr_profile_enable.argtypes = [i]
         L.omr_sh_grad_from_colors.argtypes = [i, i, i, i, vp, vp, vp, vp, vp, vp]
         L.omr_sh_grad_from_colors_packed.restype = i
@@ -581,6 +582,17 @@ def debug_wave_sum(x: torch.Tensor, lds: bool = False) -> torch.Tensor:
     out = torch.empty(9, dtype=torch.float32, device=x.device)
     fn = lib().omr_debug_wave_sum9_lds if lds else lib().omr_debug_wave_sum9
     _check(fn(x.data_ptr(), out.data_ptr(), _stream(x.device)), "debug_wave_sum")
+    return out
+
+
+def debug_wave_scans(x: torch.Tensor) -> torch.Tensor:
+    """The DPP wave scans of raster_common.h on a [2, 64] int32 device tensor (u32 bits): returns [3, 64] = the
+    inclusive sum of x[0], the inclusive max of x[1], and the wave max of x[1] on every lane."""
+    if not x.is_cuda or x.dtype != torch.int32 or tuple(x.shape) != (2, 64):
+        raise ValueError("x must be a [2, 64] int32 tensor on the HIP device")
+    x = x.contiguous()
+    out = torch.empty((3, 64), dtype=torch.int32, device=x.device)
+    _check(lib().omr_debug_wave_scans(x.data_ptr(), out.data_ptr(), _stream(x.device)), "debug_wave_scans")
     return out
 
 

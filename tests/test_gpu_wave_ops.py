@@ -55,3 +55,18 @@ def test_wave_sum_pair_lane_identity(omr):
                  dtype=np.float32)
     got = omr.rasterizer.debug_wave_sum_pair(torch.from_numpy(x).cuda()).cpu().numpy()
     np.testing.assert_array_equal(got, x.astype(np.float64).sum(axis=1))
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_dpp_wave_scans(seed, omr):
+    """raster_common.h: wave_incl_sum_u32 / wave_incl_max_u32 (row_shr + row_bcast DPP; every block scan of the sorts,
+    look-back scans and row binning) and tile_wave.h: wave_max_u32, against numpy on full 64-lane waves."""
+    import torch
+
+    rng = np.random.default_rng(seed)
+    hi = [1 << 20, 1 << 31, 4][seed]  # seed 1: large values (wrapping u32 sums), seed 2: many equal values
+    x = rng.integers(0, hi, size=(2, 64), dtype=np.uint64).astype(np.uint32)
+    got = omr.rasterizer.debug_wave_scans(torch.from_numpy(x.view(np.int32)).cuda()).cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got[0], np.cumsum(x[0], dtype=np.uint64).astype(np.uint32))
+    np.testing.assert_array_equal(got[1], np.maximum.accumulate(x[1]))
+    np.testing.assert_array_equal(got[2], np.full(64, x[1].max(), dtype=np.uint32))
