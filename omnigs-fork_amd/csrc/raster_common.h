@@ -163,12 +163,13 @@ __host__ __device__ inline size_t row_valid_offset(size_t L)
 #define OMR_BWD_CK 1024
 #endif
 constexpr uint32_t CKPT = OMR_BWD_CK;
-// bands per forward wave (render_fwd.hip): 2 = each tile is rendered by two independent waves ("groups")
-#ifndef OMR_FWD_BANDS
-#define OMR_FWD_BANDS 2
-#endif
-constexpr int FWD_BANDS = OMR_FWD_BANDS;
-constexpr int FWD_GROUPS = 4 / FWD_BANDS;
+// forward waves per tile (render_fwd.hip: launch_render_forward picks 2 bands per wave, i.e. two waves per tile, or
+// 4 bands, one wave per tile, by the view's tile count); max_contrib keeps FWD_GROUPS slots per tile either way
+constexpr int FWD_GROUPS = 2;
+// views with at least this many tiles render one wave per tile: enough waves to fill the chip without splitting, and
+// each tile's instances staged once (config E, 32 k tiles: render_fwd 0.476 -> 0.449 ms; config C, 8 k tiles: 0.272
+// with two waves per tile vs 0.295 with one, profiles/r03z_ab_fwd_bands.txt)
+constexpr uint32_t FWD_ONE_WAVE_TILES = 16384;
 __host__ __device__ inline size_t ckpt_count(size_t L) { return L / CKPT + 1; }
 __host__ __device__ inline size_t seg_count(size_t L, uint32_t T) { return (size_t)T + L / CKPT + 1; }
 // the L-indexed region of the binning buffer, after row_valid: checkpoints [ckpt_count][256 pixels] float4

@@ -25,17 +25,18 @@ namespace omr {
 
 namespace {
 
-// bands per wave (FWD_BANDS, raster_common.h): 4 = one wave per tile; 2 or 1 split a tile over 2 or 4 independent
-// waves (shorter work units for load balance; each wave stages the tile's instances itself)
+// bands per wave (NB): 4 = one wave per tile; 2 splits a tile over 2 independent waves (shorter work units for load
+// balance and occupancy on views of few tiles; each wave stages the tile's instances itself)
 #ifndef OMR_FWD_MINW
 #define OMR_FWD_MINW 8
 #endif
 
 OMR_STAMP_DECL(g_stamps_fwd)
 
-template <bool DEPTH>
+template <bool DEPTH, int FWD_BANDS>
 __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel(RenderFwdArgs a)
 {
+    constexpr uint32_t NG = 4 / FWD_BANDS;  // waves per tile
     __shared__ float4 s_geo_all[TW_WAVES][TW_BATCH];  // x, y, position in range (u32 bits), band mask (u32 bits)
     __shared__ float4 s_quad_all[TW_WAVES][TW_BATCH]; // qa, qb, qc, log2(opacity) (tile_wave.h: column_quad)
     __shared__ float4 s_rgb_all[TW_WAVES][TW_BATCH];  // feature (colour, or depth for DEPTH)
@@ -43,12 +44,12 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
     OMR_STAMP_BEGIN
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t unit = xcd_remap(blockIdx.x, gridDim.x) * TW_WAVES + wv;
-    if (unit >= a.gx * a.gy * FWD_GROUPS) return;  // wave-uniform; the block's waves never synchronise
+    if (unit >= a.gx * a.gy * NG) return;  // wave-uniform; the block's waves never synchronise
     float4* s_geo = s_geo_all[wv];
     float4* s_quad = s_quad_all[wv];
     float4* s_rgb = s_rgb_all[wv];
-    const uint32_t tile = a.tile_order[unit / FWD_GROUPS];
-    const uint32_t grp = unit % FWD_GROUPS;
+    const uint32_t tile = a.tile_order[unit / NG];
+    const uint32_t grp = unit % NG;
     const uint32_t band0 = grp * FWD_BANDS;  // this wave's bands: band0 .. band0 + FWD_BANDS - 1
     const TileLane tl(tile, a.gx);
     const uint32_t lane = tl.lane;
@@ -213,6 +214,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
     }
     maxc = wave_max_u32(maxc);
     if (lane == 0) a.max_contrib[(size_t)tile * FWD_GROUPS + grp] = maxc;
+    if (NG == 1 && lane == 1) a.max_contrib[(size_t)tile * FWD_GROUPS + 1] = 0u;  // one wave: the second slot empty
     if (lane == 0 && work) atomicAdd(&a.tile_cost[tile], work);
     OMR_STAMP_END(g_stamps_fwd, unit);
 }
@@ -223,10 +225,15 @@ void launch_render_forward(const RenderFwdArgs& a, bool depth_mode, hipStream_t 
 {
     const uint32_t T = a.gx * a.gy;
     if (T == 0) return;
-    const uint32_t units = T * FWD_GROUPS;
-    const uint32_t blocks = div_up(units, TW_WAVES);
-    if (depth_mode) render_fwd_kernel<true><<<blocks, 64 * TW_WAVES, 0, s>>>(a);
-    else render_fwd_kernel<false><<<blocks, 64 * TW_WAVES, 0, s>>>(a);
+    if (T >= FWD_ONE_WAVE_TILES) {
+        const uint32_t blocks = div_up(T, TW_WAVES);
+        if (depth_mode) render_fwd_kernel<true, 4><<<blocks, 64 * TW_WAVES, 0, s>>>(a);
+        else render_fwd_kernel<false, 4><<<blocks, 64 * TW_WAVES, 0, s>>>(a);
+    } else {
+        const uint32_t blocks = div_up(T * 2, TW_WAVES);
+        if (depth_mode) render_fwd_kernel<true, 2><<<blocks, 64 * TW_WAVES, 0, s>>>(a);
+        else render_fwd_kernel<false, 2><<<blocks, 64 * TW_WAVES, 0, s>>>(a);
+    }
 }
 
 #ifdef OMR_STAMPS
