@@ -267,6 +267,15 @@ def test_pinhole_render_depth():
     _compare(g, cam, None, render_depth=True)
 
 
+@pytest.mark.parametrize("cam_t,depth", [(LON, False), (PIN, True)], ids=["lonlat", "pinhole_depth"])
+def test_one_wave_per_tile_forward(cam_t, depth):
+    """Views of at least FWD_ONE_WAVE_TILES (16384) tiles render with one forward wave per tile (render_fwd.hip:
+    launch_render_forward, 4 bands per wave); smaller views with two. 2048 x 2048 = 128 x 128 tiles takes the
+    one-wave kernel, colour (with the backward) and depth mode, against the oracle."""
+    g, cam, dL = make_case(20000, 2048, 2048, cam_t, 31, spread=4.0)
+    _compare(g, cam, None if depth else dL, nthreads=oracle_threads(), render_depth=depth)
+
+
 def test_empty_scene_returns_zero_image():
     g, cam, dL = make_case(0, 64, 32, LON, 24)
     h = hip_run(g, cam, dL, bg=(1.0, 1.0, 1.0))
