@@ -358,7 +358,12 @@ __device__ __forceinline__ uint32_t wave_exclusive_scan_u32(uint32_t x, uint32_t
     return inc - x;
 }
 
-__global__ __launch_bounds__(256) void row_sum_kernel(RowSumArgs a)
+// six waves per SIMD (80 VGPRs, 36 B of spills) instead of five: the row sums are latency-bound (E 0.211 -> 0.205 ms,
+// C unchanged: profiles/r03z_ab_row_sums_waves.txt)
+#ifndef OMR_RS_MINW
+#define OMR_RS_MINW 6
+#endif
+__global__ __launch_bounds__(256, OMR_RS_MINW) void row_sum_kernel(RowSumArgs a)
 {
     __shared__ float s_rows_all[4][RS_ROWS * GRAD_ROW];  // row-major, 9 floats per row (odd stride: no conflicts)
     __shared__ uint32_t s_list_all[4][RS_WIN];
