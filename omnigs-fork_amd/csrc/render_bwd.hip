@@ -34,6 +34,8 @@
 // equals T_i c_i . dL/dpix - s / (1 - alpha_i): the same quantity, rounded differently.
 // T_i is recovered with v_rcp_f32 (T_{i+1} / (1 - alpha_i)), as the reference divides (backward.cu:782).
 // Instances at or behind every band's last contributor are skipped.
+#include <type_traits>
+
 #include "kernels.h"
 #include "tile_wave.h"
 #include "wave_ops.h"
@@ -82,6 +84,11 @@ __global__ __launch_bounds__(64 * TW_WAVES) void render_bwd_kernel(RenderBwdArgs
     float dp2[TW_BANDS];
     uint32_t last[TW_BANDS];
     uint32_t band_end[TW_BANDS];  // wave-uniform: max last contributor of the band
+    // wave-uniform: below this position every pixel of the tile that has a last contributor is in front of it. A pixel
+    // without one has no in-band instance in the tile's list at all (the forward blends every in-band instance until
+    // saturation, with the same arithmetic), so it imposes nothing; a pixel outside the image (T = 0, dL/dpix = 0)
+    // imposes 0 so that it never marks a row
+    uint32_t min_last = ~0u;
     // the four bands' per-pixel loads are issued together (addresses clamped to pixel 0 outside the image, the
     // values masked after), so the prologue waits for one round trip per group instead of one per band
     bool inside[TW_BANDS];
@@ -99,6 +106,7 @@ __global__ __launch_bounds__(64 * TW_WAVES) void render_bwd_kernel(RenderBwdArgs
     for (int b = 0; b < TW_BANDS; ++b) {
         last[b] = inside[b] ? last[b] : 0u;
         band_end[b] = uniform(wave_max_u32(last[b]));
+        min_last = min(min_last, ~uniform(wave_max_u32(~(inside[b] ? (last[b] ? last[b] : ~0u) : 0u))));
         max_c = max(max_c, band_end[b]);
     }
     const uint2 range = a.ranges[tile];
@@ -187,92 +195,98 @@ __global__ __launch_bounds__(64 * TW_WAVES) void render_bwd_kernel(RenderBwdArgs
         wave_sync();  // orders this wave's LDS stores before its reads below
         const uint32_t nuse = (uint32_t)__popcll(useful);
         BWD_COUNT(0, nuse);
-        for (uint32_t j = 0; j < nuse; ++j) {
-            const float4 g = s_geo[j];
-            const float4 qo = s_quad[j];
-            const float4 f = s_rgb[j];
-            const uint32_t mb = uniform(__builtin_bit_cast(uint32_t, g.w));
-            const uint32_t ipos = __builtin_bit_cast(uint32_t, g.z);
-            const Quad q = {qo.x, qo.y, qo.z};
-            const float dx = g.x - pxf;
-            const float lo = qo.w;
-            const ColQuad kq = column_quad(q, dx, lo);
-            const float dy0 = g.y - (float)tl.py0;
-            // dx is the same for all four of the lane's pixels (one column), so the x-moments are dx-multiples of
-            // the band sums: S_u dx = dx S_u, S_u dx^2 = dx^2 S_u, S_u dx dy = dx S_u dy (applied after the bands)
-            f2v s_uy = {0.f, 0.f};  // S_u, S_u dy
-            f2v sc01 = {0.f, 0.f};  // S_aT dpix_r, S_aT dpix_g
-            float suyy = 0.f, sc2 = 0.f;
-            uint32_t any = 0;  // bands with a contributing pixel (set in wave-uniform branches: an SGPR)
-#pragma unroll
-            for (int b = 0; b < TW_BANDS; ++b) {
-                if (!(mb & (1u << b))) continue;  // scalar branch
-                const float dp0b = dp01[b].x, dp1b = dp01[b].y, dp2b = dp2[b];
-                const uint32_t lastb = last[b];
-                const float dy = dy0 - (float)(4 * b);
-                const float p2 = falloff_p2(kq, dy);
-                // backward.cu:770-781: skip positions at/after the pixel's last contributor, power > 0, alpha < 1/255
-                const bool contrib = ipos < lastb && p2_in_band(p2, lo);
-                BWD_COUNT(1, 1);
-                if (!__ballot(contrib)) continue;
-                BWD_COUNT(2, 1);
-                BWD_COUNT(4, (uint32_t)__popcll(__ballot(contrib)));
-                any |= 1u << b;
-                // a lane that does not contribute gets oG = alpha = 0: inv = 1, T and s unchanged, u = wc = 0
-                const float oG = __builtin_amdgcn_exp2f(contrib ? p2 : -__builtin_inff());  // o G (column_quad)
-                const float alpha = fminf(0.99f, oG);
-                const float inv = __builtin_amdgcn_rcpf(1.0f - alpha);
-                T[b] *= inv;
-                const float Ti = T[b];
-                const float cdot = __builtin_fmaf(f.x, dp0b, __builtin_fmaf(f.y, dp1b, f.z * dp2b));
-                const float dL_dalpha = __builtin_fmaf(Ti, cdot, -s[b] * inv);
-                const float wc = alpha * Ti;  // dchannel/dcolour (backward.cu:800)
-                s[b] = __builtin_fmaf(cdot, wc, s[b]);
-                const float u = oG * dL_dalpha;  // dL/dG G; dL/dopacity gets u / o (raw_row_to_grads)
-                const float uy = u * dy;
-                s_uy += f2v{u, uy};
-                suyy = __builtin_fmaf(uy, dy, suyy);
-                sc01 = __builtin_elementwise_fma(f2v{wc, wc}, dp01[b], sc01);
-                sc2 = __builtin_fmaf(wc, dp2b, sc2);
+        // the instance loop, instantiated with and without the per-lane position test: a batch whose positions all
+        // lie below every band's smallest last contributor (band_min) needs none (one VALU per evaluated band less)
+        auto instances = [&](auto pos_test) {
+            for (uint32_t j = 0; j < nuse; ++j) {
+                const float4 g = s_geo[j];
+                const float4 qo = s_quad[j];
+                const float4 f = s_rgb[j];
+                const uint32_t mb = uniform(__builtin_bit_cast(uint32_t, g.w));
+                const uint32_t ipos = __builtin_bit_cast(uint32_t, g.z);
+                const Quad q = {qo.x, qo.y, qo.z};
+                const float dx = g.x - pxf;
+                const float lo = qo.w;
+                const ColQuad kq = column_quad(q, dx, lo);
+                const float dy0 = g.y - (float)tl.py0;
+                // dx is the same for all four of the lane's pixels (one column), so the x-moments are dx-multiples of
+                // the band sums: S_u dx = dx S_u, S_u dx^2 = dx^2 S_u, S_u dx dy = dx S_u dy (applied after the bands)
+                f2v s_uy = {0.f, 0.f};  // S_u, S_u dy
+                f2v sc01 = {0.f, 0.f};  // S_aT dpix_r, S_aT dpix_g
+                float suyy = 0.f, sc2 = 0.f;
+                uint32_t any = 0;  // bands with a contributing pixel (set in wave-uniform branches: an SGPR)
+    #pragma unroll
+                for (int b = 0; b < TW_BANDS; ++b) {
+                    if (!(mb & (1u << b))) continue;  // scalar branch
+                    const float dp0b = dp01[b].x, dp1b = dp01[b].y, dp2b = dp2[b];
+                    const uint32_t lastb = last[b];
+                    const float dy = dy0 - (float)(4 * b);
+                    const float p2 = falloff_p2(kq, dy);
+                    // backward.cu:770-781: skip positions at/after the pixel's last contributor, power > 0, alpha < 1/255
+                    const bool contrib = (decltype(pos_test)::value ? ipos < lastb : true) && p2_in_band(p2, lo);
+                    BWD_COUNT(1, 1);
+                    if (!__ballot(contrib)) continue;
+                    BWD_COUNT(2, 1);
+                    BWD_COUNT(4, (uint32_t)__popcll(__ballot(contrib)));
+                    any |= 1u << b;
+                    // a lane that does not contribute gets oG = alpha = 0: inv = 1, T and s unchanged, u = wc = 0
+                    const float oG = __builtin_amdgcn_exp2f(contrib ? p2 : -__builtin_inff());  // o G (column_quad)
+                    const float alpha = fminf(0.99f, oG);
+                    const float inv = __builtin_amdgcn_rcpf(1.0f - alpha);
+                    T[b] *= inv;
+                    const float Ti = T[b];
+                    const float cdot = __builtin_fmaf(f.x, dp0b, __builtin_fmaf(f.y, dp1b, f.z * dp2b));
+                    const float dL_dalpha = __builtin_fmaf(Ti, cdot, -s[b] * inv);
+                    const float wc = alpha * Ti;  // dchannel/dcolour (backward.cu:800)
+                    s[b] = __builtin_fmaf(cdot, wc, s[b]);
+                    const float u = oG * dL_dalpha;  // dL/dG G; dL/dopacity gets u / o (raw_row_to_grads)
+                    const float uy = u * dy;
+                    s_uy += f2v{u, uy};
+                    suyy = __builtin_fmaf(uy, dy, suyy);
+                    sc01 = __builtin_elementwise_fma(f2v{wc, wc}, dp01[b], sc01);
+                    sc2 = __builtin_fmaf(wc, dp2b, sc2);
+                }
+                const uint32_t slot_j = __builtin_bit_cast(uint32_t, f.w);
+                if (!any) continue;  // no pixel took a contribution: no row
+                BWD_COUNT(3, 1);
+                const float su = s_uy.x, suy = s_uy.y;
+                const float sux = su * dx, suxx = sux * dx, suxy = suy * dx;
+                float v[8];
+                // the raw moments: their per-Gaussian factors are applied once to the Gaussian's sums (raw_row_to_grads)
+                v[0] = sux;
+                v[1] = suy;
+                v[2] = suxx;
+                v[3] = suxy;
+                v[4] = suyy;
+                v[5] = su;                                         // dL/dopacity
+                v[6] = sc01.x;                                     // dL/dcolour
+                v[7] = sc01.y;
+                float t8;
+                float* s_red = s_red_all[wv];
+                const uint32_t slot_u = uniform(slot_j);
+                const bool held = pslot != ~0u;  // scalar
+                const uint32_t base = held ? 8u * WS_LDS_STRIDE : 0u;
+    #pragma unroll
+                for (int k = 0; k < 8; ++k) s_red[base + k * WS_LDS_STRIDE + lane] = v[k];
+                if (!held) {
+                    pv8 = sc2;
+                    pslot = slot_u;
+                    continue;
+                }
+                {
+                    const float tv = wave_sum9x2_stored(pv8, sc2, lane, s_red, &t8);
+                    // lane 4k holds value k (k < 8 the held row's, k >= 8 this one's); lanes 1 and 33 the 9th values
+                    const bool lead = (lane & 3) == 0;
+                    const uint32_t dslot = (lane < 32) ? pslot : slot_u;
+                    if (lead || (lane & 31) == 1)
+                        a.inst_grad[(size_t)dslot * GRAD_ROW + (lead ? ((lane >> 2) & 7u) : 8u)] = lead ? tv : t8;
+                    if ((lane & 31) == 0) a.row_valid[dslot] = 1;
+                    pslot = ~0u;
+                }
             }
-            const uint32_t slot_j = __builtin_bit_cast(uint32_t, f.w);
-            if (!any) continue;  // no pixel took a contribution: no row
-            BWD_COUNT(3, 1);
-            const float su = s_uy.x, suy = s_uy.y;
-            const float sux = su * dx, suxx = sux * dx, suxy = suy * dx;
-            float v[8];
-            // the raw moments: their per-Gaussian factors are applied once to the Gaussian's sums (raw_row_to_grads)
-            v[0] = sux;
-            v[1] = suy;
-            v[2] = suxx;
-            v[3] = suxy;
-            v[4] = suyy;
-            v[5] = su;                                         // dL/dopacity
-            v[6] = sc01.x;                                     // dL/dcolour
-            v[7] = sc01.y;
-            float t8;
-            float* s_red = s_red_all[wv];
-            const uint32_t slot_u = uniform(slot_j);
-            const bool held = pslot != ~0u;  // scalar
-            const uint32_t base = held ? 8u * WS_LDS_STRIDE : 0u;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) s_red[base + k * WS_LDS_STRIDE + lane] = v[k];
-            if (!held) {
-                pv8 = sc2;
-                pslot = slot_u;
-                continue;
-            }
-            {
-                const float tv = wave_sum9x2_stored(pv8, sc2, lane, s_red, &t8);
-                // lane 4k holds value k (k < 8 the held row's, k >= 8 this one's); lanes 1 and 33 the 9th values
-                const bool lead = (lane & 3) == 0;
-                const uint32_t dslot = (lane < 32) ? pslot : slot_u;
-                if (lead || (lane & 31) == 1)
-                    a.inst_grad[(size_t)dslot * GRAD_ROW + (lead ? ((lane >> 2) & 7u) : 8u)] = lead ? tv : t8;
-                if ((lane & 31) == 0) a.row_valid[dslot] = 1;
-                pslot = ~0u;
-            }
-        }
+        };
+        if ((uint32_t)(hi - 1) < min_last) instances(std::false_type{});
+        else instances(std::true_type{});
         wave_sync();  // the next batch overwrites the staging arrays
     }
     if (pslot != ~0u) {  // the unit's last contributing instance had no partner: sum its rows 0-7 alone
