@@ -33,7 +33,8 @@
 //     dL/dalpha_i = T_i (c_i - accum_rec_i) . dL/dpix - T_final / (1 - alpha_i) bg . dL/dpix
 // equals T_i c_i . dL/dpix - s / (1 - alpha_i): the same quantity, rounded differently.
 // T_i is recovered with v_rcp_f32 (T_{i+1} / (1 - alpha_i)), as the reference divides (backward.cu:782).
-// Instances at or behind every band's last contributor are skipped.
+// Instances at or behind every band's last contributor are skipped; batches in front of every pixel's last
+// contributor run an instance loop without the per-lane position test (min_last below).
 #include <type_traits>
 
 #include "kernels.h"
