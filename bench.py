@@ -560,6 +560,21 @@ def main():
             result["train_step"] = train_step_timing(omr, g, cam, dev, steps=10, warmup=3)
         except Exception as ex:  # informational only
             result["train_step"] = {"error": repr(ex)}
+    if world > 1:
+        # DESIGN.md §6's model from this run's own per-rank compute and gaussian_bwd stage time (parallel.py:
+        # predict_step_ms, link bandwidth parallel.XGMI_LINK_GBPS): the driver's SCALE record can be checked against
+        # it. Efficiency as the driver computes it, value(N) / (N value(1)), with value(1) = rank 0's view alone.
+        pr = par.predict_step_ms(world, P, per_rank_ms, stage_avg.get("gaussian_backward", 0.0), args.exchange)
+        p0 = torch.tensor([float(W * H)], dtype=torch.float64, device=dev)
+        dist.broadcast(p0, 0)
+        pix0 = float(p0.item())
+        single = pix0 / (per_rank_ms[0] * 1e-3) / 1e6 if per_rank_ms[0] > 0 else None
+        pred_value = float(pix.item()) / (pr["step_ms"] * 1e-3) / 1e6 if pr["step_ms"] > 0 else None
+        result["predicted"] = {"ms_per_step": round(pr["step_ms"], 4), "value": round(pred_value, 3) if pred_value else None,
+                               "efficiency": round(pred_value / (world * single), 4) if (pred_value and single) else None,
+                               "measured_efficiency_vs_rank0_compute": round(value / (world * single), 4) if single else None,
+                               "terms_ms": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pr.items()},
+                               "xgmi_link_GBps_assumed": par.XGMI_LINK_GBPS, "model": "DESIGN.md §6"}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -394,7 +394,8 @@ __global__ __launch_bounds__(RB_THREADS) void rows_scatter_kernel(BinArgs a)
         }
     };
     const ChunkRange cr = xcd_chunks(C);
-    RowChunk k = row_chunk(a, min(cr.first, C - 1u), M);  // (C = 0: no iteration reads it)
+    if (C == 0) return;  // nothing binned (L = 0, a capacity overflow, a failed look-back): desc_r has no entry
+    RowChunk k = row_chunk(a, min(cr.first, C - 1u), M);
     if (cr.first < cr.end) load_owners(k, cr.first);
     for (uint32_t c = cr.first; c < cr.end; c += cr.step) {
         const uint32_t cn = c + cr.step;
@@ -537,7 +538,8 @@ __global__ __launch_bounds__(RB_THREADS) void cols_hist_kernel(BinArgs a)
     __shared__ uint32_t s_wave[RB_WAVES];
     const uint32_t tid = threadIdx.x, gx = a.gx, C = a.words[1];
     const ChunkRange cr = xcd_chunks(C);
-    ColChunk k = col_chunk(a, min(cr.first, C - 1u));  // (C = 0: no iteration reads it)
+    if (C == 0) return;  // no live chunk: desc_b has no entry to prefetch
+    ColChunk k = col_chunk(a, min(cr.first, C - 1u));
     for (uint32_t c = cr.first; c < cr.end; c += cr.step) {
         const ColChunk kn = col_chunk(a, min(c + cr.step, C - 1u));
         uint32_t ex[HP], ew[HP];
@@ -663,7 +665,8 @@ __global__ __launch_bounds__(G::THREADS) void cols_scatter_kernel(BinArgs a)
     }
     const ChunkRange cr = xcd_chunks(C);
     uint32_t c = cr.first, it = 0;
-    ColChunk k = col_chunk(a, min(c, C - 1u));  // (C = 0: no iteration reads it)
+    if (C == 0) return;  // no live chunk: desc_b has no entry to prefetch
+    ColChunk k = col_chunk(a, min(c, C - 1u));
     if (c < cr.end) {
         OMR_CS_LOAD_ENTRIES(k)
         OMR_CS_LOAD_CONSTS(k)

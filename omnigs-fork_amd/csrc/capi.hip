@@ -332,7 +332,7 @@ size_t& capacity_hint(int W, int H, int camera_type)
 
 }  // namespace
 
-size_t GeomState::carve(char* base, size_t P, GeomState* s)
+size_t GeomState::carve(char* base, size_t P, GeomState* s, bool rows)
 {
     Carver c(base);
     GeomState g;
@@ -353,11 +353,18 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s)
     g.conic_op = c.take<float4>(P);
     g.huge_list = c.take<uint32_t>(P);
     g.internal_radii = c.take<int>(P);
-    g.rect = c.take<uint2>(P);
-    g.drect = c.take<uint2>(P);
-    g.row_offsets = c.take<uint32_t>(P);
-    g.desc_r = c.take<uint2>(P / 2 + 2);  // M <= BIN_MAX_GRID P slots: at most P / 2 + 1 chunks
-    g.bin_rec = c.take<float4>(2 * P);
+    // the row binning's arrays, last (bin.hip; preprocess and the forward scans write them only when present)
+    if (rows) {
+        g.rect = c.take<uint2>(P);
+        g.drect = c.take<uint2>(P);
+        g.row_offsets = c.take<uint32_t>(P);
+        g.desc_r = c.take<uint2>(P / 2 + 2);  // M <= BIN_MAX_GRID P slots: at most P / 2 + 1 chunks
+        g.bin_rec = c.take<float4>(2 * P);
+    } else {
+        g.rect = g.drect = g.desc_r = nullptr;
+        g.row_offsets = nullptr;
+        g.bin_rec = nullptr;
+    }
     g.order = g.val_a;  // the depth sort runs DEPTH_SORT_PASSES (even) passes, so its result lands in val_a
     if (s) *s = g;
     return c.size();
@@ -491,10 +498,12 @@ int forward_impl(const ForwardIn& in)
     const hipStream_t s = in.stream;
     const size_t P = (size_t)in.P;
 
-    char* geom_base = static_cast<char*>(alloc_counted(in.geometry_alloc, in.geometry_ctx, GeomState::carve(nullptr, P, nullptr)));
+    const bool rows_path = row_binning(d.gx, d.gy);  // bin.hip; sort.hip's emit + tile sort for larger views
+    char* geom_base = static_cast<char*>(
+        alloc_counted(in.geometry_alloc, in.geometry_ctx, GeomState::carve(nullptr, P, nullptr, rows_path)));
     if (!geom_base) return fail(OMR_ERR_ALLOCATION, "geometry allocation failed");
     GeomState g;
-    GeomState::carve(geom_base, P, &g);
+    GeomState::carve(geom_base, P, &g, rows_path);
     char* img_base = static_cast<char*>(alloc_counted(in.image_alloc, in.image_ctx, ImageState::carve(nullptr, d.N, d.T, nullptr)));
     if (!img_base) return fail(OMR_ERR_ALLOCATION, "image allocation failed");
     ImageState im;
@@ -526,7 +535,6 @@ int forward_impl(const ForwardIn& in)
     uint32_t* const err_dev = g.counters + 3;  // every decoupled look-back of the forward reports a give-up here
     int which; { StageScope st_(ST_DEPTH_SORT, s); which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr, nullptr, 0, DEPTH_SORT_PASSES, s, true, err_dev); }
     g.order = which ? g.val_b : g.val_a;
-    const bool rows_path = row_binning(d.gx, d.gy);  // bin.hip; sort.hip's emit + tile sort for larger views
     { StageScope st_(ST_SCAN, s); launch_forward_scans(g.tiles_touched, rows_path ? g.rect : nullptr, g.order, g.offsets, g.row_first, g.row_offsets, g.drect, g.desc_r, g.huge_list, g.counters + 2, g.scan2_status, g.counters, err_dev, P, s); }
 
     // num_rendered = offsets[P-1] (+ the prefiltered error flag) to pinned host memory, without waiting for it:

@@ -262,12 +262,14 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
         g.tiles_touched[idx] = vis ? o.area : 0u;
         const uint32_t x0 = __builtin_bit_cast(uint32_t, o.rec[3].x), y0 = __builtin_bit_cast(uint32_t, o.rec[3].y);
         const uint32_t wd = __builtin_bit_cast(uint32_t, o.rec[3].z) - x0;
-        // the row binning's rect word (fields sized for BIN_MAX_GRID tiles a side; unused past that)
-        g.rect[idx] = vis ? make_uint2((__builtin_bit_cast(uint32_t, o.rec[3].w) - y0) | (y0 << RECT_ROWS_BITS) |
-                                           (wd << 21),
-                                       x0)
-                          : make_uint2(0u, 0u);
-        if (vis) {  // the binning's band-mask constants (bin.hip: the columns pass reads them per (Gaussian, row))
+        // the row binning's rect word (fields sized for BIN_MAX_GRID tiles a side); views past that carve no rect
+        // and no bin_rec (GeomState::carve)
+        if (g.rect)
+            g.rect[idx] = vis ? make_uint2((__builtin_bit_cast(uint32_t, o.rec[3].w) - y0) | (y0 << RECT_ROWS_BITS) |
+                                               (wd << 21),
+                                           x0)
+                              : make_uint2(0u, 0u);
+        if (vis && g.bin_rec) {  // the binning's band-mask constants (bin.hip: the columns pass reads them per (Gaussian, row))
             float4 r0, r1;
             band_row_consts(band_consts(o.rec[1]), make_float2(o.rec[0].x, o.rec[0].y), r0, r1);
             g.bin_rec[2 * (size_t)idx] = r0;

@@ -121,7 +121,9 @@ struct GeomState {
                               // columns pass turns into each (Gaussian, row)'s reachable columns per band
     int* internal_radii;      // used when the caller passes radii == NULL (rasterizer_impl.cu:284-287)
 
-    static size_t carve(char* base, size_t P, GeomState* s);
+    // rows = false leaves out the row binning's arrays (rect .. bin_rec: the carve's tail, ~56 B per Gaussian) for views
+    // that take sort.hip's binning; every other array keeps its offset, so readers carve with the default
+    static size_t carve(char* base, size_t P, GeomState* s, bool rows = true);
 };
 
 // ---- image state: N pixels, T tiles ------------------------------------------------------------------------

@@ -151,12 +151,14 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
             const float lo = qo.w;
             const float dx = g.x - pxf;
             const ColQuad kq = column_quad(q, dx, lo);
-            const float dy0 = g.y - (float)tl.py(band0);
+            // dy as the backward forms it (render_bwd.hip): from the tile's first pixel row, then minus 4 x the band,
+            // so both kernels round dy — and take every contribute / skip decision — identically
+            const float dy0 = g.y - (float)tl.py0;
             uint64_t sat_any = 0;  // lanes that saturated at this instance (a wave mask: SALU only)
 #pragma unroll
             for (int b = 0; b < FWD_BANDS; ++b) {
                 if (!(mb & (1u << b))) continue;  // scalar branch
-                const float dy = dy0 - (float)(4 * b);
+                const float dy = dy0 - (float)(4 * (band0 + b));
                 const float p2 = falloff_p2(kq, dy);
                 // a done pixel (T < 0) may evaluate: its test_T is negative, so sat holds, wgt = 0, T keeps -|T| and
                 // `last` stays (wgt > 0 below) — the same results with one scalar AND less per band

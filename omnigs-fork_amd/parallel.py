@@ -213,3 +213,38 @@ class CompactExchange:
             dist.all_reduce(self.buf.flat[:REDUCED_FLOATS * self.buf.P], op=dist.ReduceOp.SUM)
         torch.cuda.current_stream().wait_stream(self.comm)
         self.rebuild_packed(self.packed_all, out=self.buf.views["dL_dsh"])
+
+
+# ---- the scaling model of DESIGN.md §6, for a SCALE record to be checked against mechanically -------------------
+# RCCL's bus bandwidth over xGMI, per link direction after protocol overhead: the ONE assumption of the model
+# (uncertain by up to 2x; a SCALE record outside that band points at RCCL's behaviour)
+XGMI_LINK_GBPS = 55.0
+# links a ring of n ranks spreads one message over (a 2-GPU job has one link; 4 GPUs three; 8 GPUs six of seven)
+XGMI_RING_LINKS = {2: 1, 4: 3, 8: 6}
+HBM_GBPS = 6300.0  # achievable HBM bandwidth (MI355X_MICROARCH.md), for the SH rebuild's passes
+
+
+def bus_gbps(n: int) -> float:
+    return XGMI_LINK_GBPS * XGMI_RING_LINKS.get(n, max(1, min(n - 1, 6)))
+
+
+def predict_step_ms(n: int, P: int, compute_ms_per_rank, gbwd_ms: float, exchange: str = "compact") -> dict:
+    """step(n) = max over ranks of forward + backward, plus the exchange's tail past the per-Gaussian
+    backward it overlaps. compact: t_AR = 2 (n-1)/n 44 B P / B(n), t_AG = (n-1) 12 B P / B(n) (each rank receives the
+    n-1 other views' colour gradients), tail = (t_AR + t_AG - t_gbwd)+ + t_rebuild (n 12 + 384 B/G over HBM); flat:
+    one all-reduce of 236 B/G after the backward. Returns the model's terms in ms."""
+    n = int(n)
+    comp = max(compute_ms_per_rank) if compute_ms_per_rank else 0.0
+    if n <= 1:
+        return dict(step_ms=comp, t_ar_ms=0.0, t_ag_ms=0.0, tail_ms=0.0, bus_GBps=None)
+    B = bus_gbps(n) * 1e9
+    if exchange == "compact":
+        t_ar = 2 * (n - 1) / n * 44 * P / B * 1e3
+        t_ag = (n - 1) * 12 * P / B * 1e3
+        t_rb = (n * 12 + 384) * P / (HBM_GBPS * 1e9) * 1e3
+        tail = max(0.0, t_ar + t_ag - gbwd_ms) + t_rb
+    else:
+        t_ar = 2 * (n - 1) / n * 236 * P / B * 1e3
+        t_ag = 0.0
+        tail = t_ar
+    return dict(step_ms=comp + tail, t_ar_ms=t_ar, t_ag_ms=t_ag, tail_ms=tail, bus_GBps=B / 1e9)

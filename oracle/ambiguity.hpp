@@ -61,6 +61,10 @@ struct AllowanceParams {
     double k_depth = 8.0;   // ulps of the largest term of the view transform, for the depth key
 };
 
+// the nine per-pixel gradient terms of one (pixel, Gaussian) pair that backward.cu:671-843 accumulates:
+// dL_dmean2D x, y; dL_dconic a, b, c; dL_dopacity; dL_dcolor r, g, b
+constexpr int NTERM = 9;
+
 struct Allowance {
     int64_t rect_gaussians = 0;    // flip & G_RECT
     int64_t radius_gaussians = 0;  // radius within its rounding window of an integer (a subset may move the rect)
@@ -72,7 +76,33 @@ struct Allowance {
     std::vector<uint8_t> flip;     // [P] G_* flags
     std::vector<uint8_t> pixel;    // [H*W] PX_* flags
     std::vector<float> bound;      // [H*W] largest colour change the flagged decisions can make (per channel)
+    // [P * NTERM], only with an upstream gradient: per Gaussian, the summed magnitude of the pixel terms its own
+    // flagged decisions can add, remove or rescale (owner_term below) — what an owner's gradient may move by
+    std::vector<float> term;
 };
+
+// |term| of Gaussian `id` at pixel (px, py) if it blends there with alpha `al` = o G behind transmittance T, a bound
+// on each of the NTERM terms of backward.cu:745-770. The accumulated colour behind it (accum_rec) and the background
+// term are bounded by the scene's colour span (cmax): |c - accum_rec| <= |c| + cmax.
+inline void owner_term(const State<float>& s, uint32_t id, double px, double py, double al, double G, double T,
+                       double T_final, const double* dLp, double cmax, double bg_dot, const float* features,
+                       double scale, float* acc)
+{
+    const double dx = (double)s.means2D[id].x - px, dy = (double)s.means2D[id].y - py;
+    const V4<float> co = s.conic_opacity[id];
+    double dLda = 0.0;
+    for (int ch = 0; ch < 3; ++ch) dLda += (std::fabs((double)features[3 * id + ch]) + cmax) * dLp[ch];
+    dLda = T * dLda + T_final / std::fmax(1.0 - al, 1e-2) * bg_dot;
+    const double dG = (double)co.w * dLda;
+    const double W2 = 0.5 * s.a.width, H2 = 0.5 * s.a.height;
+    acc[0] += (float)(scale * dG * G * std::fabs((double)co.x * dx + (double)co.y * dy) * W2);
+    acc[1] += (float)(scale * dG * G * std::fabs((double)co.z * dy + (double)co.y * dx) * H2);
+    acc[2] += (float)(scale * 0.5 * G * dx * dx * dG);
+    acc[3] += (float)(scale * 0.5 * G * std::fabs(dx * dy) * dG);
+    acc[4] += (float)(scale * 0.5 * G * dy * dy * dG);
+    acc[5] += (float)(scale * G * dLda);
+    for (int ch = 0; ch < 3; ++ch) acc[6 + ch] += (float)(scale * al * T * dLp[ch]);
+}
 
 constexpr double EPS32 = 5.9604644775390625e-08;  // 2^-24
 
@@ -136,7 +166,8 @@ inline void radius_window(const V4<float>& co, const AllowanceParams& prm, doubl
     dx = 3.0 * dlam / (2.0 * std::sqrt(std::fmax(lam, 1e-30))) + prm.k_eval * EPS32 * x;
 }
 
-inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& prm)
+// dL_dpix ([3, H, W], may be NULL): also fill Allowance::term, the owners' gradient bound in pixel-term space
+inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& prm, const float* dL_dpix = nullptr)
 {
     Allowance out;
     const Args<float>& a = s.a;
@@ -220,6 +251,8 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
     }
     int64_t na = 0, ns = 0, nz = 0, no = 0, nr = 0, npairs = 0, nany = 0;
     std::vector<std::vector<std::pair<uint32_t, uint8_t>>> marked(T);
+    std::vector<std::vector<uint32_t>> term_id(dL_dpix ? T : 0);  // per tile: flagged (pixel, Gaussian) terms
+    std::vector<std::vector<float>> term_val(dL_dpix ? T : 0);
 #pragma omp parallel for schedule(dynamic, 4) reduction(+ : na, ns, nz, no, nr, npairs, nany)
     for (int t = 0; t < (int)T; ++t) {
         const uint32_t tx = t % s.gx, ty = t / s.gx;
@@ -249,6 +282,25 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
                 double Tr = 1.0, errT = 0.0, bnd = 0.0, last_alpha = 0.0, T_before_last = 1.0;
                 uint32_t last_run = ~0u, last_run_id = 0;
                 bool behind = false;  // a decision in front of this position is ambiguous (alpha, power 0, order, rect)
+                double last_G = 0.0;
+                double dLp[3] = {0, 0, 0}, bg_dot = 0.0, T_fin = 0.0;
+                if (dL_dpix) {
+                    const size_t pid = (size_t)py * W + px;
+                    for (int ch = 0; ch < 3; ++ch) {
+                        dLp[ch] = std::fabs((double)dL_dpix[(size_t)ch * H * W + pid]);
+                        bg_dot += (double)a.background[ch] * dL_dpix[(size_t)ch * H * W + pid];
+                    }
+                    bg_dot = std::fabs(bg_dot);
+                    T_fin = s.final_T[pid];
+                }
+                // the pixel term of `id` may appear, vanish or be rescaled by `scale` in the reference
+                auto add_term = [&](uint32_t id, double al, double G, double Tt, double scale) {
+                    if (!dL_dpix) return;
+                    term_id[t].push_back(id);
+                    const size_t o = term_val[t].size();
+                    term_val[t].resize(o + NTERM, 0.f);
+                    owner_term(s, id, px, py, al, G, Tt, T_fin, dLp, cmax, bg_dot, features, scale, &term_val[t][o]);
+                };
                 auto eval = [&](uint32_t id, double& power, double& dp) {
                     const double dx = (double)s.means2D[id].x - px, dy = (double)s.means2D[id].y - py;
                     const V4<float> co = s.conic_opacity[id];
@@ -267,6 +319,8 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
                         pf |= PX_ZERO;
                         marked[t].push_back({id, G_THRESHOLD});
                         bnd += span * Tr * std::fmin(0.99, (double)co.w);
+                        const double Gz = std::exp(std::fmin(power, 0.0));
+                        add_term(id, std::fmin(0.99, co.w * Gz), Gz, Tr, 1.0);
                     }
                     if (power > 0) continue;
                     const double thr = -std::log(255.0 * co.w);  // alpha = o exp(power) = 1/255
@@ -274,6 +328,8 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
                         pf |= PX_ALPHA;
                         marked[t].push_back({id, G_THRESHOLD});
                         bnd += span * Tr * (1.0 / 255.0) * std::exp(dp + prm.eps_exp);
+                        const double Ga = std::exp(std::fmin(power + dp + prm.eps_exp, 0.0));
+                        add_term(id, std::fmin(0.99, co.w * Ga), Ga, Tr, 1.0);
                     }
                     const double alpha = std::fmin(0.99, co.w * std::exp(power));
                     if (alpha < 1.0 / 255.0) {
@@ -286,6 +342,7 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
                         if (tx == b.minx || tx + 1 == b.maxx || ty == b.miny || ty + 1 == b.maxy) {
                             pf |= PX_RECT;
                             bnd += span * Tr * alpha;
+                            add_term(id, alpha, std::exp(power), Tr, 1.0);
                         }
                     }
                     behind = behind || (pf & (PX_ALPHA | PX_ZERO | PX_ORDER | PX_RECT));
@@ -297,16 +354,22 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
                         marked[t].push_back({last_run_id, G_ORDER});
                         // swapping a, b moves (alpha_a alpha_b T_a)(c_a - c_b); T after both is unchanged
                         bnd += span * (Tr / std::fmax(1.0 - last_alpha, 1e-2)) * last_alpha * alpha;
+                        // swapped, b's transmittance grows by 1 / (1 - alpha_a), a's shrinks by (1 - alpha_b), and
+                        // both accumulated colours change: each term moves by at most itself times that factor
+                        add_term(id, alpha, std::exp(power), Tr, 1.0 + last_alpha / std::fmax(1.0 - last_alpha, 1e-2));
+                        add_term(last_run_id, last_alpha, last_G, T_before_last, 1.0 + alpha);
                     }
                     last_run = run[k];
                     last_run_id = id;
                     last_alpha = alpha;
+                    last_G = std::exp(power);
                     const double test_T = Tr * (1.0 - alpha);
                     const double errk = errT + alpha * dp;
                     if (std::fabs(test_T - 1e-4) <= (prm.eps_exp + errk) * 1e-4) {
                         pf |= PX_SAT;
                         marked[t].push_back({id, G_THRESHOLD});
                         bnd += span * Tr;  // this term and everything behind carry transmittance <= Tr
+                        add_term(id, alpha, std::exp(power), Tr, 1.0);
                     }
                     if (test_T < 1e-4) {
                         // the run's previous member blended and this one saturates: swapped, the other one may
@@ -329,6 +392,9 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
                     if (power - dp <= 0.0 && power + dp >= -std::log(255.0 * o) - prm.eps_exp) {
                         pf |= PX_RECT;
                         bnd += span * std::fmin(0.99, o * std::exp(std::fmin(0.0, power + dp)));
+                        // it may blend at any depth position: transmittance <= 1
+                        const double Gr = std::exp(std::fmin(0.0, power + dp));
+                        add_term((uint32_t)id, std::fmin(0.99, o * Gr), Gr, 1.0, 1.0);
                     }
                 }
                 na += (pf & PX_ALPHA) ? 1 : 0;
@@ -350,6 +416,12 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
     out.any_pixels = nany;
     for (const auto& v : marked)
         for (const auto& e : v) out.flip[e.first] |= e.second;
+    if (dL_dpix) {
+        out.term.assign((size_t)P * NTERM, 0.f);
+        for (uint32_t t = 0; t < T; ++t)
+            for (size_t k = 0; k < term_id[t].size(); ++k)
+                for (int j = 0; j < NTERM; ++j) out.term[(size_t)term_id[t][k] * NTERM + j] += term_val[t][k * NTERM + j];
+    }
     for (int i = 0; i < P; ++i) {
         out.flip_gaussians += (out.flip[i] & (G_THRESHOLD | G_ORDER | G_RECT)) != 0;
         out.threshold_gaussians += (out.flip[i] & G_THRESHOLD) != 0;
@@ -357,6 +429,55 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
         out.exposed_gaussians += (out.flip[i] & (G_THRESHOLD | G_ORDER | G_RECT | G_EXPOSED)) == G_EXPOSED;
     }
     return out;
+}
+
+// The owners' gradient bound in the outputs' own space. The preprocess backward (backward.cu:297-485 lonlat /
+// :156-292 pinhole, :613-669 / :557-608, SH :30-151, cov3D :489-552) is linear in the nine pixel-term sums of a
+// Gaussian at the forward's state, so |change of an output| <= sum_c |J[output][c]| term[c], J taken column by
+// column by running that backward on unit inputs. For each of the n Gaussians ids[i], out[i * K ...] holds, in
+// this order: dmean2D (3), dcolor (3), dopacity (1), dmean3D (3), dcov3D (6), dsh (M * 3), dscale (3), drot (4);
+// K = 23 + 3 M. `term` is Allowance::term ([P * NTERM]).
+inline int owner_grad_bound(const State<float>& s, const float* term, const int32_t* ids, int n, float* out)
+{
+    const int P = s.a.P, M = s.a.M;
+    const int K = 23 + 3 * M;
+    Grads<float> g;
+    g.zero(P, M);
+    const float* cov3D_ptr = s.a.cov3D_precomp != nullptr ? s.a.cov3D_precomp : s.cov3D.data();
+    const float focal_y = (float)s.a.height / (2.0f * s.a.tan_fovy);
+    const float focal_x = (float)s.a.width / (2.0f * s.a.tan_fovx);
+    for (int i = 0; i < n; ++i) {
+        const int idx = ids[i];
+        float* o = out + (size_t)i * K;
+        for (int k = 0; k < K; ++k) o[k] = 0.f;
+        if (idx < 0 || idx >= P) return -1;
+        const float* tm = term + (size_t)idx * NTERM;
+        o[0] = tm[0]; o[1] = tm[1];
+        o[3] = tm[6]; o[4] = tm[7]; o[5] = tm[8];
+        o[6] = tm[5];
+        if (!(s.radii[idx] > 0)) continue;
+        for (int c = 0; c < NTERM; ++c) {
+            if (tm[c] == 0.f) continue;
+            float in[NTERM] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+            in[c] = 1.f;
+            g.dmean2D[3 * idx] = in[0]; g.dmean2D[3 * idx + 1] = in[1]; g.dmean2D[3 * idx + 2] = 0.f;
+            g.dconic[4 * idx] = in[2]; g.dconic[4 * idx + 1] = in[3]; g.dconic[4 * idx + 3] = in[4];
+            g.dopacity[idx] = in[5];
+            g.dcolor[3 * idx] = in[6]; g.dcolor[3 * idx + 1] = in[7]; g.dcolor[3 * idx + 2] = in[8];
+            V3<float> dpx_dt = {0, 0, 0}, dpy_dt = {0, 0, 0};
+            if (s.a.camera_type == 3) computeCov2DLonLat_backward(s, idx, cov3D_ptr, g, dpx_dt, dpy_dt);
+            else computeCov2D_backward(s, idx, cov3D_ptr, focal_x, focal_y, g);
+            preprocess_backward_one(s, idx, dpx_dt, dpy_dt, g);
+            const double w = tm[c];
+            float* q = o + 7;
+            for (int k = 0; k < 3; ++k) *q++ += (float)(w * std::fabs((double)g.dmean3D[3 * idx + k]));
+            for (int k = 0; k < 6; ++k) *q++ += (float)(w * std::fabs((double)g.dcov3D[6 * idx + k]));
+            for (int k = 0; k < 3 * M; ++k) *q++ += (float)(w * std::fabs((double)g.dsh[(size_t)idx * M * 3 + k]));
+            for (int k = 0; k < 3; ++k) *q++ += (float)(w * std::fabs((double)g.dscale[3 * idx + k]));
+            for (int k = 0; k < 4; ++k) *q++ += (float)(w * std::fabs((double)g.drot[4 * idx + k]));
+        }
+    }
+    return K;
 }
 
 }  // namespace oracle

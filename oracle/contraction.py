@@ -70,8 +70,6 @@ def point_list_check(ob, ov, allow_flip, P):
 def compare_variant(ob, gb, ov, gv, allow, H, W):
     """Counts of what differs between the oracle run (ob, grads gb) and a contracted build's run (ov, gv), and of
     what the allowance does not explain (every `*_unexplained` must be 0)."""
-    from helpers import WIDE_ATOL_FRAC, WIDE_RTOL, grad_close
-
     P = ob.P
     vis = ob.get("radii") > 0
     out = {"num_rendered_delta": int(ov.num_rendered - ob.num_rendered)}
@@ -100,17 +98,15 @@ def compare_variant(ob, gb, ov, gv, allow, H, W):
     terr = np.abs(ob.get("final_T").reshape(H, W).astype(np.float64) - ov.get("final_T").reshape(H, W))
     out["final_T_unexplained"] = int((terr > 1e-4 + allow["t_bound"]).sum())
     if gb is not None:
-        g_out, g_owner, g_exposed, g_bad = 0, 0, 0, 0
-        for n in GRAD_NAMES:
-            ok = grad_close(gv[n], gb[n], elementwise=True).reshape(P, -1)
-            wide = grad_close(gv[n], gb[n], rtol=WIDE_RTOL, atol_frac=WIDE_ATOL_FRAC, elementwise=True).reshape(P, -1)
-            outside = ~ok
-            g_out += int(outside.sum())
-            g_owner += int(outside[allow["owners"]].sum())
-            g_exposed += int((outside & allow["exposed"][:, None] & ~allow["owners"][:, None]).sum())
-            g_bad += int((outside & ~allow["owners"][:, None] & ~(allow["exposed"][:, None] & wide)).sum())
-        out.update(grad_entries_outside_bar=g_out, grad_entries_on_owners=g_owner,
-                   grad_entries_on_exposed=g_exposed, grad_entries_unexplained=g_bad)
+        from helpers import grad_residuals
+
+        r = grad_residuals(gv, gb, allow, P, GRAD_NAMES)
+        out.update(grad_entries_outside_bar=r["entries_outside_strict"],
+                   grad_gaussians_outside_bar=r["gaussians_outside_strict"],
+                   grad_owner_gaussians_used=r["owner_gaussians_used"],
+                   grad_exposed_gaussians_used=r["exposed_gaussians_used"],
+                   grad_owner_bound_max_use=round(r["owner_bound_max_use"], 4),
+                   grad_entries_unexplained=r["unexplained"])
     return out
 
 
@@ -127,7 +123,7 @@ def run_config(name, threads, variants=("fma_gcc", "fma_clang"), backward=True):
     g, cam, dL = scene.config_scene(name)
     t0 = time.time()
     ob, L, gb = O.run_scene(g, cam, dL if backward else None, nthreads=threads)
-    allow = reference_allowance(ob)
+    allow = reference_allowance(ob, dL if backward else None)
     counts = dict(allow["counts"])
     V = int((ob.get("radii") > 0).sum())
     counts.update(P=g.P, V=V, L=int(L), pixels=cam.width * cam.height,
@@ -165,7 +161,7 @@ def main():
         "atan2 / radius rounding windows; order_pairs = same-tile neighbours whose depths differ by less than their "
         "rounding windows; alpha / saturation / zero_power pixels = a blend decision inside its rounding window; "
         "order_pixels = two members of an order-ambiguous run blend; flip_gaussians own such a decision (gradients "
-        "excused), exposed_gaussians blend behind one (wide bar 1e-2 / 1e-3). variants: what actually changes, and "
+        "within the owner bound of ambiguity.hpp: owner_grad_bound), exposed_gaussians blend behind one (wide bar 1e-2 / 1e-3). variants: what actually changes, and "
         "what the allowance leaves unexplained (*_unexplained, all 0 expected)")
     for name in args.configs:
         res = run_config(name, args.threads, variants=() if args.no_variants else ("fma_gcc", "fma_clang"))

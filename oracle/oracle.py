@@ -59,6 +59,8 @@ def lib(variant: str = "base"):
         L.oracle_asinf.argtypes = [f]
         L.oracle_mark_visible.argtypes = [i, vp, vp, vp, i, vp]
         L.oracle_allowance.argtypes = [vp, C.POINTER(C.c_double), vp, vp, vp, C.POINTER(C.c_int64)]
+        L.oracle_allowance_terms.argtypes = [vp, C.POINTER(C.c_double), vp, vp, vp, C.POINTER(C.c_int64), vp, vp]
+        L.oracle_owner_grad_bound.argtypes = [vp, vp, vp, i, vp]
         _libs[variant] = L
     return _libs[variant]
 
@@ -142,9 +144,11 @@ class Oracle:
     PX = dict(alpha=1, saturation=2, zero_power=4, order=8, rect=16)
     G = dict(threshold=1, order=2, rect=4, exposed=8, run=16, radius=32)
 
-    def allowance(self, **kw):
+    def allowance(self, dL=None, **kw):
         """ambiguity.hpp's allowance_scan on the last (float) forward. Returns (counts dict, flip [P] uint8 of G flags,
-        pixel [H, W] uint8 of PX flags, bound [H, W] float32: the largest colour change those decisions can make)."""
+        pixel [H, W] uint8 of PX flags, bound [H, W] float32: the largest colour change those decisions can make),
+        and with the upstream gradient dL [3, H, W] a fifth item, term [P, 9]: per Gaussian the summed magnitude of
+        the pixel terms its flagged decisions can move (dmean2D x y, dconic a b c, dopacity, dcolor r g b)."""
         if self.double:
             raise RuntimeError("allowance needs a float forward")
         prm = dict(self.ALLOWANCE_DEFAULTS, **kw)
@@ -153,11 +157,37 @@ class Oracle:
         pix = np.zeros(self.W * self.H, dtype=np.uint8)
         bound = np.zeros(self.W * self.H, dtype=np.float32)
         counts = (C.c_int64 * 13)()
-        if self.L.oracle_allowance(self.h, pv, _ptr(flip), _ptr(pix), _ptr(bound), counts) != 0:
+        d = term = None
+        if dL is not None:
+            d = np.ascontiguousarray(dL, dtype=np.float32).reshape(3, self.H, self.W)
+            term = np.zeros((self.P, 9), dtype=np.float32)
+        if self.L.oracle_allowance_terms(self.h, pv, _ptr(flip), _ptr(pix), _ptr(bound), counts, _ptr(d),
+                                         _ptr(term)) != 0:
             raise RuntimeError("allowance failed")
         out = {k: int(counts[i]) for i, k in enumerate(self.ALLOWANCE_COUNTS)}
         out.update(prm)
-        return out, flip, pix.reshape(self.H, self.W), bound.reshape(self.H, self.W)
+        res = (out, flip, pix.reshape(self.H, self.W), bound.reshape(self.H, self.W))
+        return res + (term,) if dL is not None else res
+
+    OWNER_BOUND_LAYOUT = (("dmean2D", 3), ("dcolor", 3), ("dopacity", 1), ("dmean3D", 3), ("dcov3D", 6), ("dsh", None),
+                          ("dscale", 3), ("drot", 4))
+
+    def owner_grad_bound(self, term: np.ndarray, ids: np.ndarray) -> dict:
+        """ambiguity.hpp owner_grad_bound: for the Gaussians `ids`, the bound on every output gradient element that
+        their flagged pixel terms `term` ([P, 9], allowance(dL)) can carry, through the linear preprocess backward at
+        this forward's state. Returns {name: [len(ids), k]} in the rasterizer's output layouts."""
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        term = np.ascontiguousarray(term, dtype=np.float32)
+        K = 23 + 3 * self.M
+        out = np.zeros((len(ids), K), dtype=np.float32)
+        if len(ids) and self.L.oracle_owner_grad_bound(self.h, _ptr(term), _ptr(ids), len(ids), _ptr(out)) != K:
+            raise RuntimeError("owner_grad_bound failed")
+        res, c = {}, 0
+        for name, k in self.OWNER_BOUND_LAYOUT:
+            k = 3 * self.M if k is None else k
+            res[name] = out[:, c:c + k]
+            c += k
+        return res
 
     def ambiguity(self, **kw):
         """allowance() as (counts, boolean [P] mask of the Gaussians owning an ambiguous decision)."""

@@ -81,6 +81,9 @@ template <typename R> const void* field(Handle* h, oracle::State<R>& s, oracle::
 
 extern "C" {
 
+int oracle_allowance_terms(void* hv, const double* prm, uint8_t* flip_out, uint8_t* pixel_out, float* bound_out,
+                           int64_t* counts, const float* dL_dpix, float* term_out);
+
 void* oracle_new(int dbl)
 {
     Handle* h = new Handle();
@@ -185,6 +188,14 @@ void oracle_mark_visible(int P, const float* means3D, const float* viewmatrix, c
 int oracle_allowance(void* hv, const double* prm, uint8_t* flip_out, uint8_t* pixel_out, float* bound_out,
                      int64_t* counts)
 {
+    return oracle_allowance_terms(hv, prm, flip_out, pixel_out, bound_out, counts, nullptr, nullptr);
+}
+
+// oracle_allowance, plus (dL_dpix [3, H, W] given) the owners' pixel-term bound Allowance::term into term_out
+// [P * 9]; both NULL skips it
+int oracle_allowance_terms(void* hv, const double* prm, uint8_t* flip_out, uint8_t* pixel_out, float* bound_out,
+                           int64_t* counts, const float* dL_dpix, float* term_out)
+{
     Handle* h = static_cast<Handle*>(hv);
     if (h->dbl) return -1;
     oracle::AllowanceParams p;
@@ -193,7 +204,7 @@ int oracle_allowance(void* hv, const double* prm, uint8_t* flip_out, uint8_t* pi
     p.k_eval = prm[2];
     p.k_pos = prm[3];
     p.k_depth = prm[4];
-    const oracle::Allowance a = oracle::allowance_scan(h->sf, p);
+    const oracle::Allowance a = oracle::allowance_scan(h->sf, p, term_out ? dL_dpix : nullptr);
     const int64_t c[13] = {a.rect_gaussians, a.radius_gaussians, a.alpha_pixels, a.sat_pixels, a.zero_pixels,
                            a.order_pixels, a.rect_pixels, a.order_pairs, a.flip_gaussians, a.threshold_gaussians,
                            a.order_gaussians, a.any_pixels, a.exposed_gaussians};
@@ -201,7 +212,17 @@ int oracle_allowance(void* hv, const double* prm, uint8_t* flip_out, uint8_t* pi
     if (flip_out && !a.flip.empty()) std::memcpy(flip_out, a.flip.data(), a.flip.size());
     if (pixel_out && !a.pixel.empty()) std::memcpy(pixel_out, a.pixel.data(), a.pixel.size());
     if (bound_out && !a.bound.empty()) std::memcpy(bound_out, a.bound.data(), a.bound.size() * sizeof(float));
+    if (term_out && !a.term.empty()) std::memcpy(term_out, a.term.data(), a.term.size() * sizeof(float));
     return 0;
+}
+
+// ambiguity.hpp owner_grad_bound on the last float forward: per Gaussian ids[i], the K = 23 + 3 M output-space
+// bounds. Returns K, or -1.
+int oracle_owner_grad_bound(void* hv, const float* term, const int32_t* ids, int n, float* out)
+{
+    Handle* h = static_cast<Handle*>(hv);
+    if (h->dbl) return -1;
+    return oracle::owner_grad_bound(h->sf, term, ids, n, out);
 }
 
 }  // extern "C"

@@ -29,7 +29,7 @@ def _check(g, cam, dL, Cn, variant, bg=(0.0, 0.0, 0.0)):
     import oracle as O
 
     ob, _, gb = oracle_run(g, cam, dL, bg=bg, nthreads=4)
-    allow = reference_allowance(ob)
+    allow = reference_allowance(ob, dL)
     ov = O.Oracle(False, variant)
     ov.forward(background=np.asarray(bg, np.float64), means3D=g.means3D, opacity=g.opacity, scales=g.scales,
                rotations=g.rotations, shs=g.shs, viewmatrix=cam.viewmatrix, projmatrix=cam.projmatrix,

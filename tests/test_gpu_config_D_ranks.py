@@ -1,6 +1,7 @@
-"""Config D (1 M Gaussians, eight equirect views, one per GPU; BASELINE.json) through the real exchange code: eight
-ranks over gloo, all on cuda:0 (the one-GPU box's stand-in for the 8-GPU node the driver's scaling run uses). Each
-rank renders its view of the config-C scene, runs the HIP backward into its GradBuffer and calls
+"""Config D (1 M Gaussians, eight equirect views, one per GPU; BASELINE.json) and config E (5 M Gaussians, a mixed
+batch: four 4096x2048 equirect views on ranks 0-3, four 1920x1080 pinhole views on ranks 4-7, as bench.py places
+them) through the real exchange code: eight ranks over gloo, all on cuda:0 (the one-GPU box's stand-in for the 8-GPU node the driver's scaling run uses). Each
+rank renders its view of the config's scene, runs the HIP backward into its GradBuffer and calls
 parallel.allreduce_compact_ (the exchange bench.py runs at N > 1: all-reduce of the 44 B/G xyz / opacity / scale /
 rotation gradients, all-gather of every view's colour gradient and camera position, SH gradient rebuilt on every
 rank). Checked against the eight per-view HIP gradients computed one after another in this process:
@@ -25,7 +26,14 @@ WORLD = 8
 NAMES = {"dL_dmeans3D": "dmean3D", "dL_dopacity": "dopacity", "dL_dscales": "dscale", "dL_drotations": "drot"}
 
 
-def _worker(rank, world, port, q, tmpdir):
+def _scene_name(config, rank):
+    """bench.py's placement: config E puts the second half of the ranks on pinhole views of the same scene."""
+    if config == "E":
+        return "E" if rank < WORLD // 2 else "E_pinhole"
+    return config
+
+
+def _worker(rank, world, port, q, tmpdir, config):
     import torch
     import torch.distributed as dist
 
@@ -39,7 +47,7 @@ def _worker(rank, world, port, q, tmpdir):
     try:
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
-        g, cam, dL = omr.scene.config_scene("D", view_index=rank)
+        g, cam, dL = omr.scene.config_scene(_scene_name(config, rank), view_index=rank)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)  # noqa: E731
         m, sh = t(g.means3D), t(g.shs)
         vm, pm, cp, bg, e = t(cam.viewmatrix), t(cam.projmatrix), t(cam.campos), torch.zeros(3, device=dev), \
@@ -66,7 +74,8 @@ def _worker(rank, world, port, q, tmpdir):
         dist.destroy_process_group()
 
 
-def test_config_D_eight_ranks_compact_exchange(tmp_path):
+@pytest.mark.parametrize("config", ["D", "E"])
+def test_config_eight_ranks_compact_exchange(config, tmp_path):
     import torch
 
     with socket.socket() as s:
@@ -74,7 +83,7 @@ def test_config_D_eight_ranks_compact_exchange(tmp_path):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q, str(tmp_path))) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q, str(tmp_path), config)) for r in range(WORLD)]
     for p in procs:
         p.start()
     digests = dict(q.get(timeout=420) for _ in procs)
@@ -90,7 +99,7 @@ def test_config_D_eight_ranks_compact_exchange(tmp_path):
     R, par = omr.rasterizer, omr.parallel
     sums, mags, dsh_seq, dcolors, campos = None, None, None, [], []
     for v in range(WORLD):
-        g, cam, dL = omr.scene.config_scene("D", view_index=v)
+        g, cam, dL = omr.scene.config_scene(_scene_name(config, v), view_index=v)
         h = hip_run(g, cam, dL)
         gr = h["grads"]
         part = np.concatenate([to_np(gr[NAMES[k]]).reshape(g.P, -1) for k in NAMES], axis=1).astype(np.float64)

@@ -126,3 +126,21 @@ def test_gradbuffer_layout():
         v = b.views[k]
         assert v.is_contiguous() and v.data_ptr() == b.flat.data_ptr() + 4 * off
         off += v.numel()
+
+
+def test_scaling_model_matches_design_table():
+    """parallel.predict_step_ms restates DESIGN.md §6's model (bench.py reports it at N > 1 as `predicted`): config D
+    at P = 1 M with 1.11 ms per-rank compute and gaussian_bwd 0.11 ms — t_AR / t_AG as in the DESIGN table, and a
+    single GPU is just its compute."""
+    import _omnigs
+
+    par = _omnigs.load().parallel
+    P = 1_000_000
+    one = par.predict_step_ms(1, P, [1.11], 0.11)
+    assert one["step_ms"] == 1.11 and one["tail_ms"] == 0.0
+    for n, ar, ag in ((2, 0.80, 0.22), (4, 0.40, 0.22), (8, 0.23, 0.25)):
+        r = par.predict_step_ms(n, P, [1.11] * n, 0.11)
+        assert abs(r["t_ar_ms"] - ar) < 0.01 and abs(r["t_ag_ms"] - ag) < 0.01, (n, r)
+        assert r["step_ms"] > 1.11 and r["tail_ms"] >= r["t_ar_ms"] + r["t_ag_ms"] - 0.11
+    flat = par.predict_step_ms(8, P, [1.11] * 8, 0.11, exchange="flat")
+    assert flat["step_ms"] > par.predict_step_ms(8, P, [1.11] * 8, 0.11)["step_ms"]
