@@ -210,9 +210,9 @@ def check_grads(test, ref, allow, P, names=None):
 # consumption (profiles/r04_parity_residuals.json) with headroom, at or below what the FMA-contracted proxies of the
 # reference need (profiles/ambiguity.json), so a regression that pushes pixels or Gaussians into the allowance fails.
 def default_budget(P, pixels):
-    return dict(pixels_over_1e4=max(4, pixels // 20000), final_T_over_1e4=max(4, pixels // 20000),
-                gaussians_outside_strict=max(8, P // 5000), owner_gaussians_used=max(4, P // 10000),
-                exposed_gaussians_used=max(4, P // 10000))
+    return dict(pixels_over_1e4=max(2, pixels // 100000), final_T_over_1e4=max(2, pixels // 100000),
+                n_contrib_mismatches=max(4, pixels // 50000), gaussians_outside_strict=max(4, P // 50000),
+                owner_gaussians_used=max(2, P // 100000), exposed_gaussians_used=max(2, P // 100000))
 
 
 def record_residuals(rec, budget=None):

@@ -8,10 +8,14 @@ Bars (written here, checked per case):
     power at 0, T(1-alpha) at 1e-4 inside their rounding windows, near-equal depths that may sort the other way,
     ambiguous tile rects), the largest colour change those decisions can make (helpers.check_image).
     n_contrib equal on >= 99.99 % of pixels (the GPU's v_exp vs glibc expf at such a decision);
-  * gradients: per element |gpu - oracle| <= 1e-3 |oracle| + 1e-4 max|oracle| (helpers.grad_close), except the
-    Gaussians owning such a decision (excused: they may gain or lose a whole pixel term) and the wider bar 1e-2 /
-    1e-3 max for the Gaussians blending behind one (helpers.check_grads). The same bars hold for two FMA-contracted
-    builds of the oracle, the proxy of the reference binary (tests/test_contraction_allowance.py).
+  * gradients: per element |gpu - oracle| <= 1e-3 |oracle| + 1e-4 max|oracle| (helpers.grad_close); the Gaussians
+    owning such a decision get that bar plus their owner bound (the magnitude of the pixel terms their flagged
+    decisions can move, through the linear preprocess backward: oracle/ambiguity.hpp owner_grad_bound), the ones
+    blending behind one the wider bar 1e-2 / 1e-3 max (helpers.check_grads). The same bars hold for two FMA-contracted
+    builds of the oracle, the proxy of the reference binary (tests/test_contraction_allowance.py);
+  * how much of that allowance the HIP path uses is recorded per case (helpers.record_residuals:
+    $OMR_PARITY_RESIDUALS, profiles/r04_parity_residuals.json) and capped: CONFIG_BUDGETS at the BASELINE configs,
+    helpers.default_budget elsewhere.
 """
 import os
 
@@ -168,6 +172,23 @@ def test_capacity_hint_too_small_reruns_back_half():
     _compare(g, cam, dL)
 
 
+# The HIP path's allowance budget at the BASELINE configs: about twice what it used at r04a
+# (profiles/r04_parity_residuals.json: C 2 pixels over 1e-4 / 1 Gaussian outside grad_close, E 17 / 3, E pinhole 1 / 0,
+# B 0 / 0), and below what the FMA-contracted proxies of the reference need (profiles/ambiguity.json: C 14-15 pixels
+# and 5-11 Gaussians, E 26-884 pixels). A kernel change that pushes more decisions into the allowance fails here.
+CONFIG_BUDGETS = {
+    "B": dict(pixels_over_1e4=4, final_T_over_1e4=2, n_contrib_mismatches=4, gaussians_outside_strict=4,
+              owner_gaussians_used=2, exposed_gaussians_used=2),
+    "C": dict(pixels_over_1e4=6, final_T_over_1e4=2, n_contrib_mismatches=4, gaussians_outside_strict=4,
+              owner_gaussians_used=3, exposed_gaussians_used=2),
+    "E_pinhole": dict(pixels_over_1e4=4, final_T_over_1e4=2, n_contrib_mismatches=16, gaussians_outside_strict=4,
+                      owner_gaussians_used=2, exposed_gaussians_used=2),
+    "E": dict(pixels_over_1e4=36, final_T_over_1e4=4, n_contrib_mismatches=40, gaussians_outside_strict=8,
+              owner_gaussians_used=8, exposed_gaussians_used=4),
+}
+CONFIG_BUDGETS["D"] = dict(CONFIG_BUDGETS["C"], pixels_over_1e4=8, n_contrib_mismatches=8)
+
+
 @pytest.fixture
 def oracle_mt():
     """The oracle's forward on all of the box's CPU share (its backward takes nthreads per call)."""
@@ -190,7 +211,7 @@ def test_baseline_config_full(name, oracle_mt):
          offsets in every binning kernel).
     Bars as in the module docstring: integers bit-exact, image 1e-4, gradients grad_close."""
     g, cam, dL = scene.config_scene(name)
-    _compare(g, cam, dL, nthreads=oracle_mt)
+    _compare(g, cam, dL, nthreads=oracle_mt, budget=CONFIG_BUDGETS[name])
 
 
 def test_more_than_65536_tiles_sorts_32_bit_tile_keys(oracle_mt):
@@ -240,7 +261,7 @@ def test_config_D_standin_eight_views(oracle_mt):
     for v in range(8):
         g, cam, dL = scene.config_scene("C", view_index=v)
         if v in (0, 5):
-            _compare(g, cam, dL, nthreads=oracle_mt)
+            _compare(g, cam, dL, nthreads=oracle_mt, budget=CONFIG_BUDGETS["D"])
         h = hip_run(g, cam, dL)
         gr = h["grads"]
         part = torch.cat([gr["dmean3D"].reshape(-1, 3), gr["dopacity"].reshape(-1, 1), gr["dscale"].reshape(-1, 3),
