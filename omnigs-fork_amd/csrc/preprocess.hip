@@ -79,6 +79,35 @@ __device__ __forceinline__ float3 cov2d_from_J(const float* v, const float J0[3]
     return {c00, c01, c11};
 }
 
+// The inputs preprocess_point reads, loaded up front (before the SH rows' LDS-DMA is issued: vector-memory
+// operations retire in issue order, so a load issued after the DMA would make the geometry wait for the SH rows).
+// The camera matrices are wave-uniform (SGPRs after readfirstlane).
+struct PreIn {
+    float v[16], pm[16];
+    float sx, sy, sz, opacity;
+    float4 q;
+};
+template <int CAM>
+__device__ __forceinline__ void load_pre_in(const PreprocessArgs& a, int idx, bool valid, PreIn& in)
+{
+#pragma unroll
+    for (int k = 0; k < 16; ++k) in.v[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, a.viewmatrix[k])));
+    if constexpr (CAM != CAM_LONLAT) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) in.pm[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, a.projmatrix[k])));
+    }
+    in.sx = in.sy = in.sz = in.opacity = 0.f;
+    in.q = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (valid) {
+        in.opacity = a.opacities[idx];
+        if (a.cov3D_precomp == nullptr) {
+            in.sx = a.scales[3 * idx], in.sy = a.scales[3 * idx + 1], in.sz = a.scales[3 * idx + 2];
+            if ((reinterpret_cast<uintptr_t>(a.rotations) & 15u) == 0) in.q = reinterpret_cast<const float4*>(a.rotations)[idx];
+            else in.q = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
+        }
+    }
+}
+
 // What one Gaussian's preprocess produces (forward.cu:693-702); rec = the 64-B render record (raster_common.h)
 struct PreOut {
     float4 rec[SPLAT_F4];
@@ -89,13 +118,14 @@ struct PreOut {
 };
 
 // One Gaussian, forward.cu:593-703 (lonlat) / :231-340 (pinhole). Returns false for a culled Gaussian (the caller
-// then writes radius 0, no tiles, the culled sort key). shv: the Gaussian's SH row in registers when sh16, else
-// the row is read from a.shs.
+// then writes radius 0, no tiles, the culled sort key). The colour (SH -> RGB, or colors_precomp) is evaluated here
+// only with `colour`; otherwise the caller fills o.rec[2].xyz and o.clamp_bits (the LDS-DMA staged SH path).
+// shv: the Gaussian's SH row in registers when sh16, else the row is read from a.shs.
 template <int CAM>
-__device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, int idx, float3 p_orig, bool sh16,
-                                                 const float (&shv)[48], PreOut& o)
+__device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, const PreIn& in, int idx, float3 p_orig,
+                                                 bool sh16, const float (&shv)[48], PreOut& o, bool colour = true)
 {
-    const float* v = a.viewmatrix;
+    const float* v = in.v;
     const float3 t = transformPoint4x3(p_orig, v);
     float2 point_image;
     float depth;
@@ -133,7 +163,7 @@ __device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, int id
             if (a.prefiltered) atomicOr(a.error_flag, 1);
             return false;
         }
-        const float4 p_hom = transformPoint4x4(p_orig, a.projmatrix);
+        const float4 p_hom = transformPoint4x4(p_orig, in.pm);
         const float p_w = 1.0f / (p_hom.w + 0.0000001f);
         point_image = {ndc2Pix(p_hom.x * p_w, a.W), ndc2Pix(p_hom.y * p_w, a.H)};
         depth = t.z;
@@ -157,10 +187,7 @@ __device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, int id
 #pragma unroll
         for (int k = 0; k < 6; ++k) c3[k] = a.cov3D_precomp[6 * idx + k];
     } else {
-        float4 q;
-        if ((reinterpret_cast<uintptr_t>(a.rotations) & 15u) == 0) q = reinterpret_cast<const float4*>(a.rotations)[idx];
-        else q = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
-        cov3d_from_scale_rot(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2], a.scale_modifier, q, c3);
+        cov3d_from_scale_rot(in.sx, in.sy, in.sz, a.scale_modifier, in.q, c3);
     }
     const float3 cov = cov2d_from_J(v, J0, J1, c3);
 
@@ -179,9 +206,10 @@ __device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, int id
     const uint32_t area = (y1 - y0) * (x1 - x0);
     if (area == 0) return false;
 
-    float rgb[3];
+    float rgb[3] = {0.f, 0.f, 0.f};
     uint8_t clamp_bits = 0;
-    if (a.colors_precomp == nullptr) {
+    if (!colour) {
+    } else if (a.colors_precomp == nullptr) {
         const float3 cp = {a.campos[0], a.campos[1], a.campos[2]};
         float dx = p_orig.x - cp.x, dy = p_orig.y - cp.y, dz = p_orig.z - cp.z;
         const float len = sqrtf(dx * dx + dy * dy + dz * dz);
@@ -196,7 +224,7 @@ __device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, int id
         rgb[2] = a.colors_precomp[3 * idx + 2];
     }
     o.rec[0] = {point_image.x, point_image.y, depth, 0.0f};  // .w (slot base) is written by emit
-    o.rec[1] = {conic.x, conic.y, conic.z, a.opacities[idx]};
+    o.rec[1] = {conic.x, conic.y, conic.z, in.opacity};
     o.rec[2] = {rgb[0], rgb[1], rgb[2], __builtin_bit_cast(float, x1 - x0)};
     o.rec[3] = {__builtin_bit_cast(float, x0), __builtin_bit_cast(float, y0), __builtin_bit_cast(float, x1),
                 __builtin_bit_cast(float, y1)};
@@ -211,11 +239,22 @@ __device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, int id
 // 64 render records (4 KiB) as contiguous spans through LDS (wave_rows.h). The SH rows are requested before the
 // projection math so their latency overlaps it; pinhole views, which frustum-cull most of a scene, request only
 // the rows of points in front of the camera.
+// OMR_PRE_DMA: how the SH rows are staged (0: registers through a 13-KiB image per wave, wave_rows_load; 1: LDS-DMA
+// into the same image, wave_rows_dma, with the geometry computed while it lands; 2: LDS-DMA in two column halves
+// through a 7-KiB image). Interleaved A/B at config C (profiles/r04c_ab_preprocess_dma.txt, 3 rounds): 0 0.0823 ms,
+// 1 0.0836 ms, 2 0.0957 ms — the kernel streams at ~4.2 TB/s either way, so the register path stays the default.
+#ifndef OMR_PRE_DMA
+#define OMR_PRE_DMA 0
+#endif
+
 template <int CAM>
 __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
 {
     constexpr int SH_F4 = 12;  // 16 coefficients x 3 channels
-    __shared__ float4 s_stage[4][stage_f4<SH_F4>()];
+    constexpr int HALF = SH_F4 / 2;
+    constexpr int IMG_F4 = OMR_PRE_DMA == 2 ? 64 * dma_stride<HALF>() : stage_f4<SH_F4>();
+    static_assert(IMG_F4 >= stage_f4<SPLAT_F4>(), "the image also stages the render records");
+    __shared__ float4 s_stage[4][IMG_F4];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     {   // scratch words later kernels expect zeroed (counters, tile ranges / costs, sort scratch): no memset launches
         const size_t gtid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
@@ -235,12 +274,74 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     const bool sh16 = a.colors_precomp == nullptr && a.M == 16 && (reinterpret_cast<uintptr_t>(a.shs) & 15u) == 0;
     const int nf4 = (3 * (a.D + 1) * (a.D + 1) + 3) >> 2;
     float shv[48];
+    PreIn in;
+    load_pre_in<CAM>(a, idx, valid, in);
+#if OMR_PRE_DMA
+    // LDS-DMA path: the DMA is issued first, then the geometry of every lane runs while the rows land (its inputs
+    // were loaded before the DMA, load_pre_in), then the colour from the image. The DMAs are issued with the whole
+    // wave active (a position of the image is not its lane's row). OMR_PRE_DMA == 1: the whole row in one 13-KiB
+    // image; 2: two column halves through a 7-KiB image (more waves per CU, a second round trip per wave).
+    PreOut o;
+    bool vis = false;
     if (sh16) {
-        float4 shq[SH_F4];
-        const bool want = CAM == CAM_LONLAT ? valid : valid && transformPoint4x3(p_orig, a.viewmatrix).z > 0.2f;
+        constexpr int S = OMR_PRE_DMA == 1 ? dma_stride<SH_F4>() : dma_stride<HALF>();
+        const bool want = CAM == CAM_LONLAT ? valid : valid && transformPoint4x3(p_orig, in.v).z > 0.2f;
         const uint64_t rows = __ballot(want);
-        wave_rows_load<SH_F4>(reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4, rows, nf4, stage,
-                              lane);
+        const float4* src = reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4;
+        if constexpr (OMR_PRE_DMA == 1) wave_rows_dma<SH_F4, 0, SH_F4>(src, rows, nf4, stage, lane);
+        else wave_rows_dma<SH_F4, 0, HALF>(src, rows, nf4, stage, lane);
+        vis = valid && preprocess_point<CAM>(a, in, idx, p_orig, sh16, shv, o, false);
+        float dx = 0.f, dy = 0.f, dz = 0.f, res[3];
+        if (vis) {
+            const float3 cp = {a.campos[0], a.campos[1], a.campos[2]};
+            dx = p_orig.x - cp.x, dy = p_orig.y - cp.y, dz = p_orig.z - cp.z;  // forward.cu:37-38, as preprocess_point
+            const float len = sqrtf(dx * dx + dy * dy + dz * dz);
+            dx = dx / len;
+            dy = dy / len;
+            dz = dz / len;
+        }
+        dma_wait();
+        wave_sync();
+        {
+            float h[24];
+#pragma unroll
+            for (int q = 0; q < HALF; ++q) {
+                const float4 v = q < nf4 ? stage[lane * S + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+                h[4 * q] = v.x, h[4 * q + 1] = v.y, h[4 * q + 2] = v.z, h[4 * q + 3] = v.w;
+            }
+            sh_to_rgb_part0(a.D, dx, dy, dz, h, res);
+        }
+        if constexpr (OMR_PRE_DMA != 1) {
+            wave_sync();  // the second half overwrites the image
+            if (nf4 > HALF) {
+                wave_rows_dma<SH_F4, HALF, HALF>(src, rows, nf4, stage, lane);
+                dma_wait();
+                wave_sync();
+            }
+        }
+        {
+            constexpr int C1 = OMR_PRE_DMA == 1 ? HALF : 0;  // image column of coefficient 8's float4
+            float h[24];
+#pragma unroll
+            for (int q = HALF; q < SH_F4; ++q) {
+                const float4 v = q < nf4 ? stage[lane * S + q - HALF + C1] : make_float4(0.f, 0.f, 0.f, 0.f);
+                h[4 * (q - HALF)] = v.x, h[4 * (q - HALF) + 1] = v.y, h[4 * (q - HALF) + 2] = v.z, h[4 * (q - HALF) + 3] = v.w;
+            }
+            float rgb[3];
+            sh_to_rgb_part1(a.D, dx, dy, dz, h, res, rgb, o.clamp_bits);
+            o.rec[2].x = rgb[0], o.rec[2].y = rgb[1], o.rec[2].z = rgb[2];
+        }
+        wave_sync();  // the image is reused for the records below
+    } else {
+        vis = valid && preprocess_point<CAM>(a, in, idx, p_orig, sh16, shv, o);
+    }
+#else
+    if (sh16) {
+        const bool want = CAM == CAM_LONLAT ? valid : valid && transformPoint4x3(p_orig, in.v).z > 0.2f;
+        const uint64_t rows = __ballot(want);
+        const float4* src = reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4;
+        float4 shq[SH_F4];
+        wave_rows_load<SH_F4>(src, rows, nf4, stage, lane);
         wave_sync();
 #pragma unroll
         for (int q = 0; q < SH_F4; ++q)
@@ -254,9 +355,9 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
             shv[4 * q + 3] = shq[q].w;
         }
     }
-
     PreOut o;
-    const bool vis = valid && preprocess_point<CAM>(a, idx, p_orig, sh16, shv, o);
+    const bool vis = valid && preprocess_point<CAM>(a, in, idx, p_orig, sh16, shv, o);
+#endif
     if (valid) {
         a.radii[idx] = vis ? o.rad : 0;
         g.tiles_touched[idx] = vis ? o.area : 0u;
