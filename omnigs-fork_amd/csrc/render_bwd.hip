@@ -48,6 +48,14 @@ namespace {
 
 OMR_STAMP_DECL(g_stamps_bwd)
 
+#ifndef OMR_BWD_NOSKIP
+#define OMR_BWD_NOSKIP 0
+#endif
+// diagnostic (A/B only): OMR_BWD_DIAG_EXTRA independent extra VALU per evaluated band, to price one VALU op there
+#ifndef OMR_BWD_DIAG_EXTRA
+#define OMR_BWD_DIAG_EXTRA 0
+#endif
+
 #ifdef OMR_BWD_COUNT
 // diagnostic: staged instances, (instance, band) evaluations, evaluations with a contributing pixel, instances
 // with any contribution, contributing (pixel, instance) pairs
@@ -226,10 +234,15 @@ __global__ __launch_bounds__(64 * TW_WAVES) void render_bwd_kernel(RenderBwdArgs
                     // backward.cu:770-781: skip positions at/after the pixel's last contributor, power > 0, alpha < 1/255
                     const bool contrib = (decltype(pos_test)::value ? ipos < lastb : true) && p2_in_band(p2, lo);
                     BWD_COUNT(1, 1);
+#if OMR_BWD_NOSKIP
+                    // A/B: no branch on the band's ballot; a band without a contributor runs through with zeros
+                    any |= __ballot(contrib) ? 1u << b : 0u;
+#else
                     if (!__ballot(contrib)) continue;
                     BWD_COUNT(2, 1);
                     BWD_COUNT(4, (uint32_t)__popcll(__ballot(contrib)));
                     any |= 1u << b;
+#endif
                     // a lane that does not contribute gets oG = alpha = 0: inv = 1, T and s unchanged, u = wc = 0
                     const float oG = __builtin_amdgcn_exp2f(contrib ? p2 : -__builtin_inff());  // o G (column_quad)
                     const float alpha = fminf(0.99f, oG);
@@ -246,6 +259,10 @@ __global__ __launch_bounds__(64 * TW_WAVES) void render_bwd_kernel(RenderBwdArgs
                     suyy = __builtin_fmaf(uy, dy, suyy);
                     sc01 = __builtin_elementwise_fma(f2v{wc, wc}, dp01[b], sc01);
                     sc2 = __builtin_fmaf(wc, dp2b, sc2);
+#if OMR_BWD_DIAG_EXTRA
+#pragma unroll
+                    for (int e = 0; e < OMR_BWD_DIAG_EXTRA; ++e) asm volatile("v_mov_b32 %0, %0" : "+v"(sc2));  // 1 VALU each
+#endif
                 }
                 const uint32_t slot_j = __builtin_bit_cast(uint32_t, f.w);
                 if (!any) continue;  // no pixel took a contribution: no row

@@ -33,6 +33,11 @@ namespace {
 
 OMR_STAMP_DECL(g_stamps_fwd)
 
+// diagnostic (A/B only): OMR_FWD_DIAG_EXTRA extra VALU issue slots per evaluated band, to price one VALU op there
+#ifndef OMR_FWD_DIAG_EXTRA
+#define OMR_FWD_DIAG_EXTRA 0
+#endif
+
 template <bool DEPTH, int FWD_BANDS>
 __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel(RenderFwdArgs a)
 {
@@ -182,6 +187,10 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
                 // blended iff ok and not sat (alpha >= 1/255, T >= 1e-4: wgt > 0); a done lane is sat. Both are compare
                 // masks already, so this is a scalar and-not, not a third vector compare
                 last[b] = (ok && !sat) ? contributor : last[b];
+#if OMR_FWD_DIAG_EXTRA
+#pragma unroll
+                for (int e = 0; e < OMR_FWD_DIAG_EXTRA; ++e) asm volatile("v_mov_b32 %0, %0" : "+v"(C2[b]));
+#endif
             }
             if (sat_any) {  // some pixel saturated: drop bands with no live pixel left
 #pragma unroll

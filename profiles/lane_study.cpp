@@ -44,6 +44,9 @@ int main(int argc, char** argv)
     const int gx = (W + 15) / 16, gy = (H + 15) / 16;
     // totals: [mapping][fwd/bwd] steps, contributing pairs
     double steps[4][2] = {}, evalpairs[4][2] = {}, contrib = 0, fwd_live = 0;
+    // band pairs (0, 1) and (2, 3) of a tile (one lane's two pixels of a pair share a column): per direction, the
+    // (instance, pair) evaluations that need both bands and those that need one (packed-math study)
+    double pair_both[2] = {0, 0}, pair_one[2] = {0, 0};
 #pragma omp parallel for schedule(dynamic, 16) reduction(+ : contrib, fwd_live)
     for (int t = 0; t < gx * gy; ++t) {
         const int tx = t % gx, ty = t / gx;
@@ -118,6 +121,38 @@ int main(int argc, char** argv)
             }
         };
         double ls[4][2] = {}, lp[4][2] = {};
+        {
+            // per band: window ends and reach of each instance
+            int fe[4], be[4];
+            for (int b = 0; b < 4; ++b) {
+                fe[b] = -1, be[b] = 0;
+                for (int r = 0; r < 4; ++r)
+                    for (int c = 0; c < 16; ++c) {
+                        const int p = (4 * b + r) * 16 + c;
+                        fe[b] = std::max(fe[b], done[p]);
+                        be[b] = std::max(be[b], last[p]);
+                    }
+            }
+            double both[2] = {0, 0}, one[2] = {0, 0};
+            for (uint32_t k = 0; k < n; ++k) {
+                bool rb[4];
+                for (int b = 0; b < 4; ++b) {
+                    rb[b] = false;
+                    for (int q = 0; q < 64 && !rb[b]; ++q) rb[b] = reach[(size_t)k * 256 + 64 * b + q];
+                }
+                for (int pr = 0; pr < 2; ++pr) {
+                    const int b0 = 2 * pr, b1 = b0 + 1;
+                    for (int dir = 0; dir < 2; ++dir) {
+                        const bool n0 = rb[b0] && (dir == 0 ? (int)k <= fe[b0] : (int)k < be[b0]);
+                        const bool n1 = rb[b1] && (dir == 0 ? (int)k <= fe[b1] : (int)k < be[b1]);
+                        if (n0 && n1) both[dir] += 1;
+                        else if (n0 || n1) one[dir] += 1;
+                    }
+                }
+            }
+#pragma omp critical
+            for (int dir = 0; dir < 2; ++dir) { pair_both[dir] += both[dir]; pair_one[dir] += one[dir]; }
+        }
         // band16x4
         for (int b = 0; b < 4; ++b) {
             std::vector<int> pix;
@@ -159,6 +194,8 @@ int main(int argc, char** argv)
         std::printf(", \"%s\": {\"fwd_steps\": %.0f, \"bwd_steps\": %.0f, \"fwd_lane_use\": %.4f, \"bwd_lane_use\": %.4f}",
                     names[m], steps[m][0], steps[m][1], evalpairs[m][0] / (64.0 * steps[m][0]),
                     evalpairs[m][1] / (64.0 * steps[m][1]));
+    std::printf(", \"band_pairs\": {\"fwd_both\": %.0f, \"fwd_one\": %.0f, \"bwd_both\": %.0f, \"bwd_one\": %.0f}",
+                pair_both[0], pair_one[0], pair_both[1], pair_one[1]);
     std::printf("}\n");
     (void)fwd_live;
     return 0;
