@@ -214,6 +214,8 @@ void omr_ply_close(omr_ply* ply);
 int omr_ply_save(const char* path, int P, int Mr, const float* const params[6], void* stream);
 
 /* --- scratch sizes (bytes the allocation callbacks are asked for) -------------------------------- */
+/* geometry: the size for a view that takes the row binning (at most 1024 tiles a side); wider views are asked for
+   about 56 B per Gaussian less (no row-binning arrays), so this is an upper bound for any view */
 size_t omr_geometry_bytes(int P);
 size_t omr_image_bytes(int width, int height);
 size_t omr_binning_bytes(int num_rendered, int width, int height);

@@ -64,6 +64,11 @@ static_assert(ColGeoS::N == 1u << 11 && ColGeoL::N == 1u << 12, "cb_shift 11 / 1
 // grid caps of the grid-stride chunk kernels (256 CUs: 8 resident hist blocks of 256 threads, 4 scatter blocks of
 // 256 threads and <= 40 KiB LDS, or 2 of 512 threads and <= 80 KiB)
 constexpr uint32_t BIN_GRID_HIST = 2048, BIN_GRID_SCATTER = 1024;
+// OMR_BIN_FUSED_INFO (default 1): every rows_scatter block derives the per-row info itself (a scan over the rows) and
+// block 0 publishes what the columns pass reads, instead of a one-block rows_info launch between them
+#ifndef OMR_BIN_FUSED_INFO
+#define OMR_BIN_FUSED_INFO 1
+#endif
 
 #ifdef OMR_BIN_STAMPS  // diagnostic: per-phase s_memrealtime stamps of cols_scatter_kernel (profiles/bin_stamps.py)
 constexpr int BSTAMP_ITERS = 16, BSTAMP_PH = 8;
@@ -314,32 +319,53 @@ __global__ __launch_bounds__(RB_THREADS) void rows_hist_kernel(BinArgs a)
 // count and first chunk of the columns pass: rowinfo[y] = {entry, slot, chunk_base, chunks}; the live lengths of the
 // columns pass, the zero past its counts that the scan turns into their total (the last tile's end), and the owner
 // end of every row's last columns chunk (rows_scatter_kernel writes the other owner words of desc_b).
-__global__ __launch_bounds__(BIN_MAX_GRID) void rows_info_kernel(BinArgs a)
+// rowinfo of rows [0, gy] (gy: the terminator) into ri (LDS or global): THREADS threads, NRI rows per thread; `publish`:
+// also the words, the count terminator and the owner ends of every row's last columns chunk
+template <int THREADS, int NRI>
+__device__ __forceinline__ void rows_info(const BinArgs& a, uint4* ri, bool publish, uint32_t* s_wave)
 {
-    __shared__ uint32_t s_wave[BIN_MAX_GRID / 64];
-    const uint32_t y = threadIdx.x, gy = a.gy;
+    const uint32_t gy = a.gy, tid = threadIdx.x;
     const uint32_t L = live_L(a.counters, a.cap), M = live_M(a.counters, a.cap), C = row_chunks(M);
     const size_t half = (size_t)gy * C;
     auto entry = [&](uint32_t yy) { return yy < gy ? a.hist_r[(size_t)yy * C] : M; };
     auto slot = [&](uint32_t yy) { return yy < gy ? a.hist_r[half + (size_t)yy * C] - M : L; };
-    uint32_t e0 = 0, sl0 = 0, n = 0;
-    if (y < gy && L) {
-        e0 = entry(y);
-        sl0 = slot(y);
-        n = (slot(y + 1) - sl0 + (1u << a.cb_shift) - 1u) >> a.cb_shift;
+    uint32_t e0[NRI], sl0[NRI], n[NRI], tsum = 0;
+#pragma unroll
+    for (int q = 0; q < NRI; ++q) {
+        const uint32_t y = tid * NRI + q;
+        e0[q] = sl0[q] = n[q] = 0;
+        if (y < gy && L) {
+            e0[q] = entry(y);
+            sl0[q] = slot(y);
+            n[q] = (slot(y + 1) - sl0[q] + (1u << a.cb_shift) - 1u) >> a.cb_shift;
+        }
+        tsum += n[q];
     }
     uint32_t total;
-    const uint32_t cb = bin_block_scan<BIN_MAX_GRID>(n, s_wave, &total);
-    if (y < gy) {
-        a.rowinfo[y] = make_uint4(e0, sl0, cb, n);
-        if (n) reinterpret_cast<uint32_t*>(a.desc_b)[8 * (size_t)(cb + n - 1) + 7] = entry(y + 1);
+    uint32_t cb = bin_block_scan<THREADS>(tsum, s_wave, &total);
+#pragma unroll
+    for (int q = 0; q < NRI; ++q) {
+        const uint32_t y = tid * NRI + q;
+        if (y < gy) {
+            ri[y] = make_uint4(e0[q], sl0[q], cb, n[q]);
+            if (publish && n[q]) reinterpret_cast<uint32_t*>(a.desc_b)[8 * (size_t)(cb + n[q] - 1) + 7] = entry(y + 1);
+        }
+        cb += n[q];
     }
-    if (y == 0) {
-        a.rowinfo[gy] = make_uint4(M, L, total, 0u);
-        a.words[1] = total;
-        a.words[3] = total * a.gx + 1u;
-        a.hist_b[(size_t)total * a.gx] = 0u;
+    if (tid == 0) {
+        ri[gy] = make_uint4(M, L, total, 0u);
+        if (publish) {
+            a.words[1] = total;
+            a.words[3] = total * a.gx + 1u;
+            a.hist_b[(size_t)total * a.gx] = 0u;
+        }
     }
+}
+
+__global__ __launch_bounds__(BIN_MAX_GRID) void rows_info_kernel(BinArgs a)
+{
+    __shared__ uint32_t s_wave[BIN_MAX_GRID / 64];
+    rows_info<BIN_MAX_GRID, 1>(a, a.rowinfo, true, s_wave);
 }
 
 // Per chunk: expand the slots to (owner, row), rank them by row, write the row entries (Gaussian, width | x0 << 16)
@@ -393,6 +419,14 @@ __global__ __launch_bounds__(RB_THREADS) void rows_scatter_kernel(BinArgs a)
             }
         }
     };
+#if OMR_BIN_FUSED_INFO
+    __shared__ uint4 s_ri[(1 << BITS) + 1];
+    rows_info<RB_THREADS, (1 << BITS) / RB_THREADS>(a, s_ri, blockIdx.x == 0, s_wave);
+    __syncthreads();
+    const uint4* rowinfo = s_ri;
+#else
+    const uint4* rowinfo = a.rowinfo;
+#endif
     const ChunkRange cr = xcd_chunks(C);
     if (C == 0) return;  // nothing binned (L = 0, a capacity overflow, a failed look-back): desc_r has no entry
     RowChunk k = row_chunk(a, min(cr.first, C - 1u), M);
@@ -493,11 +527,11 @@ __global__ __launch_bounds__(RB_THREADS) void rows_scatter_kernel(BinArgs a)
             a.ent_w[dst] = xw;
             a.ent_ex[dst] = ex;
             // the columns chunk whose first slot this entry holds (widths <= BIN_MAX_GRID < 2048: at most one)
-            const uint4 ri = a.rowinfo[y];
+            const uint4 ri = rowinfo[y];
             const uint32_t rel = ex - ri.y, kk = (rel + cbn - 1u) >> a.cb_shift;
             if (kk < ri.w && (kk << a.cb_shift) < rel + (xw & 0xFFFFu)) {
                 const uint32_t cc = ri.z + kk, s0 = ri.y + (kk << a.cb_shift);
-                const uint32_t s1 = min(a.rowinfo[y + 1].y, s0 + cbn);
+                const uint32_t s1 = min(rowinfo[y + 1].y, s0 + cbn);
                 reinterpret_cast<uint4*>(desc_w)[2 * (size_t)cc] = make_uint4(y, kk, ri.w, ri.z);
                 desc_w[8 * (size_t)cc + 4] = s0;
                 desc_w[8 * (size_t)cc + 5] = s1;
@@ -788,7 +822,7 @@ void launch_row_binning(const BinArgs& a_in, hipStream_t s)
     const uint32_t gh_b = std::min(cbk, BIN_GRID_HIST);
     rows_hist_kernel<<<gh_r, RB_THREADS, 0, s>>>(a);
     launch_exclusive_scan(a.hist_r, a.hist_r, nr_hist, a.words + 2, st_r, a.err, s);
-    rows_info_kernel<<<1, BIN_MAX_GRID, 0, s>>>(a);
+    if (!OMR_BIN_FUSED_INFO) rows_info_kernel<<<1, BIN_MAX_GRID, 0, s>>>(a);
     if (a.gy <= 256) rows_scatter_kernel<8><<<gs_r, RB_THREADS, 0, s>>>(a);
     else rows_scatter_kernel<10><<<gs_r, RB_THREADS, 0, s>>>(a);
     cols_hist_kernel<<<gh_b, RB_THREADS, 0, s>>>(a);

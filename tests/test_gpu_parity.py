@@ -337,6 +337,23 @@ def test_lonlat_render_depth_is_the_colour_render():
     _compare(g, cam, dL, render_depth=True)
 
 
+def test_two_wave_forward_far_centres():
+    """the two-wave forward (views below FWD_ONE_WAVE_TILES) must form dy exactly as the backward does
+    (from the tile's first pixel row, then minus 4 x the band), or an empty pixel of the position-test-free backward
+    batches could take a term the forward never blended. Large Gaussians whose centres lie many tiles away from most
+    of the tiles they reach (|dy| >> 16, where the two roundings part) on a 512-tile view, forward and backward
+    against the oracle."""
+    g, cam, dL = make_case(2000, 512, 256, LON, 98, view_index=3, spread=1.0)
+    rng = np.random.default_rng(98)
+    big = rng.choice(g.P, 60, replace=False)
+    g.scales = g.scales.copy()
+    g.scales[big] *= rng.uniform(15.0, 40.0, size=(60, 1)).astype(np.float32)
+    assert (cam.width // 16) * (cam.height // 16) < 16384  # the two-wave forward
+    o, _, _ = oracle_run(g, cam)
+    assert (o.get("tiles_touched") > 64).sum() >= 20
+    _compare(g, cam, dL)
+
+
 def test_empty_scene_returns_zero_image():
     g, cam, dL = make_case(0, 64, 32, LON, 24)
     h = hip_run(g, cam, dL, bg=(1.0, 1.0, 1.0))
