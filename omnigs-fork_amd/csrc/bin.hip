@@ -70,6 +70,11 @@ constexpr uint32_t BIN_GRID_HIST = 2048, BIN_GRID_SCATTER = 1024;
 #define OMR_BIN_FUSED_INFO 1
 #endif
 
+// OMR_BIN_RANK_OR (default 1): the rows and columns scatters rank by LDS OR peer tables (rank_items), not ballot matches
+#ifndef OMR_BIN_RANK_OR
+#define OMR_BIN_RANK_OR 1
+#endif
+
 #ifdef OMR_BIN_STAMPS  // diagnostic: per-phase s_memrealtime stamps of cols_scatter_kernel (profiles/bin_stamps.py)
 constexpr int BSTAMP_ITERS = 16, BSTAMP_PH = 8;
 __device__ uint64_t g_bin_stamps[BIN_GRID_SCATTER][BSTAMP_ITERS][BSTAMP_PH];
@@ -183,10 +188,12 @@ __device__ __forceinline__ void owner_fill(uint16_t* s_own, uint32_t* s_wave)
 // Ranks G::ITEMS items per lane in round layout (item = wave * PER_WAVE + 64 r + lane, i.e. slot order) by digit
 // d[r] < 2^BITS, stably: on return lp[r] = the item's position in the block's digit-sorted order and s_dstart[d] =
 // the block-local start of digit d. s_whist: [WAVES][2^BITS] scratch. Matches radix_downsweep_kernel (sort.hip).
+// s_peer_all (optional, [WAVES][2^BITS] u64, free from the first barrier on): the rounds' peer masks by LDS ORs
+// instead of ballot matches.
 template <int BITS, class G>
 __device__ __forceinline__ void rank_items(const uint32_t (&d)[G::ROUNDS], const bool (&valid)[G::ROUNDS],
                                            uint32_t (&lp)[G::ROUNDS], uint32_t (*s_whist)[1 << BITS],
-                                           uint32_t* s_dstart, uint32_t* s_wave)
+                                           uint32_t* s_dstart, uint32_t* s_wave, uint64_t* s_peer_all = nullptr)
 {
     constexpr uint32_t NB = 1u << BITS;
     const uint32_t tid = threadIdx.x, w = tid >> 6;
@@ -196,9 +203,16 @@ __device__ __forceinline__ void rank_items(const uint32_t (&d)[G::ROUNDS], const
     // running count of the digit after every lane of the wave has read it, with an add that returns nothing (a
     // ds_add_rtn per group plus a broadcast measured slower: config E tile sort 1.78 vs 2.14 ms)
     uint32_t lr[G::ROUNDS];
+    uint64_t pm[G::ROUNDS];
+    if (s_peer_all) {  // peer masks by LDS ORs (raster_common.h), the tables overlaid on storage free from here on
+        wave_peer_masks<G::ROUNDS, NB>(d, valid, pm, s_peer_all + (size_t)w * NB);
+    } else {
+#pragma unroll
+        for (int r = 0; r < G::ROUNDS; ++r) pm[r] = wave_match_digit<BITS>(d[r], valid[r]);
+    }
 #pragma unroll
     for (int r = 0; r < G::ROUNDS; ++r) {
-        const uint64_t peers = wave_match_digit<BITS>(d[r], valid[r]);
+        const uint64_t peers = pm[r];
         const uint32_t rank = mask_rank(peers);
         // LDS ops of a wave complete in issue order: every lane reads the count before the leader's add lands, and
         // the next round's read sees it; the add returns nothing, so no round waits for the previous one's read
@@ -378,7 +392,7 @@ __global__ __launch_bounds__(RB_THREADS) void rows_scatter_kernel(BinArgs a)
 {
     // phase 1 (expansion): per owner, its first row minus its first slot (slot s is row s + s_yoff); phase 2
     // (write-out): the slots sorted by row, owner | row << 16
-    __shared__ uint32_t s_yoff_sorted[RB_N];
+    __shared__ __attribute__((aligned(16))) uint32_t s_yoff_sorted[RB_N];  // also the rank's peer tables (u64)
     __shared__ uint32_t s_gid[RB_N];
     __shared__ uint32_t s_xw[RB_N];  // the entry word: rect width | x0 << 16
     __shared__ __attribute__((aligned(16))) uint16_t s_own[RB_N];
@@ -388,6 +402,7 @@ __global__ __launch_bounds__(RB_THREADS) void rows_scatter_kernel(BinArgs a)
     __shared__ uint32_t s_wbase[1 << BITS];
     __shared__ uint32_t s_wave[RB_WAVES];
     __shared__ uint32_t s_qtot[RB_ITEMS][RB_WAVES];
+    static_assert(BITS != 8 || sizeof(s_yoff_sorted) >= RB_WAVES * 256 * sizeof(uint64_t), "peer tables fit s_yoff");
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
     const uint32_t M = live_M(a.counters, a.cap), C = row_chunks(M), gy = a.gy;
     const size_t half = (size_t)gy * C;
@@ -473,7 +488,9 @@ __global__ __launch_bounds__(RB_THREADS) void rows_scatter_kernel(BinArgs a)
             d[r] = valid[r] ? s + s_yoff[o] : 0u;
             own[r] = o;
         }
-        rank_items<BITS, RowGeo>(d, valid, lp, s_whist, s_dstart, s_wave);  // its barriers end the expansion's reads of s_yoff
+        // its barriers end the expansion's reads of s_yoff, whose storage then holds the peer tables
+        rank_items<BITS, RowGeo>(d, valid, lp, s_whist, s_dstart, s_wave,
+                                 OMR_BIN_RANK_OR && BITS == 8 ? reinterpret_cast<uint64_t*>(s_yoff_sorted) : nullptr);
         uint32_t* s_sorted = s_yoff_sorted;
 #pragma unroll
         for (int r = 0; r < RB_ROUNDS; ++r)
@@ -659,6 +676,7 @@ __global__ __launch_bounds__(G::THREADS) void cols_scatter_kernel(BinArgs a)
     __shared__ uint32_t s_dstart[1 << BITS];
     __shared__ uint32_t s_gbase[1 << BITS];
     __shared__ uint32_t s_wave[G::WAVES];
+    static_assert(BITS != 8 || sizeof(s_raw) >= G::WAVES * 256 * sizeof(uint64_t), "peer tables fit s_raw");
     const uint32_t tid = threadIdx.x, gx = a.gx, C = a.words[1];
     const uint32_t L = live_L(a.counters, a.cap);
     uint8_t* row_valid = reinterpret_cast<uint8_t*>(a.binning + row_valid_offset(L));  // the backward's row map
@@ -758,7 +776,9 @@ __global__ __launch_bounds__(G::THREADS) void cols_scatter_kernel(BinArgs a)
             OMR_CS_LOAD_CONSTS(kn)
         }
         BSTAMP(it, 3);
-        rank_items<BITS, G>(d, valid, lp, s_whist, s_dstart, s_wave);  // its barriers end the expansion's reads of s_raw
+        // its barriers end the expansion's reads of s_raw, which then holds the peer tables
+        rank_items<BITS, G>(d, valid, lp, s_whist, s_dstart, s_wave,
+                            OMR_BIN_RANK_OR && BITS == 8 ? reinterpret_cast<uint64_t*>(s_raw) : nullptr);
         BSTAMP(it, 4);
         uint32_t* s_v = reinterpret_cast<uint32_t*>(s_raw);
         uint16_t* s_x = reinterpret_cast<uint16_t*>(s_v + G::N);

@@ -469,6 +469,31 @@ __device__ __forceinline__ uint64_t wave_match_digit(uint32_t d, bool valid)
     return ((uint64_t)hi << 32) | lo;
 }
 
+// The peer masks of R rounds of digits (the lanes of this wave whose digit equals this lane's, as wave_match_digit
+// returns them) by LDS ORs: each lane ORs its bit into its digit's 64-bit word of a wave-private table of NB words,
+// reads the word back — every lane's OR of that instruction is in it, and OR commutes, so the order in which the LDS
+// performs the atomics does not matter — and zeroes it for the next round. A wave's LDS operations complete in issue
+// order, so the R rounds' 3R operations go out back to back with one wait, instead of one ballot per digit bit per
+// round. An invalid lane ORs nothing in (its digit must still be < NB); its own mask is garbage and must not be used.
+template <int R, uint32_t NB>
+__device__ __forceinline__ void wave_peer_masks(const uint32_t (&d)[R], const bool (&valid)[R], uint64_t (&pm)[R],
+                                                uint64_t* s_peer)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t i = lane; i < NB / 2; i += 64) reinterpret_cast<uint4*>(s_peer)[i] = make_uint4(0u, 0u, 0u, 0u);
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t bit = 1ull << lane;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        __hip_atomic_fetch_or(&s_peer[d[r]], valid[r] ? bit : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __builtin_amdgcn_wave_barrier();
+        pm[r] = s_peer[d[r]];
+        __builtin_amdgcn_wave_barrier();
+        s_peer[d[r]] = 0ull;  // lands after every lane's read of this round
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 #endif  // __HIPCC__
 
 }  // namespace omr

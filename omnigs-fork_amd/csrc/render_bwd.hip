@@ -56,6 +56,10 @@ OMR_STAMP_DECL(g_stamps_bwd)
 #define OMR_BWD_PAIRS 0
 #endif
 // diagnostic (A/B only): OMR_BWD_DIAG_EXTRA independent extra VALU per evaluated band, to price one VALU op there
+// diagnostic (A/B only, wrong gradients): OMR_BWD_DIAG_NOMARK drops the row_valid marks, to price their stores
+#ifndef OMR_BWD_DIAG_NOMARK
+#define OMR_BWD_DIAG_NOMARK 0
+#endif
 #ifndef OMR_BWD_DIAG_EXTRA
 #define OMR_BWD_DIAG_EXTRA 0
 #endif
@@ -361,7 +365,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
                     const uint32_t dslot = (lane < 32) ? pslot : slot_u;
                     if (lead || (lane & 31) == 1)
                         a.inst_grad[(size_t)dslot * GRAD_ROW + (lead ? ((lane >> 2) & 7u) : 8u)] = lead ? tv : t8;
-                    if ((lane & 31) == 0) a.row_valid[dslot] = 1;
+                    if (!OMR_BWD_DIAG_NOMARK && (lane & 31) == 0) a.row_valid[dslot] = 1;
                     pslot = ~0u;
                 }
             }
@@ -378,7 +382,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
         const float tv = wave_sum9_lds(v, pv8, lane, s_red_all[wv], &t8);
         const bool lead = (lane & 7) == 0;
         if (lead || lane == 1) a.inst_grad[(size_t)pslot * GRAD_ROW + (lead ? (lane >> 3) : 8u)] = lead ? tv : t8;
-        if (lane == 0) a.row_valid[pslot] = 1;
+        if (!OMR_BWD_DIAG_NOMARK && lane == 0) a.row_valid[pslot] = 1;
     }
     OMR_STAMP_END(g_stamps_bwd, blockIdx.x);
 #ifdef OMR_BWD_COUNT

@@ -54,6 +54,11 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t* s
 // Tiles are handed out by a ticket; a tile publishes its total (AGG), looks back over its predecessors with one
 // wave, 64 tiles per round trip, until it meets an inclusive prefix (PRE), then publishes its own. 64-bit status
 // words, flag in bits 62-63, zeroed before the launch.
+// OMR_SORT_RANK_OR (default 1): the radix downsweeps / onesweep passes take their per-round digit peers from LDS OR
+// tables (raster_common.h: wave_peer_masks) overlaid on the key staging array, instead of ballot matches
+#ifndef OMR_SORT_RANK_OR
+#define OMR_SORT_RANK_OR 1
+#endif
 #ifndef OMR_LB_SPIN_MAX
 #define OMR_LB_SPIN_MAX (1u << 20)
 #endif
@@ -437,7 +442,7 @@ __global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const K* keys_
     __shared__ uint32_t s_dstart[RADIX];        // block-local start of each digit's run
     __shared__ uint32_t s_gbase[RADIX];         // global start of this block's run of each digit
     __shared__ uint32_t s_wave[THREADS / 64];
-    __shared__ K s_k[TILE_N];
+    __shared__ __attribute__((aligned(16))) K s_k[TILE_N];  // first the rank's peer tables (u64), when they fit
     __shared__ uint32_t s_v[TILE_N];
     const size_t n = live_count(n_cap, count);
     if (canon) vals_out = reinterpret_cast<uint32_t*>(canon + canonical_list_offset(n));
@@ -482,18 +487,35 @@ __global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const K* keys_
         v[r] = i < n ? vals_in[i] : 0u;
     }
     __syncthreads();
-#pragma unroll
-    for (int r = 0; r < ROUNDS; ++r) {
-        const bool valid = base + 64 * r < n;
-        const uint32_t d = (k[r] >> shift) & (RADIX - 1);
-        const uint64_t peers = wave_match_digit<RADIX_BITS>(d, valid);
+    // one round's rank: LDS ops of a wave complete in issue order, so every lane reads the count before the leader's
+    // add lands, and the next round's read sees it. The add needs no value back, so no round waits for the previous one
+    auto rank_round = [&](int r, bool valid, uint32_t d, uint64_t peers) {
         const uint32_t rank = mask_rank(peers);
-        // LDS ops of a wave complete in issue order: every lane reads the count before the leader's add lands, and
-        // the next round's read sees it. The add needs no value back, so no round waits for the previous one
         lr[r] = (valid ? s_whist[w][d] : 0u) + rank;
         __builtin_amdgcn_wave_barrier();
         if (valid && rank == 0) atomicAdd(&s_whist[w][d], (uint32_t)__popcll(peers));
         __builtin_amdgcn_wave_barrier();
+    };
+    if constexpr (OMR_SORT_RANK_OR && sizeof(s_k) >= WAVES * RADIX * sizeof(uint64_t)) {
+        // s_k is not written before the ranks are known: it holds the wave-private peer tables
+        uint32_t dd[ROUNDS];
+        bool vv[ROUNDS];
+        uint64_t pm[ROUNDS];
+#pragma unroll
+        for (int r = 0; r < ROUNDS; ++r) {
+            vv[r] = base + 64 * r < n;
+            dd[r] = (k[r] >> shift) & (RADIX - 1);
+        }
+        wave_peer_masks<ROUNDS, RADIX>(dd, vv, pm, reinterpret_cast<uint64_t*>(s_k) + (size_t)w * RADIX);
+#pragma unroll
+        for (int r = 0; r < ROUNDS; ++r) rank_round(r, vv[r], dd[r], pm[r]);
+    } else {
+#pragma unroll
+        for (int r = 0; r < ROUNDS; ++r) {
+            const bool valid = base + 64 * r < n;
+            const uint32_t d = (k[r] >> shift) & (RADIX - 1);
+            rank_round(r, valid, d, wave_match_digit<RADIX_BITS>(d, valid));
+        }
     }
     __syncthreads();
     {   // thread = digit: per-wave exclusive offsets, then the block-wide exclusive scan of the digit totals
@@ -634,7 +656,7 @@ __global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, 
     __shared__ uint32_t s_dstart[RADIX];        // block-local start of each digit's run
     __shared__ uint32_t s_gbase[RADIX];         // global start of this block's run of each digit
     __shared__ uint32_t s_wave[OS_THREADS / 64];
-    __shared__ K s_k[TILE_N];
+    __shared__ __attribute__((aligned(16))) K s_k[TILE_N];  // first the rank's peer tables (u64), when they fit
     __shared__ uint32_t s_v[TILE_N];
     __shared__ uint32_t s_vb;
     const uint32_t tid = threadIdx.x;
@@ -659,16 +681,34 @@ __global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, 
         k[r] = i < n ? keys_in[i] : 0u;
         v[r] = i < n ? vals_in[i] : 0u;
     }
-#pragma unroll
-    for (int r = 0; r < ROUNDS; ++r) {
-        const bool valid = base + 64 * r < n;
-        const uint32_t d = (k[r] >> shift) & (RADIX - 1);
-        const uint64_t peers = wave_match_digit<RADIX_BITS>(d, valid);
+    // one round's rank (in-order LDS: read, then the leader's add, as in radix_downsweep_kernel)
+    auto rank_round = [&](int r, bool valid, uint32_t d, uint64_t peers) {
         const uint32_t rank = mask_rank(peers);
-        lr[r] = (valid ? s_whist[w][d] : 0u) + rank;  // in-order LDS: read, then the leader's add (as above)
+        lr[r] = (valid ? s_whist[w][d] : 0u) + rank;
         __builtin_amdgcn_wave_barrier();
         if (valid && rank == 0) atomicAdd(&s_whist[w][d], (uint32_t)__popcll(peers));
         __builtin_amdgcn_wave_barrier();
+    };
+    if constexpr (OMR_SORT_RANK_OR && sizeof(s_k) >= WAVES * RADIX * sizeof(uint64_t)) {
+        // s_k is not written before the ranks are known: it holds the wave-private peer tables
+        uint32_t dd[ROUNDS];
+        bool vv[ROUNDS];
+        uint64_t pm[ROUNDS];
+#pragma unroll
+        for (int r = 0; r < ROUNDS; ++r) {
+            vv[r] = base + 64 * r < n;
+            dd[r] = (k[r] >> shift) & (RADIX - 1);
+        }
+        wave_peer_masks<ROUNDS, RADIX>(dd, vv, pm, reinterpret_cast<uint64_t*>(s_k) + (size_t)w * RADIX);
+#pragma unroll
+        for (int r = 0; r < ROUNDS; ++r) rank_round(r, vv[r], dd[r], pm[r]);
+    } else {
+#pragma unroll
+        for (int r = 0; r < ROUNDS; ++r) {
+            const bool valid = base + 64 * r < n;
+            const uint32_t d = (k[r] >> shift) & (RADIX - 1);
+            rank_round(r, valid, d, wave_match_digit<RADIX_BITS>(d, valid));
+        }
     }
     __syncthreads();
     {   // thread = digit: per-wave exclusive offsets, block-local digit starts, then the look-back
