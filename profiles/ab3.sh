@@ -7,7 +7,7 @@ ROUNDS=${ROUNDS:-3}
 rm -rf "$R/gpurun_out/ab3"
 mkdir -p "$R/gpurun_out/ab3"
 builds=("base:")
-for so in "$R"/omnigs-fork_amd/lib/exp/*.so; do
+for so in "${EXP_DIR:-$R/omnigs-fork_amd/lib/exp}"/*.so; do
     [ -e "$so" ] && builds+=("$(basename "$so" .so):$so")
 done
 for ((r = 0; r < ROUNDS; r++)); do
