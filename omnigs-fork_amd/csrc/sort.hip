@@ -54,10 +54,12 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t* s
 // Tiles are handed out by a ticket; a tile publishes its total (AGG), looks back over its predecessors with one
 // wave, 64 tiles per round trip, until it meets an inclusive prefix (PRE), then publishes its own. 64-bit status
 // words, flag in bits 62-63, zeroed before the launch.
-// OMR_SORT_RANK_OR (default 1): the radix downsweeps / onesweep passes take their per-round digit peers from LDS OR
-// tables (raster_common.h: wave_peer_masks) overlaid on the key staging array, instead of ballot matches
+// OMR_SORT_RANK_OR (default 0): the radix downsweeps / onesweep passes take their per-round digit peers from LDS OR
+// tables (raster_common.h: wave_peer_masks) overlaid on the key staging array, instead of ballot matches. Unlike the
+// binning scatters, the depth sort is faster with the ballots (interleaved A/B, profiles/r04i_ab_{A,C,E}.txt: C
+// 0.0793 vs 0.0801 ms, E 0.180 vs 0.189 ms, A equal)
 #ifndef OMR_SORT_RANK_OR
-#define OMR_SORT_RANK_OR 1
+#define OMR_SORT_RANK_OR 0
 #endif
 #ifndef OMR_LB_SPIN_MAX
 #define OMR_LB_SPIN_MAX (1u << 20)
