@@ -9,7 +9,9 @@
 //             four groups by one instance of their own list, so a band costs max over its 4 blocks of the list length;
 //   q8x8      the same with the four 4x4 blocks of an 8x8 quadrant as the groups (a round = one quadrant);
 //   blk4x4_bbox  blk4x4 with the block lists the render kernel can form cheaply: the binning's exact 16x4 band mask
-//             times the columns the ellipse's x-extent meets.
+//             times the columns the ellipse's x-extent meets;
+//   quad8x8   the current algorithm with 8x8 quadrants in place of 16x4 bands: per quadrant, every instance whose
+//             ellipse reaches it is evaluated by all 64 lanes (one pixel each; one instance per step, as today).
 // Input: raw little-endian arrays written by lane_study.py into a directory.
 #include <algorithm>
 #include <cmath>
@@ -43,7 +45,7 @@ int main(int argc, char** argv)
     const auto rg = load<uint32_t>(d + "/ranges.bin");
     const int gx = (W + 15) / 16, gy = (H + 15) / 16;
     // totals: [mapping][fwd/bwd] steps, contributing pairs
-    double steps[4][2] = {}, evalpairs[4][2] = {}, contrib = 0, fwd_live = 0;
+    double steps[5][2] = {}, evalpairs[5][2] = {}, contrib = 0, fwd_live = 0;
     // band pairs (0, 1) and (2, 3) of a tile (one lane's two pixels of a pair share a column): per direction, the
     // (instance, pair) evaluations that need both bands and those that need one (packed-math study)
     double pair_both[2] = {0, 0}, pair_one[2] = {0, 0};
@@ -120,7 +122,7 @@ int main(int argc, char** argv)
                 if (k < bend) { ++bsteps; bpairs += live_b; }
             }
         };
-        double ls[4][2] = {}, lp[4][2] = {};
+        double ls[5][2] = {}, lp[5][2] = {};
         {
             // per band: window ends and reach of each instance
             int fe[4], be[4];
@@ -162,6 +164,15 @@ int main(int argc, char** argv)
             count(pix, fs, bs, fp, bp);
             ls[0][0] += fs; ls[0][1] += bs; lp[0][0] += fp; lp[0][1] += bp;
         }
+        // quad8x8: the band algorithm on 8x8 quadrants
+        for (int q = 0; q < 4; ++q) {
+            std::vector<int> pix;
+            for (int y = 0; y < 8; ++y)
+                for (int x = 0; x < 8; ++x) pix.push_back((8 * (q / 2) + y) * 16 + 8 * (q % 2) + x);
+            int fs, bs, fp, bp;
+            count(pix, fs, bs, fp, bp);
+            ls[4][0] += fs; ls[4][1] += bs; lp[4][0] += fp; lp[4][1] += bp;
+        }
         // blk4x4 rounds = bands; q8x8 rounds = quadrants
         for (int mode = 1; mode < 4; ++mode)
             for (int r = 0; r < 4; ++r) {
@@ -185,12 +196,12 @@ int main(int argc, char** argv)
             }
         bbox_band = -1;
 #pragma omp critical
-        for (int m = 0; m < 4; ++m)
+        for (int m = 0; m < 5; ++m)
             for (int k = 0; k < 2; ++k) { steps[m][k] += ls[m][k]; evalpairs[m][k] += lp[m][k]; }
     }
-    const char* names[4] = {"band16x4", "blk4x4", "q8x8", "blk4x4_bbox"};
+    const char* names[5] = {"band16x4", "blk4x4", "q8x8", "blk4x4_bbox", "quad8x8"};
     std::printf("{\"W\": %d, \"H\": %d, \"contributing_pairs\": %.0f", W, H, contrib);
-    for (int m = 0; m < 4; ++m)
+    for (int m = 0; m < 5; ++m)
         std::printf(", \"%s\": {\"fwd_steps\": %.0f, \"bwd_steps\": %.0f, \"fwd_lane_use\": %.4f, \"bwd_lane_use\": %.4f}",
                     names[m], steps[m][0], steps[m][1], evalpairs[m][0] / (64.0 * steps[m][0]),
                     evalpairs[m][1] / (64.0 * steps[m][1]));
