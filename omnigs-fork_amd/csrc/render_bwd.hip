@@ -76,12 +76,19 @@ __device__ unsigned long long g_bwd_counts[5];
 #ifndef OMR_BWD_MINW
 #define OMR_BWD_MINW 1
 #endif
+// OMR_BWD_BATCH: positions staged per batch (<= TW_BATCH). The staging arrays take 48 B per position; with 64 the
+// workgroup's LDS is 7424 B, which caps residency at 22 waves per CU, below the 24 (6 per SIMD) its 78 VGPRs allow
+#ifndef OMR_BWD_BATCH
+#define OMR_BWD_BATCH TW_BATCH
+#endif
+constexpr int BWD_BATCH = OMR_BWD_BATCH;
+static_assert(BWD_BATCH <= TW_BATCH, "one position per lane");
 __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel(RenderBwdArgs a)
 {
     OMR_STAMP_BEGIN
-    __shared__ float4 s_geo_all[TW_WAVES][TW_BATCH];   // x, y, position in range (u32 bits), band mask (u32 bits)
-    __shared__ float4 s_quad_all[TW_WAVES][TW_BATCH];  // qa, qb, qc, log2(opacity) (tile_wave.h: column_quad)
-    __shared__ float4 s_rgb_all[TW_WAVES][TW_BATCH];   // colour, gradient row slot (u32 bits)
+    __shared__ float4 s_geo_all[TW_WAVES][BWD_BATCH];   // x, y, position in range (u32 bits), band mask (u32 bits)
+    __shared__ float4 s_quad_all[TW_WAVES][BWD_BATCH];  // qa, qb, qc, log2(opacity) (tile_wave.h: column_quad)
+    __shared__ float4 s_rgb_all[TW_WAVES][BWD_BATCH];   // colour, gradient row slot (u32 bits)
     // rows 0-7: the held instance's eight values, rows 8-15: its partner's (wave_sum9x2_stored)
     __shared__ __attribute__((aligned(16))) float s_red_all[TW_WAVES][16 * WS_LDS_STRIDE];
 
@@ -190,9 +197,9 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
     float pv8 = 0.f;        // the held instance's 9th value (its first eight wait in rows 0-7 of s_red)
     uint32_t pslot = ~0u;   // its gradient row slot (wave-uniform: an SGPR); ~0: nothing held
 
-    // positions seg_hi-1 .. seg_lo, 64 per batch, back to front: batch entry `lane` <-> position hi-1-lane
-    for (int hi = (int)seg_hi; hi > (int)seg_lo; hi -= TW_BATCH) {
-        const int cnt = min(hi - (int)seg_lo, TW_BATCH);
+    // positions seg_hi-1 .. seg_lo, BWD_BATCH per batch, back to front: batch entry `lane` <-> position hi-1-lane
+    for (int hi = (int)seg_hi; hi > (int)seg_lo; hi -= BWD_BATCH) {
+        const int cnt = min(hi - (int)seg_lo, BWD_BATCH);
         uint32_t m = 0;
         float4 p, co, c;
         uint32_t pos = 0, slot = 0;
