@@ -76,15 +76,18 @@ __device__ unsigned long long g_bwd_counts[5];
 #ifndef OMR_BWD_MINW
 #define OMR_BWD_MINW 1
 #endif
-// OMR_BWD_BATCH: positions staged per batch (<= TW_BATCH). The staging arrays take 48 B per position; with 64 the
-// workgroup's LDS is 7424 B, which caps residency at 22 waves per CU, below the 24 (6 per SIMD) its 78 VGPRs allow
+// Positions staged per batch (<= TW_BATCH). The staging arrays take 48 B per position: with 64 the workgroup's LDS is
+// 7424 B, which caps residency at 21-22 waves per CU, below the 24 (6 per SIMD) its 78 VGPRs allow; with 40 it is
+// 6272 B. Views with more units than resident wave slots (launch_render_backward) take OMR_BWD_BATCH (interleaved A/B,
+// profiles/r04n_ab_*.txt: render_bwd C 0.3935 -> 0.3880 ms, E 0.8003 -> 0.7853 ms with 40); views whose units all fit
+// at once keep 64, where the extra batches' round trips cost more than residency gains (B 0.0756 vs 0.0770 ms).
 #ifndef OMR_BWD_BATCH
-#define OMR_BWD_BATCH TW_BATCH
+#define OMR_BWD_BATCH 40
 #endif
-constexpr int BWD_BATCH = OMR_BWD_BATCH;
-static_assert(BWD_BATCH <= TW_BATCH, "one position per lane");
+template <int BWD_BATCH>
 __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel(RenderBwdArgs a)
 {
+    static_assert(BWD_BATCH <= TW_BATCH, "one position per lane");
     OMR_STAMP_BEGIN
     __shared__ float4 s_geo_all[TW_WAVES][BWD_BATCH];   // x, y, position in range (u32 bits), band mask (u32 bits)
     __shared__ float4 s_quad_all[TW_WAVES][BWD_BATCH];  // qa, qb, qc, log2(opacity) (tile_wave.h: column_quad)
@@ -423,11 +426,16 @@ void launch_render_backward(const RenderBwdArgs& a, size_t max_units, hipStream_
                             hipEvent_t ev_stop)
 {
     if (max_units == 0) return;
-    if (ev_start || ev_stop)
-        hipExtLaunchKernelGGL(render_bwd_kernel, dim3((uint32_t)max_units), dim3(64 * TW_WAVES), 0, s, ev_start, ev_stop,
-                              0, a);
-    else
-        render_bwd_kernel<<<(uint32_t)max_units, 64 * TW_WAVES, 0, s>>>(a);
+    // max_units (tiles + L / CKPT + 1) bounds the unit count; 24 waves per CU on 256 CUs are resident at once
+    constexpr size_t RESIDENT = 24 * 256;
+    auto launch = [&](auto kernel) {
+        if (ev_start || ev_stop)
+            hipExtLaunchKernelGGL(kernel, dim3((uint32_t)max_units), dim3(64 * TW_WAVES), 0, s, ev_start, ev_stop, 0, a);
+        else
+            kernel<<<(uint32_t)max_units, 64 * TW_WAVES, 0, s>>>(a);
+    };
+    if (max_units > RESIDENT) launch(render_bwd_kernel<OMR_BWD_BATCH>);
+    else launch(render_bwd_kernel<TW_BATCH>);
 }
 
 }  // namespace omr
