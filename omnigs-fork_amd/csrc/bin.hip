@@ -628,7 +628,7 @@ __global__ __launch_bounds__(RB_THREADS) void cols_hist_kernel(BinArgs a)
 template <bool STAGED, class G>
 __device__ __forceinline__ void col_expand(const BinArgs& a, const ColChunk& k, const uint16_t* s_own,
                                            const uint32_t* s_xoff, const uint4* s_iv, const uint32_t* s_gid,
-                                           uint8_t* row_valid, uint32_t (&d)[G::ROUNDS],
+                                           uint32_t (&d)[G::ROUNDS],
                                            uint32_t (&val)[G::ROUNDS], bool (&valid)[G::ROUNDS])
 {
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
@@ -652,7 +652,6 @@ __device__ __forceinline__ void col_expand(const BinArgs& a, const ColChunk& k, 
             }
             d[r] = x;
             val[r] = gid | (band_mask_of_intervals(iv, x) << PL_GID_BITS);
-            row_valid[s] = 0;
         }
     }
 }
@@ -679,7 +678,6 @@ __global__ __launch_bounds__(G::THREADS) void cols_scatter_kernel(BinArgs a)
     static_assert(BITS != 8 || sizeof(s_raw) >= G::WAVES * 256 * sizeof(uint64_t), "peer tables fit s_raw");
     const uint32_t tid = threadIdx.x, gx = a.gx, C = a.words[1];
     const uint32_t L = live_L(a.counters, a.cap);
-    uint8_t* row_valid = reinterpret_cast<uint8_t*>(a.binning + row_valid_offset(L));  // the backward's row map
     uint32_t* point_list = reinterpret_cast<uint32_t*>(a.binning + canonical_list_offset(L));
     // software pipeline: the next chunk's descriptor, count bases and its first PF x 256 owners' entries and band
     // constants are loaded into registers while the current chunk is expanded and ranked (more would cost the VGPRs
@@ -770,8 +768,8 @@ __global__ __launch_bounds__(G::THREADS) void cols_scatter_kernel(BinArgs a)
         BSTAMP(it, 2);
         uint32_t d[G::ROUNDS], val[G::ROUNDS], lp[G::ROUNDS];
         bool valid[G::ROUNDS];
-        if (staged) col_expand<true, G>(a, k, s_own, s_xoff, s_iv, s_gid, row_valid, d, val, valid);
-        else col_expand<false, G>(a, k, s_own, s_xoff, s_iv, s_gid, row_valid, d, val, valid);
+        if (staged) col_expand<true, G>(a, k, s_own, s_xoff, s_iv, s_gid, d, val, valid);
+        else col_expand<false, G>(a, k, s_own, s_xoff, s_iv, s_gid, d, val, valid);
         if (cn < cr.end) {
             OMR_CS_LOAD_CONSTS(kn)
         }

@@ -717,7 +717,7 @@ int backward_impl(const BackwardIn& in)
     uint32_t* unit_count = reinterpret_cast<uint32_t*>(lb + unit_words_offset(R, d.T));
     rb.units = units;
     rb.unit_count = unit_count;
-    // b.row_valid [R] was zeroed by the forward's emit (row_valid_offset)
+    // b.row_valid [R] was zeroed by the forward's render_fwd (row_valid_offset)
     // (tile, depth segment) units, costliest first per XCD share (outside the render_backward stage, so the stage,
     // the bench's roofline duration and the rocprofv3 kernel average all time render_bwd_kernel alone)
     if (R > 0)

@@ -93,7 +93,6 @@ constexpr int EMIT_THREADS = OMR_EMIT_THREADS;
 constexpr int EMIT_PER = OMR_EMIT_PER;                // consecutive instance slots per emit thread (1, 2 or 4)
 constexpr int EMIT_SLOTS = EMIT_THREADS * EMIT_PER;   // slots per emit block (block_owner granularity)
 size_t emit_index_size(size_t L_cap);
-// also zeroes the backward's row_valid bytes at binning + row_valid_offset(L)
 // Words the host reads back (capi.hip: HostRead): src[0..n) into pinned fine-grained memory at dst, then seq into
 // seq_dst once they are acknowledged, with system-scope vector stores. Written by the first wave of a kernel that runs
 // anyway (emit_index or the row binning's first kernel, backward_schedule), or by host_words_kernel; dst == NULL: nothing to write.

@@ -143,13 +143,13 @@ struct ImageState {
 // waits for the host; the backward only learns R = L. So the two arrays the backward reads sit at offsets that
 // depend on L alone: inst_grad at 0, the sorted point list right after R rows of it (canonical_list_offset), then
 // row_valid (row_valid_offset). In the forward, the region [0, align(36 cap) + align(4 cap) + cap) is reserved for
-// them; the final tile-sort pass writes the point list to base + canonical_list_offset(L) and emit zeroes row_valid
+// them; the final tile-sort pass writes the point list to base + canonical_list_offset(L) and render_fwd zeroes row_valid
 // at base + row_valid_offset(L), with L read on the device.
 __host__ __device__ inline size_t canonical_list_offset(size_t L)
 {
     return (L * GRAD_ROW * sizeof(float) + ALIGN - 1) & ~(ALIGN - 1);
 }
-// the backward's row_valid bytes [L], right after the point list; emit zeroes them during the forward
+// the backward's row_valid bytes [L], right after the point list; render_fwd zeroes them (render_fwd.hip)
 __host__ __device__ inline size_t row_valid_offset(size_t L)
 {
     return canonical_list_offset(L) + ((L * sizeof(uint32_t) + ALIGN - 1) & ~(ALIGN - 1));
@@ -213,7 +213,7 @@ struct BinningState {
     uint4* bin_rowinfo;     // [gy + 1]
     uint32_t* bin_words;    // [4]
     uint32_t* bin_zero;     // bin_zero_words look-back words
-    uint8_t* row_valid;     // backward: 1 where inst_grad holds a row (at row_valid_offset(L); zeroed by emit)
+    uint8_t* row_valid;     // backward: 1 where inst_grad holds a row (at row_valid_offset(L); zeroed by render_fwd)
     uint32_t* point_keys;  // sorted tile ids (points at key_a or key_b)
     // carve for capacity cap; point_list is set for L = cap (exact sizing: backward, debug, omr_binning_bytes)
     static size_t carve(char* base, size_t cap, uint32_t gx, uint32_t gy, BinningState* s);

@@ -30,6 +30,12 @@ namespace {
 #ifndef OMR_FWD_MINW
 #define OMR_FWD_MINW 8
 #endif
+// OMR_FWD_BATCH: positions staged per batch (<= TW_BATCH; A/B knob)
+#ifndef OMR_FWD_BATCH
+#define OMR_FWD_BATCH TW_BATCH
+#endif
+constexpr uint32_t FWD_BATCH = OMR_FWD_BATCH;
+static_assert(FWD_BATCH <= (uint32_t)TW_BATCH, "one position per lane");
 
 OMR_STAMP_DECL(g_stamps_fwd)
 
@@ -50,9 +56,9 @@ template <bool DEPTH, int FWD_BANDS>
 __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel(RenderFwdArgs a)
 {
     constexpr uint32_t NG = 4 / FWD_BANDS;  // waves per tile
-    __shared__ float4 s_geo_all[TW_WAVES][TW_BATCH];  // x, y, position in range (u32 bits), band mask (u32 bits)
-    __shared__ float4 s_quad_all[TW_WAVES][TW_BATCH]; // qa, qb, qc, log2(opacity) (tile_wave.h: column_quad)
-    __shared__ float4 s_rgb_all[TW_WAVES][TW_BATCH];  // feature (colour, or depth for DEPTH)
+    __shared__ float4 s_geo_all[TW_WAVES][FWD_BATCH];  // x, y, position in range (u32 bits), band mask (u32 bits)
+    __shared__ float4 s_quad_all[TW_WAVES][FWD_BATCH]; // qa, qb, qc, log2(opacity) (tile_wave.h: column_quad)
+    __shared__ float4 s_rgb_all[TW_WAVES][FWD_BATCH];  // feature (colour, or depth for DEPTH)
 
     OMR_STAMP_BEGIN
     const uint32_t wv = threadIdx.x >> 6;
@@ -100,9 +106,9 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
     const size_t ck_bytes = L ? ckpt_count(L) * BLOCK_SIZE * sizeof(float4) : 0;
     const __amdgpu_buffer_rsrc_t ck_rsrc = __builtin_amdgcn_make_buffer_rsrc(
         a.binning + ckpt_offset(L), (short)0, (int)(uint32_t)ck_bytes, 0x00020000);
-    auto batch_end = [&](uint32_t s0) {  // [s0, end): at most TW_BATCH positions, never past a boundary or n
+    auto batch_end = [&](uint32_t s0) {  // [s0, end): at most FWD_BATCH positions, never past a boundary or n
         const uint32_t nb = (range.x + s0) / CKPT * CKPT + CKPT - range.x;
-        return min(min(s0 + TW_BATCH, n), nb);
+        return min(min(s0 + FWD_BATCH, n), nb);
     };
     // checkpoint stores of the batch that starts at `start` (OOB offset = dropped); issued as the last vector-memory
     // operations of each batch, and twice after the prologue's prefetch too, so that the loop head sees the same
@@ -286,6 +292,16 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
     if (lane == 0) a.max_contrib[(size_t)tile * FWD_GROUPS + grp] = maxc;
     if (NG == 1 && lane == 1) a.max_contrib[(size_t)tile * FWD_GROUPS + 1] = 0u;  // one wave: the second slot empty
     if (lane == 0 && work) atomicAdd(&a.tile_cost[tile], work);
+    // The backward's row_valid map is zeroed here, one slice per wave with 16-B stores after the wave's image stores, in
+    // the shadow of the VALU-bound blend, rather than by the binning's latency-bound scatter loop (one byte store per
+    // instance there: config E tile sort 1.090 -> 1.044 ms, C and A unchanged, profiles/r04p_ab_*.txt)
+    if (L) {  // raster_common.h: row_valid_offset, align_up(L) bytes
+        uint4* rv = reinterpret_cast<uint4*>(a.binning + row_valid_offset(L));
+        const uint32_t n16 = (uint32_t)(align_up(L) / sizeof(uint4)), nw = a.gx * a.gy * NG;
+        const uint32_t per = (n16 + nw - 1u) / nw, span = (per + 63u) & ~63u;
+        const uint32_t b0 = unit * span, b1 = min(b0 + span, n16);
+        for (uint32_t i = b0 + lane; i < b1; i += 64u) rv[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
     OMR_STAMP_END(g_stamps_fwd, unit);
 }
 

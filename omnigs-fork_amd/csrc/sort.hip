@@ -948,7 +948,6 @@ __global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap,
 #pragma unroll
         for (int j = 0; j < EMIT_PER; ++j) emit_one(splat, gid[j], kk[j], gx, &key[j], &val[j]);
     }
-    uint8_t* row_valid = reinterpret_cast<uint8_t*>(binning + row_valid_offset(L));  // the backward's row map
     if (EMIT_PER % 4 == 0 && nmine == (uint32_t)EMIT_PER) {
 #pragma unroll
         for (int q = 0; q < EMIT_PER; q += 4) {
@@ -958,7 +957,6 @@ __global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap,
                 *reinterpret_cast<uint2*>(tile_keys + eb + q) =
                     make_uint2(key[q] | (key[q + 1] << 16), key[q + 2] | (key[q + 3] << 16));
             *reinterpret_cast<uint4*>(gauss_vals + eb + q) = make_uint4(val[q], val[q + 1], val[q + 2], val[q + 3]);
-            *reinterpret_cast<uint32_t*>(row_valid + eb + q) = 0u;  // row_valid_offset is 256-B aligned
         }
     } else {
 #pragma unroll
@@ -966,7 +964,6 @@ __global__ __launch_bounds__(EMIT_THREADS) void emit_kernel(int P, size_t L_cap,
             if ((uint32_t)j >= nmine) break;
             tile_keys[eb + j] = (K)key[j];
             gauss_vals[eb + j] = val[j];
-            row_valid[eb + j] = 0;
         }
     }
 }
