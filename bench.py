@@ -141,7 +141,8 @@ def stage_bytes(stage, P, V, L, N, T, M=16, D=3, rows=None):
         tile_sort = 2 * 2 * (kb + 4) * L           # 2 passes x (tile id + point-list entry, read + write)
         tile_ranges = kb * L + 16 * T
     return {
-        "preprocess": 32 * P + (40 + sh + 45 + 40) * V,  # + the 8-B rect word and the 32-B bin record
+        # + the 8-B rect word, the 32-B bin record and the 36-B dRGB/ddir (sh_jac) for gaussian_bwd
+        "preprocess": 32 * P + (40 + sh + 45 + 40 + 36) * V,
         "depth_sort": 4 * 2 * 8 * P,               # 4 passes x (key+value read + write)
         # order, tiles_touched (index order) and row_first; sort path: tiles_touched in depth order and offsets; row
         # path: the 8-B rect words in depth order (read and written) and row_offsets
@@ -154,9 +155,9 @@ def stage_bytes(stage, P, V, L, N, T, M=16, D=3, rows=None):
         # tiles_touched + row_first + row_valid bytes + one 36-B sum row written per Gaussian; the marked 36-B
         # instance rows it reads depend on the scene and are not counted
         "row_sums": 8 * P + L + 36 * P,
-        # reads radii 4P + (row sums 36, xyz 12, scale 12, rot 16, SH, clamped 1) per visible Gaussian;
-        # writes every gradient output: 3+3+1+3+6+3*M(coeffs)+3+4 floats per Gaussian
-        "gaussian_backward": 4 * P + (36 + 12 + 12 + 16 + sh + 1) * V + (92 + 12 * M) * P,
+        # reads radii 4P + (row sums 36, xyz 12, scale 12, rot 16, the forward's dRGB/ddir 36 in place of the SH row,
+        # clamped 1) per visible Gaussian; writes every gradient output: 3+3+1+3+6+3*M(coeffs)+3+4 floats per Gaussian
+        "gaussian_backward": 4 * P + (36 + 12 + 12 + 16 + 36 + 1) * V + (92 + 12 * M) * P,
     }.get(stage, 0)
 
 

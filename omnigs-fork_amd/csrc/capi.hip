@@ -353,6 +353,7 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s, bool rows)
     g.conic_op = c.take<float4>(P);
     g.huge_list = c.take<uint32_t>(P);
     g.internal_radii = c.take<int>(P);
+    g.sh_jac = c.take<float>(9 * P);
     // the row binning's arrays, last (bin.hip; preprocess and the forward scans write them only when present)
     if (rows) {
         g.rect = c.take<uint2>(P);
@@ -737,6 +738,8 @@ int backward_impl(const BackwardIn& in)
     ga.focal_y = (float)in.height / (2.0f * in.tan_fovy);
     ga.focal_x = (float)in.width / (2.0f * in.tan_fovx);
     ga.clamped = g.clamped;
+    ga.sh_jac = g.sh_jac;
+    ga.jac_flag = g.counters + 5;
     ga.row_sums = g.row_sums;
     ga.conic_op = g.conic_op;
     ga.dL_dmean2D = in.dL_dmean2D; ga.dL_dconic = in.dL_dconic; ga.dL_dopacity = in.dL_dopacity; ga.dL_dcolor = in.dL_dcolor;

@@ -127,10 +127,12 @@ __device__ __forceinline__ void cov3d_forward(float sx, float sy, float sz, floa
 // MC == 16: the SH row is read as 12 float4 from row4 and the dL_dsh row written as 12 float4 to out4 (both the
 // lane's row of the wave's LDS staging image, or both global rows; the row is read before it is overwritten);
 // otherwise both are read/written in global memory at idx.
+// jac != NULL: the forward's dRGB/ddir of this Gaussian (GeomState::sh_jac: gx, gy, gz per channel), and the SH row is
+// not read at all.
 template <int MC>
 __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const float* campos, const float* shs,
                                           const float4* row4, uint8_t clamp_bits, F3 dRGB, float* dL_dsh,
-                                          float4* out4)
+                                          float4* out4, const float* jac = nullptr)
 {
     const int Mr = MC > 0 ? MC : M;
     const float dox = pos.x - campos[0], doy = pos.y - campos[1], doz = pos.z - campos[2];
@@ -139,10 +141,15 @@ __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const
     if (clamp_bits & 1) dRGB.x = 0.f;
     if (clamp_bits & 2) dRGB.y = 0.f;
     if (clamp_bits & 4) dRGB.z = 0.f;
-    const float* sh_row = shs + (size_t)idx * Mr * 3;
-    float shv[MC == 16 ? 48 : 1];
-    if constexpr (MC == 16) {
+    float coef[16];
+    sh_basis(deg, x, y, z, coef);
+    float gx[3], gy[3], gz[3];  // dRGB/dx etc per channel
+    if (jac) {
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) gx[ch] = jac[ch], gy[ch] = jac[3 + ch], gz[ch] = jac[6 + ch];
+    } else if constexpr (MC == 16) {
         const int nf4 = (3 * (deg + 1) * (deg + 1) + 3) >> 2;
+        float shv[48];
 #pragma unroll
         for (int q = 0; q < 12; ++q) {
             const float4 v = q < nf4 ? row4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -151,35 +158,10 @@ __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const
             shv[4 * q + 2] = v.z;
             shv[4 * q + 3] = v.w;
         }
-    }
-    float coef[16];
-    sh_basis(deg, x, y, z, coef);
-    float gx[3] = {0.f, 0.f, 0.f}, gy[3] = {0.f, 0.f, 0.f}, gz[3] = {0.f, 0.f, 0.f};  // dRGB/dx etc per channel
-    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-        auto s = [&](int k) { return MC == 16 ? shv[3 * k + ch] : sh_row[3 * k + ch]; };
-        if (deg > 0) {
-            gx[ch] = -SH_C1 * s(3);
-            gy[ch] = -SH_C1 * s(1);
-            gz[ch] = SH_C1 * s(2);
-            if (deg > 1) {
-                gx[ch] += SH_C2[0] * y * s(4) + SH_C2[2] * 2.f * -x * s(6) + SH_C2[3] * z * s(7) + SH_C2[4] * 2.f * x * s(8);
-                gy[ch] += SH_C2[0] * x * s(4) + SH_C2[1] * z * s(5) + SH_C2[2] * 2.f * -y * s(6) + SH_C2[4] * 2.f * -y * s(8);
-                gz[ch] += SH_C2[1] * y * s(5) + SH_C2[2] * 2.f * 2.f * z * s(6) + SH_C2[3] * x * s(7);
-                if (deg > 2) {
-                    gx[ch] += (SH_C3[0] * s(9) * 3.f * 2.f * xy + SH_C3[1] * s(10) * yz + SH_C3[2] * s(11) * -2.f * xy +
-                               SH_C3[3] * s(12) * -3.f * 2.f * xz + SH_C3[4] * s(13) * (-3.f * xx + 4.f * zz - yy) +
-                               SH_C3[5] * s(14) * 2.f * xz + SH_C3[6] * s(15) * 3.f * (xx - yy));
-                    gy[ch] += (SH_C3[0] * s(9) * 3.f * (xx - yy) + SH_C3[1] * s(10) * xz +
-                               SH_C3[2] * s(11) * (-3.f * yy + 4.f * zz - xx) + SH_C3[3] * s(12) * -3.f * 2.f * yz +
-                               SH_C3[4] * s(13) * -2.f * xy + SH_C3[5] * s(14) * -2.f * yz + SH_C3[6] * s(15) * -3.f * 2.f * xy);
-                    gz[ch] += (SH_C3[1] * s(10) * xy + SH_C3[2] * s(11) * 4.f * 2.f * yz +
-                               SH_C3[3] * s(12) * 3.f * (2.f * zz - xx - yy) + SH_C3[4] * s(13) * 4.f * 2.f * xz +
-                               SH_C3[5] * s(14) * (xx - yy));
-                }
-            }
-        }
+        sh_dir_grad(deg, x, y, z, [&](int k, int ch) { return shv[3 * k + ch]; }, gx, gy, gz);
+    } else {
+        const float* sh_row = shs + (size_t)idx * Mr * 3;
+        sh_dir_grad(deg, x, y, z, [&](int k, int ch) { return sh_row[3 * k + ch]; }, gx, gy, gz);
     }
     const float d[3] = {dRGB.x, dRGB.y, dRGB.z};
     if constexpr (MC == 16) {
@@ -521,7 +503,7 @@ __global__ __launch_bounds__(256, OMR_RS_MINW) void row_sum_kernel(RowSumArgs a)
 // Everything after the row sums for one visible Gaussian idx (radii > 0). dsh4: where the MC == 16 dL_dsh row goes.
 template <int CAM, int MC>
 __device__ __forceinline__ void gaussian_bwd_point(const GaussBwdArgs& a, int idx, float (&g)[GRAD_ROW],
-                                                   const float4* sh4, float4* dsh4)
+                                                   const float4* sh4, float4* dsh4, const float* jac = nullptr)
 {
     const int Mr = MC > 0 ? MC : a.M;
     // 1. this Gaussian's summed instance rows
@@ -661,7 +643,7 @@ __device__ __forceinline__ void gaussian_bwd_point(const GaussBwdArgs& a, int id
     // 3. SH backward
     if (a.shs) {
         const F3 dm = sh_backward<MC>(idx, a.D, a.M, mean, a.campos, a.shs, sh4, a.clamped[idx], F3{g[6], g[7], g[8]},
-                                      a.dL_dsh, dsh4);
+                                      a.dL_dsh, dsh4, jac);
         dmean.x += dm.x;
         dmean.y += dm.y;
         dmean.z += dm.z;
@@ -749,8 +731,10 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
     // MC == 16 only (the MC == 0 path reads and writes the rows itself, and skips the write for dL_dsh == NULL)
     float4* dsh4 = STAGED ? stage + lane * stage_stride<SH_F4>() : nullptr;
     const float4* sh4 = dsh4;
+    // the forward stored dRGB/ddir (sh_jac) when it staged these rows: the SH rows are then not needed here
+    const bool jac = STAGED && a.shs && a.sh_jac && *a.jac_flag == SH_JAC_WRITTEN;  // wave-uniform
     if constexpr (STAGED) {
-        if (a.shs) {
+        if (a.shs && !jac) {
             const int nf4 = (3 * (a.D + 1) * (a.D + 1) + 3) >> 2;
             wave_rows_load<SH_F4>(reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4, __ballot(vis), nf4,
                                   stage, lane);
@@ -759,7 +743,7 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
     }
     if (vis) {
         raw_row_to_grads(g, co, a.W, a.H);
-        gaussian_bwd_point<CAM, MC>(a, idx, g, sh4, dsh4);
+        gaussian_bwd_point<CAM, MC>(a, idx, g, sh4, dsh4, jac ? a.sh_jac + (size_t)idx * 9 : nullptr);
     }
     else if (valid) gaussian_bwd_culled<MC>(a, idx, dsh4);
     if constexpr (STAGED) {

@@ -19,6 +19,11 @@ namespace omr {
 
 #pragma clang fp contract(off)
 
+// OMR_SH_JAC (default 1): preprocess stores each visible Gaussian's dRGB/ddir (GeomState::sh_jac) for gaussian_bwd
+#ifndef OMR_SH_JAC
+#define OMR_SH_JAC 1
+#endif
+
 namespace {
 
 constexpr float INV_PI = 0.318309886183790671537767526745028724f;  // M_1_PIf32
@@ -216,8 +221,20 @@ __device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, const 
         dx = dx / len;
         dy = dy / len;
         dz = dz / len;
-        if (sh16) sh_to_rgb(a.D, dx, dy, dz, shv, rgb, clamp_bits);
-        else sh_to_rgb(a.D, dx, dy, dz, a.shs + (size_t)idx * a.M * 3, rgb, clamp_bits);
+        if (sh16) {
+            sh_to_rgb(a.D, dx, dy, dz, shv, rgb, clamp_bits);
+#if OMR_SH_JAC
+            // the backward's dRGB/ddir from the row in registers (sh_eval.h: sh_dir_grad; gaussian_bwd reads these 36 B
+            // instead of the 192-B row)
+            float gx[3], gy[3], gz[3];
+            sh_dir_grad(a.D, dx, dy, dz, [&](int k, int ch) { return shv[3 * k + ch]; }, gx, gy, gz);
+            float* j = a.g.sh_jac + (size_t)idx * 9;
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) j[ch] = gx[ch], j[3 + ch] = gy[ch], j[6 + ch] = gz[ch];
+#endif
+        } else {
+            sh_to_rgb(a.D, dx, dy, dz, a.shs + (size_t)idx * a.M * 3, rgb, clamp_bits);
+        }
     } else {
         rgb[0] = a.colors_precomp[3 * idx];
         rgb[1] = a.colors_precomp[3 * idx + 1];
@@ -247,6 +264,7 @@ __device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, const 
 #define OMR_PRE_DMA 0
 #endif
 
+
 template <int CAM>
 __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
 {
@@ -268,6 +286,9 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     const bool valid = idx < a.P;
     float4* stage = s_stage[wv];
     GeomState& g = a.g;
+    const bool sh16_in = a.colors_precomp == nullptr && a.M == 16 && (reinterpret_cast<uintptr_t>(a.shs) & 15u) == 0;
+    // sh_jac stored (preprocess_point's sh16 rows; the LDS-DMA colour path does not compute it)
+    if (idx == 0) g.counters[5] = sh16_in && !OMR_PRE_DMA && OMR_SH_JAC ? SH_JAC_WRITTEN : 0u;
 
     const float3 p_orig = valid ? make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2])
                                 : make_float3(0.f, 0.f, 0.f);

@@ -106,7 +106,8 @@ struct GeomState {
     uint32_t* scan2_status;   // look-back words of the forward scans (launch_forward_scans), zeroed by preprocess
     uint32_t* offsets;        // inclusive scan of tiles_touched in depth order
     uint32_t* counters;       // [0] num_rendered, [1] prefiltered-cull flag, [2] huge_list count, [3] look-back error,
-                              // [4] M = row slots of the row binning (sum of rect heights)
+                              // [4] M = row slots of the row binning (sum of rect heights), [5] SH_JAC_WRITTEN when
+                              // preprocess stored sh_jac
     uint32_t* order;          // depth order (points at val_a or val_b after the sort)
     uint32_t* row_first;      // first gradient row of each Gaussian (index-order exclusive scan, launch_forward_scans)
     float* row_sums;          // backward: [P][GRAD_ROW] each Gaussian's instance rows summed (launch_row_sums)
@@ -120,6 +121,8 @@ struct GeomState {
     float4* bin_rec;          // [P][2] {x, y, k, dd}, {1/a, t, dyR, Dt} (band_row_consts): the constants the binning's
                               // columns pass turns into each (Gaussian, row)'s reachable columns per band
     int* internal_radii;      // used when the caller passes radii == NULL (rasterizer_impl.cu:284-287)
+    float* sh_jac;            // [P][9] dRGB/ddir per channel (gx[3], gy[3], gz[3]; sh_eval.h: sh_dir_grad) of the
+                              // visible Gaussians, stored by preprocess for gaussian_bwd when it stages 16-coefficient rows
 
     // rows = false leaves out the row binning's arrays (rect .. bin_rec: the carve's tail, ~56 B per Gaussian) for views
     // that take sort.hip's binning; every other array keeps its offset, so readers carve with the default
@@ -172,6 +175,8 @@ constexpr int FWD_GROUPS = 2;
 // each tile's instances staged once (config E, 32 k tiles: render_fwd 0.476 -> 0.449 ms; config C, 8 k tiles: 0.272
 // with two waves per tile vs 0.295 with one, profiles/r03z_ab_fwd_bands.txt)
 constexpr uint32_t FWD_ONE_WAVE_TILES = 16384;
+// GeomState::counters[5] after a forward that stored sh_jac
+constexpr uint32_t SH_JAC_WRITTEN = 0x4A41430Bu;
 __host__ __device__ inline size_t ckpt_count(size_t L) { return L / CKPT + 1; }
 __host__ __device__ inline size_t seg_count(size_t L, uint32_t T) { return (size_t)T + L / CKPT + 1; }
 // the L-indexed region of the binning buffer, after row_valid: checkpoints [ckpt_count][256 pixels] float4

@@ -103,6 +103,46 @@ __device__ __forceinline__ void sh_to_rgb_part1(int deg, float x, float y, float
     }
 }
 
+// dRGB/ddir of backward.cu:56-112 per channel (gx = dRGB/dx etc.), s(k, ch) = coefficient k of channel ch. They depend
+// on the SH row and the view direction only, so the forward evaluates them where it has the row in registers
+// (preprocess.hip, stored as GeomState::sh_jac) and gaussian_bwd reads 36 B instead of the 192-B row; both sites run this
+// one function, compiled without contraction, so the values are the same bits either way.
+template <class S>
+__device__ __forceinline__ void sh_dir_grad(int deg, float x, float y, float z, S s, float gx[3], float gy[3],
+                                            float gz[3])
+{
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        gx[ch] = gy[ch] = gz[ch] = 0.f;
+        if (deg > 0) {
+            gx[ch] = -SH_C1 * s(3, ch);
+            gy[ch] = -SH_C1 * s(1, ch);
+            gz[ch] = SH_C1 * s(2, ch);
+            if (deg > 1) {
+                gx[ch] += SH_C2[0] * y * s(4, ch) + SH_C2[2] * 2.f * -x * s(6, ch) + SH_C2[3] * z * s(7, ch) +
+                          SH_C2[4] * 2.f * x * s(8, ch);
+                gy[ch] += SH_C2[0] * x * s(4, ch) + SH_C2[1] * z * s(5, ch) + SH_C2[2] * 2.f * -y * s(6, ch) +
+                          SH_C2[4] * 2.f * -y * s(8, ch);
+                gz[ch] += SH_C2[1] * y * s(5, ch) + SH_C2[2] * 2.f * 2.f * z * s(6, ch) + SH_C2[3] * x * s(7, ch);
+                if (deg > 2) {
+                    gx[ch] += (SH_C3[0] * s(9, ch) * 3.f * 2.f * xy + SH_C3[1] * s(10, ch) * yz +
+                               SH_C3[2] * s(11, ch) * -2.f * xy + SH_C3[3] * s(12, ch) * -3.f * 2.f * xz +
+                               SH_C3[4] * s(13, ch) * (-3.f * xx + 4.f * zz - yy) + SH_C3[5] * s(14, ch) * 2.f * xz +
+                               SH_C3[6] * s(15, ch) * 3.f * (xx - yy));
+                    gy[ch] += (SH_C3[0] * s(9, ch) * 3.f * (xx - yy) + SH_C3[1] * s(10, ch) * xz +
+                               SH_C3[2] * s(11, ch) * (-3.f * yy + 4.f * zz - xx) +
+                               SH_C3[3] * s(12, ch) * -3.f * 2.f * yz + SH_C3[4] * s(13, ch) * -2.f * xy +
+                               SH_C3[5] * s(14, ch) * -2.f * yz + SH_C3[6] * s(15, ch) * -3.f * 2.f * xy);
+                    gz[ch] += (SH_C3[1] * s(10, ch) * xy + SH_C3[2] * s(11, ch) * 4.f * 2.f * yz +
+                               SH_C3[3] * s(12, ch) * 3.f * (2.f * zz - xx - yy) + SH_C3[4] * s(13, ch) * 4.f * 2.f * xz +
+                               SH_C3[5] * s(14, ch) * (xx - yy));
+                }
+            }
+        }
+    }
+}
+
 // dRGB/dsh_k of backward.cu:56-112 (the SH basis values): coef[k] for k < (deg+1)^2, zero beyond
 __device__ __forceinline__ void sh_basis(int deg, float x, float y, float z, float coef[16])
 {
