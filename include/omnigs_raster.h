@@ -35,6 +35,10 @@
  *     dL_dconic ([P,4], slots 0,1,3) and, for lonlat, dpx_dt / dpy_dt ([P,3]) are optional (NULL = skip), and
  *     so is dL_dsh (its SH backward still feeds dL_dmean3D; a view-parallel host rebuilds the summed SH gradient
  *     from the colour gradients instead, omr_sh_grad_from_colors_packed);
+ *   - the forward keeps, in the geometry buffer, what the backward would otherwise recompute from the inputs it
+ *     is passed again: with 16-coefficient SH rows, each visible Gaussian's dRGB/ddir (from the forward's SH
+ *     rows and camera position). The backward must therefore be given the forward's inputs, as the reference's
+ *     autograd callers do (its gradients are those of that forward);
  *   - errors: calls return OMR_OK (0) or an OMR_ERR_* code; omr_last_error() gives the message of the last
  *     failing call on this thread. The reference throws std::runtime_error / traps instead.
  */
@@ -256,8 +260,12 @@ int omr_debug_image_state(char* image_buffer, int width, int height, float* fina
 /* the forward's per-tile count of (instance, 16x4 band) evaluations [T] (the backward's schedule key) */
 int omr_debug_tile_cost(char* image_buffer, int width, int height, uint32_t* dst, void* stream);
 /* the forward's count words: [0] num_rendered, [1] prefiltered flag, [2] huge-Gaussian count, [3] look-back error,
- * [4] row slots M of the row binning (bin.hip; 0 on sort.hip's path); dst: 8 device words */
+ * [4] row slots M of the row binning (bin.hip; 0 on sort.hip's path), [5] the stored-dRGB/ddir flag (sh_jac);
+ * dst: 8 device words */
 int omr_debug_counters(char* geom_buffer, int P, uint32_t* dst, void* stream);
+/* clears (0) or sets (1) the flag by which the backward uses the forward's stored dRGB/ddir (GeomState::sh_jac)
+ * instead of reading the SH rows: lets a test run both backward paths on one forward */
+int omr_debug_set_sh_jac(char* geom_buffer, int P, int enabled, void* stream);
 /* per-Gaussian pixel centre [P,2], conic+opacity [P,4], rgb [P,3], depth [P], tiles_touched [P] */
 /* one wave64 through the render backward's gradient reduction: in [64][9] -> out [9] (column sums) */
 int omr_debug_wave_sum9(const float* in, float* out, void* stream); /* wave_sum9_rows */

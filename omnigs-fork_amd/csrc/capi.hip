@@ -1268,6 +1268,18 @@ int omr_debug_counters(char* geom_buffer, int P, uint32_t* dst, void* stream)
     return OMR_OK;
 }
 
+int omr_debug_set_sh_jac(char* geom_buffer, int P, int enabled, void* stream)
+{
+    g_last_error.clear();
+    GeomState g;
+    GeomState::carve(geom_buffer, (size_t)std::max(P, 0), &g);
+    static const uint32_t words[2] = {0u, SH_JAC_WRITTEN};
+    OMR_HIP(hipMemcpyAsync(g.counters + 5, &words[enabled ? 1 : 0], sizeof(uint32_t), hipMemcpyHostToDevice,
+                           (hipStream_t)stream));
+    OMR_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return OMR_OK;
+}
+
 int omr_debug_geometry(char* geom_buffer, int P, float* means2D, float* conic_opacity, float* rgb, float* depths,
                        uint32_t* tiles_touched, void* stream)
 {

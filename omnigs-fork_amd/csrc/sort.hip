@@ -1055,6 +1055,13 @@ __global__ __launch_bounds__(ORDER_THREADS) void tile_order_kernel(const uint2* 
 // maps onto XCD blockIdx.x), costs them by their positions below the tile's last contributor and counting-sorts
 // them, longest first.
 constexpr int SCHED_THREADS = 1024;
+// tiles whose loads the schedule issues together (per-thread tile loop, share extraction)
+#ifndef OMR_SCHED_UNROLL
+#define OMR_SCHED_UNROLL 4
+#endif
+#ifndef OMR_SCHED_SG
+#define OMR_SCHED_SG 8
+#endif
 constexpr int SCHED_LDS_UNITS = 4096;  // 48 KiB of LDS
 __device__ __forceinline__ uint32_t tile_units(const uint2* ranges, const uint32_t* max_contrib, uint32_t t,
                                                uint32_t* rx, uint32_t* mc_out)
@@ -1086,7 +1093,7 @@ __global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(HostWo
     const uint32_t per = (T + SCHED_THREADS - 1) / SCHED_THREADS;
     const uint32_t t0 = min(T, tid * per), t1 = min(T, t0 + per);
     uint32_t mine = 0;
-#pragma unroll 4
+#pragma unroll OMR_SCHED_UNROLL
     for (uint32_t t = t0; t < t1; ++t) {
         uint32_t rx, mc;
         mine += tile_units(ranges, max_contrib, t, &rx, &mc);
@@ -1105,7 +1112,7 @@ __global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(HostWo
     if (first0 < hi && first0 + mine > lo) {
         // tiles in groups of SG whose loads are all issued before the group's stores (the stores may alias the
         // loads as far as the compiler knows: one tile at a time, each load waited for a global round trip)
-        constexpr uint32_t SG = 8;
+        constexpr uint32_t SG = OMR_SCHED_SG;
         uint32_t first = first0;
         for (uint32_t tg = t0; tg < t1 && first < hi; tg += SG) {
             uint32_t rxs[SG], mcs[SG], cs[SG];

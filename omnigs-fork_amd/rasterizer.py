@@ -73,6 +73,8 @@ def lib() -> C.CDLL:
         L.omr_debug_image_state.argtypes = [vp, i, i, vp, vp, vp]
         L.omr_debug_tile_cost.argtypes = [vp, i, i, vp, vp]
         L.omr_debug_counters.argtypes = [vp, i, vp, vp]
+        L.omr_debug_set_sh_jac.restype = i
+        L.omr_debug_set_sh_jac.argtypes = [vp, i, i, vp]
         L.omr_debug_geometry.argtypes = [vp, i, vp, vp, vp, vp, vp, vp]
         L.omr_debug_wave_sum9.argtypes = [vp, vp, vp]
         L.omr_debug_wave_sum9_lds.argtypes = [vp, vp, vp]
@@ -508,8 +510,15 @@ def debug_counters(P, geomBuffer) -> dict:
     out = torch.zeros((8,), dtype=torch.int32, device=geomBuffer.device)
     _check(lib().omr_debug_counters(geomBuffer.data_ptr(), int(P), out.data_ptr(), _stream(geomBuffer.device)),
            "debug_counters")
-    c = [int(v) for v in out.cpu().tolist()]
-    return {"num_rendered": c[0], "prefiltered_flag": c[1], "huge": c[2], "error": c[3], "row_slots": c[4]}
+    c = [int(v) & 0xFFFFFFFF for v in out.cpu().tolist()]
+    return {"num_rendered": c[0], "prefiltered_flag": c[1], "huge": c[2], "error": c[3], "row_slots": c[4],
+            "sh_jac": c[5] == 0x4A41430B}
+
+
+def debug_set_sh_jac(P, geomBuffer, enabled: bool):
+    """Sets or clears the flag by which the backward takes the forward's stored dRGB/ddir (omr_debug_set_sh_jac)."""
+    _check(lib().omr_debug_set_sh_jac(geomBuffer.data_ptr(), int(P), 1 if enabled else 0, _stream(geomBuffer.device)),
+           "debug_set_sh_jac")
 
 
 # --------------------------------------------------------------------------------------------------------------
