@@ -64,16 +64,10 @@ static_assert(ColGeoS::N == 1u << 11 && ColGeoL::N == 1u << 12, "cb_shift 11 / 1
 // grid caps of the grid-stride chunk kernels (256 CUs: 8 resident hist blocks of 256 threads, 4 scatter blocks of
 // 256 threads and <= 40 KiB LDS, or 2 of 512 threads and <= 80 KiB)
 constexpr uint32_t BIN_GRID_HIST = 2048, BIN_GRID_SCATTER = 1024;
-// OMR_BIN_FUSED_INFO (default 1): every rows_scatter block derives the per-row info itself (a scan over the rows) and
-// block 0 publishes what the columns pass reads, instead of a one-block rows_info launch between them
-#ifndef OMR_BIN_FUSED_INFO
-#define OMR_BIN_FUSED_INFO 1
-#endif
-
-// OMR_BIN_RANK_OR (default 1): the rows and columns scatters rank by LDS OR peer tables (rank_items), not ballot matches
-#ifndef OMR_BIN_RANK_OR
-#define OMR_BIN_RANK_OR 1
-#endif
+// Every rows_scatter block derives the per-row info itself (a scan over the rows) and block 0 publishes what the
+// columns pass reads, instead of a one-block rows_info launch between them. The rows and columns scatters rank by LDS
+// OR peer tables (rank_items) where the digit has 8 bits, by ballot matches otherwise. (The launch-separated info and
+// the all-ballot ranks measured slower, §4; their code is in profiles/r04_pruned_experiments.patch.)
 
 #ifdef OMR_BIN_STAMPS  // diagnostic: per-phase s_memrealtime stamps of cols_scatter_kernel (profiles/bin_stamps.py)
 constexpr int BSTAMP_ITERS = 16, BSTAMP_PH = 8;
@@ -329,12 +323,11 @@ __global__ __launch_bounds__(RB_THREADS) void rows_hist_kernel(BinArgs a)
 }
 
 // ---- between the scans -------------------------------------------------------------------------------------------
-// One block: per row y, its first entry and first instance slot (the scanned counts and width sums at chunk 0), chunk
-// count and first chunk of the columns pass: rowinfo[y] = {entry, slot, chunk_base, chunks}; the live lengths of the
-// columns pass, the zero past its counts that the scan turns into their total (the last tile's end), and the owner
-// end of every row's last columns chunk (rows_scatter_kernel writes the other owner words of desc_b).
-// rowinfo of rows [0, gy] (gy: the terminator) into ri (LDS or global): THREADS threads, NRI rows per thread; `publish`:
-// also the words, the count terminator and the owner ends of every row's last columns chunk
+// Run by every rows_scatter block: per row y, its first entry and first instance slot (the scanned counts and width
+// sums at chunk 0), chunk count and first chunk of the columns pass: ri[y] = {entry, slot, chunk_base, chunks} for rows
+// [0, gy] (gy: the terminator), in LDS; THREADS threads, NRI rows per thread. `publish` (block 0): also the live lengths
+// of the columns pass, the zero past its counts that the scan turns into their total (the last tile's end), and the
+// owner end of every row's last columns chunk (rows_scatter_kernel writes the other owner words of desc_b).
 template <int THREADS, int NRI>
 __device__ __forceinline__ void rows_info(const BinArgs& a, uint4* ri, bool publish, uint32_t* s_wave)
 {
@@ -374,12 +367,6 @@ __device__ __forceinline__ void rows_info(const BinArgs& a, uint4* ri, bool publ
             a.hist_b[(size_t)total * a.gx] = 0u;
         }
     }
-}
-
-__global__ __launch_bounds__(BIN_MAX_GRID) void rows_info_kernel(BinArgs a)
-{
-    __shared__ uint32_t s_wave[BIN_MAX_GRID / 64];
-    rows_info<BIN_MAX_GRID, 1>(a, a.rowinfo, true, s_wave);
 }
 
 // Per chunk: expand the slots to (owner, row), rank them by row, write the row entries (Gaussian, width | x0 << 16)
@@ -434,14 +421,10 @@ __global__ __launch_bounds__(RB_THREADS) void rows_scatter_kernel(BinArgs a)
             }
         }
     };
-#if OMR_BIN_FUSED_INFO
     __shared__ uint4 s_ri[(1 << BITS) + 1];
     rows_info<RB_THREADS, (1 << BITS) / RB_THREADS>(a, s_ri, blockIdx.x == 0, s_wave);
     __syncthreads();
     const uint4* rowinfo = s_ri;
-#else
-    const uint4* rowinfo = a.rowinfo;
-#endif
     const ChunkRange cr = xcd_chunks(C);
     if (C == 0) return;  // nothing binned (L = 0, a capacity overflow, a failed look-back): desc_r has no entry
     RowChunk k = row_chunk(a, min(cr.first, C - 1u), M);
@@ -490,7 +473,7 @@ __global__ __launch_bounds__(RB_THREADS) void rows_scatter_kernel(BinArgs a)
         }
         // its barriers end the expansion's reads of s_yoff, whose storage then holds the peer tables
         rank_items<BITS, RowGeo>(d, valid, lp, s_whist, s_dstart, s_wave,
-                                 OMR_BIN_RANK_OR && BITS == 8 ? reinterpret_cast<uint64_t*>(s_yoff_sorted) : nullptr);
+                                 BITS == 8 ? reinterpret_cast<uint64_t*>(s_yoff_sorted) : nullptr);
         uint32_t* s_sorted = s_yoff_sorted;
 #pragma unroll
         for (int r = 0; r < RB_ROUNDS; ++r)
@@ -567,7 +550,7 @@ struct ColChunk {
     uint32_t y, kk, nch, cb, s0, s1, e_lo, nr;
 };
 // desc_b[c] = {y, kk, chunks of the row, row's first chunk}, {s0, s1, first owner, owner end} (rows_scatter_kernel,
-// rows_info_kernel)
+// rows_info)
 __device__ __forceinline__ ColChunk col_chunk(const BinArgs& a, uint32_t c)
 {
     const uint4 d0 = a.desc_b[2 * (size_t)c], d1 = a.desc_b[2 * (size_t)c + 1];
@@ -776,7 +759,7 @@ __global__ __launch_bounds__(G::THREADS) void cols_scatter_kernel(BinArgs a)
         BSTAMP(it, 3);
         // its barriers end the expansion's reads of s_raw, which then holds the peer tables
         rank_items<BITS, G>(d, valid, lp, s_whist, s_dstart, s_wave,
-                            OMR_BIN_RANK_OR && BITS == 8 ? reinterpret_cast<uint64_t*>(s_raw) : nullptr);
+                            BITS == 8 ? reinterpret_cast<uint64_t*>(s_raw) : nullptr);
         BSTAMP(it, 4);
         uint32_t* s_v = reinterpret_cast<uint32_t*>(s_raw);
         uint16_t* s_x = reinterpret_cast<uint16_t*>(s_v + G::N);
@@ -840,7 +823,6 @@ void launch_row_binning(const BinArgs& a_in, hipStream_t s)
     const uint32_t gh_b = std::min(cbk, BIN_GRID_HIST);
     rows_hist_kernel<<<gh_r, RB_THREADS, 0, s>>>(a);
     launch_exclusive_scan(a.hist_r, a.hist_r, nr_hist, a.words + 2, st_r, a.err, s);
-    if (!OMR_BIN_FUSED_INFO) rows_info_kernel<<<1, BIN_MAX_GRID, 0, s>>>(a);
     if (a.gy <= 256) rows_scatter_kernel<8><<<gs_r, RB_THREADS, 0, s>>>(a);
     else rows_scatter_kernel<10><<<gs_r, RB_THREADS, 0, s>>>(a);
     cols_hist_kernel<<<gh_b, RB_THREADS, 0, s>>>(a);

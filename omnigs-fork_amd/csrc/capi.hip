@@ -431,7 +431,6 @@ size_t BinningState::carve(char* base, size_t cap, uint32_t gx, uint32_t gy, Bin
     b.bin_hist_r = c.take<uint32_t>(rows ? 2 * (size_t)gy * bin_chunks_r(cap) : 0);
     b.bin_hist_b = c.take<uint32_t>(rows ? bin_chunks_b(cap, gy) * gx : 0);
     b.bin_desc_b = c.take<uint4>(rows ? 2 * bin_chunks_b(cap, gy) : 0);
-    b.bin_rowinfo = c.take<uint4>(rows ? gy + 1 : 0);
     b.bin_words = c.take<uint32_t>(rows ? 4 : 0);
     b.bin_zero = c.take<uint32_t>(rows ? bin_zero_words(cap, gx, gy) : 0);
     if (s) *s = b;
@@ -600,7 +599,7 @@ int forward_impl(const ForwardIn& in)
             ba.ent_gid = b.key_a; ba.ent_w = b.key_b; ba.ent_ex = b.val_a;
             ba.hist_r = b.bin_hist_r; ba.chunks_r = bin_chunks_r(capacity); ba.desc_r = g.desc_r; ba.drect = g.drect;
             ba.hist_b = b.bin_hist_b; ba.chunks_b = bin_chunks_b(capacity, d.gy); ba.desc_b = b.bin_desc_b;
-            ba.rowinfo = b.bin_rowinfo; ba.words = b.bin_words; ba.zero = b.bin_zero; ba.nzero = 0;
+            ba.words = b.bin_words; ba.zero = b.bin_zero; ba.nzero = 0;
             ba.ranges = im.ranges; ba.binning = bin_base;
             StageScope st_(ST_TILE_SORT, s);
             launch_row_binning(ba, s);

@@ -138,7 +138,6 @@ struct BinArgs {
     uint32_t cb_shift;          // columns-pass chunk = 1 << cb_shift slots (bin_cols_shift; set by launch_row_binning)
     uint4* desc_b;              // [chunks_b][2] column chunks: {y, chunk of the row, row chunks, row's first chunk},
                                 // {first slot, end slot, first owner entry, owners}
-    uint4* rowinfo;             // [gy + 1]
     uint32_t* words;            // [0] live M, [1] column chunks, [2] live hist_r length, [3] live hist_b length
     uint32_t* zero;             // look-back words of the two scans (bin_zero_words)
     size_t nzero;

@@ -84,9 +84,8 @@ __device__ __forceinline__ float3 cov2d_from_J(const float* v, const float J0[3]
     return {c00, c01, c11};
 }
 
-// The inputs preprocess_point reads, loaded up front (before the SH rows' LDS-DMA is issued: vector-memory
-// operations retire in issue order, so a load issued after the DMA would make the geometry wait for the SH rows).
-// The camera matrices are wave-uniform (SGPRs after readfirstlane).
+// The inputs preprocess_point reads, loaded up front. The camera matrices are wave-uniform (SGPRs after
+// readfirstlane).
 struct PreIn {
     float v[16], pm[16];
     float sx, sy, sz, opacity;
@@ -123,12 +122,11 @@ struct PreOut {
 };
 
 // One Gaussian, forward.cu:593-703 (lonlat) / :231-340 (pinhole). Returns false for a culled Gaussian (the caller
-// then writes radius 0, no tiles, the culled sort key). The colour (SH -> RGB, or colors_precomp) is evaluated here
-// only with `colour`; otherwise the caller fills o.rec[2].xyz and o.clamp_bits (the LDS-DMA staged SH path).
+// then writes radius 0, no tiles, the culled sort key).
 // shv: the Gaussian's SH row in registers when sh16, else the row is read from a.shs.
 template <int CAM>
 __device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, const PreIn& in, int idx, float3 p_orig,
-                                                 bool sh16, const float (&shv)[48], PreOut& o, bool colour = true)
+                                                 bool sh16, const float (&shv)[48], PreOut& o)
 {
     const float* v = in.v;
     const float3 t = transformPoint4x3(p_orig, v);
@@ -213,8 +211,7 @@ __device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, const 
 
     float rgb[3] = {0.f, 0.f, 0.f};
     uint8_t clamp_bits = 0;
-    if (!colour) {
-    } else if (a.colors_precomp == nullptr) {
+    if (a.colors_precomp == nullptr) {
         const float3 cp = {a.campos[0], a.campos[1], a.campos[2]};
         float dx = p_orig.x - cp.x, dy = p_orig.y - cp.y, dz = p_orig.z - cp.z;
         const float len = sqrtf(dx * dx + dy * dy + dz * dz);
@@ -255,22 +252,14 @@ __device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, const 
 // One wave per 64 consecutive Gaussians. The wave reads its 64 SH rows (12 KiB) and writes its
 // 64 render records (4 KiB) as contiguous spans through LDS (wave_rows.h). The SH rows are requested before the
 // projection math so their latency overlaps it; pinhole views, which frustum-cull most of a scene, request only
-// the rows of points in front of the camera.
-// OMR_PRE_DMA: how the SH rows are staged (0: registers through a 13-KiB image per wave, wave_rows_load; 1: LDS-DMA
-// into the same image, wave_rows_dma, with the geometry computed while it lands; 2: LDS-DMA in two column halves
-// through a 7-KiB image). Interleaved A/B at config C (profiles/r04c_ab_preprocess_dma.txt, 3 rounds): 0 0.0823 ms,
-// 1 0.0836 ms, 2 0.0957 ms — the kernel streams at ~4.2 TB/s either way, so the register path stays the default.
-#ifndef OMR_PRE_DMA
-#define OMR_PRE_DMA 0
-#endif
-
-
+// the rows of points in front of the camera. (Staging the rows by LDS-DMA instead, with the geometry computed while
+// they land, measured no faster — the kernel streams at ~4.2 TB/s either way: profiles/r04c_ab_preprocess_dma.txt;
+// the code is kept in profiles/r04_pruned_experiments.patch.)
 template <int CAM>
 __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
 {
     constexpr int SH_F4 = 12;  // 16 coefficients x 3 channels
-    constexpr int HALF = SH_F4 / 2;
-    constexpr int IMG_F4 = OMR_PRE_DMA == 2 ? 64 * dma_stride<HALF>() : stage_f4<SH_F4>();
+    constexpr int IMG_F4 = stage_f4<SH_F4>();
     static_assert(IMG_F4 >= stage_f4<SPLAT_F4>(), "the image also stages the render records");
     __shared__ float4 s_stage[4][IMG_F4];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -287,8 +276,8 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     float4* stage = s_stage[wv];
     GeomState& g = a.g;
     const bool sh16_in = a.colors_precomp == nullptr && a.M == 16 && (reinterpret_cast<uintptr_t>(a.shs) & 15u) == 0;
-    // sh_jac stored (preprocess_point's sh16 rows; the LDS-DMA colour path does not compute it)
-    if (idx == 0) g.counters[5] = sh16_in && !OMR_PRE_DMA && OMR_SH_JAC ? SH_JAC_WRITTEN : 0u;
+    // sh_jac stored (preprocess_point's sh16 rows)
+    if (idx == 0) g.counters[5] = sh16_in && OMR_SH_JAC ? SH_JAC_WRITTEN : 0u;
 
     const float3 p_orig = valid ? make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2])
                                 : make_float3(0.f, 0.f, 0.f);
@@ -297,66 +286,6 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     float shv[48];
     PreIn in;
     load_pre_in<CAM>(a, idx, valid, in);
-#if OMR_PRE_DMA
-    // LDS-DMA path: the DMA is issued first, then the geometry of every lane runs while the rows land (its inputs
-    // were loaded before the DMA, load_pre_in), then the colour from the image. The DMAs are issued with the whole
-    // wave active (a position of the image is not its lane's row). OMR_PRE_DMA == 1: the whole row in one 13-KiB
-    // image; 2: two column halves through a 7-KiB image (more waves per CU, a second round trip per wave).
-    PreOut o;
-    bool vis = false;
-    if (sh16) {
-        constexpr int S = OMR_PRE_DMA == 1 ? dma_stride<SH_F4>() : dma_stride<HALF>();
-        const bool want = CAM == CAM_LONLAT ? valid : valid && transformPoint4x3(p_orig, in.v).z > 0.2f;
-        const uint64_t rows = __ballot(want);
-        const float4* src = reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4;
-        if constexpr (OMR_PRE_DMA == 1) wave_rows_dma<SH_F4, 0, SH_F4>(src, rows, nf4, stage, lane);
-        else wave_rows_dma<SH_F4, 0, HALF>(src, rows, nf4, stage, lane);
-        vis = valid && preprocess_point<CAM>(a, in, idx, p_orig, sh16, shv, o, false);
-        float dx = 0.f, dy = 0.f, dz = 0.f, res[3];
-        if (vis) {
-            const float3 cp = {a.campos[0], a.campos[1], a.campos[2]};
-            dx = p_orig.x - cp.x, dy = p_orig.y - cp.y, dz = p_orig.z - cp.z;  // forward.cu:37-38, as preprocess_point
-            const float len = sqrtf(dx * dx + dy * dy + dz * dz);
-            dx = dx / len;
-            dy = dy / len;
-            dz = dz / len;
-        }
-        dma_wait();
-        wave_sync();
-        {
-            float h[24];
-#pragma unroll
-            for (int q = 0; q < HALF; ++q) {
-                const float4 v = q < nf4 ? stage[lane * S + q] : make_float4(0.f, 0.f, 0.f, 0.f);
-                h[4 * q] = v.x, h[4 * q + 1] = v.y, h[4 * q + 2] = v.z, h[4 * q + 3] = v.w;
-            }
-            sh_to_rgb_part0(a.D, dx, dy, dz, h, res);
-        }
-        if constexpr (OMR_PRE_DMA != 1) {
-            wave_sync();  // the second half overwrites the image
-            if (nf4 > HALF) {
-                wave_rows_dma<SH_F4, HALF, HALF>(src, rows, nf4, stage, lane);
-                dma_wait();
-                wave_sync();
-            }
-        }
-        {
-            constexpr int C1 = OMR_PRE_DMA == 1 ? HALF : 0;  // image column of coefficient 8's float4
-            float h[24];
-#pragma unroll
-            for (int q = HALF; q < SH_F4; ++q) {
-                const float4 v = q < nf4 ? stage[lane * S + q - HALF + C1] : make_float4(0.f, 0.f, 0.f, 0.f);
-                h[4 * (q - HALF)] = v.x, h[4 * (q - HALF) + 1] = v.y, h[4 * (q - HALF) + 2] = v.z, h[4 * (q - HALF) + 3] = v.w;
-            }
-            float rgb[3];
-            sh_to_rgb_part1(a.D, dx, dy, dz, h, res, rgb, o.clamp_bits);
-            o.rec[2].x = rgb[0], o.rec[2].y = rgb[1], o.rec[2].z = rgb[2];
-        }
-        wave_sync();  // the image is reused for the records below
-    } else {
-        vis = valid && preprocess_point<CAM>(a, in, idx, p_orig, sh16, shv, o);
-    }
-#else
     if (sh16) {
         const bool want = CAM == CAM_LONLAT ? valid : valid && transformPoint4x3(p_orig, in.v).z > 0.2f;
         const uint64_t rows = __ballot(want);
@@ -378,7 +307,6 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     }
     PreOut o;
     const bool vis = valid && preprocess_point<CAM>(a, in, idx, p_orig, sh16, shv, o);
-#endif
     if (valid) {
         a.radii[idx] = vis ? o.rad : 0;
         g.tiles_touched[idx] = vis ? o.area : 0u;

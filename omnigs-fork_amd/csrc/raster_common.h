@@ -215,7 +215,6 @@ struct BinningState {
     uint32_t* bin_hist_r;   // [2][gy][bin_chunks_r]
     uint32_t* bin_hist_b;   // [bin_chunks_b][gx]
     uint4* bin_desc_b;      // [bin_chunks_b][2]
-    uint4* bin_rowinfo;     // [gy + 1]
     uint32_t* bin_words;    // [4]
     uint32_t* bin_zero;     // bin_zero_words look-back words
     uint8_t* row_valid;     // backward: 1 where inst_grad holds a row (at row_valid_offset(L); zeroed by render_fwd)

@@ -48,13 +48,6 @@ namespace {
 
 OMR_STAMP_DECL(g_stamps_bwd)
 
-#ifndef OMR_BWD_NOSKIP
-#define OMR_BWD_NOSKIP 0
-#endif
-// OMR_BWD_PAIRS: bands b, b + 1 of a lane (one column) evaluated together with packed f32 math (A/B)
-#ifndef OMR_BWD_PAIRS
-#define OMR_BWD_PAIRS 0
-#endif
 // diagnostic (A/B only): OMR_BWD_DIAG_EXTRA independent extra VALU per evaluated band, to price one VALU op there
 // diagnostic (A/B only, wrong gradients): OMR_BWD_DIAG_NOMARK drops the row_valid marks, to price their stores
 #ifndef OMR_BWD_DIAG_NOMARK
@@ -180,18 +173,6 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
         }
     }
 
-#if OMR_BWD_PAIRS
-    // the pair layout of the lane's per-pixel state (bands 2p, 2p + 1 side by side)
-    f2v T2[TW_BANDS / 2], s2[TW_BANDS / 2], dpr2[TW_BANDS / 2], dpg2[TW_BANDS / 2], dpb2[TW_BANDS / 2];
-#pragma unroll
-    for (int p = 0; p < TW_BANDS / 2; ++p) {
-        T2[p] = f2v{T[2 * p], T[2 * p + 1]};
-        s2[p] = f2v{s[2 * p], s[2 * p + 1]};
-        dpr2[p] = f2v{dp01[2 * p].x, dp01[2 * p + 1].x};
-        dpg2[p] = f2v{dp01[2 * p].y, dp01[2 * p + 1].y};
-        dpb2[p] = f2v{dp2[2 * p], dp2[2 * p + 1]};
-    }
-#endif
     // instances behind every pixel's last contributor get no row (row_valid stays 0 for them)
 
 #ifdef OMR_BWD_COUNT
@@ -253,49 +234,6 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
                 const float dy0 = g.y - (float)tl.py0;
                 // dx is the same for all four of the lane's pixels (one column), so the x-moments are dx-multiples of
                 // the band sums: S_u dx = dx S_u, S_u dx^2 = dx^2 S_u, S_u dx dy = dx S_u dy (applied after the bands)
-#if OMR_BWD_PAIRS
-                // per band pair, the lane's two pixels side by side: T, s, dL/dpix and the moment sums as VGPR pairs
-                f2v a_u = {0.f, 0.f}, a_uy = {0.f, 0.f}, a_uyy = {0.f, 0.f}, a_r = {0.f, 0.f}, a_g = {0.f, 0.f},
-                    a_b = {0.f, 0.f};
-                uint32_t any = 0;
-    #pragma unroll
-                for (int b = 0; b < TW_BANDS; b += 2) {
-                    const int p = b >> 1;
-                    const uint32_t pm = (mb >> b) & 3u;  // scalar
-                    if (!pm) continue;
-                    const f2v dy = f2v{dy0, dy0} - f2v{(float)(4 * b), (float)(4 * (b + 1))};
-                    const f2v p2 = __builtin_elementwise_fma(dy, __builtin_elementwise_fma(f2v{kq.C, kq.C}, dy, f2v{kq.B, kq.B}),
-                                                             f2v{kq.A, kq.A});
-                    const bool c0 = (pm & 1u) && (decltype(pos_test)::value ? ipos < last[b] : true) && p2_in_band(p2.x, lo);
-                    const bool c1 = (pm & 2u) && (decltype(pos_test)::value ? ipos < last[b + 1] : true) && p2_in_band(p2.y, lo);
-                    const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
-                    if (!(b0 | b1)) continue;
-                    any |= (b0 ? 1u << b : 0u) | (b1 ? 2u << b : 0u);
-                    const f2v oG = {__builtin_amdgcn_exp2f(c0 ? p2.x : -__builtin_inff()),
-                                    __builtin_amdgcn_exp2f(c1 ? p2.y : -__builtin_inff())};
-                    const f2v alpha = {fminf(0.99f, oG.x), fminf(0.99f, oG.y)};
-                    const f2v oma = f2v{1.0f, 1.0f} - alpha;
-                    const f2v inv = {__builtin_amdgcn_rcpf(oma.x), __builtin_amdgcn_rcpf(oma.y)};
-                    T2[p] *= inv;
-                    const f2v Ti = T2[p];
-                    const f2v cdot = __builtin_elementwise_fma(f2v{f.x, f.x}, dpr2[p],
-                                                               __builtin_elementwise_fma(f2v{f.y, f.y}, dpg2[p], f2v{f.z, f.z} * dpb2[p]));
-                    const f2v dL_dalpha = __builtin_elementwise_fma(Ti, cdot, -s2[p] * inv);
-                    const f2v wc = alpha * Ti;
-                    s2[p] = __builtin_elementwise_fma(cdot, wc, s2[p]);
-                    const f2v u = oG * dL_dalpha;
-                    const f2v uy = u * dy;
-                    a_u += u;
-                    a_uy += uy;
-                    a_uyy = __builtin_elementwise_fma(uy, dy, a_uyy);
-                    a_r = __builtin_elementwise_fma(wc, dpr2[p], a_r);
-                    a_g = __builtin_elementwise_fma(wc, dpg2[p], a_g);
-                    a_b = __builtin_elementwise_fma(wc, dpb2[p], a_b);
-                }
-                const f2v s_uy = {a_u.x + a_u.y, a_uy.x + a_uy.y};
-                const f2v sc01 = {a_r.x + a_r.y, a_g.x + a_g.y};
-                const float suyy = a_uyy.x + a_uyy.y, sc2 = a_b.x + a_b.y;
-#else
                 f2v s_uy = {0.f, 0.f};  // S_u, S_u dy
                 f2v sc01 = {0.f, 0.f};  // S_aT dpix_r, S_aT dpix_g
                 float suyy = 0.f, sc2 = 0.f;
@@ -310,15 +248,10 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
                     // backward.cu:770-781: skip positions at/after the pixel's last contributor, power > 0, alpha < 1/255
                     const bool contrib = (decltype(pos_test)::value ? ipos < lastb : true) && p2_in_band(p2, lo);
                     BWD_COUNT(1, 1);
-#if OMR_BWD_NOSKIP
-                    // A/B: no branch on the band's ballot; a band without a contributor runs through with zeros
-                    any |= __ballot(contrib) ? 1u << b : 0u;
-#else
                     if (!__ballot(contrib)) continue;
                     BWD_COUNT(2, 1);
                     BWD_COUNT(4, (uint32_t)__popcll(__ballot(contrib)));
                     any |= 1u << b;
-#endif
                     // a lane that does not contribute gets oG = alpha = 0: inv = 1, T and s unchanged, u = wc = 0
                     const float oG = __builtin_amdgcn_exp2f(contrib ? p2 : -__builtin_inff());  // o G (column_quad)
                     const float alpha = fminf(0.99f, oG);
@@ -340,7 +273,6 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
                     for (int e = 0; e < OMR_BWD_DIAG_EXTRA; ++e) asm volatile("v_mov_b32 %0, %0" : "+v"(sc2));  // 1 VALU each
 #endif
                 }
-#endif
                 const uint32_t slot_j = __builtin_bit_cast(uint32_t, f.w);
                 if (!any) continue;  // no pixel took a contribution: no row
                 BWD_COUNT(3, 1);

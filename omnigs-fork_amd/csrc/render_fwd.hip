@@ -39,14 +39,6 @@ static_assert(FWD_BATCH <= (uint32_t)TW_BATCH, "one position per lane");
 
 OMR_STAMP_DECL(g_stamps_fwd)
 
-// OMR_FWD_TSUB: test_T = T - alpha T instead of T (1 - alpha) (A/B)
-#ifndef OMR_FWD_TSUB
-#define OMR_FWD_TSUB 0
-#endif
-// OMR_FWD_PAIRS: the two bands of a lane pair evaluated with packed f32 math where an instance reaches both (A/B)
-#ifndef OMR_FWD_PAIRS
-#define OMR_FWD_PAIRS 0
-#endif
 // diagnostic (A/B only): OMR_FWD_DIAG_EXTRA extra VALU issue slots per evaluated band, to price one VALU op there
 #ifndef OMR_FWD_DIAG_EXTRA
 #define OMR_FWD_DIAG_EXTRA 0
@@ -183,16 +175,8 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
                 const bool ok = p2_in_band(p2, lo);  // power <= 0, alpha >= 1/255 (tile_wave.h)
                 // a lane that is not ok gets alpha = 0: test_T = T, wgt = 0; v_exp_f32 returns o G (column_quad)
                 const float alpha = fminf(0.99f, __builtin_amdgcn_exp2f(ok ? p2 : -__builtin_inff()));
-#if OMR_FWD_TSUB
-                // T (1 - alpha) as T - alpha T: alpha T is the blend weight anyway, so one VALU less per band (it
-                // rounds differently from the reference's product by an ulp of T: inside the saturation window of
-                // the parity allowance, oracle/ambiguity.hpp)
-                const float aT = alpha * T[b];
-                const float test_T = T[b] - aT;
-#else
                 const float aT = alpha * T[b];
                 const float test_T = T[b] * (1.0f - alpha);
-#endif
                 // a live T is >= 1e-4 (T only takes values that passed this test) and a lane that is not ok has
                 // test_T = T, so `sat` holds for newly saturated and already done (negative) pixels alike
                 const bool sat = test_T < 0.0001f;
@@ -214,49 +198,11 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
                 for (int e = 0; e < OMR_FWD_DIAG_EXTRA; ++e) asm volatile("v_mov_b32 %0, %0" : "+v"(C2[b]));
 #endif
             };
-#if OMR_FWD_PAIRS
-            // bands b, b + 1 of one lane share its column: both evaluated with packed f32 math (v_pk_fma / mul / add:
-            // one instruction for the two pixels' same operation, each rounded as the single-band code rounds it)
-#pragma unroll
-            for (int b = 0; b < FWD_BANDS; b += 2) {
-                const uint32_t pm = (mb >> b) & 3u;  // scalar
-                if (pm == 3u) {
-                    const f2v dy = f2v{dy0, dy0} - f2v{(float)(4 * (band0 + b)), (float)(4 * (band0 + b + 1))};
-                    const f2v p2 = __builtin_elementwise_fma(dy, __builtin_elementwise_fma(f2v{kq.C, kq.C}, dy, f2v{kq.B, kq.B}),
-                                                             f2v{kq.A, kq.A});
-                    const bool ok0 = p2_in_band(p2.x, lo), ok1 = p2_in_band(p2.y, lo);
-                    const f2v alpha = {fminf(0.99f, __builtin_amdgcn_exp2f(ok0 ? p2.x : -__builtin_inff())),
-                                       fminf(0.99f, __builtin_amdgcn_exp2f(ok1 ? p2.y : -__builtin_inff()))};
-                    const f2v Tp = {T[b], T[b + 1]};
-                    const f2v test_T = Tp * (f2v{1.0f, 1.0f} - alpha);
-                    const bool sat0 = test_T.x < 0.0001f, sat1 = test_T.y < 0.0001f;
-                    const uint64_t satm0 = __ballot(sat0), satm1 = __ballot(sat1);
-                    sat_any |= (satm0 & ~done[b]) | (satm1 & ~done[b + 1]);
-                    done[b] |= satm0;
-                    done[b + 1] |= satm1;
-                    const f2v aw = alpha * Tp;
-                    const f2v wgt = {sat0 ? 0.0f : aw.x, sat1 ? 0.0f : aw.y};
-                    const f2v c0 = __builtin_elementwise_fma(f2v{f.x, f.x}, wgt, f2v{C0[b], C0[b + 1]});
-                    const f2v c1 = __builtin_elementwise_fma(f2v{f.y, f.y}, wgt, f2v{C1[b], C1[b + 1]});
-                    const f2v c2 = __builtin_elementwise_fma(f2v{f.z, f.z}, wgt, f2v{C2[b], C2[b + 1]});
-                    C0[b] = c0.x, C0[b + 1] = c0.y, C1[b] = c1.x, C1[b + 1] = c1.y, C2[b] = c2.x, C2[b + 1] = c2.y;
-                    T[b] = sat0 ? -fabsf(T[b]) : test_T.x;
-                    T[b + 1] = sat1 ? -fabsf(T[b + 1]) : test_T.y;
-                    last[b] = (ok0 && !sat0) ? contributor : last[b];
-                    last[b + 1] = (ok1 && !sat1) ? contributor : last[b + 1];
-                } else if (pm == 1u) {
-                    band(b);
-                } else if (pm == 2u) {
-                    band(b + 1);
-                }
-            }
-#else
 #pragma unroll
             for (int b = 0; b < FWD_BANDS; ++b) {
                 if (!(mb & (1u << b))) continue;  // scalar branch
                 band(b);
             }
-#endif
             if (sat_any) {  // some pixel saturated: drop bands with no live pixel left
 #pragma unroll
                 for (int b = 0; b < FWD_BANDS; ++b)

@@ -56,53 +56,6 @@ __device__ __forceinline__ void sh_to_rgb(int deg, float x, float y, float z, co
     }
 }
 
-// sh_to_rgb in two parts over the row's halves (LDS-DMA staging, preprocess.hip): h0 = coefficients 0..7 (floats
-// 0..23), h1 = coefficients 8..15. The float operations and their order are sh_to_rgb's exactly: part 0 ends after
-// the t7 term of the degree-2 sum, part 1 adds t8, the degree-3 sum, the 0.5 and the clamp, so the results are
-// bit-identical.
-__device__ __forceinline__ void sh_to_rgb_part0(int deg, float x, float y, float z, const float* h0, float res[3])
-{
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-        auto s = [&](int k) { return h0[3 * k + ch]; };
-        float r = SH_C0 * s(0);
-        if (deg > 0) {
-            r = r - SH_C1 * y * s(1) + SH_C1 * z * s(2) - SH_C1 * x * s(3);
-            if (deg > 1) {
-                const float xx = x * x, yy = y * y, zz = z * z;
-                const float xy = x * y, yz = y * z, xz = x * z;
-                r = r + SH_C2[0] * xy * s(4) + SH_C2[1] * yz * s(5) + SH_C2[2] * (2.0f * zz - xx - yy) * s(6) +
-                    SH_C2[3] * xz * s(7);
-            }
-        }
-        res[ch] = r;
-    }
-}
-__device__ __forceinline__ void sh_to_rgb_part1(int deg, float x, float y, float z, const float* h1, float res[3],
-                                                float out[3], uint8_t& clamp_bits)
-{
-    clamp_bits = 0;
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-        auto s = [&](int k) { return h1[3 * (k - 8) + ch]; };
-        float r = res[ch];
-        if (deg > 1) {
-            const float xx = x * x, yy = y * y, zz = z * z;
-            const float xy = x * y;
-            r = r + SH_C2[4] * (xx - yy) * s(8);
-            if (deg > 2) {
-                r = r + SH_C3[0] * y * (3.0f * xx - yy) * s(9) + SH_C3[1] * xy * z * s(10) +
-                    SH_C3[2] * y * (4.0f * zz - xx - yy) * s(11) + SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * s(12) +
-                    SH_C3[4] * x * (4.0f * zz - xx - yy) * s(13) + SH_C3[5] * z * (xx - yy) * s(14) +
-                    SH_C3[6] * x * (xx - 3.0f * yy) * s(15);
-            }
-        }
-        r += 0.5f;
-        if (r < 0) clamp_bits |= (uint8_t)(1u << ch);
-        out[ch] = fmaxf(r, 0.0f);
-    }
-}
-
 // dRGB/ddir of backward.cu:56-112 per channel (gx = dRGB/dx etc.), s(k, ch) = coefficient k of channel ch. They depend
 // on the SH row and the view direction only, so the forward evaluates them where it has the row in registers
 // (preprocess.hip, stored as GeomState::sh_jac) and gaussian_bwd reads 36 B instead of the 192-B row; both sites run this

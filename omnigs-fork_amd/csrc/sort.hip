@@ -54,13 +54,10 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t* s
 // Tiles are handed out by a ticket; a tile publishes its total (AGG), looks back over its predecessors with one
 // wave, 64 tiles per round trip, until it meets an inclusive prefix (PRE), then publishes its own. 64-bit status
 // words, flag in bits 62-63, zeroed before the launch.
-// OMR_SORT_RANK_OR (default 0): the radix downsweeps / onesweep passes take their per-round digit peers from LDS OR
-// tables (raster_common.h: wave_peer_masks) overlaid on the key staging array, instead of ballot matches. Unlike the
-// binning scatters, the depth sort is faster with the ballots (interleaved A/B, profiles/r04i_ab_{A,C,E}.txt: C
-// 0.0793 vs 0.0801 ms, E 0.180 vs 0.189 ms, A equal)
-#ifndef OMR_SORT_RANK_OR
-#define OMR_SORT_RANK_OR 0
-#endif
+// The radix ranks take each round's digit peers from ballot matches (wave_match_digit). The binning scatters'
+// LDS OR peer tables (raster_common.h: wave_peer_masks) measured slower here (interleaved A/B,
+// profiles/r04i_ab_{A,C,E}.txt: C 0.0801 vs 0.0793 ms, E 0.189 vs 0.180 ms, A equal; the code is in
+// profiles/r04_pruned_experiments.patch).
 #ifndef OMR_LB_SPIN_MAX
 #define OMR_LB_SPIN_MAX (1u << 20)
 #endif
@@ -498,26 +495,11 @@ __global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const K* keys_
         if (valid && rank == 0) atomicAdd(&s_whist[w][d], (uint32_t)__popcll(peers));
         __builtin_amdgcn_wave_barrier();
     };
-    if constexpr (OMR_SORT_RANK_OR && sizeof(s_k) >= WAVES * RADIX * sizeof(uint64_t)) {
-        // s_k is not written before the ranks are known: it holds the wave-private peer tables
-        uint32_t dd[ROUNDS];
-        bool vv[ROUNDS];
-        uint64_t pm[ROUNDS];
 #pragma unroll
-        for (int r = 0; r < ROUNDS; ++r) {
-            vv[r] = base + 64 * r < n;
-            dd[r] = (k[r] >> shift) & (RADIX - 1);
-        }
-        wave_peer_masks<ROUNDS, RADIX>(dd, vv, pm, reinterpret_cast<uint64_t*>(s_k) + (size_t)w * RADIX);
-#pragma unroll
-        for (int r = 0; r < ROUNDS; ++r) rank_round(r, vv[r], dd[r], pm[r]);
-    } else {
-#pragma unroll
-        for (int r = 0; r < ROUNDS; ++r) {
-            const bool valid = base + 64 * r < n;
-            const uint32_t d = (k[r] >> shift) & (RADIX - 1);
-            rank_round(r, valid, d, wave_match_digit<RADIX_BITS>(d, valid));
-        }
+    for (int r = 0; r < ROUNDS; ++r) {
+        const bool valid = base + 64 * r < n;
+        const uint32_t d = (k[r] >> shift) & (RADIX - 1);
+        rank_round(r, valid, d, wave_match_digit<RADIX_BITS>(d, valid));
     }
     __syncthreads();
     {   // thread = digit: per-wave exclusive offsets, then the block-wide exclusive scan of the digit totals
@@ -691,26 +673,11 @@ __global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, 
         if (valid && rank == 0) atomicAdd(&s_whist[w][d], (uint32_t)__popcll(peers));
         __builtin_amdgcn_wave_barrier();
     };
-    if constexpr (OMR_SORT_RANK_OR && sizeof(s_k) >= WAVES * RADIX * sizeof(uint64_t)) {
-        // s_k is not written before the ranks are known: it holds the wave-private peer tables
-        uint32_t dd[ROUNDS];
-        bool vv[ROUNDS];
-        uint64_t pm[ROUNDS];
 #pragma unroll
-        for (int r = 0; r < ROUNDS; ++r) {
-            vv[r] = base + 64 * r < n;
-            dd[r] = (k[r] >> shift) & (RADIX - 1);
-        }
-        wave_peer_masks<ROUNDS, RADIX>(dd, vv, pm, reinterpret_cast<uint64_t*>(s_k) + (size_t)w * RADIX);
-#pragma unroll
-        for (int r = 0; r < ROUNDS; ++r) rank_round(r, vv[r], dd[r], pm[r]);
-    } else {
-#pragma unroll
-        for (int r = 0; r < ROUNDS; ++r) {
-            const bool valid = base + 64 * r < n;
-            const uint32_t d = (k[r] >> shift) & (RADIX - 1);
-            rank_round(r, valid, d, wave_match_digit<RADIX_BITS>(d, valid));
-        }
+    for (int r = 0; r < ROUNDS; ++r) {
+        const bool valid = base + 64 * r < n;
+        const uint32_t d = (k[r] >> shift) & (RADIX - 1);
+        rank_round(r, valid, d, wave_match_digit<RADIX_BITS>(d, valid));
     }
     __syncthreads();
     {   // thread = digit: per-wave exclusive offsets, block-local digit starts, then the look-back

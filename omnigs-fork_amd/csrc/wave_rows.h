@@ -68,31 +68,4 @@ __device__ __forceinline__ void wave_rows_store(float4* __restrict__ dst, uint64
     }
 }
 
-// LDS-DMA staging (global_load_lds_dwordx4, gfx950): columns [C0, C0 + NC) of the 64 rows go straight from HBM to
-// LDS, no VGPR holds them. One DMA wave-instruction writes 64 consecutive float4 of LDS (lane l -> base + 16 l), so
-// the odd row stride of the image (S = NC | 1: conflict-free per-lane row reads, as above) is made on the SOURCE side:
-// LDS position p = q * 64 + lane holds row p / S, column p % S; a padding slot (column NC) or an unselected row loads
-// src[0] (a line the wave reads anyway) and lands where no reader looks. S instructions per call. The caller waits with
-// dma_wait() and orders with wave_sync() before reading the image.
-template <int NC>
-constexpr int dma_stride()
-{
-    return NC | 1;
-}
-template <int NF4, int C0, int NC>
-__device__ __forceinline__ void wave_rows_dma(const float4* __restrict__ src, uint64_t rows, int ncols, float4* lds,
-                                              uint32_t lane)
-{
-    constexpr int S = dma_stride<NC>();
-#pragma unroll
-    for (int q = 0; q < S; ++q) {
-        const uint32_t p = (uint32_t)q * 64u + lane;
-        const uint32_t r = p / S, c = p - r * S;
-        const bool ok = (c < (uint32_t)NC) & (((rows >> r) & 1u) != 0) & ((int)(C0 + c) < ncols);  // branch-free
-        __builtin_amdgcn_global_load_lds(src + (ok ? r * NF4 + C0 + c : 0u), lds + q * 64, 16, 0, 0);
-    }
-}
-// every LDS-DMA of the wave has landed (they count in vmcnt with the wave's other vector-memory operations)
-__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
 }  // namespace omr
