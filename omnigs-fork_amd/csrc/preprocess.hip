@@ -124,9 +124,33 @@ struct PreOut {
 // One Gaussian, forward.cu:593-703 (lonlat) / :231-340 (pinhole). Returns false for a culled Gaussian (the caller
 // then writes radius 0, no tiles, the culled sort key).
 // shv: the Gaussian's SH row in registers when sh16, else the row is read from a.shs.
+// The view direction (forward.cu:37-38) and, from the SH row in registers, the colour (sh_eval.h) and the backward's
+// dRGB/ddir: preprocess_point's sh16 colour, restated for rows staged after the geometry (the same expressions, so
+// the same bits).
+__device__ __forceinline__ void sh16_colour(const PreprocessArgs& a, int idx, float3 p_orig, const float (&shv)[48],
+                                            float rgb[3], uint8_t& clamp_bits)
+{
+    const float3 cp = {a.campos[0], a.campos[1], a.campos[2]};
+    float dx = p_orig.x - cp.x, dy = p_orig.y - cp.y, dz = p_orig.z - cp.z;
+    const float len = sqrtf(dx * dx + dy * dy + dz * dz);
+    dx = dx / len;
+    dy = dy / len;
+    dz = dz / len;
+    sh_to_rgb(a.D, dx, dy, dz, shv, rgb, clamp_bits);
+#if OMR_SH_JAC
+    float gx[3], gy[3], gz[3];
+    sh_dir_grad(a.D, dx, dy, dz, [&](int k, int ch) { return shv[3 * k + ch]; }, gx, gy, gz);
+    float* j = a.g.sh_jac + (size_t)idx * 9;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) j[ch] = gx[ch], j[3 + ch] = gy[ch], j[6 + ch] = gz[ch];
+#endif
+}
+
+// sh16_late: the SH row is not in shv yet; the caller stages it for the visible lanes and fills o.rec[2].xyz and
+// o.clamp_bits with sh16_colour afterwards.
 template <int CAM>
 __device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, const PreIn& in, int idx, float3 p_orig,
-                                                 bool sh16, const float (&shv)[48], PreOut& o)
+                                                 bool sh16, const float (&shv)[48], PreOut& o, bool sh16_late = false)
 {
     const float* v = in.v;
     const float3 t = transformPoint4x3(p_orig, v);
@@ -219,16 +243,18 @@ __device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, const 
         dy = dy / len;
         dz = dz / len;
         if (sh16) {
-            sh_to_rgb(a.D, dx, dy, dz, shv, rgb, clamp_bits);
+            if (!sh16_late) {
+                sh_to_rgb(a.D, dx, dy, dz, shv, rgb, clamp_bits);
 #if OMR_SH_JAC
-            // the backward's dRGB/ddir from the row in registers (sh_eval.h: sh_dir_grad; gaussian_bwd reads these 36 B
-            // instead of the 192-B row)
-            float gx[3], gy[3], gz[3];
-            sh_dir_grad(a.D, dx, dy, dz, [&](int k, int ch) { return shv[3 * k + ch]; }, gx, gy, gz);
-            float* j = a.g.sh_jac + (size_t)idx * 9;
+                // the backward's dRGB/ddir from the row in registers (sh_eval.h: sh_dir_grad; gaussian_bwd reads these
+                // 36 B instead of the 192-B row)
+                float gx[3], gy[3], gz[3];
+                sh_dir_grad(a.D, dx, dy, dz, [&](int k, int ch) { return shv[3 * k + ch]; }, gx, gy, gz);
+                float* j = a.g.sh_jac + (size_t)idx * 9;
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) j[ch] = gx[ch], j[3 + ch] = gy[ch], j[6 + ch] = gz[ch];
+                for (int ch = 0; ch < 3; ++ch) j[ch] = gx[ch], j[3 + ch] = gy[ch], j[6 + ch] = gz[ch];
 #endif
+            }
         } else {
             sh_to_rgb(a.D, dx, dy, dz, a.shs + (size_t)idx * a.M * 3, rgb, clamp_bits);
         }
@@ -250,9 +276,9 @@ __device__ __forceinline__ bool preprocess_point(const PreprocessArgs& a, const 
 }
 
 // One wave per 64 consecutive Gaussians. The wave reads its 64 SH rows (12 KiB) and writes its
-// 64 render records (4 KiB) as contiguous spans through LDS (wave_rows.h). The SH rows are requested before the
-// projection math so their latency overlaps it; pinhole views, which frustum-cull most of a scene, request only
-// the rows of points in front of the camera. (Staging the rows by LDS-DMA instead, with the geometry computed while
+// 64 render records (4 KiB) as contiguous spans through LDS (wave_rows.h). Equirect views request the SH rows before
+// the projection math so their latency overlaps it; pinhole views request only the rows of the visible points, after
+// the geometry (below). (Staging the rows by LDS-DMA instead, with the geometry computed while
 // they land, measured no faster — the kernel streams at ~4.2 TB/s either way: profiles/r04c_ab_preprocess_dma.txt;
 // the code is kept in profiles/r04_pruned_experiments.patch.)
 template <int CAM>
@@ -286,9 +312,13 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     float shv[48];
     PreIn in;
     load_pre_in<CAM>(a, idx, valid, in);
-    if (sh16) {
-        const bool want = CAM == CAM_LONLAT ? valid : valid && transformPoint4x3(p_orig, in.v).z > 0.2f;
-        const uint64_t rows = __ballot(want);
+    // Pinhole views request the rows after the geometry, for the visible lanes only: a frustum culls most of a scene
+    // (88 % at E pinhole), and the rows of the visible ones are all the colour needs. Interleaved A/B at E pinhole (profiles/r04p3_ab_Ep.txt): preprocess 0.314 -> 0.300 ms,
+    // 1295 -> 1317 MP/s, against requesting the rows of every point in front of the camera before the geometry.
+    // Equirect views see every point, so their rows are requested first and their latency overlaps the projection.
+    constexpr bool LATE = CAM != CAM_LONLAT;
+    if (sh16 && !LATE) {
+        const uint64_t rows = __ballot(valid);
         const float4* src = reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4;
         float4 shq[SH_F4];
         wave_rows_load<SH_F4>(src, rows, nf4, stage, lane);
@@ -306,7 +336,26 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
         }
     }
     PreOut o;
-    const bool vis = valid && preprocess_point<CAM>(a, in, idx, p_orig, sh16, shv, o);
+    const bool vis = valid && preprocess_point<CAM>(a, in, idx, p_orig, sh16, shv, o, LATE);
+    if (LATE && sh16) {
+        const uint64_t rows = __ballot(vis);
+        if (rows) {  // wave-uniform
+            wave_rows_load<SH_F4>(reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4, rows, nf4, stage,
+                                  lane);
+            wave_sync();
+#pragma unroll
+            for (int q = 0; q < SH_F4; ++q) {
+                const float4 v = q < nf4 ? stage[lane * stage_stride<SH_F4>() + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+                shv[4 * q] = v.x, shv[4 * q + 1] = v.y, shv[4 * q + 2] = v.z, shv[4 * q + 3] = v.w;
+            }
+            wave_sync();  // the image is reused for the records below
+            if (vis) {
+                float rgb[3];
+                sh16_colour(a, idx, p_orig, shv, rgb, o.clamp_bits);
+                o.rec[2].x = rgb[0], o.rec[2].y = rgb[1], o.rec[2].z = rgb[2];
+            }
+        }
+    }
     if (valid) {
         a.radii[idx] = vis ? o.rad : 0;
         g.tiles_touched[idx] = vis ? o.area : 0u;
