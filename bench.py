@@ -161,6 +161,15 @@ def stage_bytes(stage, P, V, L, N, T, M=16, D=3, rows=None):
     }.get(stage, 0)
 
 
+def survey_step_bytes(P, V, L, N, T, camera_type):
+    """algorithmic bytes of one fwd+bwd of one view as the reference's kernels move them (SH in the
+    rasterizer, D = 3): B = 364 P + 1068 V + 124 L + 40 N + 32 T (lonlat), 340 P + 1020 V + ... (pinhole: no
+    dpx_dt / dpy_dt)."""
+    if camera_type == 1:
+        return 340 * P + 1020 * V + 124 * L + 40 * N + 32 * T
+    return 364 * P + 1068 * V + 124 * L + 40 * N + 32 * T
+
+
 def workload_text(cfg_name, config, world, P, W, H, camera_type, sh_degree, exchange="compact"):
     cam = lambda w, h, t: f"{w}x{h} " + ("equirect (camera_type=3)" if t == 3 else "pinhole (camera_type=1)")
     if config == "E" and world > 1:
@@ -467,8 +476,9 @@ def main():
         ach = b / (ms_k * 1e-3) / 1e9 if ms_k > 0 else 0.0
         tr = pmc.get(k, {}).get("hbm_bytes_per_launch")
         lo = pmc.get(k, {}).get("hbm_bytes_lower")
-        # the committed rocprofv3 --stats average of the same kernel (profiles/<tag>_kernel_stats.csv, all launches of
-        # that run including warm-up): `frac` recomputes from it as algorithmic bytes / avg / peak
+        # the committed rocprofv3 average of the same kernel over the timed loop of a profiled bench run
+        # (profiles/<tag>_kernel_stats_timed.csv, profiles/pmc_summarize.py: timed_window): `frac_rocprof` recomputes
+        # `frac` from it as algorithmic bytes / avg / peak
         rp = pmc.get(k, {}).get("rocprof_avg_ms")
         ach_rp = b / (rp * 1e-3) / 1e9 if rp else None
         # traffic = (2 FETCH + WRITE): exact for 16-B/lane streams, an upper bound for gathers, which
@@ -482,6 +492,7 @@ def main():
                 "rocprof_file": pmc_file if rp else None}
 
     d = stage_entry(dom)
+    survey_b = survey_step_bytes(P, V, L, N, T, cam.camera_type)
     algo_total = sum(stage_bytes(s, P, V, L, N, T, M, g.sh_degree, rows_slots) for s in stage_avg)
     # VALU secondary: pixel-instance evaluations = the forward's (instance, 16x4 band) pairs x 64,
     # at nominal 20 flop (forward) / 60 flop (backward) each, against the f32 vector peak; the backward evaluates at
@@ -536,6 +547,12 @@ def main():
                      "avg_launch_ms_rocprof": d["avg_launch_ms_rocprof"], "frac_rocprof": d["frac_rocprof"],
                      "rocprof_file": d["rocprof_file"],
                      "step_algorithmic_GBps": round(algo_total / (ms_per_step * 1e-3) / 1e9, 2),
+                     "step_algorithmic_bytes": int(algo_total),
+                     # SURVEY.md §8(d)'s whole-step formula (the reference's own kernels' compulsory bytes, its 324 B/G
+                     # zero-fill and atomic RMW included) beside the per-stage accounting above
+                     "step_survey_B_bytes": survey_b,
+                     "step_survey_B_GBps": round(survey_b / (ms_per_step * 1e-3) / 1e9, 2),
+                     "step_survey_B_frac": round(survey_b / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "top_stages": [stage_entry(k) for k in ranked[:3]]},
         "stages_ms": {k: round(v, 4) for k, v in stage_avg.items()},
         "valu_secondary": valu,

@@ -218,8 +218,9 @@ void omr_ply_close(omr_ply* ply);
 int omr_ply_save(const char* path, int P, int Mr, const float* const params[6], void* stream);
 
 /* --- scratch sizes (bytes the allocation callbacks are asked for) -------------------------------- */
-/* geometry: the size for a view that takes the row binning (at most 1024 tiles a side); wider views are asked for
-   about 56 B per Gaussian less (no row-binning arrays), so this is an upper bound for any view */
+/* geometry: the size for a view that takes the row binning (at most 1024 tiles a side) with colours from 16-coefficient
+   SH rows (the forward then stores dRGB/ddir, 36 B per Gaussian); wider views are asked for about 56 B per Gaussian
+   less (no row-binning arrays) and other colour sources 36 B less, so this is an upper bound for any forward */
 size_t omr_geometry_bytes(int P);
 size_t omr_image_bytes(int width, int height);
 size_t omr_binning_bytes(int num_rendered, int width, int height);
@@ -260,10 +261,11 @@ int omr_debug_image_state(char* image_buffer, int width, int height, float* fina
 /* the forward's per-tile count of (instance, 16x4 band) evaluations [T] (the backward's schedule key) */
 int omr_debug_tile_cost(char* image_buffer, int width, int height, uint32_t* dst, void* stream);
 /* the forward's count words: [0] num_rendered, [1] prefiltered flag, [2] huge-Gaussian count, [3] look-back error,
- * [4] row slots M of the row binning (bin.hip; 0 on sort.hip's path), [5] the stored-dRGB/ddir flag (sh_jac);
- * dst: 8 device words */
+ * [4] row slots M of the row binning (bin.hip; 0 on sort.hip's path), [5] the stored-dRGB/ddir key (sh_jac: a key of
+ * the forward's SH array, means and campos, 0 if not stored), [6] omr_debug_set_sh_jac's copy of [5]; dst: 8 device
+ * words */
 int omr_debug_counters(char* geom_buffer, int P, uint32_t* dst, void* stream);
-/* clears (0) or sets (1) the flag by which the backward uses the forward's stored dRGB/ddir (GeomState::sh_jac)
+/* clears (0) or restores (1) the key by which the backward uses the forward's stored dRGB/ddir (GeomState::sh_jac)
  * instead of reading the SH rows: lets a test run both backward paths on one forward */
 int omr_debug_set_sh_jac(char* geom_buffer, int P, int enabled, void* stream);
 /* per-Gaussian pixel centre [P,2], conic+opacity [P,4], rgb [P,3], depth [P], tiles_touched [P] */

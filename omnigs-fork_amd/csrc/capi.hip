@@ -332,7 +332,7 @@ size_t& capacity_hint(int W, int H, int camera_type)
 
 }  // namespace
 
-size_t GeomState::carve(char* base, size_t P, GeomState* s, bool rows)
+size_t GeomState::carve(char* base, size_t P, GeomState* s, bool rows, bool jac)
 {
     Carver c(base);
     GeomState g;
@@ -353,8 +353,8 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s, bool rows)
     g.conic_op = c.take<float4>(P);
     g.huge_list = c.take<uint32_t>(P);
     g.internal_radii = c.take<int>(P);
-    g.sh_jac = c.take<float>(9 * P);
-    // the row binning's arrays, last (bin.hip; preprocess and the forward scans write them only when present)
+    // the optional tail: the row binning's arrays (bin.hip; preprocess and the forward scans write them only when
+    // present), then sh_jac (preprocess writes it exactly when sh_jac_stored holds, which is when the forward carves it)
     if (rows) {
         g.rect = c.take<uint2>(P);
         g.drect = c.take<uint2>(P);
@@ -366,6 +366,7 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s, bool rows)
         g.row_offsets = nullptr;
         g.bin_rec = nullptr;
     }
+    g.sh_jac = jac ? c.take<float>(9 * P) : nullptr;
     g.order = g.val_a;  // the depth sort runs DEPTH_SORT_PASSES (even) passes, so its result lands in val_a
     if (s) *s = g;
     return c.size();
@@ -499,11 +500,12 @@ int forward_impl(const ForwardIn& in)
     const size_t P = (size_t)in.P;
 
     const bool rows_path = row_binning(d.gx, d.gy);  // bin.hip; sort.hip's emit + tile sort for larger views
+    const bool jac = sh_jac_stored(in.colors_precomp, in.M, in.shs);
     char* geom_base = static_cast<char*>(
-        alloc_counted(in.geometry_alloc, in.geometry_ctx, GeomState::carve(nullptr, P, nullptr, rows_path)));
+        alloc_counted(in.geometry_alloc, in.geometry_ctx, GeomState::carve(nullptr, P, nullptr, rows_path, jac)));
     if (!geom_base) return fail(OMR_ERR_ALLOCATION, "geometry allocation failed");
     GeomState g;
-    GeomState::carve(geom_base, P, &g, rows_path);
+    GeomState::carve(geom_base, P, &g, rows_path, jac);
     char* img_base = static_cast<char*>(alloc_counted(in.image_alloc, in.image_ctx, ImageState::carve(nullptr, d.N, d.T, nullptr)));
     if (!img_base) return fail(OMR_ERR_ALLOCATION, "image allocation failed");
     ImageState im;
@@ -686,8 +688,9 @@ int backward_impl(const BackwardIn& in)
     const Dims d = dims(in.width, in.height);
     const hipStream_t s = in.stream;
     const size_t P = (size_t)in.P;
-    GeomState g;
-    GeomState::carve(in.geom_buffer, P, &g);
+    GeomState g;  // as the forward carved it for this view and these inputs (sh_jac is used only if its key matches)
+    GeomState::carve(in.geom_buffer, P, &g, row_binning(d.gx, d.gy),
+                     sh_jac_stored(in.colors_precomp, in.M, in.shs));
     BinningState b;
     BinningState::carve(in.binning_buffer, (size_t)in.R, d.gx, d.gy, &b);
     ImageState im;
@@ -1104,7 +1107,10 @@ int omr_forward_status(char* geom_buffer, int P, void* stream)
     return OMR_OK;
 }
 
-size_t omr_geometry_bytes(int P) { return GeomState::carve(nullptr, (size_t)std::max(P, 0), nullptr); }
+size_t omr_geometry_bytes(int P)  // the largest geometry buffer a forward of P Gaussians allocates (both optional tails)
+{
+    return GeomState::carve(nullptr, (size_t)std::max(P, 0), nullptr, true, true);
+}
 
 size_t omr_image_bytes(int width, int height)
 {
@@ -1272,9 +1278,15 @@ int omr_debug_set_sh_jac(char* geom_buffer, int P, int enabled, void* stream)
     g_last_error.clear();
     GeomState g;
     GeomState::carve(geom_buffer, (size_t)std::max(P, 0), &g);
-    static const uint32_t words[2] = {0u, SH_JAC_WRITTEN};
-    OMR_HIP(hipMemcpyAsync(g.counters + 5, &words[enabled ? 1 : 0], sizeof(uint32_t), hipMemcpyHostToDevice,
-                           (hipStream_t)stream));
+    // clearing keeps the forward's key in counters[6]; setting restores it
+    if (enabled) {
+        OMR_HIP(hipMemcpyAsync(g.counters + 5, g.counters + 6, sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                               (hipStream_t)stream));
+    } else {
+        OMR_HIP(hipMemcpyAsync(g.counters + 6, g.counters + 5, sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                               (hipStream_t)stream));
+        OMR_HIP(hipMemsetAsync(g.counters + 5, 0, sizeof(uint32_t), (hipStream_t)stream));
+    }
     OMR_HIP(hipStreamSynchronize((hipStream_t)stream));
     return OMR_OK;
 }

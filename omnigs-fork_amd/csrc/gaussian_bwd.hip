@@ -731,8 +731,11 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
     // MC == 16 only (the MC == 0 path reads and writes the rows itself, and skips the write for dL_dsh == NULL)
     float4* dsh4 = STAGED ? stage + lane * stage_stride<SH_F4>() : nullptr;
     const float4* sh4 = dsh4;
-    // the forward stored dRGB/ddir (sh_jac) when it staged these rows: the SH rows are then not needed here
-    const bool jac = STAGED && a.shs && a.sh_jac && *a.jac_flag == SH_JAC_WRITTEN;  // wave-uniform
+    // the forward stored dRGB/ddir (sh_jac) when it staged these rows: the SH rows are then not needed here, unless
+    // this backward was handed other SH, means or campos than that forward (raster_common.h: sh_jac_key)
+    const bool jac = STAGED && a.shs && a.sh_jac && a.campos &&
+                     *a.jac_flag == sh_jac_key(a.shs, a.means3D, __float_as_uint(a.campos[0]),
+                                               __float_as_uint(a.campos[1]), __float_as_uint(a.campos[2]));  // uniform
     if constexpr (STAGED) {
         if (a.shs && !jac) {
             const int nf4 = (3 * (a.D + 1) * (a.D + 1) + 3) >> 2;

@@ -234,7 +234,7 @@ struct GaussBwdArgs {
     float tan_fovx, tan_fovy, focal_x, focal_y;
     const uint8_t* clamped;
     const float* sh_jac;       // [P][9] the forward's dRGB/ddir (GeomState::sh_jac), used when *jac_flag says it is there
-    const uint32_t* jac_flag;  // GeomState::counters + 5 (SH_JAC_WRITTEN)
+    const uint32_t* jac_flag;  // GeomState::counters + 5 (sh_jac_key of the forward's inputs, 0: none)
     const float* row_sums;  // [P][GRAD_ROW] each Gaussian's instance rows summed (launch_row_sums)
     const float4* conic_op;  // [P] conic + opacity (GeomState) for the raw-moment rows
     float* dL_dmean2D;   // [P,3]

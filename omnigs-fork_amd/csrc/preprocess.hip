@@ -19,11 +19,6 @@ namespace omr {
 
 #pragma clang fp contract(off)
 
-// OMR_SH_JAC (default 1): preprocess stores each visible Gaussian's dRGB/ddir (GeomState::sh_jac) for gaussian_bwd
-#ifndef OMR_SH_JAC
-#define OMR_SH_JAC 1
-#endif
-
 namespace {
 
 constexpr float INV_PI = 0.318309886183790671537767526745028724f;  // M_1_PIf32
@@ -301,9 +296,12 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     const bool valid = idx < a.P;
     float4* stage = s_stage[wv];
     GeomState& g = a.g;
-    const bool sh16_in = a.colors_precomp == nullptr && a.M == 16 && (reinterpret_cast<uintptr_t>(a.shs) & 15u) == 0;
-    // sh_jac stored (preprocess_point's sh16 rows)
-    if (idx == 0) g.counters[5] = sh16_in && OMR_SH_JAC ? SH_JAC_WRITTEN : 0u;
+    // sh_jac stored (preprocess_point's sh16 rows; the host carved it on the same condition): the key of the inputs
+    if (idx == 0)
+        g.counters[5] = sh_jac_stored(a.colors_precomp, a.M, a.shs)
+                            ? sh_jac_key(a.shs, a.means3D, __float_as_uint(a.campos[0]), __float_as_uint(a.campos[1]),
+                                         __float_as_uint(a.campos[2]))
+                            : 0u;
 
     const float3 p_orig = valid ? make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2])
                                 : make_float3(0.f, 0.f, 0.f);

@@ -106,8 +106,8 @@ struct GeomState {
     uint32_t* scan2_status;   // look-back words of the forward scans (launch_forward_scans), zeroed by preprocess
     uint32_t* offsets;        // inclusive scan of tiles_touched in depth order
     uint32_t* counters;       // [0] num_rendered, [1] prefiltered-cull flag, [2] huge_list count, [3] look-back error,
-                              // [4] M = row slots of the row binning (sum of rect heights), [5] SH_JAC_WRITTEN when
-                              // preprocess stored sh_jac
+                              // [4] M = row slots of the row binning (sum of rect heights), [5] sh_jac_key of the
+                              // inputs when preprocess stored sh_jac (else 0), [6] omr_debug_set_sh_jac's copy of [5]
     uint32_t* order;          // depth order (points at val_a or val_b after the sort)
     uint32_t* row_first;      // first gradient row of each Gaussian (index-order exclusive scan, launch_forward_scans)
     float* row_sums;          // backward: [P][GRAD_ROW] each Gaussian's instance rows summed (launch_row_sums)
@@ -124,9 +124,10 @@ struct GeomState {
     float* sh_jac;            // [P][9] dRGB/ddir per channel (gx[3], gy[3], gz[3]; sh_eval.h: sh_dir_grad) of the
                               // visible Gaussians, stored by preprocess for gaussian_bwd when it stages 16-coefficient rows
 
-    // rows = false leaves out the row binning's arrays (rect .. bin_rec: the carve's tail, ~56 B per Gaussian) for views
-    // that take sort.hip's binning; every other array keeps its offset, so readers carve with the default
-    static size_t carve(char* base, size_t P, GeomState* s, bool rows = true);
+    // The carve's tail is optional: the row binning's arrays (rect .. bin_rec, ~56 B per Gaussian) only for views that
+    // take it (capi.hip: row_binning), then sh_jac only when preprocess stores it (sh_jac_stored). Every other array
+    // keeps its offset, so a reader that needs neither carves with the defaults, which leave the tail's pointers NULL.
+    static size_t carve(char* base, size_t P, GeomState* s, bool rows = false, bool jac = false);
 };
 
 // ---- image state: N pixels, T tiles ------------------------------------------------------------------------
@@ -175,8 +176,36 @@ constexpr int FWD_GROUPS = 2;
 // each tile's instances staged once (config E, 32 k tiles: render_fwd 0.476 -> 0.449 ms; config C, 8 k tiles: 0.272
 // with two waves per tile vs 0.295 with one, profiles/r03z_ab_fwd_bands.txt)
 constexpr uint32_t FWD_ONE_WAVE_TILES = 16384;
-// GeomState::counters[5] after a forward that stored sh_jac
-constexpr uint32_t SH_JAC_WRITTEN = 0x4A41430Bu;
+// OMR_SH_JAC (default 1): preprocess stores each visible Gaussian's dRGB/ddir (GeomState::sh_jac) for gaussian_bwd
+// when it stages 16-coefficient SH rows (0: never; gaussian_bwd then reads the SH rows)
+#ifndef OMR_SH_JAC
+#define OMR_SH_JAC 1
+#endif
+// whether a forward with these inputs stores sh_jac: preprocess's sh16 condition (colours from 16-coefficient rows on
+// a 16-B aligned array), evaluated on the host to size the geometry buffer and in the kernel to write it
+__host__ __device__ inline bool sh_jac_stored(const float* colors_precomp, int M, const float* shs)
+{
+    return OMR_SH_JAC && colors_precomp == nullptr && shs != nullptr && M == 16 &&
+           (reinterpret_cast<uintptr_t>(shs) & 15u) == 0;
+}
+// GeomState::counters[5] after a forward that stored sh_jac: a key of the inputs sh_jac was computed from (the SH
+// array, the means and the camera position; sh_eval.h: sh_dir_grad). gaussian_bwd takes sh_jac only if its own
+// inputs give the same key, so a backward called with other SH, means or campos than its forward recomputes
+// dRGB/ddir from its own SH rows, as the reference does (backward.cu:56-112). Never 0 (0 = not stored).
+__host__ __device__ inline uint32_t sh_jac_key(const float* shs, const float* means3D, uint32_t cx, uint32_t cy,
+                                               uint32_t cz)
+{
+    const uint64_t words[4] = {(uint64_t)reinterpret_cast<uintptr_t>(shs),
+                               (uint64_t)reinterpret_cast<uintptr_t>(means3D), (uint64_t)cx | ((uint64_t)cy << 32),
+                               (uint64_t)cz};
+    uint64_t h = 0x4A41430B9E3779B9ull;
+    for (int i = 0; i < 4; ++i) {
+        h ^= words[i];
+        h *= 0xFF51AFD7ED558CCDull;
+        h ^= h >> 33;
+    }
+    return (uint32_t)h | 1u;
+}
 __host__ __device__ inline size_t ckpt_count(size_t L) { return L / CKPT + 1; }
 __host__ __device__ inline size_t seg_count(size_t L, uint32_t T) { return (size_t)T + L / CKPT + 1; }
 // the L-indexed region of the binning buffer, after row_valid: checkpoints [ckpt_count][256 pixels] float4

@@ -23,13 +23,51 @@ void* resize_cb(void* ctx, size_t n)
     return t->data_ptr();
 }
 
-// empty tensor -> NULL ("absent"); otherwise a contiguous float32 view kept alive by `keep`
-const float* fptr(const torch::Tensor& t, std::vector<torch::Tensor>& keep)
+bool present(const torch::Tensor& t) { return t.defined() && t.numel() != 0; }
+
+// A present input must live on the device of means3D (the kernels get raw device pointers: a host tensor or one on
+// another GPU would fault there, so the mistake is reported here as a c10::Error instead) and hold `numel` elements
+// when numel >= 0. The reference checks means3D's shape only (rasterize_points.cu:72-75).
+void check_on(const torch::Tensor& t, const char* name, const c10::Device& dev, int64_t numel = -1)
 {
-    if (!t.defined() || t.numel() == 0) return nullptr;
-    TORCH_CHECK(t.scalar_type() == torch::kFloat32, "rasterizer inputs must be float32");
+    if (!present(t)) return;
+    TORCH_CHECK(t.device() == dev, name, " must be on ", dev, " (the device of means3D), got ", t.device());
+    TORCH_CHECK(numel < 0 || t.numel() == numel, name, " must hold ", numel, " elements, got ", t.numel(), " (shape ",
+                t.sizes(), ")");
+}
+
+// empty tensor -> NULL ("absent"); otherwise a contiguous float32 view kept alive by `keep`
+const float* fptr(const torch::Tensor& t, std::vector<torch::Tensor>& keep, const char* name = "rasterizer input")
+{
+    if (!present(t)) return nullptr;
+    TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be float32, got ", t.scalar_type());
     keep.push_back(t.contiguous());
     return keep.back().data_ptr<float>();
+}
+
+// the inputs both directions share: devices and element counts of everything the kernels index by P
+void check_inputs(const torch::Tensor& background, const torch::Tensor& means3D, const torch::Tensor& colors,
+                  const torch::Tensor& scales, const torch::Tensor& rotations, const torch::Tensor& cov3D_precomp,
+                  const torch::Tensor& viewmatrix, const torch::Tensor& projmatrix, const torch::Tensor& sh,
+                  const torch::Tensor& campos, int camera_type)
+{
+    const int64_t P = means3D.size(0);
+    TORCH_CHECK(P == 0 || means3D.is_cuda(), "means3D must be a HIP device tensor (the rasterizer has no CPU path), got ",
+                means3D.device());
+    const c10::Device dev = means3D.device();
+    check_on(background, "background", dev, 3);
+    check_on(colors, "colors", dev, 3 * P);
+    check_on(scales, "scales", dev, 3 * P);
+    check_on(rotations, "rotations", dev, 4 * P);
+    check_on(cov3D_precomp, "cov3D_precomp", dev, 6 * P);
+    check_on(viewmatrix, "viewmatrix", dev, 16);
+    check_on(projmatrix, "projmatrix", dev, camera_type == 1 ? 16 : -1);
+    check_on(campos, "campos", dev, 3);
+    check_on(sh, "sh", dev);
+    if (present(sh))
+        TORCH_CHECK(sh.dim() == 3 && sh.size(0) == P && sh.size(2) == 3, "sh must be [P, M, 3] with P = ", P,
+                    ", got ", sh.sizes());
+    TORCH_CHECK(P == 0 || present(background), "background is required");
 }
 
 void* stream_of(const torch::Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
@@ -60,6 +98,10 @@ RasterizeGaussiansCUDA(const torch::Tensor& background, const torch::Tensor& mea
     const int P = means3D.size(0);
     const int H = image_height;
     const int W = image_width;
+    check_inputs(background, means3D, colors, scales, rotations, cov3D_precomp, viewmatrix, projmatrix, sh, campos,
+                 camera_type);
+    check_on(opacity, "opacity", means3D.device(), P);
+    TORCH_CHECK(H > 0 && W > 0, "image_height and image_width must be positive, got ", H, " x ", W);
     c10::DeviceGuard guard(means3D.device());
     auto float_opts = means3D.options().dtype(torch::kFloat32);
     // every pixel / Gaussian is written by the kernels when P > 0, so only P == 0 needs the zero fill
@@ -115,11 +157,45 @@ RasterizeGaussiansBackwardCUDA(const torch::Tensor& background, const torch::Ten
                                const int R, const torch::Tensor& binningBuffer, const torch::Tensor& imageBuffer,
                                const int camera_type)
 {
+    if (means3D.ndimension() != 2 || means3D.size(1) != 3) {
+        AT_ERROR("means3D must have dimensions (num_points, 3)");
+    }
     const int P = means3D.size(0);
+    check_inputs(background, means3D, colors, scales, rotations, cov3D_precomp, viewmatrix, projmatrix, sh, campos,
+                 camera_type);
+    const c10::Device dev = means3D.device();
+    // dL_dout_color is [3, H, W] of the view the forward rendered: the image buffer the backward re-reads was sized
+    // for exactly that view (omr_image_bytes), and the binning buffer for R instances of it
+    TORCH_CHECK(dL_dout_color.dim() == 3 && dL_dout_color.size(0) == 3 && dL_dout_color.size(1) > 0 &&
+                    dL_dout_color.size(2) > 0,
+                "dL_dout_color must be [3, H, W], got ", dL_dout_color.sizes());
+    check_on(dL_dout_color, "dL_dout_color", dev);
     const int H = dL_dout_color.size(1);
     const int W = dL_dout_color.size(2);
     int M = 0;
     if (sh.size(0) != 0) M = sh.size(1);
+    TORCH_CHECK(R >= 0, "R (num_rendered) must be >= 0, got ", R);
+    if (P != 0) {
+        TORCH_CHECK(radii.defined() && radii.dim() == 1 && radii.size(0) == P && radii.scalar_type() == torch::kInt32,
+                    "radii must be the forward's [P] int32 tensor with P = ", P, ", got ",
+                    radii.defined() ? radii.sizes() : c10::IntArrayRef{}, " ",
+                    radii.defined() ? radii.scalar_type() : torch::kInt32);
+        check_on(radii, "radii", dev);
+        for (const auto* b : {&geomBuffer, &binningBuffer, &imageBuffer}) {
+            TORCH_CHECK(b->defined() && b->scalar_type() == torch::kByte && b->dim() == 1,
+                        "scratch buffers must be the forward's uint8 geomBuffer / binningBuffer / imgBuffer");
+            if (b->numel() != 0) check_on(*b, "scratch buffer", dev);
+        }
+        TORCH_CHECK(geomBuffer.numel() > 0 && imageBuffer.numel() > 0,
+                    "geomBuffer / imgBuffer are empty: pass the buffers the forward returned");
+        TORCH_CHECK((size_t)imageBuffer.numel() == omr_image_bytes(W, H),
+                    "dL_dout_color is [3, ", H, ", ", W, "] but imgBuffer (", imageBuffer.numel(),
+                    " bytes) was sized by the forward for a different view (", omr_image_bytes(W, H),
+                    " bytes for this one)");
+        TORCH_CHECK(R == 0 || (size_t)binningBuffer.numel() >= omr_binning_bytes(R, W, H), "binningBuffer (",
+                    binningBuffer.numel(), " bytes) is too small for R = ", R, " instances of a ", W, " x ", H,
+                    " view: pass the forward's num_rendered and buffers");
+    }
     c10::DeviceGuard guard(means3D.device());
     auto o = means3D.options().dtype(torch::kFloat32);
     // the gfx950 backward writes every element, so only P == 0 needs zeros (rasterize_points.cu:200-208 zero-fill)
@@ -177,21 +253,29 @@ RasterizeGaussiansBackwardCUDA(const torch::Tensor& background, const torch::Ten
 torch::Tensor markVisible(torch::Tensor& means3D, torch::Tensor& viewmatrix, torch::Tensor& projmatrix,
                           const int camera_type)
 {
+    if (means3D.ndimension() != 2 || means3D.size(1) != 3) {
+        AT_ERROR("means3D must have dimensions (num_points, 3)");
+    }
     const int P = means3D.size(0);
+    TORCH_CHECK(P == 0 || means3D.is_cuda(), "means3D must be a HIP device tensor, got ", means3D.device());
+    check_on(viewmatrix, "viewmatrix", means3D.device(), 16);
+    check_on(projmatrix, "projmatrix", means3D.device(), 16);
+    TORCH_CHECK(camera_type != 1 || P == 0 || (present(viewmatrix) && present(projmatrix)),
+                "pinhole markVisible needs viewmatrix and projmatrix");
     c10::DeviceGuard guard(means3D.device());
-    torch::Tensor present = torch::full({P}, false, means3D.options().dtype(at::kBool));
+    torch::Tensor visible = torch::full({P}, false, means3D.options().dtype(at::kBool));
     if (P != 0) {
         std::vector<torch::Tensor> keep;
         int rc;
         if (camera_type == 1) {
             rc = omr_rasterizer_mark_visible(P, fptr(means3D, keep), fptr(viewmatrix, keep), fptr(projmatrix, keep),
-                                             present.data_ptr<bool>(), stream_of(means3D));
+                                             visible.data_ptr<bool>(), stream_of(means3D));
         } else if (camera_type == 3) {
-            rc = omr_lonlat_mark_visible(P, present.data_ptr<bool>(), stream_of(means3D));
+            rc = omr_lonlat_mark_visible(P, visible.data_ptr<bool>(), stream_of(means3D));
         } else {
             throw std::runtime_error("[CudaRasterizer]Invalid camera_type");
         }
         throw_status(rc, "markVisible");
     }
-    return present;
+    return visible;
 }

@@ -358,8 +358,24 @@ void launch_render_backward(const RenderBwdArgs& a, size_t max_units, hipStream_
                             hipEvent_t ev_stop)
 {
     if (max_units == 0) return;
-    // max_units (tiles + L / CKPT + 1) bounds the unit count; 24 waves per CU on 256 CUs are resident at once
-    constexpr size_t RESIDENT = 24 * 256;
+    // max_units (tiles + L / CKPT + 1) bounds the unit count; it is compared with the one-wave workgroups of the
+    // batch-BWD_BATCH kernel the device holds at once (24 per CU on MI355X's 256 CUs: 6144), asked of the runtime once
+    // per device
+    static thread_local int cached_dev = -1;
+    static thread_local size_t resident = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (dev != cached_dev) {
+        int cus = 0, per_cu = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_bwd_kernel<OMR_BWD_BATCH>, 64 * TW_WAVES, 0) !=
+                hipSuccess ||
+            per_cu <= 0)
+            per_cu = 24;
+        resident = (size_t)cus * (size_t)per_cu;
+        cached_dev = dev;
+    }
+    const size_t RESIDENT = resident;
     auto launch = [&](auto kernel) {
         if (ev_start || ev_stop)
             hipExtLaunchKernelGGL(kernel, dim3((uint32_t)max_units), dim3(64 * TW_WAVES), 0, s, ev_start, ev_stop, 0, a);

@@ -145,14 +145,26 @@ def _ptr(t: Optional[torch.Tensor]):
     return t.data_ptr()
 
 
-def _dev_f32(t: Optional[torch.Tensor], name: str) -> Optional[torch.Tensor]:
+def _dev_f32(t: Optional[torch.Tensor], name: str, dev: Optional[torch.device] = None,
+             numel: Optional[int] = None) -> Optional[torch.Tensor]:
+    """A present input as a contiguous float32 tensor on `dev` (the device of means3D) holding `numel` elements: the
+    kernels get raw device pointers, so a host tensor, one on another GPU or a short one would fault there."""
     if t is None or t.numel() == 0:
         return None
     if t.device.type != "cuda":
         raise RasterizerError(f"{name} must be on a HIP device (got {t.device}); the rasterizer has no CPU path")
+    if dev is not None and t.device != dev:
+        raise RasterizerError(f"{name} must be on {dev} (the device of means3D), got {t.device}")
     if t.dtype != torch.float32:
         raise RasterizerError(f"{name} must be float32 (got {t.dtype})")
+    if numel is not None and t.numel() != numel:
+        raise RasterizerError(f"{name} must hold {numel} elements, got {t.numel()} (shape {tuple(t.shape)})")
     return t.contiguous()
+
+
+def _check_sh(sh, P):
+    if sh is not None and sh.numel() != 0 and (sh.dim() != 3 or sh.shape[0] != P or sh.shape[2] != 3):
+        raise RasterizerError(f"sh must be [P, M, 3] with P = {P}, got {tuple(sh.shape)}")
 
 
 def _stream(device: torch.device) -> int:
@@ -203,13 +215,19 @@ def RasterizeGaussiansCUDA(background, means3D, colors, opacity, scales, rotatio
         radii = torch.zeros((0,), dtype=torch.int32, device=dev)
         return 0, out_color, radii, geom.tensor, binning.tensor, img.tensor
     m = _dev_f32(means3D, "means3D")
+    if H <= 0 or W <= 0:
+        raise RasterizerError(f"image_height and image_width must be positive, got {H} x {W}")
+    _check_sh(sh, P)
+    M = int(sh.shape[1]) if sh is not None and sh.numel() != 0 and sh.shape[0] != 0 else 0
+    bg, shc, col, op = (_dev_f32(background, "background", dev, 3), _dev_f32(sh, "sh", dev),
+                        _dev_f32(colors, "colors", dev, 3 * P), _dev_f32(opacity, "opacity", dev, P))
+    sc, rot, cov = (_dev_f32(scales, "scales", dev, 3 * P), _dev_f32(rotations, "rotations", dev, 4 * P),
+                    _dev_f32(cov3D_precomp, "cov3D_precomp", dev, 6 * P))
+    vm, pm, cp = (_dev_f32(viewmatrix, "viewmatrix", dev, 16),
+                  _dev_f32(projmatrix, "projmatrix", dev, 16 if camera_type == CAMERA_PINHOLE else None),
+                  _dev_f32(campos, "campos", dev, 3))
     out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)  # every pixel is written
     radii = torch.empty((P,), dtype=torch.int32, device=dev)  # every Gaussian is written
-    M = int(sh.shape[1]) if sh is not None and sh.numel() != 0 and sh.shape[0] != 0 else 0
-    bg, shc, col, op = (_dev_f32(background, "background"), _dev_f32(sh, "sh"), _dev_f32(colors, "colors"),
-                        _dev_f32(opacity, "opacity"))
-    sc, rot, cov = _dev_f32(scales, "scales"), _dev_f32(rotations, "rotations"), _dev_f32(cov3D_precomp, "cov3D_precomp")
-    vm, pm, cp = _dev_f32(viewmatrix, "viewmatrix"), _dev_f32(projmatrix, "projmatrix"), _dev_f32(campos, "campos")
     nr = C.c_int(0)
     L = lib()
     if camera_type == CAMERA_PINHOLE:
@@ -252,10 +270,33 @@ def RasterizeGaussiansBackwardCUDA(background, means3D, radii, colors, scales, r
                      backward_chunk_ranges(P, n) and event k is recorded once range k's gradients are final."""
     if camera_type not in (CAMERA_PINHOLE, CAMERA_LONLAT):
         raise RasterizerError("[CudaRasterizer]Invalid camera_type")
+    if means3D.ndim != 2 or means3D.shape[1] != 3:
+        raise RasterizerError("means3D must have dimensions (num_points, 3)")
     dev = means3D.device
     P = int(means3D.shape[0])
+    if dL_dout_color.dim() != 3 or dL_dout_color.shape[0] != 3 or min(dL_dout_color.shape[1:]) <= 0:
+        raise RasterizerError(f"dL_dout_color must be [3, H, W], got {tuple(dL_dout_color.shape)}")
     H, W = int(dL_dout_color.shape[1]), int(dL_dout_color.shape[2])
+    _check_sh(sh, P)
     M = int(sh.shape[1]) if sh is not None and sh.numel() != 0 and sh.shape[0] != 0 else 0
+    if int(R) < 0:
+        raise RasterizerError(f"R (num_rendered) must be >= 0, got {R}")
+    if P != 0:
+        if radii is None or radii.dim() != 1 or radii.shape[0] != P or radii.dtype != torch.int32 or radii.device != dev:
+            raise RasterizerError(f"radii must be the forward's [P] int32 tensor on {dev} with P = {P}, got "
+                                  f"{None if radii is None else (tuple(radii.shape), radii.dtype, radii.device)}")
+        for name, b in (("geomBuffer", geomBuffer), ("binningBuffer", binningBuffer), ("imageBuffer", imageBuffer)):
+            if b.dtype != torch.uint8 or (b.numel() != 0 and b.device != dev):
+                raise RasterizerError(f"{name} must be the forward's uint8 buffer on {dev}")
+        if geomBuffer.numel() == 0 or imageBuffer.numel() == 0:
+            raise RasterizerError("geomBuffer / imageBuffer are empty: pass the buffers the forward returned")
+        need = int(lib().omr_image_bytes(W, H))
+        if imageBuffer.numel() != need:
+            raise RasterizerError(f"dL_dout_color is [3, {H}, {W}] but imageBuffer ({imageBuffer.numel()} bytes) was "
+                                  f"sized by the forward for a different view ({need} bytes for this one)")
+        if int(R) > 0 and binningBuffer.numel() < int(lib().omr_binning_bytes(int(R), W, H)):
+            raise RasterizerError(f"binningBuffer ({binningBuffer.numel()} bytes) is too small for R = {R} instances "
+                                  f"of a {W} x {H} view")
     shapes = dict(dL_dmeans2D=(P, 3), dL_dcolors=(P, 3), dL_dopacity=(P, 1), dL_dmeans3D=(P, 3), dL_dcov3D=(P, 6),
                   dL_dsh=(P, M, 3), dL_dscales=(P, 3), dL_drotations=(P, 4))
     o = {}
@@ -271,11 +312,12 @@ def RasterizeGaussiansBackwardCUDA(background, means3D, radii, colors, scales, r
         o[k] = t
     if P != 0:
         L = lib()
-        args_common = dict(bg=_dev_f32(background, "background"), m=_dev_f32(means3D, "means3D"),
-                           shc=_dev_f32(sh, "sh"), col=_dev_f32(colors, "colors"), sc=_dev_f32(scales, "scales"),
-                           rot=_dev_f32(rotations, "rotations"), cov=_dev_f32(cov3D_precomp, "cov3D_precomp"),
-                           vm=_dev_f32(viewmatrix, "viewmatrix"), cp=_dev_f32(campos, "campos"),
-                           dl=_dev_f32(dL_dout_color, "dL_dout_color"))
+        args_common = dict(bg=_dev_f32(background, "background", dev, 3), m=_dev_f32(means3D, "means3D"),
+                           shc=_dev_f32(sh, "sh", dev), col=_dev_f32(colors, "colors", dev, 3 * P),
+                           sc=_dev_f32(scales, "scales", dev, 3 * P), rot=_dev_f32(rotations, "rotations", dev, 4 * P),
+                           cov=_dev_f32(cov3D_precomp, "cov3D_precomp", dev, 6 * P),
+                           vm=_dev_f32(viewmatrix, "viewmatrix", dev, 16), cp=_dev_f32(campos, "campos", dev, 3),
+                           dl=_dev_f32(dL_dout_color, "dL_dout_color", dev))
         a = args_common
         rad = radii.contiguous()
         gb, bb, ib = geomBuffer.data_ptr(), binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr()
@@ -290,7 +332,7 @@ def RasterizeGaussiansBackwardCUDA(background, means3D, radii, colors, scales, r
             arr = (C.c_void_p * len(chunk_events))(*[ev.cuda_event for ev in chunk_events])
             L.omr_backward_chunk_events(len(chunk_events), arr)
         if camera_type == CAMERA_PINHOLE:
-            pm = _dev_f32(projmatrix, "projmatrix")
+            pm = _dev_f32(projmatrix, "projmatrix", dev, 16)
             rc = L.omr_rasterizer_backward(P, int(degree), M, int(R), _ptr(a["bg"]), W, H, _ptr(a["m"]), _ptr(a["shc"]),
                                            _ptr(a["col"]), _ptr(a["sc"]), float(scale_modifier), _ptr(a["rot"]),
                                            _ptr(a["cov"]), _ptr(a["vm"]), _ptr(pm), _ptr(a["cp"]), float(tan_fovx),
@@ -512,11 +554,11 @@ def debug_counters(P, geomBuffer) -> dict:
            "debug_counters")
     c = [int(v) & 0xFFFFFFFF for v in out.cpu().tolist()]
     return {"num_rendered": c[0], "prefiltered_flag": c[1], "huge": c[2], "error": c[3], "row_slots": c[4],
-            "sh_jac": c[5] == 0x4A41430B}
+            "sh_jac": c[5] != 0, "sh_jac_key": c[5]}
 
 
 def debug_set_sh_jac(P, geomBuffer, enabled: bool):
-    """Sets or clears the flag by which the backward takes the forward's stored dRGB/ddir (omr_debug_set_sh_jac)."""
+    """Clears or restores the key by which the backward takes the forward's stored dRGB/ddir (omr_debug_set_sh_jac)."""
     _check(lib().omr_debug_set_sh_jac(geomBuffer.data_ptr(), int(P), 1 if enabled else 0, _stream(geomBuffer.device)),
            "debug_set_sh_jac")
 

@@ -8,6 +8,11 @@ WRITE_SIZE averages) and profiles/pmc_latest.json, which bench.py reads for roof
 
 HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: rocprofv3 reports both in KiB, and on gfx950
 FETCH_SIZE counts half the bytes of wide coalesced reads (MI355X_MICROARCH.md § HBM), so it is doubled.
+
+The --stats summary averages every launch of the run: warm-ups, and the bench's per-stage pass, whose events at every
+stage boundary end in system-scope releases (L2 write-back) and so slow the kernel that follows. The timed loop's
+launches are the bench's live measurement, so profiles/<tag>_kernel_stats_timed.csv restates the same kernel trace
+over the timed loop only (timed_window below), and pmc_latest.json's rocprof_avg_ms comes from it.
 """
 import csv
 import glob
@@ -57,17 +62,67 @@ def per_kernel(counter_dir, counter):
     return {k: (sum(d.values()) / len(d), len(d)) for k, d in acc.items()}
 
 
+def timed_window(trace_csv, bench_json):
+    """Per-kernel statistics of the bench's timed loop alone, from a rocprofv3 --kernel-trace CSV of `bench.py`.
+
+    bench.py runs `warmup` steps, then a per-stage pass of min(steps, 10) steps, then the `steps` timed ones; every
+    step launches preprocess_kernel exactly once, so the timed loop starts at the (warmup + min(steps, 10))-th
+    preprocess dispatch (0-based) and runs to the end of the trace (the bench under rocprof runs with
+    --no-train-step; the CPU baseline launches nothing)."""
+    with open(bench_json) as f:
+        bench = json.loads([ln for ln in f if ln.startswith("{")][-1])
+    steps, warmup = int(bench["steps"]), int(bench["warmup"])
+    skip = warmup + min(steps, 10)
+    rows = []
+    with open(trace_csv) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    pre = [t0 for t0, _, k in rows if "preprocess_kernel" in k]
+    if len(pre) != skip + steps:
+        raise RuntimeError(f"{trace_csv}: {len(pre)} preprocess dispatches, expected {skip} + {steps}")
+    t_start = pre[skip]
+    acc = {}
+    for t0, t1, k in rows:
+        if t0 >= t_start:
+            acc.setdefault(k, []).append((t1 - t0) * 1e-6)  # ns -> ms
+    out = {}
+    for k, d in acc.items():
+        d.sort()
+        out[k] = {"calls": len(d), "avg_ms": sum(d) / len(d), "min_ms": d[0], "max_ms": d[-1],
+                  "median_ms": d[len(d) // 2], "total_ms": sum(d)}
+    return out, steps, (rows[-1][1] - t_start) * 1e-6
+
+
+def write_timed_stats(tag, timed, steps, window_ms):
+    path = os.path.join(HERE, f"{tag}_kernel_stats_timed.csv")
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Name", "Calls", "AverageNs", "MinNs", "MaxNs", "MedianNs", "TotalDurationNs", "Percentage",
+                     "TimedSteps", "WindowNs"])
+        tot = sum(v["total_ms"] for v in timed.values()) or 1.0
+        for k, v in sorted(timed.items(), key=lambda kv: -kv[1]["total_ms"]):
+            w.writerow([k, v["calls"], round(v["avg_ms"] * 1e6, 1), round(v["min_ms"] * 1e6, 1),
+                        round(v["max_ms"] * 1e6, 1), round(v["median_ms"] * 1e6, 1), round(v["total_ms"] * 1e6, 1),
+                        round(100.0 * v["total_ms"] / tot, 3), steps, round(window_ms * 1e6)])
+    return path
+
+
 def main():
     tag = sys.argv[1]
     stats = glob.glob(os.path.join(OUT, f"prof_{tag}", "**", "*kernel_stats.csv"), recursive=True)
-    rocprof_avg = {}  # stage -> rocprofv3 --stats average duration (ms) of its kernel, same build as the PMC passes
+    traces = glob.glob(os.path.join(OUT, f"prof_{tag}", "**", "*kernel_trace.csv"), recursive=True)
+    rocprof_avg = {}  # stage -> rocprofv3 average duration (ms) of its kernel over the bench's timed loop
+    timed_file = None
     if stats:
         shutil.copy(stats[0], os.path.join(HERE, f"{tag}_kernel_stats.csv"))
-        with open(stats[0]) as f:
-            for row in csv.DictReader(f):
-                for frag, stage in STAGES.items():
-                    if frag in row["Name"]:
-                        rocprof_avg[stage] = (float(row["AverageNs"]) * 1e-6, int(row["Calls"]))
+    if traces:
+        timed, steps, window_ms = timed_window(traces[0], os.path.join(OUT, f"bench_prof_{tag}.json"))
+        timed_file = os.path.relpath(write_timed_stats(tag, timed, steps, window_ms), ROOT)
+        for name, v in timed.items():
+            for frag, stage in STAGES.items():
+                if frag in name:
+                    rocprof_avg[stage] = (v["avg_ms"], v["calls"])
     fetch = per_kernel(os.path.join(OUT, f"pmc_fetch_{tag}"), "FETCH_SIZE")
     write = per_kernel(os.path.join(OUT, f"pmc_write_{tag}"), "WRITE_SIZE")
     with open(os.path.join(OUT, f"bench_pmc_fetch_{tag}.json")) as f:
@@ -95,7 +150,9 @@ def main():
         w.writerows(rows)
     latest = {"tag": tag, "config": cfg, "P": bench["config"]["P"], "L": bench["config"]["L"],
               "method": "(2*FETCH_SIZE + WRITE_SIZE) KiB * 1024, separate --pmc passes, gfx950 FETCH x2 correction",
-              "kernel_stats_file": f"profiles/{tag}_kernel_stats.csv" if stats else None, "kernels": kernels}
+              "kernel_stats_file": timed_file,
+              "kernel_stats_all_launches_file": f"profiles/{tag}_kernel_stats.csv" if stats else None,
+              "rocprof_avg_over": "the bench's timed loop only (pmc_summarize.timed_window)", "kernels": kernels}
     with open(os.path.join(HERE, "pmc_latest.json"), "w") as f:
         json.dump(latest, f, indent=1)
     print(json.dumps(latest, indent=1))

@@ -4,7 +4,10 @@ them) through the real exchange code: eight ranks over gloo, all on cuda:0 (the 
 rank renders its view of the config's scene, runs the HIP backward into its GradBuffer and calls
 parallel.allreduce_compact_ (the exchange bench.py runs at N > 1: all-reduce of the 44 B/G xyz / opacity / scale /
 rotation gradients, all-gather of every view's colour gradient and camera position, SH gradient rebuilt on every
-rank). Checked against the eight per-view HIP gradients computed one after another in this process:
+rank), and through the overlapped parallel.CompactExchange that bench.py runs by default (colour all-gather on a side
+stream behind the backward's colours event, dL_dsh not written by the backward; ar_chunks 1 and 3, the latter
+all-reducing the 44 B/G per Gaussian range behind the chunk events). Every exchange is checked
+against the eight per-view HIP gradients computed one after another in this process:
   * every rank holds the same buffer, bit for bit;
   * the 44 B/G part equals the per-view sum to float32 summation-order error (gloo's ring adds the eight views in
     another order than a sequential loop: |diff| <= 8 ulp of the sum of magnitudes);
@@ -33,6 +36,9 @@ def _scene_name(config, rank):
     return config
 
 
+MODES = ("call", "overlap1", "overlap3")  # allreduce_compact_ after the backward; CompactExchange, ar_chunks 1 / 3
+
+
 def _worker(rank, world, port, q, tmpdir, config):
     import torch
     import torch.distributed as dist
@@ -52,30 +58,44 @@ def _worker(rank, world, port, q, tmpdir, config):
         m, sh = t(g.means3D), t(g.shs)
         vm, pm, cp, bg, e = t(cam.viewmatrix), t(cam.projmatrix), t(cam.campos), torch.zeros(3, device=dev), \
             torch.empty(0, device=dev)
-        buf = par.GradBuffer(g.P, g.shs.shape[1], dev)
-        out = buf.out_dict(dev)
-        nr, color, radii, gb, bb, ib = R.RasterizeGaussiansCUDA(bg, m, e, t(g.opacity), t(g.scales), t(g.rotations),
-                                                                1.0, e, vm, pm, cam.tanfovx, cam.tanfovy, cam.height,
-                                                                cam.width, sh, g.sh_degree, cp, False, cam.camera_type,
-                                                                False)
-        R.RasterizeGaussiansBackwardCUDA(bg, m, radii, e, t(g.scales), t(g.rotations), 1.0, e, vm, pm, cam.tanfovx,
-                                         cam.tanfovy, t(dL), sh, g.sh_degree, cp, gb, nr, bb, ib, cam.camera_type,
-                                         out=out)
-        torch.cuda.synchronize()
-        par.allreduce_compact_(buf, par.DistInfo(rank, world, 0), out["dL_dcolors"], cp, None,
-                               rebuild_packed=lambda pk, out: R.sh_grad_from_colors_packed(m, sh, g.sh_degree, pk,
-                                                                                           out=out))
-        torch.cuda.synchronize()
-        flat = buf.flat.cpu().numpy()
-        if rank == 0:
-            np.save(os.path.join(tmpdir, "flat0.npy"), flat)
-        q.put((rank, hashlib.sha1(flat.tobytes()).hexdigest()))
+        op, sc, rot, dLt = t(g.opacity), t(g.scales), t(g.rotations), t(dL)
+        info = par.DistInfo(rank, world, 0)
+        rebuild = lambda pk, out: R.sh_grad_from_colors_packed(m, sh, g.sh_degree, pk, out=out)  # noqa: E731
+        digests = {}
+        for mode in MODES:
+            buf = par.GradBuffer(g.P, g.shs.shape[1], dev)
+            buf.flat.fill_(float("nan"))  # every element must be written by the backward or the exchange
+            out = buf.out_dict(dev)
+            cx = None
+            if mode != "call":
+                cx = par.CompactExchange(buf, info, cp, rebuild, dev, any_backend=True, ar_chunks=int(mode[-1]))
+                assert cx.overlap and cx.ar_chunks == int(mode[-1])
+            nr, color, radii, gb, bb, ib = R.RasterizeGaussiansCUDA(bg, m, e, op, sc, rot, 1.0, e, vm, pm, cam.tanfovx,
+                                                                    cam.tanfovy, cam.height, cam.width, sh,
+                                                                    g.sh_degree, cp, False, cam.camera_type, False)
+            R.RasterizeGaussiansBackwardCUDA(bg, m, radii, e, sc, rot, 1.0, e, vm, pm, cam.tanfovx, cam.tanfovy, dLt,
+                                             sh, g.sh_degree, cp, gb, nr, bb, ib, cam.camera_type, out=out,
+                                             **(cx.backward_kwargs(cp) if cx else {}))
+            if cx is None:
+                torch.cuda.synchronize()
+                par.allreduce_compact_(buf, info, out["dL_dcolors"], cp, None, rebuild_packed=rebuild)
+            else:
+                cx.start()
+                cx.finish()
+            torch.cuda.synchronize()
+            flat = buf.flat.cpu().numpy()
+            if rank == 0:
+                np.save(os.path.join(tmpdir, f"flat0_{mode}.npy"), flat)
+            digests[mode] = hashlib.sha1(flat.tobytes()).hexdigest()
+            del buf, out, cx, gb, bb, ib
+        q.put((rank, digests))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("config", ["D", "E"])
 def test_config_eight_ranks_compact_exchange(config, tmp_path):
+    """allreduce_compact_ after the backward and the overlapped CompactExchange (ar_chunks 1, 3) at eight ranks."""
     import torch
 
     with socket.socket() as s:
@@ -86,12 +106,13 @@ def test_config_eight_ranks_compact_exchange(config, tmp_path):
     procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q, str(tmp_path), config)) for r in range(WORLD)]
     for p in procs:
         p.start()
-    digests = dict(q.get(timeout=420) for _ in procs)
+    digests = dict(q.get(timeout=600) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert len(set(digests.values())) == 1, digests  # identical replicas, bit for bit
-    flat0 = np.load(os.path.join(str(tmp_path), "flat0.npy"))
+    for mode in MODES:
+        per_rank = {r: d[mode] for r, d in digests.items()}
+        assert len(set(per_rank.values())) == 1, (mode, per_rank)  # identical replicas, bit for bit
 
     sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
     from helpers import hip_run, omr, to_np
@@ -110,16 +131,18 @@ def test_config_eight_ranks_compact_exchange(config, tmp_path):
         campos.append(torch.from_numpy(cam.campos).cuda())
         del h, gr
     P = g.P
-    buf = par.GradBuffer(P, g.shs.shape[1], torch.device("cpu"))
-    buf.flat.copy_(torch.from_numpy(flat0))
-    got = np.concatenate([buf.views[k].numpy().reshape(P, -1) for k in NAMES], axis=1).astype(np.float64)
-    tol = 8 * np.finfo(np.float32).eps * mags + np.finfo(np.float32).tiny
-    bad = np.abs(got - sums) > tol
-    assert not bad.any(), f"{int(bad.sum())} entries of the 44 B/G sum off by more than 8 ulp of their magnitude sum"
     dev = dsh_seq.device
     packed = torch.cat([torch.stack(dcolors), torch.stack(campos)[:, None, :]], dim=1).contiguous()
     rebuilt = R.sh_grad_from_colors_packed(torch.from_numpy(g.means3D).to(dev), torch.from_numpy(g.shs).to(dev),
                                            g.sh_degree, packed)
     torch.cuda.synchronize()
-    np.testing.assert_array_equal(buf.views["dL_dsh"].numpy(), to_np(rebuilt))
     np.testing.assert_array_equal(to_np(rebuilt), to_np(dsh_seq))
+    tol = 8 * np.finfo(np.float32).eps * mags + np.finfo(np.float32).tiny
+    for mode in MODES:
+        buf = par.GradBuffer(P, g.shs.shape[1], torch.device("cpu"))
+        buf.flat.copy_(torch.from_numpy(np.load(os.path.join(str(tmp_path), f"flat0_{mode}.npy"))))
+        assert not torch.isnan(buf.flat).any(), mode
+        got = np.concatenate([buf.views[k].numpy().reshape(P, -1) for k in NAMES], axis=1).astype(np.float64)
+        bad = np.abs(got - sums) > tol
+        assert not bad.any(), f"{mode}: {int(bad.sum())} entries of the 44 B/G sum off by more than 8 ulp"
+        np.testing.assert_array_equal(buf.views["dL_dsh"].numpy(), to_np(rebuilt), err_msg=mode)

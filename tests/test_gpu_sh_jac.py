@@ -60,3 +60,45 @@ def test_precomputed_colours_store_no_direction_gradient():
     colors = np.random.default_rng(5).random((g.P, 3)).astype(np.float32)
     _, fwd = _forward(g, cam, colors=colors)
     assert not R.debug_counters(g.P, fwd[3])["sh_jac"]
+
+
+@pytest.mark.parametrize("camera", [scene.CAMERA_LONLAT, scene.CAMERA_PINHOLE])
+def test_sh_row_path_alone_matches_the_oracle(camera):
+    """The backward's own dRGB/ddir evaluation (the MC == 16 row-reading path, flag cleared) against the oracle, not
+    only against the stored path: a wrong sh_dir_grad shared by both sites would fail here."""
+    from helpers import grad_close, oracle_run, to_np
+
+    g, cam, dL = make_case(2000, 256, 128, camera, 23, view_index=3, spread=2.0)
+    args, fwd = _forward(g, cam)
+    R.debug_set_sh_jac(g.P, fwd[3], False)
+    grads = _backward(g, cam, args, fwd, dL)
+    _, L, og = oracle_run(g, cam, dL)
+    assert fwd[0] == L
+    for name, idx in (("dmean3D", 3), ("dsh", 5), ("dopacity", 2), ("dscale", 6), ("drot", 7)):
+        ok, emax, nbad = grad_close(to_np(grads[idx]), og[name])
+        assert ok, (name, emax, nbad)
+
+
+def test_backward_with_other_inputs_recomputes_the_direction_gradient():
+    """sh_jac is keyed to the forward's SH array, means and campos (raster_common.h: sh_jac_key): a backward handed
+    another camera position uses its own inputs, as the reference's backward does (backward.cu:56-112), and equals
+    the row-reading path on those inputs bit for bit."""
+    g, cam, dL = make_case(2000, 256, 128, scene.CAMERA_LONLAT, 24, view_index=1, spread=2.0)
+    args, fwd = _forward(g, cam)
+    geomB = fwd[3]
+    key = R.debug_counters(g.P, geomB)["sh_jac_key"]
+    assert key != 0
+    same = _backward(g, cam, args, fwd, dL)
+    moved = dict(args, campos=args["campos"] + torch.tensor([0.05, -0.02, 0.03], device=args["campos"].device))
+    other = _backward(g, cam, moved, fwd, dL)
+    R.debug_set_sh_jac(g.P, geomB, False)
+    other_rows = _backward(g, cam, moved, fwd, dL)
+    R.debug_set_sh_jac(g.P, geomB, True)
+    assert R.debug_counters(g.P, geomB)["sh_jac_key"] == key  # restored
+    for a, b in zip(other, other_rows):
+        assert torch.equal(a, b)
+    assert not torch.equal(other[5], same[5])  # dL/dsh depends on the view direction
+    # a copy of the SH array (another pointer, the same values) also takes the row path: the same bits
+    copied = dict(args, sh=args["sh"].clone())
+    for a, b in zip(_backward(g, cam, copied, fwd, dL), same):
+        assert torch.equal(a, b)
