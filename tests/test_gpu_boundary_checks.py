@@ -23,7 +23,8 @@ def _inputs(cam_type):
 
 
 def _fwd(api, g, cam, d, cam_type, **over):
-    x = dict(d, **over)
+    x = dict(d)
+    x.update(over)
     return api.RasterizeGaussiansCUDA(x["bg"], x["means"], x["e"], x["op"], x["sc"], x["rot"], 1.0, x["e"], x["vm"],
                                       x["pm"], cam.tanfovx, cam.tanfovy, cam.height, cam.width, x["sh"], g.sh_degree,
                                       x["cp"], False, cam_type, False)
@@ -31,7 +32,8 @@ def _fwd(api, g, cam, d, cam_type, **over):
 
 def _bwd(api, g, cam, d, cam_type, fwd, **over):
     nr, _, radii, gb, bb, ib = fwd
-    x = dict(d, radii=radii, nr=nr, gb=gb, bb=bb, ib=ib, **over)
+    x = dict(d, radii=radii, nr=nr, gb=gb, bb=bb, ib=ib)
+    x.update(over)
     return api.RasterizeGaussiansBackwardCUDA(x["bg"], x["means"], x["radii"], x["e"], x["sc"], x["rot"], 1.0, x["e"],
                                               x["vm"], x["pm"], cam.tanfovx, cam.tanfovy, x["dL"], x["sh"],
                                               g.sh_degree, x["cp"], x["gb"], x["nr"], x["bb"], x["ib"], cam_type)
