@@ -343,8 +343,9 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s, bool rows, bool jac)
     g.key_b = c.take<uint32_t>(P);
     g.val_a = c.take<uint32_t>(P);
     g.val_b = c.take<uint32_t>(P);
-    g.hist = c.take<uint32_t>(radix_scratch_words(P, DEPTH_SORT_PASSES));
-    g.scan_partials = c.take<uint32_t>(radix_partials_words(P));
+    // the depth sort's scratch (or, under OMR_DEPTH_SORT=bytes, the 4 x 8-bit radix sort's)
+    g.hist = c.take<uint32_t>(std::max(depth_sort_scratch_words(P), radix_scratch_words(P, DEPTH_SORT_PASSES)));
+    g.scan_partials = c.take<uint32_t>(std::max(depth_sort_partials_words(P), radix_partials_words(P)));
     g.scan2_status = c.take<uint32_t>(scan2_status_words(P));
     g.offsets = c.take<uint32_t>(P);
     g.counters = c.take<uint32_t>(8);
@@ -353,6 +354,7 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s, bool rows, bool jac)
     g.conic_op = c.take<float4>(P);
     g.huge_list = c.take<uint32_t>(P);
     g.internal_radii = c.take<int>(P);
+    g.order = c.take<uint32_t>(P);
     // the optional tail: the row binning's arrays (bin.hip; preprocess and the forward scans write them only when
     // present), then sh_jac (preprocess writes it exactly when sh_jac_stored holds, which is when the forward carves it)
     if (rows) {
@@ -367,7 +369,6 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s, bool rows, bool jac)
         g.bin_rec = nullptr;
     }
     g.sh_jac = jac ? c.take<float>(9 * P) : nullptr;
-    g.order = g.val_a;  // the depth sort runs DEPTH_SORT_PASSES (even) passes, so its result lands in val_a
     if (s) *s = g;
     return c.size();
 }
@@ -400,6 +401,17 @@ static bool sort_binning_forced()
     static const bool forced = [] {
         const char* v = std::getenv("OMR_BINNING");
         return v && std::strcmp(v, "sort") == 0;
+    }();
+    return forced;
+}
+// OMR_DEPTH_SORT=bytes (read once) sorts the depth keys with the 4 x 8-bit radix sort over all 32 bits instead of
+// depth_sort's 9-bit passes over the bits the visible keys span: an A/B switch (same permutation of the visible
+// Gaussians)
+static bool depth_sort_bytes_forced()
+{
+    static const bool forced = [] {
+        const char* v = std::getenv("OMR_DEPTH_SORT");
+        return v && std::strcmp(v, "bytes") == 0;
     }();
     return forced;
 }
@@ -518,7 +530,8 @@ int forward_impl(const ForwardIn& in)
     pa.zero[0] = {g.counters + 2, 2};                                  // huge-list count (scan), look-back error word
     pa.zero[1] = {reinterpret_cast<uint32_t*>(im.ranges), 2 * (size_t)d.T};  // tile_ranges writes boundaries only
     pa.zero[2] = {im.tile_cost, (size_t)d.T};                          // render_forward adds into it
-    pa.zero[3] = radix_zero_span(g.hist, P, DEPTH_SORT_PASSES);        // the depth sort's digit totals / tickets
+    pa.zero[3] = depth_sort_bytes_forced() ? radix_zero_span(g.hist, P, DEPTH_SORT_PASSES)
+                                           : depth_sort_zero_span(g.hist, P);  // the depth sort's totals / words
     pa.zero[4] = {g.scan2_status, scan2_status_words(P)};             // the forward scans' look-back words
     pa.P = in.P; pa.D = in.D; pa.M = in.M; pa.W = in.width; pa.H = in.height; pa.gx = d.gx; pa.gy = d.gy;
     pa.means3D = in.means3D; pa.scales = in.scales; pa.scale_modifier = in.scale_modifier; pa.rotations = in.rotations;
@@ -535,8 +548,16 @@ int forward_impl(const ForwardIn& in)
 
     // depth order of the Gaussians (stable: ties keep index order)
     uint32_t* const err_dev = g.counters + 3;  // every decoupled look-back of the forward reports a give-up here
-    int which; { StageScope st_(ST_DEPTH_SORT, s); which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr, nullptr, 0, DEPTH_SORT_PASSES, s, true, err_dev); }
-    g.order = which ? g.val_b : g.val_a;
+    {
+        StageScope st_(ST_DEPTH_SORT, s);
+        if (depth_sort_bytes_forced()) {  // A/B: the 4 x 8-bit radix sort over all 32 key bits
+            const int which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr,
+                                               nullptr, 0, DEPTH_SORT_PASSES, s, true, err_dev);
+            g.order = which ? g.val_b : g.val_a;
+        } else {
+            depth_sort(g.key_a, g.key_b, g.val_a, g.val_b, g.order, g.hist, g.scan_partials, P, s, err_dev);
+        }
+    }
     { StageScope st_(ST_SCAN, s); launch_forward_scans(g.tiles_touched, rows_path ? g.rect : nullptr, g.order, g.offsets, g.row_first, g.row_offsets, g.drect, g.desc_r, g.huge_list, g.counters + 2, g.scan2_status, g.counters, err_dev, P, s); }
 
     // num_rendered = offsets[P-1] (+ the prefiltered error flag) to pinned host memory, without waiting for it:

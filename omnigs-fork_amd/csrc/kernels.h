@@ -75,6 +75,16 @@ int radix_sort_pairs(K* key_a, K* key_b, uint32_t* val_a, uint32_t* val_b, uint3
                      bool scratch_zeroed = false, uint32_t* err = nullptr);
 // the words of `hist` a sort of n items over `passes` passes needs zeroed before it starts (possibly none)
 ZeroSpan radix_zero_span(uint32_t* hist, size_t n, int passes);
+// The depth sort (sort.hip, DepthPass): stable sort of the n Gaussians' depth keys (float bits; culled = 0xFFFFFFFF)
+// over the bits the visible keys span, 9-bit digits, 3 passes for spans below 2^26 ulps (4 otherwise); the
+// permutation of the visible Gaussians, ties in index order, then the culled ones, lands in `order` (key_a / val_a:
+// the keys and 0..n-1 on entry; key_b / val_b: scratch). hist: depth_sort_scratch_words(n) words, of which
+// depth_sort_zero_span(hist, n) zeroed before the call; scan_partials: depth_sort_partials_words(n) words.
+size_t depth_sort_scratch_words(size_t n);
+size_t depth_sort_partials_words(size_t n);
+ZeroSpan depth_sort_zero_span(uint32_t* hist, size_t n);
+void depth_sort(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* order, uint32_t* hist,
+                uint32_t* scan_partials, size_t n, hipStream_t s, uint32_t* err);
 // one-launch exclusive scan of n u32 (in may equal out) of in[i] & mask; n_dev (device word, may be NULL) = live
 // length <= n; status: scan_status_words(n) words zeroed before the launch; err: the look-back error word (NULL: a
 // private one)

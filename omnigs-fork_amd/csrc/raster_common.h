@@ -108,7 +108,7 @@ struct GeomState {
     uint32_t* counters;       // [0] num_rendered, [1] prefiltered-cull flag, [2] huge_list count, [3] look-back error,
                               // [4] M = row slots of the row binning (sum of rect heights), [5] sh_jac_key of the
                               // inputs when preprocess stored sh_jac (else 0), [6] omr_debug_set_sh_jac's copy of [5]
-    uint32_t* order;          // depth order (points at val_a or val_b after the sort)
+    uint32_t* order;          // [P] depth order: the visible Gaussians by depth key (ties by index), then the culled (depth_sort)
     uint32_t* row_first;      // first gradient row of each Gaussian (index-order exclusive scan, launch_forward_scans)
     float* row_sums;          // backward: [P][GRAD_ROW] each Gaussian's instance rows summed (launch_row_sums)
     float4* conic_op;         // [P] conic + opacity (= splat record slot 1), contiguous for gaussian_bwd's coalesced

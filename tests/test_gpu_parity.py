@@ -233,6 +233,44 @@ def test_views_past_1024_tiles_a_side_take_the_radix_binning(oracle_mt):
     assert omr.rasterizer.debug_counters(g.P, h["geom"])["row_slots"] == 0  # the rows scan did not run
 
 
+def _depths_between(g, lo, hi, seed, levels=None):
+    """Move every Gaussian along its direction to a radius in [lo, hi] (log-uniform, or one of `levels` values)."""
+    rng = np.random.default_rng(seed)
+    d = g.means3D / np.linalg.norm(g.means3D, axis=1, keepdims=True)
+    r = np.exp(rng.uniform(np.log(lo), np.log(hi), g.P)) if levels is None else rng.choice(levels, g.P)
+    g.means3D = (d * r[:, None]).astype(np.float32)
+
+
+@pytest.mark.parametrize("P,W,H,cam_t", [(20000, 256, 128, LON), (20000, 320, 180, PIN)])
+def test_depth_sort_wide_depth_span_runs_the_fourth_pass(P, W, H, cam_t):
+    """depth_sort (sort.hip): 9-bit passes over V = key - (smallest visible key rounded down to 256); three passes
+    cover spans below 2^26 ulps (every BASELINE config), a wider span runs the fourth. Depths 0.3 .. 3000 m span
+    about 2^26.8 ulps: the onesweep path with four passes, forward and backward against the oracle (the point list
+    is the reference's (tile, depth, index) order bit for bit)."""
+    g, cam, dL = make_case(P, W, H, cam_t, 61, view_index=1, spread=2.0)
+    _depths_between(g, 0.3, 3000.0, 62)
+    bits = np.array([1.0, 3000.0], dtype=np.float32).view(np.uint32)
+    assert int(bits[1]) - int(bits[0]) > 2 ** 26  # the visible depths cover at least [1, 3000] m
+    _compare(g, cam, dL)
+
+
+def test_depth_sort_equal_depths_keep_index_order():
+    """Many Gaussians on a few spheres around a camera at the origin: depth keys tie in large runs, which every pass
+    must keep in index order (stable passes; the culled bucket of pass 0 included)."""
+    g, cam, dL = make_case(30000, 256, 128, LON, 63, view_index=0, spread=1.5)
+    _depths_between(g, 0, 0, 64, levels=np.array([2.0, 3.0, 4.0, 0.1], dtype=np.float32))  # 0.1: too close, culled
+    _compare(g, cam, dL)
+
+
+def test_depth_sort_multi_launch_path_four_passes(oracle_mt):
+    """Sorts past 2 M keys take the upsweep / look-back scan / downsweep passes (config E's 5 M: three passes, tested
+    at full size above); 2.2 M Gaussians between 0.3 and 3000 m run all four there. Forward integers bit-exact and
+    the image against the oracle."""
+    g, cam, _ = make_case(2_200_000, 256, 128, LON, 65, view_index=2, spread=0.3)
+    _depths_between(g, 0.3, 3000.0, 66)
+    _compare(g, cam, None, nthreads=oracle_mt)
+
+
 def test_row_binning_reports_its_row_slots():
     """bin.hip's rows pass: M = the sum of the visible Gaussians' rect heights (counters[4])."""
     g, cam, _ = make_case(3000, 512, 256, LON, 53, view_index=1, spread=1.5)
