@@ -363,7 +363,8 @@ __device__ __forceinline__ size_t live_count(size_t n, const uint32_t* count)
 // ulps), and the culled Gaussians' keys (0xFFFFFFFF) only need to end up behind the visible ones: they own no tiles,
 // so nothing downstream depends on their order. So the sort runs 9-bit digits over the bits that vary:
 //   pass 0: all P keys; digit = the low 8 bits of a visible key, bucket 256 for a culled one: the pass also moves the
-//           culled Gaussians behind the visible ones;
+//           culled Gaussians behind the visible ones, straight into their final places [nvis, P) of the result
+//           (every entry of the permutation must be a Gaussian index: the forward scans read all P);
 //   pass p >= 1: the nvis visible keys (the first nvis positions after pass 0) alone; digit p of V = key - sub, where
 //           sub is the smallest visible key rounded down to a multiple of 256 (V keeps the key's low 8 bits):
 //           V's bits [8 + 9 (p - 1), 8 + 9 p). Passes 1 and 2 cover V < 2^26 (any depth span of at most 2^26 ulps,
@@ -620,6 +621,10 @@ __global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const K* keys_
         const uint32_t kk = s_k[j];
         const uint32_t d = digit(kk);
         const uint32_t dst = s_gbase[d] + (j - s_dstart[d]);
+        if (depth && d == DEPTH_CULLED_BUCKET) {  // pass 0: a culled Gaussian's final place, [nvis, n) in index order
+            dp.vals_final[dst] = s_v[j];
+            continue;
+        }
         if (keys_out) keys_out[dst] = (K)kk;  // NULL: the depth sort's last pass (only the permutation is kept)
         vals_out[dst] = s_v[j];
     }
@@ -842,6 +847,10 @@ __global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, 
         const uint32_t kk = s_k[j];
         const uint32_t d = digit(kk);
         const uint32_t dst = s_gbase[d] + (j - s_dstart[d]);
+        if (depth && d == DEPTH_CULLED_BUCKET) {  // pass 0: a culled Gaussian's final place, [nvis, n) in index order
+            dp.vals_final[dst] = s_v[j];
+            continue;
+        }
         if (keys_out) keys_out[dst] = (K)kk;  // NULL: the depth sort's last pass (only the permutation is kept)
         vals_out[dst] = s_v[j];
     }
