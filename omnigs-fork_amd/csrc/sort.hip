@@ -621,7 +621,7 @@ __global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const K* keys_
         const uint32_t kk = s_k[j];
         const uint32_t d = digit(kk);
         const uint32_t dst = s_gbase[d] + (j - s_dstart[d]);
-        if (depth && d == DEPTH_CULLED_BUCKET) {  // pass 0: a culled Gaussian's final place, [nvis, n) in index order
+        if (depth && dp.pass == 0 && d == DEPTH_CULLED_BUCKET) {  // pass 0: a culled Gaussian's final place, [nvis, n) in index order
             dp.vals_final[dst] = s_v[j];
             continue;
         }
@@ -847,7 +847,7 @@ __global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, 
         const uint32_t kk = s_k[j];
         const uint32_t d = digit(kk);
         const uint32_t dst = s_gbase[d] + (j - s_dstart[d]);
-        if (depth && d == DEPTH_CULLED_BUCKET) {  // pass 0: a culled Gaussian's final place, [nvis, n) in index order
+        if (depth && dp.pass == 0 && d == DEPTH_CULLED_BUCKET) {  // pass 0: a culled Gaussian's final place, [nvis, n) in index order
             dp.vals_final[dst] = s_v[j];
             continue;
         }
