@@ -343,9 +343,8 @@ size_t GeomState::carve(char* base, size_t P, GeomState* s, bool rows, bool jac)
     g.key_b = c.take<uint32_t>(P);
     g.val_a = c.take<uint32_t>(P);
     g.val_b = c.take<uint32_t>(P);
-    // the depth sort's scratch (or, under OMR_DEPTH_SORT=bytes, the 4 x 8-bit radix sort's)
-    g.hist = c.take<uint32_t>(std::max(depth_sort_scratch_words(P), radix_scratch_words(P, DEPTH_SORT_PASSES)));
-    g.scan_partials = c.take<uint32_t>(std::max(depth_sort_partials_words(P), radix_partials_words(P)));
+    g.hist = c.take<uint32_t>(depth_sort_scratch_words(P));  // also fits the plain sort (OMR_DEPTH_SORT=bytes)
+    g.scan_partials = c.take<uint32_t>(depth_sort_partials_words(P));
     g.scan2_status = c.take<uint32_t>(scan2_status_words(P));
     g.offsets = c.take<uint32_t>(P);
     g.counters = c.take<uint32_t>(8);
@@ -404,9 +403,8 @@ static bool sort_binning_forced()
     }();
     return forced;
 }
-// OMR_DEPTH_SORT=bytes (read once) sorts the depth keys with the 4 x 8-bit radix sort over all 32 bits instead of
-// depth_sort's 9-bit passes over the bits the visible keys span: an A/B switch (same permutation of the visible
-// Gaussians)
+// OMR_DEPTH_SORT=bytes (read once) sorts the depth keys with the plain 4 x 8-bit radix sort over all P keys in every
+// pass instead of depth_sort's (the culled ones set aside in pass 0): an A/B switch (the same permutation)
 static bool depth_sort_bytes_forced()
 {
     static const bool forced = [] {
@@ -550,7 +548,7 @@ int forward_impl(const ForwardIn& in)
     uint32_t* const err_dev = g.counters + 3;  // every decoupled look-back of the forward reports a give-up here
     {
         StageScope st_(ST_DEPTH_SORT, s);
-        if (depth_sort_bytes_forced()) {  // A/B: the 4 x 8-bit radix sort over all 32 key bits
+        if (depth_sort_bytes_forced()) {  // A/B: the plain 4 x 8-bit radix sort over all P keys
             const int which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr,
                                                nullptr, 0, DEPTH_SORT_PASSES, s, true, err_dev);
             g.order = which ? g.val_b : g.val_a;

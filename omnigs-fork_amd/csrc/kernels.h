@@ -75,11 +75,12 @@ int radix_sort_pairs(K* key_a, K* key_b, uint32_t* val_a, uint32_t* val_b, uint3
                      bool scratch_zeroed = false, uint32_t* err = nullptr);
 // the words of `hist` a sort of n items over `passes` passes needs zeroed before it starts (possibly none)
 ZeroSpan radix_zero_span(uint32_t* hist, size_t n, int passes);
-// The depth sort (sort.hip, DepthPass): stable sort of the n Gaussians' depth keys (float bits; culled = 0xFFFFFFFF)
-// over the bits the visible keys span, 9-bit digits, 3 passes for spans below 2^26 ulps (4 otherwise); the
-// permutation of the visible Gaussians, ties in index order, then the culled ones, lands in `order` (key_a / val_a:
-// the keys and 0..n-1 on entry; key_b / val_b: scratch). hist: depth_sort_scratch_words(n) words, of which
-// depth_sort_zero_span(hist, n) zeroed before the call; scan_partials: depth_sort_partials_words(n) words.
+// The depth sort (sort.hip, DepthPass): stable sort of the n Gaussians' depth keys (float bits of positive depths;
+// culled = 0xFFFFFFFF) in four 8-bit-wide passes, of which the first also moves the culled Gaussians behind the
+// visible ones and the other three sort the visible keys alone; the permutation of the visible Gaussians, ties in
+// index order, then the culled ones in index order, lands in `order` (key_a / val_a: the keys and 0..n-1 on entry;
+// key_b / val_b: scratch). hist: depth_sort_scratch_words(n) words, of which depth_sort_zero_span(hist, n) zeroed
+// before the call; scan_partials: depth_sort_partials_words(n) words.
 size_t depth_sort_scratch_words(size_t n);
 size_t depth_sort_partials_words(size_t n);
 ZeroSpan depth_sort_zero_span(uint32_t* hist, size_t n);

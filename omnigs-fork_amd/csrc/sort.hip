@@ -359,84 +359,51 @@ __device__ __forceinline__ size_t live_count(size_t n, const uint32_t* count)
 }
 
 // ---- the depth sort's digits (depth_sort below) -----------------------------------------------------------------
-// The depth keys are float bits of positive depths, which span far fewer than 32 bits (config C: 1.7 .. 12.3 m, 2^25
-// ulps), and the culled Gaussians' keys (0xFFFFFFFF) only need to end up behind the visible ones: they own no tiles,
-// so nothing downstream depends on their order. So the sort runs 9-bit digits over the bits that vary:
-//   pass 0: all P keys; digit = the low 8 bits of a visible key, bucket 256 for a culled one: the pass also moves the
-//           culled Gaussians behind the visible ones, straight into their final places [nvis, P) of the result
-//           (every entry of the permutation must be a Gaussian index: the forward scans read all P);
-//   pass p >= 1: the nvis visible keys (the first nvis positions after pass 0) alone; digit p of V = key - sub, where
-//           sub is the smallest visible key rounded down to a multiple of 256 (V keeps the key's low 8 bits):
-//           V's bits [8 + 9 (p - 1), 8 + 9 p). Passes 1 and 2 cover V < 2^26 (any depth span of at most 2^26 ulps,
-//           e.g. 0.2 m to 800 m); a wider span runs pass 3 (V's bits 26..31), which otherwise returns at once.
-// Stable passes over consistent digits of V order the visible keys exactly as the 32-bit key sort does (V is the key
-// minus a constant), ties in index order. The words (DepthWords) are {nvis, max of ~key, max of key, 0} over the
-// visible keys, zeroed before the sort and accumulated by its pass-0 histogram; words[3] stays 0, so binning_count
-// (live_count) reads nvis from them.
-constexpr int DEPTH_RB = 9;                  // digit bits of the depth sort's passes (pass 0 uses 257 of the 512 buckets)
-constexpr uint32_t DEPTH_CULLED_BUCKET = 256;
-__device__ __forceinline__ uint32_t depth_sub(const uint32_t* w) { return (~w[1]) & ~255u; }
-__device__ __forceinline__ int depth_passes(const uint32_t* w)
+// The culled Gaussians' keys (0xFFFFFFFF) only need to end up behind the visible ones: they own no tiles, so nothing
+// downstream depends on their order. The depth keys are float bits of positive depths (bit 31 clear), so 31 bits
+// order the visible ones:
+//   pass 0: all P keys; digit = bits 0..6 of a visible key, bucket 128 for a culled one: the pass moves the culled
+//           Gaussians straight into their final places [nvis, P) of the result (index order) and the visible ones
+//           into [0, nvis); its block 0 publishes nvis = the start of bucket 128 (DepthPass::words[0]);
+//   passes 1..3: the nvis visible keys alone, bits [8p - 1, 8p + 7): 8-bit digits as the plain sort's.
+// At a frustum that culls most of a scene (config E pinhole: 88 %) passes 1..3 move an eighth of the keys.
+// Stable passes order the visible keys exactly as the 32-bit key sort does, ties in index order.
+// words[3] stays 0 (zeroed before the sort), so binning_count (live_count) reads nvis from the words.
+constexpr uint32_t DEPTH_CULLED_BUCKET = 128;
+constexpr int DEPTH_PASSES = 4;
+__device__ __forceinline__ uint32_t depth_digit(uint32_t k, int pass)
 {
-    const uint32_t r = w[0] ? w[2] - depth_sub(w) : 0u;  // the largest V
-    return r < (1u << 26) ? 3 : 4;
+    if (pass == 0) return k == 0xFFFFFFFFu ? DEPTH_CULLED_BUCKET : (k & 127u);
+    return (k >> (8 * pass - 1)) & (RADIX - 1u);
 }
-__device__ __forceinline__ uint32_t depth_digit(uint32_t k, int pass, uint32_t sub)
-{
-    if (pass == 0) return k == 0xFFFFFFFFu ? DEPTH_CULLED_BUCKET : (k & 255u);
-    return ((k - sub) >> (8 + DEPTH_RB * (pass - 1))) & ((1u << DEPTH_RB) - 1u);
-}
-// one launch of a depth-sort pass: the pass index, the words, where the result goes when this pass is the last
-// (vals_final; keys are not written then), and, for pass 0, the digit totals of passes 1..3 it accumulates
+// one launch of a depth-sort pass: the pass index, the words, and where the permutation goes (the last pass writes
+// only it, no keys; pass 0 the culled Gaussians' entries)
 struct DepthPass {
-    int pass = -1;  // < 0: a plain LSD pass (digit = bits [shift, shift + RB) of the key)
+    int pass = -1;  // < 0: a plain LSD pass (digit = bits [shift, shift + 8) of the key)
     uint32_t* words = nullptr;
     uint32_t* vals_final = nullptr;
-    uint32_t* ghist_next = nullptr;  // onesweep pass 0: digit totals [3][512] of passes 1..3 (zeroed before)
 };
-// Routing of a depth pass: pass 2 writes the result when 3 passes suffice, pass 3 otherwise (and is skipped when
-// they do). Returns false when this pass has nothing to do.
-__device__ __forceinline__ bool depth_route(const DepthPass& dp, uint32_t*& keys_out, uint32_t*& vals_out)
-{
-    const int np = depth_passes(dp.words);
-    if (dp.pass >= np) return false;
-    if (dp.pass == np - 1) {
-        keys_out = nullptr;
-        vals_out = dp.vals_final;
-    }
-    return true;
-}
-template <typename K>
-__device__ __forceinline__ bool depth_route(const DepthPass&, K*&, uint32_t*&)
-{
-    return true;  // 16-bit keys never take the depth passes
-}
 
 // BLOCK_MAJOR: hist[block][digit] (read back by the self-scanning downsweep of small sorts); else hist[digit][block].
 // Key arrays are 16-B aligned (Carver) for the 16-B loads.
-// dp (depth sort, RB = DEPTH_RB): the pass's digits and routing (DepthPass); pass 0 also accumulates the depth words
-// (nvis, max ~key, max key over the visible keys) into dp.words, which later passes read.
-template <typename K, bool BLOCK_MAJOR, int ITEMS, int THREADS, int RB = RADIX_BITS>
+// DEPTH: a depth-sort pass (dp: DepthPass); its digits
+template <typename K, bool BLOCK_MAJOR, int ITEMS, int THREADS, bool DEPTH = false>
 __global__ __launch_bounds__(THREADS) void radix_upsweep_kernel(const K* keys, size_t n_cap,
                                                                      const uint32_t* count, int shift, uint32_t* hist,
                                                                      uint32_t nblocks, uint32_t* zero, uint32_t nzero,
                                                                      DepthPass dp = {})
 {
     constexpr int TILE_N = THREADS * ITEMS;
-    constexpr uint32_t NR = 1u << RB;
+    constexpr uint32_t NR = RADIX;
     {   // the look-back words of the histogram scan that follows (scan_lookback_kernel)
         const uint32_t z = blockIdx.x * THREADS + threadIdx.x;
         if (z < nzero) zero[z] = 0u;
     }
-    const bool depth = RB == DEPTH_RB && dp.pass >= 0;  // compile-time false for the 8-bit sorts
-    if (depth && dp.pass >= depth_passes(dp.words)) return;  // a depth pass the key span does not need
-    const uint32_t sub = depth && dp.pass > 0 ? depth_sub(dp.words) : 0u;
+    constexpr bool depth = DEPTH;
     const size_t n = live_count(n_cap, count);
     static_assert(THREADS % NR == 0, "thread = digit phases");
     __shared__ uint32_t s_hist[NR];
-    __shared__ uint32_t s_dw[3];
     if (threadIdx.x < NR) s_hist[threadIdx.x] = 0;
-    if (threadIdx.x < 3) s_dw[threadIdx.x] = 0;
     __syncthreads();
     const size_t base = (size_t)blockIdx.x * TILE_N;
     // 16-B loads (4 per thread, each wave instruction one contiguous KiB), one LDS atomic per key (one add per
@@ -466,38 +433,17 @@ __global__ __launch_bounds__(THREADS) void radix_upsweep_kernel(const K* keys, s
             for (int j = 0; j < KPL; ++j) kv[KPL * k + j] = i + j < n ? (uint32_t)keys[i + j] : 0u;
         }
     }
-    uint32_t vis = 0, kmax = 0, nkmin = 0;  // depth pass 0: this thread's visible keys
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
         const size_t i = base + KPL * ((size_t)(j / KPL) * THREADS + threadIdx.x) + (j % KPL);
         const bool valid = i < n;
-        const uint32_t d = depth ? depth_digit(kv[j], dp.pass, sub) : (kv[j] >> shift) & (NR - 1);
+        const uint32_t d = depth ? depth_digit(kv[j], dp.pass) : (kv[j] >> shift) & (NR - 1);
         if (valid) atomicAdd(&s_hist[d], 1u);
-        if (depth && dp.pass == 0 && valid && kv[j] != 0xFFFFFFFFu) {
-            ++vis;
-            kmax = max(kmax, kv[j]);
-            nkmin = max(nkmin, ~kv[j]);
-        }
-    }
-    if (depth && dp.pass == 0) {
-        vis = wave_incl_sum_u32(vis);
-        kmax = wave_incl_max_u32(kmax);
-        nkmin = wave_incl_max_u32(nkmin);
-        if ((threadIdx.x & 63u) == 63u && vis) {
-            atomicAdd(&s_dw[0], vis);
-            atomicMax(&s_dw[1], nkmin);
-            atomicMax(&s_dw[2], kmax);
-        }
     }
     __syncthreads();
     if (threadIdx.x < NR) {
         if (BLOCK_MAJOR) hist[(size_t)blockIdx.x * NR + threadIdx.x] = s_hist[threadIdx.x];
         else hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = s_hist[threadIdx.x];
-    }
-    if (depth && dp.pass == 0 && threadIdx.x == 0 && s_dw[0]) {
-        atomicAdd(&dp.words[0], s_dw[0]);
-        atomicMax(&dp.words[1], s_dw[1]);
-        atomicMax(&dp.words[2], s_dw[2]);
     }
 }
 
@@ -510,7 +456,7 @@ __global__ __launch_bounds__(THREADS) void radix_upsweep_kernel(const K* keys, s
 // SELF_SCAN (small sorts, few blocks): hist is the raw block-major histogram and each block derives its global
 // digit offsets itself (column prefix over the blocks before it + scan of the digit totals), which saves the
 // three scan launches per pass; else hist is the scanned [digit][block] histogram.
-template <typename K, bool SELF_SCAN, int ITEMS, int THREADS, int RB = RADIX_BITS>
+template <typename K, bool SELF_SCAN, int ITEMS, int THREADS, bool DEPTH = false>
 __global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const K* keys_in, const uint32_t* vals_in,
                                                                        K* keys_out, uint32_t* vals_out,
                                                                        size_t n_cap, const uint32_t* count, char* canon,
@@ -521,17 +467,19 @@ __global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const K* keys_
     constexpr int WAVES = THREADS / 64;
     constexpr int PER_WAVE = TILE_N / WAVES;
     constexpr int ROUNDS = PER_WAVE / 64;
-    constexpr uint32_t NR = 1u << RB;
+    constexpr uint32_t NR = RADIX;
     __shared__ uint32_t s_whist[WAVES][NR];  // running digit counts per wave, then per-wave digit offsets
     __shared__ uint32_t s_dstart[NR];        // block-local start of each digit's run
     __shared__ uint32_t s_gbase[NR];         // global start of this block's run of each digit
     __shared__ uint32_t s_wave[THREADS / 64];
     __shared__ __attribute__((aligned(16))) K s_k[TILE_N];  // first the rank's peer tables (u64), when they fit
     __shared__ uint32_t s_v[TILE_N];
-    const bool depth = RB == DEPTH_RB && dp.pass >= 0;  // compile-time false for the 8-bit sorts
-    if (depth && !depth_route(dp, keys_out, vals_out)) return;  // block-uniform
-    const uint32_t sub = depth && dp.pass > 0 ? depth_sub(dp.words) : 0u;
-    auto digit = [&](uint32_t kk) { return depth ? depth_digit(kk, dp.pass, sub) : (kk >> shift) & (NR - 1); };
+    constexpr bool depth = DEPTH;
+    if (depth && dp.pass == DEPTH_PASSES - 1) {  // the depth sort's last pass keeps only the permutation
+        keys_out = nullptr;
+        vals_out = dp.vals_final;
+    }
+    auto digit = [&](uint32_t kk) { return depth ? depth_digit(kk, dp.pass) : (kk >> shift) & (NR - 1); };
     const size_t n = live_count(n_cap, count);
     if (canon) vals_out = reinterpret_cast<uint32_t*>(canon + canonical_list_offset(n));
     const uint32_t tid = threadIdx.x;
@@ -565,6 +513,8 @@ __global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const K* keys_
         if (dig) s_gbase[tid] = before + ex;
     } else if (dig) {
         s_gbase[tid] = hist_scanned[(size_t)tid * nblocks + blockIdx.x];
+        // depth pass 0: block 0's start of the culled bucket = the number of visible keys, for passes 1..3
+        if (depth && dp.pass == 0 && blockIdx.x == 0 && tid == DEPTH_CULLED_BUCKET) dp.words[0] = s_gbase[tid];
     }
     const size_t base = tile0 + (size_t)w * PER_WAVE + lane;
     uint32_t k[ROUNDS], v[ROUNDS], lr[ROUNDS];
@@ -588,7 +538,7 @@ __global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const K* keys_
     for (int r = 0; r < ROUNDS; ++r) {
         const bool valid = base + 64 * r < n;
         const uint32_t d = digit(k[r]);
-        rank_round(r, valid, d, wave_match_digit<RB>(d, valid));
+        rank_round(r, valid, d, wave_match_digit<RADIX_BITS>(d, valid));
     }
     __syncthreads();
     {   // thread = digit: per-wave exclusive offsets, then the block-wide exclusive scan of the digit totals
@@ -625,7 +575,7 @@ __global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const K* keys_
             dp.vals_final[dst] = s_v[j];
             continue;
         }
-        if (keys_out) keys_out[dst] = (K)kk;  // NULL: the depth sort's last pass (only the permutation is kept)
+        if (!depth || keys_out) keys_out[dst] = (K)kk;  // NULL: the depth sort's last pass (only the permutation is kept)
         vals_out[dst] = s_v[j];
     }
 }
@@ -719,8 +669,8 @@ __device__ __forceinline__ uint32_t lb_load(const uint32_t* p)
 }
 
 // one pass: status = this pass's [blocks][RADIX] words (zeroed), ghist = its digit totals, ticket = its tile counter;
-// dp: a depth-sort pass (RB = DEPTH_RB; DepthPass)
-template <typename K, int TILE_N, int RB = RADIX_BITS>
+// DEPTH: a depth-sort pass (dp: DepthPass)
+template <typename K, int TILE_N, bool DEPTH = false>
 __global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, const uint32_t* vals_in,
                                                                 K* keys_out, uint32_t* vals_out, size_t n_cap,
                                                                 const uint32_t* count, char* canon, int shift,
@@ -730,7 +680,7 @@ __global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, 
     constexpr int WAVES = OS_THREADS / 64;
     constexpr int PER_WAVE = TILE_N / WAVES;
     constexpr int ROUNDS = PER_WAVE / 64;
-    constexpr uint32_t NR = 1u << RB;
+    constexpr uint32_t NR = RADIX;
     __shared__ uint32_t s_whist[WAVES][NR];  // running digit counts per wave, then per-wave digit offsets
     __shared__ uint32_t s_dstart[NR];        // block-local start of each digit's run
     __shared__ uint32_t s_gbase[NR];         // global start of this block's run of each digit
@@ -738,10 +688,12 @@ __global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, 
     __shared__ __attribute__((aligned(16))) K s_k[TILE_N];  // first the rank's peer tables (u64), when they fit
     __shared__ uint32_t s_v[TILE_N];
     __shared__ uint32_t s_vb;
-    const bool depth = RB == DEPTH_RB && dp.pass >= 0;  // compile-time false for the 8-bit sorts
-    if (depth && !depth_route(dp, keys_out, vals_out)) return;  // every block of a pass the key span does not need
-    const uint32_t sub = depth ? depth_sub(dp.words) : 0u;
-    auto digit = [&](uint32_t kk) { return depth ? depth_digit(kk, dp.pass, sub) : (kk >> shift) & (NR - 1); };
+    constexpr bool depth = DEPTH;
+    if (depth && dp.pass == DEPTH_PASSES - 1) {  // the depth sort's last pass keeps only the permutation
+        keys_out = nullptr;
+        vals_out = dp.vals_final;
+    }
+    auto digit = [&](uint32_t kk) { return depth ? depth_digit(kk, dp.pass) : (kk >> shift) & (NR - 1); };
     const uint32_t tid = threadIdx.x;
     if (tid == 0) s_vb = atomicAdd(ticket, 1u);
     const size_t n = live_count(n_cap, count);
@@ -756,6 +708,8 @@ __global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, 
     if (tile0 >= n) return;  // block-uniform; no block looks back at a tile past the live count
     uint32_t total_unused;
     const uint32_t gstart = block_exclusive_scan<OS_THREADS>(dig ? ghist[tid] : 0u, s_wave, &total_unused);
+    // depth pass 0: the start of the culled bucket = the number of visible keys, for passes 1..3
+    if (depth && dp.pass == 0 && vb == 0 && tid == DEPTH_CULLED_BUCKET) dp.words[0] = gstart;
     const size_t base = tile0 + (size_t)w * PER_WAVE + lane;
     uint32_t k[ROUNDS], v[ROUNDS], lr[ROUNDS];
 #pragma unroll
@@ -776,7 +730,7 @@ __global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, 
     for (int r = 0; r < ROUNDS; ++r) {
         const bool valid = base + 64 * r < n;
         const uint32_t d = digit(k[r]);
-        rank_round(r, valid, d, wave_match_digit<RB>(d, valid));
+        rank_round(r, valid, d, wave_match_digit<RADIX_BITS>(d, valid));
     }
     __syncthreads();
     {   // thread = digit: per-wave exclusive offsets, block-local digit starts, then the look-back
@@ -851,72 +805,32 @@ __global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, 
             dp.vals_final[dst] = s_v[j];
             continue;
         }
-        if (keys_out) keys_out[dst] = (K)kk;  // NULL: the depth sort's last pass (only the permutation is kept)
+        if (!depth || keys_out) keys_out[dst] = (K)kk;  // NULL: the depth sort's last pass (only the permutation is kept)
         vals_out[dst] = s_v[j];
-    }
-    if (depth && dp.pass == 0) {
-        // the digit totals of passes 1..3 (their digits depend on the smallest visible key, known only since the
-        // histogram launch): the tile's visible keys are still in registers; s_k is free again after the barrier
-        static_assert(TILE_N * sizeof(K) >= 3 * NR * sizeof(uint32_t), "pass totals fit the key staging array");
-        uint32_t* s_h3 = reinterpret_cast<uint32_t*>(s_k);
-        __syncthreads();
-        for (uint32_t i = tid; i < 3 * NR; i += OS_THREADS) s_h3[i] = 0;
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < ROUNDS; ++r) {
-            if (base + 64 * r < n && k[r] != 0xFFFFFFFFu) {
-#pragma unroll
-                for (int q = 1; q <= 3; ++q) atomicAdd(&s_h3[(q - 1) * NR + depth_digit(k[r], q, sub)], 1u);
-            }
-        }
-        __syncthreads();
-        for (uint32_t i = tid; i < 3 * NR; i += OS_THREADS)
-            if (s_h3[i]) atomicAdd(&dp.ghist_next[i], s_h3[i]);
     }
 }
 
-// the depth sort's histogram launch (onesweep path): pass 0's digit totals over all keys, the depth words (nvis, max
-// ~key, max key over the visible keys; DepthPass) and the zeroed look-back status words of every pass
-template <int RB>
+// the depth sort's histogram launch (onesweep path): the digit totals of all four passes from one read of the keys
+// (pass 0 over every key, passes 1..3 over the visible ones) and the zeroed look-back status words of every pass
 __global__ __launch_bounds__(OS_HIST_THREADS) void depth_hist_kernel(const uint32_t* keys, size_t n, uint32_t* status,
-                                                                     size_t status_words, uint32_t* ghist,
-                                                                     uint32_t* words)
+                                                                     size_t status_words, uint32_t* ghist)
 {
-    constexpr uint32_t NR = 1u << RB;
-    __shared__ uint32_t s_h[NR];
-    __shared__ uint32_t s_dw[3];
+    __shared__ uint32_t s_h[DEPTH_PASSES][RADIX];
     const uint32_t tid = threadIdx.x;
     const size_t stride = (size_t)gridDim.x * OS_HIST_THREADS;
     for (size_t i = (size_t)blockIdx.x * OS_HIST_THREADS + tid; i < status_words; i += stride) status[i] = 0;
-    for (uint32_t i = tid; i < NR; i += OS_HIST_THREADS) s_h[i] = 0;
-    if (tid < 3) s_dw[tid] = 0;
+    for (uint32_t i = tid; i < DEPTH_PASSES * RADIX; i += OS_HIST_THREADS) (&s_h[0][0])[i] = 0;
     __syncthreads();
-    uint32_t vis = 0, kmax = 0, nkmin = 0;
     for (size_t i = (size_t)blockIdx.x * OS_HIST_THREADS + tid; i < n; i += stride) {
         const uint32_t key = keys[i];
-        atomicAdd(&s_h[depth_digit(key, 0, 0u)], 1u);
-        if (key != 0xFFFFFFFFu) {
-            ++vis;
-            kmax = max(kmax, key);
-            nkmin = max(nkmin, ~key);
-        }
-    }
-    vis = wave_incl_sum_u32(vis);
-    kmax = wave_incl_max_u32(kmax);
-    nkmin = wave_incl_max_u32(nkmin);
-    if ((tid & 63u) == 63u && vis) {
-        atomicAdd(&s_dw[0], vis);
-        atomicMax(&s_dw[1], nkmin);
-        atomicMax(&s_dw[2], kmax);
+        atomicAdd(&s_h[0][depth_digit(key, 0)], 1u);
+        if (key != 0xFFFFFFFFu)
+            for (int p = 1; p < DEPTH_PASSES; ++p) atomicAdd(&s_h[p][depth_digit(key, p)], 1u);
     }
     __syncthreads();
-    for (uint32_t i = tid; i < NR; i += OS_HIST_THREADS)
-        if (s_h[i]) atomicAdd(&ghist[i], s_h[i]);
-    if (tid == 0 && s_dw[0]) {
-        atomicAdd(&words[0], s_dw[0]);
-        atomicMax(&words[1], s_dw[1]);
-        atomicMax(&words[2], s_dw[2]);
-    }
+    if (tid < RADIX)
+        for (int p = 0; p < DEPTH_PASSES; ++p)
+            if (s_h[p][tid]) atomicAdd(&ghist[p * RADIX + tid], s_h[p][tid]);
 }
 
 // ---- instances -------------------------------------------------------------------------------------------
@@ -1446,29 +1360,23 @@ int radix_sort_pairs(K* key_a, K* key_b, uint32_t* val_a, uint32_t* val_b, uint3
     return cur;
 }
 
-// ---- the depth sort (DepthPass above): a 9-bit onesweep or upsweep / scan / downsweep per pass --------------------
-// scratch (hist): onesweep: status [4][nb][512] | digit totals [4][512] | tickets [4] | depth words [4];
-//                 otherwise: [512][nb] histogram | depth words [4]
-constexpr uint32_t DEPTH_NR = 1u << DEPTH_RB;
-constexpr int DEPTH_PASSES_MAX = 4;
-static size_t depth_nb(size_t n) { return use_onesweep(n) ? div_up(n, os_tile(n)) : div_up(n, SORT_TILE); }
-size_t depth_sort_scratch_words(size_t n)
+// ---- the depth sort (DepthPass above): four onesweep passes, or upsweep / scan / downsweep per pass -----------------
+// scratch (hist): the plain sort's over four passes (radix_scratch_words), then the depth words [4]
+static size_t depth_words_at(size_t n)
 {
-    const size_t nb = depth_nb(n);
-    if (use_onesweep(n)) return (size_t)DEPTH_PASSES_MAX * (nb + 1) * DEPTH_NR + DEPTH_PASSES_MAX + 4;
-    return (size_t)DEPTH_NR * nb + 4;
+    return use_onesweep(n) ? onesweep_words(n, DEPTH_PASSES) : radix_hist_size(n);
 }
-size_t depth_sort_partials_words(size_t n) { return 2 * scan_partials_size((size_t)DEPTH_NR * div_up(n, SORT_TILE)) + 2; }
+size_t depth_sort_scratch_words(size_t n) { return radix_scratch_words(n, DEPTH_PASSES) + 4; }
+size_t depth_sort_partials_words(size_t n) { return radix_partials_words(n); }
 ZeroSpan depth_sort_zero_span(uint32_t* hist, size_t n)
 {
     ZeroSpan z;
     if (n == 0) return z;
-    const size_t nb = depth_nb(n);
-    if (use_onesweep(n)) {
-        z.p = hist + (size_t)DEPTH_PASSES_MAX * nb * DEPTH_NR;
-        z.n = (size_t)DEPTH_PASSES_MAX * (DEPTH_NR + 1) + 4;
+    if (use_onesweep(n)) {  // digit totals, tickets, error word (radix_zero_span), then the words, contiguous
+        z = radix_zero_span(hist, n, DEPTH_PASSES);
+        z.n += 4;
     } else {
-        z.p = hist + (size_t)DEPTH_NR * nb;
+        z.p = hist + depth_words_at(n);
         z.n = 4;
     }
     return z;
@@ -1478,46 +1386,45 @@ void depth_sort(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val
                 uint32_t* scan_partials, size_t n, hipStream_t s, uint32_t* err)
 {
     if (n == 0) return;
-    const uint32_t nb = (uint32_t)depth_nb(n);
+    uint32_t* words = hist + depth_words_at(n);
     uint32_t *ki = key_a, *ko = key_b, *vi = val_a, *vo = val_b;
     if (use_onesweep(n)) {
+        const uint32_t nb = div_up(n, os_tile(n));
         uint32_t* status = hist;
-        uint32_t* ghist = hist + (size_t)DEPTH_PASSES_MAX * nb * DEPTH_NR;
-        uint32_t* tickets = ghist + (size_t)DEPTH_PASSES_MAX * DEPTH_NR;
-        uint32_t* words = tickets + DEPTH_PASSES_MAX;
-        depth_hist_kernel<DEPTH_RB><<<std::min(div_up(n, OS_HIST_THREADS), OS_HIST_BLOCKS), OS_HIST_THREADS, 0, s>>>(
-            key_a, n, status, (size_t)DEPTH_PASSES_MAX * nb * DEPTH_NR, ghist, words);
-        for (int p = 0; p < DEPTH_PASSES_MAX; ++p) {
+        uint32_t* ghist = hist + (size_t)DEPTH_PASSES * nb * RADIX;
+        uint32_t* tickets = ghist + (size_t)DEPTH_PASSES * RADIX;
+        depth_hist_kernel<<<std::min(div_up(n, OS_HIST_THREADS), OS_HIST_BLOCKS), OS_HIST_THREADS, 0, s>>>(
+            key_a, n, status, (size_t)DEPTH_PASSES * nb * RADIX, ghist);
+        for (int p = 0; p < DEPTH_PASSES; ++p) {
             DepthPass dp;
             dp.pass = p;
             dp.words = words;
             dp.vals_final = order;
-            dp.ghist_next = ghist + DEPTH_NR;
-            auto kern = os_tile(n) == OS_TILE ? onesweep_kernel<uint32_t, OS_TILE, DEPTH_RB>
-                                              : onesweep_kernel<uint32_t, OS_TILE_SMALL, DEPTH_RB>;
+            auto kern = os_tile(n) == OS_TILE ? onesweep_kernel<uint32_t, OS_TILE, true>
+                                              : onesweep_kernel<uint32_t, OS_TILE_SMALL, true>;
             kern<<<nb, OS_THREADS, 0, s>>>(ki, vi, ko, vo, n, p == 0 ? nullptr : words, nullptr, 0,
-                                            status + (size_t)p * nb * DEPTH_NR, ghist + (size_t)p * DEPTH_NR,
-                                            tickets + p, err, dp);
+                                            status + (size_t)p * nb * RADIX, ghist + (size_t)p * RADIX, tickets + p,
+                                            err, dp);
             std::swap(ki, ko);
             std::swap(vi, vo);
         }
         return;
     }
-    uint32_t* words = hist + (size_t)DEPTH_NR * nb;
-    const uint32_t nbs = div_up((size_t)DEPTH_NR * nb, SCAN_TILE);
+    const uint32_t nb = div_up(n, SORT_TILE);
+    const uint32_t nbs = div_up((size_t)RADIX * nb, SCAN_TILE);
     uint64_t* lb = reinterpret_cast<uint64_t*>(scan_partials);
     uint32_t* lb_ticket = scan_partials + 2 * (size_t)nbs;
-    for (int p = 0; p < DEPTH_PASSES_MAX; ++p) {
+    for (int p = 0; p < DEPTH_PASSES; ++p) {
         DepthPass dp;
         dp.pass = p;
         dp.words = words;
         dp.vals_final = order;
         const uint32_t* count = p == 0 ? nullptr : words;
-        radix_upsweep_kernel<uint32_t, false, SORT_ITEMS_S, SORT_THREADS_S, DEPTH_RB><<<nb, SORT_THREADS_S, 0, s>>>(
+        radix_upsweep_kernel<uint32_t, false, SORT_ITEMS_S, SORT_THREADS_S, true><<<nb, SORT_THREADS_S, 0, s>>>(
             ki, n, count, 0, hist, nb, scan_partials, 2 * nbs + 2, dp);
         scan_lookback_kernel<<<std::min(nbs, SCAN_GRID_MAX), SCAN_THREADS, 0, s>>>(
-            hist, hist, (size_t)DEPTH_NR * nb, nullptr, lb, lb_ticket, err ? err : lb_ticket + 1);
-        radix_downsweep_kernel<uint32_t, false, SORT_ITEMS_S, SORT_THREADS_S, DEPTH_RB><<<nb, SORT_THREADS_S, 0, s>>>(
+            hist, hist, (size_t)RADIX * nb, nullptr, lb, lb_ticket, err ? err : lb_ticket + 1);
+        radix_downsweep_kernel<uint32_t, false, SORT_ITEMS_S, SORT_THREADS_S, true><<<nb, SORT_THREADS_S, 0, s>>>(
             ki, vi, ko, vo, n, count, nullptr, 0, hist, nb, dp);
         std::swap(ki, ko);
         std::swap(vi, vo);
