@@ -242,15 +242,13 @@ def _depths_between(g, lo, hi, seed, levels=None):
 
 
 @pytest.mark.parametrize("P,W,H,cam_t", [(20000, 256, 128, LON), (20000, 320, 180, PIN)])
-def test_depth_sort_wide_depth_span_runs_the_fourth_pass(P, W, H, cam_t):
-    """depth_sort (sort.hip): 9-bit passes over V = key - (smallest visible key rounded down to 256); three passes
-    cover spans below 2^26 ulps (every BASELINE config), a wider span runs the fourth. Depths 0.3 .. 3000 m span
-    about 2^26.8 ulps: the onesweep path with four passes, forward and backward against the oracle (the point list
-    is the reference's (tile, depth, index) order bit for bit)."""
+def test_depth_sort_wide_depth_span(P, W, H, cam_t):
+    """depth_sort (sort.hip): pass 0 sorts bits 0..6 and sets the culled Gaussians aside (bucket 128, straight to
+    their final places behind the visible ones), passes 1..3 sort bits 7..30 of the visible keys alone. Depths 0.1 ..
+    3000 m make every one of those bits vary and cull the closest (lonlat: r <= 0.2; pinhole: z <= 0.2), forward and
+    backward against the oracle (the point list is the reference's (tile, depth, index) order bit for bit)."""
     g, cam, dL = make_case(P, W, H, cam_t, 61, view_index=1, spread=2.0)
-    _depths_between(g, 0.3, 3000.0, 62)
-    bits = np.array([1.0, 3000.0], dtype=np.float32).view(np.uint32)
-    assert int(bits[1]) - int(bits[0]) > 2 ** 26  # the visible depths cover at least [1, 3000] m
+    _depths_between(g, 0.1, 3000.0, 62)
     _compare(g, cam, dL)
 
 
@@ -262,12 +260,13 @@ def test_depth_sort_equal_depths_keep_index_order():
     _compare(g, cam, dL)
 
 
-def test_depth_sort_multi_launch_path_four_passes(oracle_mt):
-    """Sorts past 2 M keys take the upsweep / look-back scan / downsweep passes (config E's 5 M: three passes, tested
-    at full size above); 2.2 M Gaussians between 0.3 and 3000 m run all four there. Forward integers bit-exact and
-    the image against the oracle."""
+def test_depth_sort_multi_launch_path_with_culled_gaussians(oracle_mt):
+    """Sorts past 2 M keys take the upsweep / look-back scan / downsweep passes (config E's 5 M at full size above);
+    here 2.2 M Gaussians between 0.1 and 3000 m, some culled (too close): pass 0's downsweep publishes the visible
+    count and passes 1..3 run over the visible keys only. Forward integers bit-exact and the image against the
+    oracle."""
     g, cam, _ = make_case(2_200_000, 256, 128, LON, 65, view_index=2, spread=0.3)
-    _depths_between(g, 0.3, 3000.0, 66)
+    _depths_between(g, 0.1, 3000.0, 66)
     _compare(g, cam, None, nthreads=oracle_mt)
 
 
