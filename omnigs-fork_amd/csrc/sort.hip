@@ -364,7 +364,8 @@ __device__ __forceinline__ size_t live_count(size_t n, const uint32_t* count)
 // order the visible ones:
 //   pass 0: all P keys; digit = bits 0..6 of a visible key, bucket 128 for a culled one: the pass moves the culled
 //           Gaussians straight into their final places [nvis, P) of the result (index order) and the visible ones
-//           into [0, nvis); its block 0 publishes nvis = the start of bucket 128 (DepthPass::words[0]);
+//           into [0, nvis); passes 1..3 take nvis from their digit totals (onesweep) or from DepthPass::words[0],
+//           which block 0 of pass 0's downsweep sets to the start of bucket 128 (upsweep / scan / downsweep);
 //   passes 1..3: the nvis visible keys alone, bits [8p - 1, 8p + 7): 8-bit digits as the plain sort's.
 // At a frustum that culls most of a scene (config E pinhole: 88 %) passes 1..3 move an eighth of the keys.
 // Stable passes order the visible keys exactly as the 32-bit key sort does, ties in index order.
@@ -696,20 +697,20 @@ __global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, 
     auto digit = [&](uint32_t kk) { return depth ? depth_digit(kk, dp.pass) : (kk >> shift) & (NR - 1); };
     const uint32_t tid = threadIdx.x;
     if (tid == 0) s_vb = atomicAdd(ticket, 1u);
-    const size_t n = live_count(n_cap, count);
-    if (canon) vals_out = reinterpret_cast<uint32_t*>(canon + canonical_list_offset(n));
+    const size_t n_live = live_count(n_cap, count);
+    if (canon) vals_out = reinterpret_cast<uint32_t*>(canon + canonical_list_offset(n_live));
     const uint32_t w = tid >> 6, lane = tid & 63;
     static_assert(OS_THREADS % NR == 0, "thread = digit phases");
     const bool dig = tid < NR;  // this thread also owns digit tid in the per-digit phases
     for (uint32_t i = tid; i < (uint32_t)(WAVES * NR); i += OS_THREADS) (&s_whist[0][0])[i] = 0;
     __syncthreads();
     const uint32_t vb = s_vb;
+    uint32_t total;
+    const uint32_t gstart = block_exclusive_scan<OS_THREADS>(dig ? ghist[tid] : 0u, s_wave, &total);
+    // depth passes 1..3 sort the visible keys alone, which their digit totals count: no count word to wait for
+    const size_t n = depth && dp.pass > 0 ? (size_t)total : n_live;
     const size_t tile0 = (size_t)vb * TILE_N;
     if (tile0 >= n) return;  // block-uniform; no block looks back at a tile past the live count
-    uint32_t total_unused;
-    const uint32_t gstart = block_exclusive_scan<OS_THREADS>(dig ? ghist[tid] : 0u, s_wave, &total_unused);
-    // depth pass 0: the start of the culled bucket = the number of visible keys, for passes 1..3
-    if (depth && dp.pass == 0 && vb == 0 && tid == DEPTH_CULLED_BUCKET) dp.words[0] = gstart;
     const size_t base = tile0 + (size_t)w * PER_WAVE + lane;
     uint32_t k[ROUNDS], v[ROUNDS], lr[ROUNDS];
 #pragma unroll
@@ -1398,11 +1399,10 @@ void depth_sort(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val
         for (int p = 0; p < DEPTH_PASSES; ++p) {
             DepthPass dp;
             dp.pass = p;
-            dp.words = words;
             dp.vals_final = order;
             auto kern = os_tile(n) == OS_TILE ? onesweep_kernel<uint32_t, OS_TILE, true>
                                               : onesweep_kernel<uint32_t, OS_TILE_SMALL, true>;
-            kern<<<nb, OS_THREADS, 0, s>>>(ki, vi, ko, vo, n, p == 0 ? nullptr : words, nullptr, 0,
+            kern<<<nb, OS_THREADS, 0, s>>>(ki, vi, ko, vo, n, nullptr, nullptr, 0,
                                             status + (size_t)p * nb * RADIX, ghist + (size_t)p * RADIX, tickets + p,
                                             err, dp);
             std::swap(ki, ko);
