@@ -268,6 +268,11 @@ int omr_debug_counters(char* geom_buffer, int P, uint32_t* dst, void* stream);
 /* clears (0) or restores (1) the key by which the backward uses the forward's stored dRGB/ddir (GeomState::sh_jac)
  * instead of reading the SH rows: lets a test run both backward paths on one forward */
 int omr_debug_set_sh_jac(char* geom_buffer, int P, int enabled, void* stream);
+/* the forward's depth sort: 0 = by camera type (pinhole: the sort that sets culled Gaussians aside first; lonlat: the
+ * plain 4 x 8-bit radix sort), 1 = always the plain sort, 2 = always the culled-aside sort (the same permutation);
+ * process-wide, for tests and A/B runs (the environment's OMR_DEPTH_SORT=bytes / visible sets the start value).
+ * Returns the previous mode, or -1 for a mode outside 0..2 (omr_last_error says why) */
+int omr_debug_depth_sort_mode(int mode);
 /* per-Gaussian pixel centre [P,2], conic+opacity [P,4], rgb [P,3], depth [P], tiles_touched [P] */
 /* one wave64 through the render backward's gradient reduction: in [64][9] -> out [9] (column sums) */
 int omr_debug_wave_sum9(const float* in, float* out, void* stream); /* wave_sum9_rows */

@@ -403,15 +403,26 @@ static bool sort_binning_forced()
     }();
     return forced;
 }
-// OMR_DEPTH_SORT=bytes (read once) sorts the depth keys with the plain 4 x 8-bit radix sort over all P keys in every
-// pass instead of depth_sort's (the culled ones set aside in pass 0): an A/B switch (the same permutation)
-static bool depth_sort_bytes_forced()
+// The depth sort: pinhole views take depth_sort (sort.hip), whose first pass sets the culled Gaussians aside so the
+// other three sort the visible keys alone (config E pinhole culls 88 %: 0.206 -> 0.137 ms); lonlat views cull only
+// what is too close to the camera, and there the plain 4 x 8-bit radix sort of every key is 2-4 us faster (C 0.0795
+// vs 0.0812 ms, A 0.029 vs 0.033: profiles/r05e_ab_*.txt). The same permutation either way. OMR_DEPTH_SORT (read once)
+// forces one for A/B runs and tests: "bytes" the plain sort, "visible" depth_sort.
+static std::atomic<int>& depth_sort_mode()  // 0: by camera type, 1: plain, 2: depth_sort (omr_debug_depth_sort_mode)
 {
-    static const bool forced = [] {
+    static std::atomic<int> mode{[] {
         const char* v = std::getenv("OMR_DEPTH_SORT");
-        return v && std::strcmp(v, "bytes") == 0;
-    }();
-    return forced;
+        if (v && std::strcmp(v, "bytes") == 0) return 1;
+        if (v && std::strcmp(v, "visible") == 0) return 2;
+        return 0;
+    }()};
+    return mode;
+}
+static int depth_sort_forced() { return depth_sort_mode().load(std::memory_order_relaxed); }
+static bool depth_sort_plain(int camera_type)
+{
+    const int f = depth_sort_forced();
+    return f ? f == 1 : camera_type != CAM_PINHOLE;
 }
 static bool row_binning(uint32_t gx, uint32_t gy)
 {
@@ -528,8 +539,9 @@ int forward_impl(const ForwardIn& in)
     pa.zero[0] = {g.counters + 2, 2};                                  // huge-list count (scan), look-back error word
     pa.zero[1] = {reinterpret_cast<uint32_t*>(im.ranges), 2 * (size_t)d.T};  // tile_ranges writes boundaries only
     pa.zero[2] = {im.tile_cost, (size_t)d.T};                          // render_forward adds into it
-    pa.zero[3] = depth_sort_bytes_forced() ? radix_zero_span(g.hist, P, DEPTH_SORT_PASSES)
-                                           : depth_sort_zero_span(g.hist, P);  // the depth sort's totals / words
+    const bool plain_sort = depth_sort_plain(in.camera_type);
+    pa.zero[3] = plain_sort ? radix_zero_span(g.hist, P, DEPTH_SORT_PASSES)
+                            : depth_sort_zero_span(g.hist, P);  // the depth sort's digit totals / tickets / words
     pa.zero[4] = {g.scan2_status, scan2_status_words(P)};             // the forward scans' look-back words
     pa.P = in.P; pa.D = in.D; pa.M = in.M; pa.W = in.width; pa.H = in.height; pa.gx = d.gx; pa.gy = d.gy;
     pa.means3D = in.means3D; pa.scales = in.scales; pa.scale_modifier = in.scale_modifier; pa.rotations = in.rotations;
@@ -548,7 +560,7 @@ int forward_impl(const ForwardIn& in)
     uint32_t* const err_dev = g.counters + 3;  // every decoupled look-back of the forward reports a give-up here
     {
         StageScope st_(ST_DEPTH_SORT, s);
-        if (depth_sort_bytes_forced()) {  // A/B: the plain 4 x 8-bit radix sort over all P keys
+        if (plain_sort) {  // the plain 4 x 8-bit radix sort over all P keys
             const int which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr,
                                                nullptr, 0, DEPTH_SORT_PASSES, s, true, err_dev);
             g.order = which ? g.val_b : g.val_a;
@@ -1290,6 +1302,16 @@ int omr_debug_counters(char* geom_buffer, int P, uint32_t* dst, void* stream)
     GeomState::carve(geom_buffer, (size_t)std::max(P, 0), &g);
     OMR_HIP(hipMemcpyAsync(dst, g.counters, 8 * sizeof(uint32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
     return OMR_OK;
+}
+
+int omr_debug_depth_sort_mode(int mode)
+{
+    if (mode < 0 || mode > 2) {
+        fail(OMR_ERR_INVALID_ARGUMENT, "depth sort mode: 0 (by camera type), 1, 2");
+        return -1;
+    }
+    const int old = depth_sort_mode().exchange(mode);
+    return old;
 }
 
 int omr_debug_set_sh_jac(char* geom_buffer, int P, int enabled, void* stream)

@@ -73,6 +73,8 @@ def lib() -> C.CDLL:
         L.omr_debug_image_state.argtypes = [vp, i, i, vp, vp, vp]
         L.omr_debug_tile_cost.argtypes = [vp, i, i, vp, vp]
         L.omr_debug_counters.argtypes = [vp, i, vp, vp]
+        L.omr_debug_depth_sort_mode.restype = i
+        L.omr_debug_depth_sort_mode.argtypes = [i]
         L.omr_debug_set_sh_jac.restype = i
         L.omr_debug_set_sh_jac.argtypes = [vp, i, i, vp]
         L.omr_debug_geometry.argtypes = [vp, i, vp, vp, vp, vp, vp, vp]
@@ -555,6 +557,15 @@ def debug_counters(P, geomBuffer) -> dict:
     c = [int(v) & 0xFFFFFFFF for v in out.cpu().tolist()]
     return {"num_rendered": c[0], "prefiltered_flag": c[1], "huge": c[2], "error": c[3], "row_slots": c[4],
             "sh_jac": c[5] != 0, "sh_jac_key": c[5]}
+
+
+def debug_depth_sort_mode(mode: int) -> int:
+    """The forward's depth sort, process-wide (omr_debug_depth_sort_mode): 0 by camera type, 1 the plain 4 x 8-bit
+    radix sort, 2 the sort that sets culled Gaussians aside first. Returns the previous mode."""
+    rc = int(lib().omr_debug_depth_sort_mode(int(mode)))
+    if rc < 0:
+        raise RasterizerError(f"debug_depth_sort_mode({mode}): {lib().omr_last_error().decode()}")
+    return rc
 
 
 def debug_set_sh_jac(P, geomBuffer, enabled: bool):

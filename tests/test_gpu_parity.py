@@ -241,8 +241,16 @@ def _depths_between(g, lo, hi, seed, levels=None):
     g.means3D = (d * r[:, None]).astype(np.float32)
 
 
+@pytest.fixture(params=[1, 2], ids=["plain_sort", "culled_aside_sort"])
+def depth_sort_mode(request):
+    """Both depth sorts (capi.hip: depth_sort_plain; omr_debug_depth_sort_mode) on every camera type."""
+    old = omr.rasterizer.debug_depth_sort_mode(request.param)
+    yield request.param
+    omr.rasterizer.debug_depth_sort_mode(old)
+
+
 @pytest.mark.parametrize("P,W,H,cam_t", [(20000, 256, 128, LON), (20000, 320, 180, PIN)])
-def test_depth_sort_wide_depth_span(P, W, H, cam_t):
+def test_depth_sort_wide_depth_span(P, W, H, cam_t, depth_sort_mode):
     """depth_sort (sort.hip): pass 0 sorts bits 0..6 and sets the culled Gaussians aside (bucket 128, straight to
     their final places behind the visible ones), passes 1..3 sort bits 7..30 of the visible keys alone. Depths 0.1 ..
     3000 m make every one of those bits vary and cull the closest (lonlat: r <= 0.2; pinhole: z <= 0.2), forward and
@@ -252,7 +260,7 @@ def test_depth_sort_wide_depth_span(P, W, H, cam_t):
     _compare(g, cam, dL)
 
 
-def test_depth_sort_equal_depths_keep_index_order():
+def test_depth_sort_equal_depths_keep_index_order(depth_sort_mode):
     """Many Gaussians on a few spheres around a camera at the origin: depth keys tie in large runs, which every pass
     must keep in index order (stable passes; the culled bucket of pass 0 included)."""
     g, cam, dL = make_case(30000, 256, 128, LON, 63, view_index=0, spread=1.5)
@@ -260,7 +268,7 @@ def test_depth_sort_equal_depths_keep_index_order():
     _compare(g, cam, dL)
 
 
-def test_depth_sort_multi_launch_path_with_culled_gaussians(oracle_mt):
+def test_depth_sort_multi_launch_path_with_culled_gaussians(oracle_mt, depth_sort_mode):
     """Sorts past 2 M keys take the upsweep / look-back scan / downsweep passes (config E's 5 M at full size above);
     here 2.2 M Gaussians between 0.1 and 3000 m, some culled (too close): pass 0's downsweep publishes the visible
     count and passes 1..3 run over the visible keys only. Forward integers bit-exact and the image against the
