@@ -170,6 +170,12 @@ int omr_l1_ssim_loss(const float* img, const float* gt, int C, int H, int W, flo
 int omr_adam_step(int P, int Mr, float* const params[6], float* const exp_avg[6], float* const exp_avg_sq[6],
                   const float* const grads[6], int grad_kind, const float lr[6], const int64_t step[6], float beta1,
                   float beta2, float eps, void* stream);
+/* The renderer's activations of the six raw groups in one launch (gaussian_model.cpp:54-77 as
+ * gaussian_renderer.cpp:175-200 applies them): shs = cat(features_dc, features_rest) [P,Mr+1,3] (skipped when shs is
+ * NULL), opacity = sigmoid(params[3]) [P], scales = exp(params[4]) [P,3], rotations = normalize(params[5]) [P,4]
+ * (x / max(||x||_2, 1e-12)); xyz (params[0]) is used as is. params[5], rotations and shs 16-byte aligned. */
+int omr_activate(int P, int Mr, const float* const params[6], float* shs, float* opacity, float* scales,
+                 float* rotations, void* stream);
 /* addDensificationStats (gaussian_model.cpp:839-853) + the max_radii2D update (gaussian_mapper.cpp:427-432) for
  * visibility_filter = radii > 0: accum[i] += |viewspace_grad[i][0:2]|, denom[i] += 1, max_radii2D[i] =
  * max(max_radii2D[i], radii[i]). viewspace_grad is dL_dmeans2D with row stride viewspace_stride (3). */

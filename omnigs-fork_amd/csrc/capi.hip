@@ -988,6 +988,26 @@ int omr_adam_step(int P, int Mr, float* const params[6], float* const exp_avg[6]
     return hip_check("adam_step");
 }
 
+int omr_activate(int P, int Mr, const float* const params[6], float* shs, float* opacity, float* scales,
+                 float* rotations, void* stream)
+{
+    g_last_error.clear();
+    if (P < 0 || Mr < 0 || Mr > 15) return fail(OMR_ERR_INVALID_ARGUMENT, "bad P / Mr");
+    if (P == 0) return OMR_OK;
+    if (!params || !params[3] || !params[4] || !params[5] || !opacity || !scales || !rotations ||
+        (shs && (!params[1] || (Mr > 0 && !params[2]))))
+        return fail(OMR_ERR_INVALID_ARGUMENT, "missing array");
+    if (!aligned16(params[5]) || !aligned16(rotations) || (shs && !aligned16(shs)))
+        return fail(OMR_ERR_INVALID_ARGUMENT, "rotation / SH arrays not 16-byte aligned");
+    if ((size_t)P * 3 * (size_t)(Mr + 1) > 0xFFFFFFF0u) return fail(OMR_ERR_INVALID_ARGUMENT, "P too large");
+    ActivateArgs a{};
+    a.P = P, a.Mr = Mr;
+    a.f_dc = params[1], a.f_rest = params[2], a.opacity = params[3], a.scaling = params[4], a.rotation = params[5];
+    a.shs = shs, a.opacity_out = opacity, a.scales_out = scales, a.rotations_out = rotations;
+    launch_activate(a, (hipStream_t)stream);
+    return hip_check("activate");
+}
+
 int omr_densification_stats(int P, const int* radii, const float* viewspace_grad, int viewspace_stride,
                             float* xyz_gradient_accum, float* denom, float* max_radii2D, void* stream)
 {

@@ -307,6 +307,13 @@ struct AdamArgs {
     float beta1, beta2, omb1, omb2, eps;
 };
 void launch_adam(AdamArgs a, hipStream_t s);
+// the renderer's activations of the raw parameters in one launch (optim.hip: activate_kernel)
+struct ActivateArgs {
+    int P, Mr;
+    const float *f_dc, *f_rest, *opacity, *scaling, *rotation;  // [P,1,3], [P,Mr,3], [P], [P,3], [P,4] (16-B aligned)
+    float *shs, *opacity_out, *scales_out, *rotations_out;      // [P,Mr+1,3] (NULL: no SH copy), [P], [P,3], [P,4]
+};
+void launch_activate(const ActivateArgs& a, hipStream_t s);
 void launch_densification_stats(int P, const int* radii, const float* vgrad, int vstride, float* accum, float* denom,
                                 float* max_radii, hipStream_t s);
 struct DensifyParams {

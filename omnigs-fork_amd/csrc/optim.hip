@@ -369,7 +369,57 @@ __global__ __launch_bounds__(256) void reset_opacity_kernel(int P, float* opacit
     if (v) v[i] = 0.f;
 }
 
+// ---- the activations of the renderer (gaussian_model.cpp:54-77, gaussian_renderer.cpp:175-200) --------------------
+// One launch instead of torch's cat + sigmoid + exp + normalize (six launches, 0.20 ms at config C in
+// profiles/r05e_train_kernel_stats.csv): blocks [0, sh_blocks) copy cat(f_dc, f_rest) into the [P, Mr + 1, 3] SH
+// array the rasterizer reads (16 B of output per thread, gathered from the two inputs), the rest apply sigmoid /
+// exp / normalize per Gaussian. The expressions are torch's: 1 / (1 + exp(-x)), exp(x), x / max(||x||_2, 1e-12)
+// (F.normalize), the norm summed left to right without contraction (optim.hip builds with -ffp-contract=off).
+constexpr int ACT_THREADS = 256;
+__global__ __launch_bounds__(ACT_THREADS) void activate_kernel(ActivateArgs a, uint32_t sh_blocks)
+{
+    if (blockIdx.x < sh_blocks) {
+        const uint32_t row = 3u * (uint32_t)(a.Mr + 1);  // floats per Gaussian in the output
+        const size_t n = (size_t)a.P * row;
+        const size_t e0 = ((size_t)blockIdx.x * ACT_THREADS + threadIdx.x) * 4;
+        if (e0 >= n) return;
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const size_t e = e0 + j;
+            if (e >= n) {
+                o[j] = 0.f;
+                continue;
+            }
+            const size_t g = e / row;
+            const uint32_t k = (uint32_t)(e - g * row);
+            o[j] = k < 3u ? a.f_dc[3 * g + k] : a.f_rest[g * (row - 3) + (k - 3)];
+        }
+        if (e0 + 4 <= n) *reinterpret_cast<float4*>(a.shs + e0) = make_float4(o[0], o[1], o[2], o[3]);
+        else
+            for (int j = 0; j < 4 && e0 + j < n; ++j) a.shs[e0 + j] = o[j];
+        return;
+    }
+    const uint32_t i = (blockIdx.x - sh_blocks) * ACT_THREADS + threadIdx.x;
+    if (i >= (uint32_t)a.P) return;
+    a.opacity_out[i] = sigmoidf(a.opacity[i]);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) a.scales_out[3 * i + c] = expf(a.scaling[3 * i + c]);
+    const float4 q = *reinterpret_cast<const float4*>(a.rotation + 4 * (size_t)i);
+    const float d = fmaxf(sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w), 1e-12f);
+    *reinterpret_cast<float4*>(a.rotations_out + 4 * (size_t)i) = make_float4(q.x / d, q.y / d, q.z / d, q.w / d);
+}
+
 // ---- launchers -------------------------------------------------------------------------------------------------
+void launch_activate(const ActivateArgs& a, hipStream_t s)
+{
+    if (a.P <= 0) return;
+    const uint32_t sh_blocks =
+        a.shs ? (uint32_t)div_up(div_up((size_t)a.P * 3 * (a.Mr + 1), (size_t)4), (size_t)ACT_THREADS) : 0u;
+    const uint32_t blocks = sh_blocks + div_up((uint32_t)a.P, (uint32_t)ACT_THREADS);
+    activate_kernel<<<blocks, ACT_THREADS, 0, s>>>(a, sh_blocks);
+}
+
 void launch_adam(AdamArgs a, hipStream_t s)
 {
     uint32_t blocks = 0;

@@ -154,6 +154,25 @@ class GaussianOptimizer:
     def set_rotation_learning_rate(self, lr: float):
         self.lr[5] = lr
 
+    # ---- the renderer's activations (gaussian_model.cpp:54-77) ----------------------------------------------------
+    def activate(self, out: Optional[dict] = None) -> dict:
+        """cat(features_dc, features_rest), sigmoid(opacity), exp(scaling), normalize(rotation) in one launch
+        (omr_activate), into the tensors of `out` (keys shs, opacity, scales, rotations; reused when their shapes
+        match, else allocated). xyz is passed through. Returns the dict."""
+        ps = self.params()
+        P, Mr, dev = self.P, self.Mr, ps[0].device
+        shapes = dict(shs=(P, Mr + 1, 3), opacity=(P, 1), scales=(P, 3), rotations=(P, 4))
+        out = {} if out is None else out
+        for k, shp in shapes.items():
+            t = out.get(k)
+            if t is None or tuple(t.shape) != shp or t.device != dev:
+                out[k] = torch.empty(shp, dtype=torch.float32, device=dev)
+        rc = R.lib().omr_activate(P, Mr, _p6(ps), out["shs"].data_ptr(), out["opacity"].data_ptr(),
+                                  out["scales"].data_ptr(), out["rotations"].data_ptr(), R._stream(dev))
+        R._check(rc, "omr_activate")
+        out["xyz"] = ps[0]
+        return out
+
     # ---- Adam ------------------------------------------------------------------------------------------------
     def step(self, raster_grads: Optional[dict] = None):
         """optimizer_->step(). Without arguments: Adam on each parameter's .grad (groups whose .grad is None are

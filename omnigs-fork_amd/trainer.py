@@ -23,11 +23,13 @@ from .parallel import DistInfo, GradBuffer, allreduce_compact_
 
 
 class TrainStep:
-    """Reusable buffers for train_step (the gradient buffer is sized once per P)."""
+    """Reusable buffers for train_step (the gradient buffer is sized once per P, the activated tensors' buffers
+    likewise)."""
 
     def __init__(self):
         self.buf: Optional[GradBuffer] = None
         self.dimg: Optional[torch.Tensor] = None
+        self.act: dict = {}
 
 
 def skip_bottom_rows(image_height: int, skip_bottom_ratio: float) -> int:
@@ -57,12 +59,9 @@ def train_step(opt: O.GaussianOptimizer, viewpoint, image_height: int, image_wid
     state = state or TrainStep()
     P, Mr = opt.P, opt.Mr
     dev = pc.xyz.device
-    with torch.no_grad():
-        means3D = pc.xyz
-        shs = torch.cat([pc.features_dc, pc.features_rest], dim=1)
-        opacity = torch.sigmoid(pc.opacity)
-        scales = torch.exp(pc.scaling)
-        rotations = torch.nn.functional.normalize(pc.rotation)
+    # the activations (cat / sigmoid / exp / normalize) in one launch (omr_activate; six torch launches before)
+    act = opt.activate(state.act)
+    means3D, shs, opacity, scales, rotations = act["xyz"], act["shs"], act["opacity"], act["scales"], act["rotations"]
     if camera_type == R.CAMERA_PINHOLE:  # std::tan(FoV * 0.5f) in float (gaussian_renderer.cpp:58-59)
         tanfovx = float(np.tan(np.float32(viewpoint.FoVx) * np.float32(0.5)))
         tanfovy = float(np.tan(np.float32(viewpoint.FoVy) * np.float32(0.5)))

@@ -286,3 +286,28 @@ def test_fused_train_step_matches_autograd_reference_composition(masked, skip_bo
     np.testing.assert_allclose(to_np(opt1.xyz_gradient_accum), to_np(opt2.xyz_gradient_accum), rtol=2e-3,
                                atol=1e-3 * float(opt2.xyz_gradient_accum.abs().max()))
     np.testing.assert_array_equal(to_np(opt1.denom), to_np(opt2.denom))
+
+
+def test_activate_matches_the_torch_activations():
+    """omr_activate (optim.hip: activate_kernel) against gaussian_model.cpp:54-77's torch expressions: the SH
+    concatenation, sigmoid and exp bit for bit; normalize within an ulp of torch's (its norm reduction may sum the
+    four squares in another order)."""
+    from helpers import make_case, scene
+
+    g, _, _ = make_case(5000, 64, 32, scene.CAMERA_LONLAT, 31)
+    rng = np.random.default_rng(2)
+    o = np.clip(g.opacity.astype(np.float64), 1e-4, 1 - 1e-4)
+    params = [g.means3D, g.shs[:, :1], g.shs[:, 1:], np.log(o / (1 - o)), np.log(g.scales),
+              g.rotations * rng.uniform(0.5, 2.0, (g.P, 1))]
+    m = _model([np.ascontiguousarray(p, dtype=np.float32) for p in params])
+    opt = OPT.GaussianOptimizer(m, OPT.OptimizationParams())
+    act = opt.activate()
+    again = opt.activate(act)  # reuses the buffers
+    assert all(again[k] is act[k] for k in ("shs", "opacity", "scales", "rotations"))
+    torch.cuda.synchronize()
+    assert act["xyz"] is m.xyz
+    assert torch.equal(act["shs"], torch.cat([m.features_dc, m.features_rest], dim=1))
+    assert torch.equal(act["opacity"], torch.sigmoid(m.opacity))
+    assert torch.equal(act["scales"], torch.exp(m.scaling))
+    ref = torch.nn.functional.normalize(m.rotation)
+    torch.testing.assert_close(act["rotations"], ref, rtol=2.4e-7, atol=0)
