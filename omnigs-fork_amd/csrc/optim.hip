@@ -84,20 +84,22 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(AdamArgs a)
         }
     }
     // gradient of the raw parameter
+    uint32_t shi[4] = {0u, 0u, 0u, 0u};  // SH groups: each element's index in dL_dsh (= in cat(f_dc, f_rest))
     switch (G.kind) {
     case ADAM_SH_DC: {  // f_dc element e = 3 q + k  <-  dL_dsh[q][0][k]
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t ej = e + j, q = ej / 3u;
-            g[j] = j < (int)cnt ? G.g[ej + q * 3u * (a.M - 1)] : 0.f;
+            shi[j] = ej + q * 3u * (a.M - 1);
+            g[j] = j < (int)cnt ? G.g[shi[j]] : 0.f;
         }
     } break;
     case ADAM_SH_REST: {  // f_rest element e = 3 Mr q + k  <-  dL_dsh[q][1 + k / 3][k % 3]
         RestIndex ri(e, 3u * (a.M - 1));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t idx = ri.next();
-            g[j] = j < (int)cnt ? G.g[idx] : 0.f;
+            shi[j] = ri.next();
+            g[j] = j < (int)cnt ? G.g[shi[j]] : 0.f;
         }
     } break;
     case ADAM_ROTATION: {  // normalize backward (torch::nn::functional::normalize, eps 1e-12); n == 4P, cnt == 4
@@ -140,6 +142,9 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(AdamArgs a)
     } else {
         for (uint32_t j = 0; j < cnt; ++j) G.p[e + j] = p[j], G.m[e + j] = m[j], G.v[e + j] = v[j];
     }
+    // the renderer's next SH input, cat(f_dc, f_rest), kept current here instead of re-gathered by omr_activate
+    if (a.sh_out && (G.kind == ADAM_SH_DC || G.kind == ADAM_SH_REST))
+        for (uint32_t j = 0; j < cnt; ++j) a.sh_out[shi[j]] = p[j];
 }
 
 // addDensificationStats (gaussian_model.cpp:839-853) and the max_radii2D update (gaussian_mapper.cpp:427-432)
@@ -378,26 +383,21 @@ __global__ __launch_bounds__(256) void reset_opacity_kernel(int P, float* opacit
 constexpr int ACT_THREADS = 256;
 __global__ __launch_bounds__(ACT_THREADS) void activate_kernel(ActivateArgs a, uint32_t sh_blocks)
 {
-    if (blockIdx.x < sh_blocks) {
+    if (blockIdx.x < sh_blocks) {  // 32-bit indices: P * 3 (Mr + 1) < 2^32 (omr_activate)
         const uint32_t row = 3u * (uint32_t)(a.Mr + 1);  // floats per Gaussian in the output
-        const size_t n = (size_t)a.P * row;
-        const size_t e0 = ((size_t)blockIdx.x * ACT_THREADS + threadIdx.x) * 4;
+        const uint32_t n = (uint32_t)a.P * row;
+        const uint32_t e0 = (blockIdx.x * ACT_THREADS + threadIdx.x) * 4u;
         if (e0 >= n) return;
+        uint32_t g = e0 / row, k = e0 - g * row;
         float o[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const size_t e = e0 + j;
-            if (e >= n) {
-                o[j] = 0.f;
-                continue;
-            }
-            const size_t g = e / row;
-            const uint32_t k = (uint32_t)(e - g * row);
-            o[j] = k < 3u ? a.f_dc[3 * g + k] : a.f_rest[g * (row - 3) + (k - 3)];
+            o[j] = e0 + j >= n ? 0.f : (k < 3u ? a.f_dc[3u * g + k] : a.f_rest[g * (row - 3u) + (k - 3u)]);
+            if (++k == row) k = 0, ++g;
         }
-        if (e0 + 4 <= n) *reinterpret_cast<float4*>(a.shs + e0) = make_float4(o[0], o[1], o[2], o[3]);
+        if (e0 + 4u <= n) *reinterpret_cast<float4*>(a.shs + e0) = make_float4(o[0], o[1], o[2], o[3]);
         else
-            for (int j = 0; j < 4 && e0 + j < n; ++j) a.shs[e0 + j] = o[j];
+            for (uint32_t j = 0; j < 4u && e0 + j < n; ++j) a.shs[e0 + j] = o[j];
         return;
     }
     const uint32_t i = (blockIdx.x - sh_blocks) * ACT_THREADS + threadIdx.x;

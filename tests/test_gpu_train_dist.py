@@ -86,10 +86,10 @@ def test_view_parallel_train_step_replicas_agree_with_summed_views():
     bg = torch.zeros(3, device=dev)
     for it in range(2):
         total = None
-        with torch.no_grad():
-            shs = torch.cat([model.features_dc, model.features_rest], 1)
-            act = (model.xyz, torch.sigmoid(model.opacity), torch.exp(model.scaling),
-                   torch.nn.functional.normalize(model.rotation))
+        # the trainer's activations (omr_activate; against torch's in tests/test_gpu_optim.py)
+        a = opt.activate()
+        shs = a["shs"]
+        act = (a["xyz"], a["opacity"], a["scales"], a["rotations"])
         for vp, gt in ((vp0, gt0), (vp1, gt1)):
             nr, img, radii, gb, bb, ib = R.RasterizeGaussiansCUDA(bg, act[0], None, act[1], act[2], act[3], 1.0, None,
                                                                   vp.world_view_transform, vp.full_proj_transform,
