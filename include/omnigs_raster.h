@@ -176,12 +176,6 @@ int omr_adam_step(int P, int Mr, float* const params[6], float* const exp_avg[6]
  * (x / max(||x||_2, 1e-12)); xyz (params[0]) is used as is. params[5], rotations and shs 16-byte aligned. */
 int omr_activate(int P, int Mr, const float* const params[6], float* shs, float* opacity, float* scales,
                  float* rotations, void* stream);
-/* omr_adam_step (OMR_ADAM_RASTER_GRADS only) that also writes the updated features_dc / features_rest as
- * shs_out = cat(f_dc, f_rest) [P,Mr+1,3]: the SH input of the next forward, kept current in the same pass (the
- * trainer then skips omr_activate's SH copy). shs_out NULL: omr_adam_step. */
-int omr_adam_step_sh_out(int P, int Mr, float* const params[6], float* const exp_avg[6], float* const exp_avg_sq[6],
-                         const float* const grads[6], int grad_kind, const float lr[6], const int64_t step[6],
-                         float beta1, float beta2, float eps, float* shs_out, void* stream);
 /* addDensificationStats (gaussian_model.cpp:839-853) + the max_radii2D update (gaussian_mapper.cpp:427-432) for
  * visibility_filter = radii > 0: accum[i] += |viewspace_grad[i][0:2]|, denom[i] += 1, max_radii2D[i] =
  * max(max_radii2D[i], radii[i]). viewspace_grad is dL_dmeans2D with row stride viewspace_stride (3). */

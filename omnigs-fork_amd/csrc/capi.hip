@@ -955,14 +955,6 @@ int omr_adam_step(int P, int Mr, float* const params[6], float* const exp_avg[6]
                   const float* const grads[6], int grad_kind, const float lr[6], const int64_t step[6], float beta1,
                   float beta2, float eps, void* stream)
 {
-    return omr_adam_step_sh_out(P, Mr, params, exp_avg, exp_avg_sq, grads, grad_kind, lr, step, beta1, beta2, eps,
-                                nullptr, stream);
-}
-
-int omr_adam_step_sh_out(int P, int Mr, float* const params[6], float* const exp_avg[6], float* const exp_avg_sq[6],
-                         const float* const grads[6], int grad_kind, const float lr[6], const int64_t step[6],
-                         float beta1, float beta2, float eps, float* shs_out, void* stream)
-{
     g_last_error.clear();
     if (P < 0 || Mr < 0 || Mr > 15) return fail(OMR_ERR_INVALID_ARGUMENT, "bad P / Mr");
     if (grad_kind != OMR_ADAM_RAW_GRADS && grad_kind != OMR_ADAM_RASTER_GRADS)
@@ -971,11 +963,8 @@ int omr_adam_step_sh_out(int P, int Mr, float* const params[6], float* const exp
     if ((size_t)P * 3 * (size_t)Mr > 0xFFFFFFF0u) return fail(OMR_ERR_INVALID_ARGUMENT, "P too large");
     const uint32_t width[6] = {3u, 3u, 3u * (uint32_t)Mr, 1u, 3u, 4u};
     static const int raster_kind[6] = {ADAM_PLAIN, ADAM_SH_DC, ADAM_SH_REST, ADAM_OPACITY, ADAM_SCALING, ADAM_ROTATION};
-    if (shs_out && grad_kind != OMR_ADAM_RASTER_GRADS)
-        return fail(OMR_ERR_INVALID_ARGUMENT, "shs_out needs OMR_ADAM_RASTER_GRADS");
     AdamArgs a{};
     a.M = Mr + 1;
-    a.sh_out = shs_out;
     a.beta1 = beta1, a.beta2 = beta2, a.omb1 = (float)(1.0 - (double)beta1), a.omb2 = (float)(1.0 - (double)beta2);
     a.eps = eps;
     for (int k = 0; k < 6; ++k) {

@@ -305,7 +305,6 @@ struct AdamArgs {
     int ngroups;
     int M;                             // SH coefficients per Gaussian in dL_dsh (f_dc + f_rest)
     float beta1, beta2, omb1, omb2, eps;
-    float* sh_out;  // raster mode: the updated f_dc / f_rest also written as cat(f_dc, f_rest) [P,M,3] (NULL: not)
 };
 void launch_adam(AdamArgs a, hipStream_t s);
 // the renderer's activations of the raw parameters in one launch (optim.hip: activate_kernel)

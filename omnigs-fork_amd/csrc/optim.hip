@@ -84,22 +84,20 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(AdamArgs a)
         }
     }
     // gradient of the raw parameter
-    uint32_t shi[4] = {0u, 0u, 0u, 0u};  // SH groups: each element's index in dL_dsh (= in cat(f_dc, f_rest))
     switch (G.kind) {
     case ADAM_SH_DC: {  // f_dc element e = 3 q + k  <-  dL_dsh[q][0][k]
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t ej = e + j, q = ej / 3u;
-            shi[j] = ej + q * 3u * (a.M - 1);
-            g[j] = j < (int)cnt ? G.g[shi[j]] : 0.f;
+            g[j] = j < (int)cnt ? G.g[ej + q * 3u * (a.M - 1)] : 0.f;
         }
     } break;
     case ADAM_SH_REST: {  // f_rest element e = 3 Mr q + k  <-  dL_dsh[q][1 + k / 3][k % 3]
         RestIndex ri(e, 3u * (a.M - 1));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            shi[j] = ri.next();
-            g[j] = j < (int)cnt ? G.g[shi[j]] : 0.f;
+            const uint32_t idx = ri.next();
+            g[j] = j < (int)cnt ? G.g[idx] : 0.f;
         }
     } break;
     case ADAM_ROTATION: {  // normalize backward (torch::nn::functional::normalize, eps 1e-12); n == 4P, cnt == 4
@@ -142,9 +140,6 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(AdamArgs a)
     } else {
         for (uint32_t j = 0; j < cnt; ++j) G.p[e + j] = p[j], G.m[e + j] = m[j], G.v[e + j] = v[j];
     }
-    // the renderer's next SH input, cat(f_dc, f_rest), kept current here instead of re-gathered by omr_activate
-    if (a.sh_out && (G.kind == ADAM_SH_DC || G.kind == ADAM_SH_REST))
-        for (uint32_t j = 0; j < cnt; ++j) a.sh_out[shi[j]] = p[j];
 }
 
 // addDensificationStats (gaussian_model.cpp:839-853) and the max_radii2D update (gaussian_mapper.cpp:427-432)

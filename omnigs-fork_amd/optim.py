@@ -115,7 +115,6 @@ class GaussianOptimizer:
         self.max_radii2D = torch.zeros((P,), device=dev)
         self.exist_since_iter = torch.zeros((P,), dtype=torch.int32, device=dev)
         self._plan = None
-        self._sh_epoch = 0  # advanced by every Adam step (activate's SH copy is current only for the same epoch)
 
     # ---- parameters ------------------------------------------------------------------------------------------
     def params(self):
@@ -156,19 +155,10 @@ class GaussianOptimizer:
         self.lr[5] = lr
 
     # ---- the renderer's activations (gaussian_model.cpp:54-77) ----------------------------------------------------
-    def _sh_key(self):
-        """What out["shs"] was last made from: the SH parameters' storage and autograd versions (an in-place torch
-        op on them bumps the version; this class's raw-pointer updates do not, and keep out["shs"] current)."""
-        m = self.model
-        return (m.features_dc.data_ptr(), m.features_rest.data_ptr(), m.features_dc._version,
-                m.features_rest._version, self.P, self.Mr, self._sh_epoch)
-
     def activate(self, out: Optional[dict] = None) -> dict:
         """cat(features_dc, features_rest), sigmoid(opacity), exp(scaling), normalize(rotation) in one launch
         (omr_activate), into the tensors of `out` (keys shs, opacity, scales, rotations; reused when their shapes
-        match, else allocated). xyz is passed through. Returns the dict.
-        The SH concatenation is skipped when out["shs"] is still current: step(raster_grads=..., activated=out)
-        writes the updated SH groups there as well (omr_adam_step_sh_out), and nothing changed them since."""
+        match, else allocated). xyz is passed through. Returns the dict."""
         ps = self.params()
         P, Mr, dev = self.P, self.Mr, ps[0].device
         shapes = dict(shs=(P, Mr + 1, 3), opacity=(P, 1), scales=(P, 3), rotations=(P, 4))
@@ -177,25 +167,18 @@ class GaussianOptimizer:
             t = out.get(k)
             if t is None or tuple(t.shape) != shp or t.device != dev:
                 out[k] = torch.empty(shp, dtype=torch.float32, device=dev)
-                if k == "shs":
-                    out.pop("shs_key", None)
-        sh_current = out.get("shs_key") == self._sh_key()
-        rc = R.lib().omr_activate(P, Mr, _p6(ps), None if sh_current else out["shs"].data_ptr(),
-                                  out["opacity"].data_ptr(), out["scales"].data_ptr(), out["rotations"].data_ptr(),
-                                  R._stream(dev))
+        rc = R.lib().omr_activate(P, Mr, _p6(ps), out["shs"].data_ptr(), out["opacity"].data_ptr(),
+                                  out["scales"].data_ptr(), out["rotations"].data_ptr(), R._stream(dev))
         R._check(rc, "omr_activate")
-        out["shs_key"] = self._sh_key()
         out["xyz"] = ps[0]
         return out
 
     # ---- Adam ------------------------------------------------------------------------------------------------
-    def step(self, raster_grads: Optional[dict] = None, activated: Optional[dict] = None):
+    def step(self, raster_grads: Optional[dict] = None):
         """optimizer_->step(). Without arguments: Adam on each parameter's .grad (groups whose .grad is None are
         skipped, as adam.cpp does). With raster_grads = the rasterizer backward's outputs (dL_dmeans3D, dL_dsh,
         dL_dopacity, dL_dscales, dL_drotations — e.g. parallel.GradBuffer.views), the activation backward is fused
-        into the same launch and no .grad is needed; `activated` (a dict activate() filled, raster mode only) also
-        receives the updated SH groups as its cat(f_dc, f_rest) (omr_adam_step_sh_out), so the next activate()
-        skips that copy."""
+        into the same launch and no .grad is needed."""
         ps = self.params()
         P, Mr = self.P, self.Mr
         if raster_grads is not None:
@@ -222,19 +205,9 @@ class GaussianOptimizer:
         use = lambda ts: [t if active[k] else None for k, t in enumerate(ts)]  # noqa: E731
         lr = (C.c_float * 6)(*self.lr)
         st = (C.c_int64 * 6)(*[max(s, 1) for s in self.steps])
-        sh_out = None
-        if activated is not None and raster_grads is not None and activated.get("shs_key") == self._sh_key():
-            sh_out = activated["shs"]  # current before this step: keep it current through it
-        rc = R.lib().omr_adam_step_sh_out(P, Mr, _p6(use(ps)), _p6(self.exp_avg), _p6(self.exp_avg_sq),
-                                          _p6(use(grads)), kind, lr, st, self.betas[0], self.betas[1], self.eps,
-                                          None if sh_out is None else sh_out.data_ptr(), R._stream(ps[0].device))
+        rc = R.lib().omr_adam_step(P, Mr, _p6(use(ps)), _p6(self.exp_avg), _p6(self.exp_avg_sq), _p6(use(grads)), kind,
+                                   lr, st, self.betas[0], self.betas[1], self.eps, R._stream(ps[0].device))
         R._check(rc, "omr_adam_step")
-        self._sh_epoch += 1
-        if activated is not None:
-            if sh_out is not None:
-                activated["shs_key"] = self._sh_key()  # written by this step
-            else:
-                activated.pop("shs_key", None)  # the SH groups moved without it: stale
 
     def zero_grad(self):
         """zero_grad(true): gradients are set to None."""

@@ -102,5 +102,5 @@ def train_step(opt: O.GaussianOptimizer, viewpoint, image_height: int, image_wid
                            lambda c, d, out: R.sh_grad_from_colors(means3D, shs, pc.active_sh_degree, c, d, out=out),
                            rebuild_packed=lambda pk, out: R.sh_grad_from_colors_packed(means3D, shs,
                                                                                       pc.active_sh_degree, pk, out=out))
-    opt.step(raster_grads=out, activated=state.act)  # also keeps state.act["shs"] current (omr_adam_step_sh_out)
+    opt.step(raster_grads=out)
     return terms, image, radii

@@ -312,38 +312,3 @@ def test_activate_matches_the_torch_activations():
     ref = torch.nn.functional.normalize(m.rotation)
     torch.testing.assert_close(act["rotations"], ref, rtol=2.4e-7, atol=0)
 
-
-def test_train_step_keeps_the_sh_copy_current():
-    """trainer.train_step gathers cat(f_dc, f_rest) once (omr_activate); afterwards every Adam step writes the updated
-    SH groups into it as well (omr_adam_step_sh_out) and the gather is skipped. After several iterations the copy
-    equals the concatenation of the parameters bit for bit; an Adam step without the copy, an in-place edit of the
-    parameters and a densification each make the next activate() gather again."""
-    from helpers import make_case, scene
-
-    W, H = 128, 64
-    g, cam, _ = make_case(2000, W, H, scene.CAMERA_LONLAT, 33, spread=2.0)
-    t = lambda a: torch.tensor(np.ascontiguousarray(a, dtype=np.float32), device="cuda")  # noqa: E731
-    model = RD.GaussianModelParams.from_activated(t(g.means3D), t(g.scales), t(g.rotations),
-                                                  t(g.opacity).reshape(-1, 1), t(g.shs), g.sh_degree)
-    for name in ("xyz", "features_dc", "features_rest", "opacity", "scaling", "rotation"):
-        setattr(model, name, getattr(model, name).contiguous())
-    opt = OPT.GaussianOptimizer(model, OPT.OptimizationParams())
-    vp = RD.Viewpoint(t(cam.viewmatrix), t(cam.projmatrix), t(cam.campos))
-    gt = torch.rand((3, H, W), device="cuda", generator=torch.Generator(device="cuda").manual_seed(3))
-    bg = torch.zeros(3, device="cuda")
-    state = omr.trainer.TrainStep()
-    cat = lambda: torch.cat([model.features_dc, model.features_rest], dim=1)  # noqa: E731
-    for it in range(4):
-        omr.trainer.train_step(opt, vp, H, W, gt, bg, state=state)
-        torch.cuda.synchronize()
-        assert state.act.get("shs_key") == opt._sh_key()  # current: the next activate() skips the gather
-        assert torch.equal(state.act["shs"], cat())
-    key = state.act["shs_key"]
-    with torch.no_grad():
-        model.features_rest.mul_(1.01)  # in place: the autograd version moves
-    assert opt._sh_key() != key
-    assert torch.equal(opt.activate(state.act)["shs"], cat())
-    # a step without the copy makes it stale
-    opt.step(raster_grads=state.buf.views, activated=None)
-    assert state.act.get("shs_key") != opt._sh_key()
-    assert torch.equal(opt.activate(state.act)["shs"], cat())
