@@ -835,9 +835,14 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_compact_kerne
         for (int c = 0; c < GRAD_ROW; ++c) g[c] = a.row_sums[(size_t)idx * GRAD_ROW + c];
         const float4 co = a.conic_op[idx];
         raw_row_to_grads(g, co, a.W, a.H);
-        float4* dsh4 = a.dL_dsh ? reinterpret_cast<float4*>(a.dL_dsh) + (size_t)idx * SH_F4 : nullptr;
         const float4* sh4 = a.shs ? reinterpret_cast<const float4*>(a.shs) + (size_t)idx * SH_F4 : nullptr;
-        gaussian_bwd_point<CAM, 16>(a, idx, g, sh4, dsh4, jac ? a.sh_jac + (size_t)idx * 9 : nullptr);
+        const float* jr = jac ? a.sh_jac + (size_t)idx * 9 : nullptr;
+        if (a.dL_dsh) {  // uniform
+            gaussian_bwd_point<CAM, 16>(a, idx, g, sh4, reinterpret_cast<float4*>(a.dL_dsh) + (size_t)idx * SH_F4, jr);
+        } else {  // the compact exchange's skip_dsh: sh_backward<16> still writes a row, into registers nobody reads
+            float4 sink[SH_F4];
+            gaussian_bwd_point<CAM, 16>(a, idx, g, sh4, sink, jr);
+        }
     }
 }
 

@@ -278,13 +278,16 @@ def test_depth_sort_multi_launch_path_with_culled_gaussians(oracle_mt, depth_sor
     _compare(g, cam, None, nthreads=oracle_mt)
 
 
-@pytest.mark.parametrize("P,W,H,view,jac", [(30000, 320, 180, 3, True), (30000, 320, 180, 5, False),
-                                           (5000, 160, 90, 0, True)])
-def test_compacted_gaussian_backward_matches_the_wave_kernel(P, W, H, view, jac):
+@pytest.mark.parametrize("P,W,H,view,jac,skip_dsh", [(30000, 320, 180, 3, True, False),
+                                                    (30000, 320, 180, 5, False, False),
+                                                    (5000, 160, 90, 0, True, False), (30000, 320, 180, 3, True, True),
+                                                    (30000, 320, 180, 5, False, True)])
+def test_compacted_gaussian_backward_matches_the_wave_kernel(P, W, H, view, jac, skip_dsh):
     """Pinhole views run the per-Gaussian backward compacted (gaussian_bwd.hip: gaussian_bwd_compact_kernel; a
     workgroup lists its span's visible Gaussians and runs them densely, zeros the culled ones' outputs). Same
     arithmetic per Gaussian as the wave-per-64 kernel: every gradient bitwise equal, with the stored dRGB/ddir and
-    with the SH rows read (jac False), and against the oracle (test_parity's pinhole cases, E_pinhole at full size)."""
+    with the SH rows read (jac False), with dL_dsh not written (skip_dsh: the compact exchange's backward), and
+    against the oracle (test_parity's pinhole cases, E_pinhole at full size)."""
     g, cam, dL = make_case(P, W, H, PIN, 71, view_index=view, spread=2.0)
     R = omr.rasterizer
 
@@ -300,9 +303,11 @@ def test_compacted_gaussian_backward_matches_the_wave_kernel(P, W, H, view, jac)
                                               t(g.scales), t(g.rotations), 1.0, e, t(cam.viewmatrix),
                                               t(cam.projmatrix), cam.tanfovx, cam.tanfovy, t(dL), t(g.shs),
                                               g.sh_degree, t(cam.campos), h["geom"], h["L"], h["binning"], h["img"],
-                                              cam.camera_type)
+                                              cam.camera_type, skip_dsh=skip_dsh)
         torch.cuda.synchronize()
-        return [to_np(x) for x in gr], to_np(h["radii"])
+        if skip_dsh:
+            assert gr[5] is None
+        return [to_np(x) for x in gr if x is not None], to_np(h["radii"])
 
     old = R.debug_gbwd_compact(True)
     try:
