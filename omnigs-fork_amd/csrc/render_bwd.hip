@@ -69,16 +69,6 @@ __device__ unsigned long long g_bwd_counts[5];
 #ifndef OMR_BWD_MINW
 #define OMR_BWD_MINW 1
 #endif
-// A/B levers against the band chain's latency, 0 = off:
-//   OMR_BWD_PREFETCH 1: the next staged instance's position record (s_geo) is read from LDS before the current
-//                       instance's band chain; 2: all three of its records (12 VGPRs held across the chain)
-//   OMR_BWD_PRIO     1: s_setprio 1 around the band chain, 0 for the pair reduction and row stores; 2: the reverse
-#ifndef OMR_BWD_PREFETCH
-#define OMR_BWD_PREFETCH 0
-#endif
-#ifndef OMR_BWD_PRIO
-#define OMR_BWD_PRIO 0
-#endif
 // Positions staged per batch (<= TW_BATCH). The staging arrays take 48 B per position: with 64 the workgroup's LDS is
 // 7424 B, which caps residency at 21-22 waves per CU, below the 24 (6 per SIMD) its 78 VGPRs allow; with 40 it is
 // 6272 B. Views with more units than resident wave slots (launch_render_backward) take OMR_BWD_BATCH (interleaved A/B,
@@ -231,31 +221,10 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
         // the instance loop, instantiated with and without the per-lane position test: a batch whose positions all
         // lie below every band's smallest last contributor (band_min) needs none (one VALU per evaluated band less)
         auto instances = [&](auto pos_test) {
-#if OMR_BWD_PREFETCH
-            float4 g_nx = s_geo[0];
-#if OMR_BWD_PREFETCH >= 2
-            float4 qo_nx = s_quad[0], f_nx = s_rgb[0];
-#endif
-#endif
             for (uint32_t j = 0; j < nuse; ++j) {
-#if OMR_BWD_PREFETCH
-                const uint32_t jn = min(j + 1, (uint32_t)BWD_BATCH - 1);  // staged or stale: read only if j + 1 < nuse
-                const float4 g = g_nx;
-                g_nx = s_geo[jn];
-#if OMR_BWD_PREFETCH >= 2
-                const float4 qo = qo_nx;
-                const float4 f = f_nx;
-                qo_nx = s_quad[jn];
-                f_nx = s_rgb[jn];
-#else
-                const float4 qo = s_quad[j];
-                const float4 f = s_rgb[j];
-#endif
-#else
                 const float4 g = s_geo[j];
                 const float4 qo = s_quad[j];
                 const float4 f = s_rgb[j];
-#endif
                 const uint32_t mb = uniform(__builtin_bit_cast(uint32_t, g.w));
                 const uint32_t ipos = __builtin_bit_cast(uint32_t, g.z);
                 const Quad q = {qo.x, qo.y, qo.z};
@@ -269,11 +238,6 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
                 f2v sc01 = {0.f, 0.f};  // S_aT dpix_r, S_aT dpix_g
                 float suyy = 0.f, sc2 = 0.f;
                 uint32_t any = 0;  // bands with a contributing pixel (set in wave-uniform branches: an SGPR)
-#if OMR_BWD_PRIO == 1
-                __builtin_amdgcn_s_setprio(1);
-#elif OMR_BWD_PRIO == 2
-                __builtin_amdgcn_s_setprio(0);
-#endif
     #pragma unroll
                 for (int b = 0; b < TW_BANDS; ++b) {
                     if (!(mb & (1u << b))) continue;  // scalar branch
@@ -310,11 +274,6 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
 #endif
                 }
                 const uint32_t slot_j = __builtin_bit_cast(uint32_t, f.w);
-#if OMR_BWD_PRIO == 1
-                __builtin_amdgcn_s_setprio(0);
-#elif OMR_BWD_PRIO == 2
-                __builtin_amdgcn_s_setprio(1);
-#endif
                 if (!any) continue;  // no pixel took a contribution: no row
                 BWD_COUNT(3, 1);
                 const float su = s_uy.x, suy = s_uy.y;
