@@ -279,11 +279,6 @@ int omr_debug_set_sh_jac(char* geom_buffer, int P, int enabled, void* stream);
  * process-wide, for tests and A/B runs (the environment's OMR_DEPTH_SORT=bytes / visible sets the start value).
  * Returns the previous mode, or -1 for a mode outside 0..2 (omr_last_error says why) */
 int omr_debug_depth_sort_mode(int mode);
-/* the backward's per-Gaussian kernel on pinhole views: 1 = the compacted one (a workgroup lists its span's visible
- * Gaussians and runs their chain densely; the default), 0 = one wave per 64 Gaussians as on lonlat views (bitwise
- * the same gradients). Process-wide, for tests and A/B runs (OMR_GBWD_COMPACT=0 sets the start value). Returns the
- * previous setting. */
-int omr_debug_gbwd_compact(int on);
 /* per-Gaussian pixel centre [P,2], conic+opacity [P,4], rgb [P,3], depth [P], tiles_touched [P] */
 /* one wave64 through the render backward's gradient reduction: in [64][9] -> out [9] (column sums) */
 int omr_debug_wave_sum9(const float* in, float* out, void* stream); /* wave_sum9_rows */

@@ -1324,8 +1324,6 @@ int omr_debug_counters(char* geom_buffer, int P, uint32_t* dst, void* stream)
     return OMR_OK;
 }
 
-int omr_debug_gbwd_compact(int on) { return gbwd_compact_set(on); }
-
 int omr_debug_depth_sort_mode(int mode)
 {
     if (mode < 0 || mode > 2) {

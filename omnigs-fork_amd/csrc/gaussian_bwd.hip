@@ -13,9 +13,6 @@
 // Every output element is written exactly once (zeros for culled Gaussians and unused SH slots), so the
 // caller needs no zero-initialised gradient tensors (the reference zero-fills ~324 B/Gaussian first,
 // rasterize_points.cu:200-208).
-#include <atomic>
-#include <cstdlib>
-
 #include "kernels.h"
 #include "sh_eval.h"
 #include "tile_wave.h"
@@ -693,9 +690,8 @@ __device__ __forceinline__ void gaussian_bwd_culled(const GaussBwdArgs& a, int i
         for (int c = 0; c < 4; ++c) a.dL_dconic[4 * idx + c] = 0.f;
     if (a.dL_dsh) {
         if constexpr (MC == 16) {
-            if (dsh4)  // NULL: the caller writes the row (gaussian_bwd_compact_kernel)
 #pragma unroll
-                for (int q = 0; q < 12; ++q) dsh4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int q = 0; q < 12; ++q) dsh4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         } else {
             for (int c = 0; c < Mr * 3; ++c) a.dL_dsh[(size_t)idx * Mr * 3 + c] = 0.f;
         }
@@ -758,90 +754,6 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
             wave_sync();
             wave_rows_store<SH_F4>(reinterpret_cast<float4*>(a.dL_dsh) + (size_t)wave_first * SH_F4, __ballot(valid),
                                    stage, lane);
-        }
-    }
-}
-
-// Views that cull most of the scene (a pinhole frustum; config E pinhole: 88 % of 5 M): the wave-per-64 kernel above
-// runs the visible path's load -> compute -> store chain in every wave (0.88^64 ~ 0: every wave holds some visible
-// lanes), so its time is that chain times the waves. Here a workgroup takes a span of GB_SPAN consecutive Gaussians:
-//   1. each thread reads the radii of its GB_SPAN / 256 Gaussians and the span's visible ones are listed in index
-//      order in LDS (ballots + a workgroup prefix);
-//   2. every thread writes the culled Gaussians' outputs as zeros: the small [P, k] outputs by natural index
-//      (coalesced), the 192-B dL_dsh rows wave-cooperatively, 64 rows a step, 1 KiB contiguous per instruction,
-//      skipping the visible rows (a row is exactly three 64-B lines, so no line is shared with a visible row);
-//   3. thread j takes the span's j-th visible Gaussian and runs gaussian_bwd_point on it, its SH row read and its
-//      dL_dsh row written in global memory (12 float4, three whole lines).
-// So the visible chain runs in ceil(visible / 64) waves per span instead of in all of them. Same arithmetic as the
-// kernel above per Gaussian: bitwise the same gradients.
-constexpr int GB_SPAN = 1024;
-constexpr int GB_PER = GB_SPAN / 256;
-template <int CAM>
-__global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_compact_kernel(GaussBwdArgs a)
-{
-    constexpr int SH_F4 = 12;
-    __shared__ uint16_t s_list[GB_SPAN];
-    __shared__ uint32_t s_wave[4][GB_PER];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    const int span0 = a.g_begin + (int)blockIdx.x * GB_SPAN;
-    // 1. visibility; sub-span k of wave wv = local rows [256 k + 64 wv, +64): thread tid owns rows 256 k + tid
-    uint64_t vmask[GB_PER];
-    bool vis[GB_PER], valid[GB_PER];
-#pragma unroll
-    for (int k = 0; k < GB_PER; ++k) {
-        const int idx = span0 + 256 * k + (int)tid;
-        valid[k] = idx < a.g_end;
-        vis[k] = valid[k] && a.radii[idx] > 0;
-        vmask[k] = __ballot(vis[k]);
-        if (lane == 0) s_wave[wv][k] = (uint32_t)__popcll(vmask[k]);
-    }
-    __syncthreads();
-    uint32_t nv = 0, before[GB_PER];  // list order: (k, wave, lane) = local row order
-#pragma unroll
-    for (int k = 0; k < GB_PER; ++k)
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            if (w == (int)wv) before[k] = nv;
-            nv += s_wave[w][k];
-        }
-#pragma unroll
-    for (int k = 0; k < GB_PER; ++k)
-        if (vis[k]) s_list[before[k] + mask_rank(vmask[k])] = (uint16_t)(256 * k + tid);
-    // 2. the culled Gaussians' outputs
-#pragma unroll
-    for (int k = 0; k < GB_PER; ++k) {
-        const int idx = span0 + 256 * k + (int)tid;
-        if (valid[k] && !vis[k]) gaussian_bwd_culled<16>(a, idx, nullptr);
-        if (a.dL_dsh) {
-            const int row0 = span0 + 256 * k + 64 * (int)wv;  // this wave's 64 rows
-            const uint64_t zrows = __ballot(valid[k] && !vis[k]);
-            float4* dst = reinterpret_cast<float4*>(a.dL_dsh) + (size_t)row0 * SH_F4;
-#pragma unroll
-            for (int q = 0; q < SH_F4; ++q) {
-                const uint32_t e = (uint32_t)q * 64u + lane, r = e / SH_F4;
-                if ((zrows >> r) & 1u) dst[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-        }
-    }
-    __syncthreads();
-    // 3. the visible ones, densely
-    const bool jac = a.shs && a.sh_jac && a.campos &&
-                     *a.jac_flag == sh_jac_key(a.shs, a.means3D, __float_as_uint(a.campos[0]),
-                                               __float_as_uint(a.campos[1]), __float_as_uint(a.campos[2]));
-    for (uint32_t j = tid; j < nv; j += 256) {
-        const int idx = span0 + (int)s_list[j];
-        float g[GRAD_ROW];
-#pragma unroll
-        for (int c = 0; c < GRAD_ROW; ++c) g[c] = a.row_sums[(size_t)idx * GRAD_ROW + c];
-        const float4 co = a.conic_op[idx];
-        raw_row_to_grads(g, co, a.W, a.H);
-        const float4* sh4 = a.shs ? reinterpret_cast<const float4*>(a.shs) + (size_t)idx * SH_F4 : nullptr;
-        const float* jr = jac ? a.sh_jac + (size_t)idx * 9 : nullptr;
-        if (a.dL_dsh) {  // uniform
-            gaussian_bwd_point<CAM, 16>(a, idx, g, sh4, reinterpret_cast<float4*>(a.dL_dsh) + (size_t)idx * SH_F4, jr);
-        } else {  // the compact exchange's skip_dsh: sh_backward<16> still writes a row, into registers nobody reads
-            float4 sink[SH_F4];
-            gaussian_bwd_point<CAM, 16>(a, idx, g, sh4, sink, jr);
         }
     }
 }
@@ -958,19 +870,6 @@ void launch_row_sums(int g_begin, int g_end, bool huge, const uint32_t* row_firs
     row_sum_kernel<<<main_blocks + a.huge_blocks, 256, 0, s>>>(a);
 }
 
-// pinhole views take gaussian_bwd_compact_kernel unless OMR_GBWD_COMPACT=0 (the start value) or
-// omr_debug_gbwd_compact(0) says otherwise (A/B runs, tests)
-static std::atomic<int>& gbwd_compact_flag()
-{
-    static std::atomic<int> on{[] {
-        const char* v = std::getenv("OMR_GBWD_COMPACT");
-        return (v && v[0] == '0') ? 0 : 1;
-    }()};
-    return on;
-}
-static bool gbwd_compact_enabled() { return gbwd_compact_flag().load(std::memory_order_relaxed) != 0; }
-int gbwd_compact_set(int on) { return gbwd_compact_flag().exchange(on ? 1 : 0); }
-
 void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s, hipEvent_t ev_start,
                               hipEvent_t ev_stop)
 {
@@ -978,15 +877,10 @@ void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_
     const dim3 grid(div_up(a.g_end - a.g_begin, 256));
     const bool m16 = a.M == 16 && (reinterpret_cast<uintptr_t>(a.dL_dsh) % 16) == 0 &&
                      (reinterpret_cast<uintptr_t>(a.shs) % 16) == 0;
-    // pinhole views (frustum culling) take the compacted kernel; lonlat views see (nearly) every Gaussian
-    const bool compact = m16 && camera_type == CAM_PINHOLE && gbwd_compact_enabled();
     auto k = camera_type == CAM_LONLAT ? (m16 ? gaussian_bwd_kernel<CAM_LONLAT, 16> : gaussian_bwd_kernel<CAM_LONLAT, 0>)
-                                       : (compact ? gaussian_bwd_compact_kernel<CAM_PINHOLE>
-                                                  : (m16 ? gaussian_bwd_kernel<CAM_PINHOLE, 16>
-                                                         : gaussian_bwd_kernel<CAM_PINHOLE, 0>));
-    const dim3 g = compact ? dim3(div_up(a.g_end - a.g_begin, GB_SPAN)) : grid;
-    if (ev_start || ev_stop) hipExtLaunchKernelGGL(k, g, dim3(256), 0, s, ev_start, ev_stop, 0, a);
-    else k<<<g, 256, 0, s>>>(a);
+                                       : (m16 ? gaussian_bwd_kernel<CAM_PINHOLE, 16> : gaussian_bwd_kernel<CAM_PINHOLE, 0>);
+    if (ev_start || ev_stop) hipExtLaunchKernelGGL(k, grid, dim3(256), 0, s, ev_start, ev_stop, 0, a);
+    else k<<<grid, 256, 0, s>>>(a);
 }
 
 }  // namespace omr

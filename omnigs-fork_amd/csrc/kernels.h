@@ -260,7 +260,6 @@ struct GaussBwdArgs {
     float* dpx_dt;       // [P,3] optional (lonlat only; may be null)
     float* dpy_dt;       // [P,3] optional
 };
-int gbwd_compact_set(int on);  // gaussian_bwd.hip: pinhole views' compacted kernel on / off; returns the previous
 void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_t s, hipEvent_t ev_start = nullptr,
                               hipEvent_t ev_stop = nullptr);
 // Per-Gaussian sums of the render backward's instance rows: Gaussian i owns rows [row_first[i], row_first[i] +

@@ -1361,29 +1361,25 @@ int radix_sort_pairs(K* key_a, K* key_b, uint32_t* val_a, uint32_t* val_b, uint3
     return cur;
 }
 
-// ---- the depth sort (DepthPass above) -----------------------------------------------------------------------------
-// One histogram launch (depth_hist_kernel: the digit totals of all four passes), then pass 0 over all n keys and
-// passes 1..3 over the visible ones, each a onesweep launch whose blocks past the visible count return at once. Past
-// OS_MAX_BLOCKS tiles pass 0 runs as upsweep / look-back scan / downsweep instead (one onesweep launch over 5 M keys
-// takes 70 us against 52; profiles); passes 1..3 stay onesweep over the capacity grid, whose live
-// part is the visible keys' (config E pinhole: 0.6 M of 5 M).
-// scratch (hist): onesweep status [4][nb][RADIX] | digit totals [4][RADIX] | tickets [4] | error word | depth words [4]
-//                 | pass 0's [RADIX][nb0] histogram (upsweep path only)
-static size_t depth_os_words(size_t n)
+// ---- the depth sort (DepthPass above): four onesweep passes, or upsweep / scan / downsweep per pass -----------------
+// scratch (hist): the plain sort's over four passes (radix_scratch_words), then the depth words [4]
+static size_t depth_words_at(size_t n)
 {
-    return (size_t)DEPTH_PASSES * div_up(n, os_tile(n)) * RADIX + (size_t)DEPTH_PASSES * (RADIX + 1) + 1;
+    return use_onesweep(n) ? onesweep_words(n, DEPTH_PASSES) : radix_hist_size(n);
 }
-size_t depth_sort_scratch_words(size_t n)
-{
-    return depth_os_words(n) + 4 + (use_onesweep(n) ? 0 : radix_hist_size(n));
-}
+size_t depth_sort_scratch_words(size_t n) { return radix_scratch_words(n, DEPTH_PASSES) + 4; }
 size_t depth_sort_partials_words(size_t n) { return radix_partials_words(n); }
 ZeroSpan depth_sort_zero_span(uint32_t* hist, size_t n)
 {
     ZeroSpan z;
     if (n == 0) return z;
-    z.p = hist + (size_t)DEPTH_PASSES * div_up(n, os_tile(n)) * RADIX;  // digit totals, tickets, error word, words
-    z.n = (size_t)DEPTH_PASSES * (RADIX + 1) + 1 + 4;
+    if (use_onesweep(n)) {  // digit totals, tickets, error word (radix_zero_span), then the words, contiguous
+        z = radix_zero_span(hist, n, DEPTH_PASSES);
+        z.n += 4;
+    } else {
+        z.p = hist + depth_words_at(n);
+        z.n = 4;
+    }
     return z;
 }
 
@@ -1391,37 +1387,45 @@ void depth_sort(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val
                 uint32_t* scan_partials, size_t n, hipStream_t s, uint32_t* err)
 {
     if (n == 0) return;
-    const uint32_t nb = div_up(n, os_tile(n));
-    uint32_t* status = hist;
-    uint32_t* ghist = hist + (size_t)DEPTH_PASSES * nb * RADIX;
-    uint32_t* tickets = ghist + (size_t)DEPTH_PASSES * RADIX;
-    uint32_t* words = hist + depth_os_words(n);
+    uint32_t* words = hist + depth_words_at(n);
     uint32_t *ki = key_a, *ko = key_b, *vi = val_a, *vo = val_b;
-    depth_hist_kernel<<<std::min(div_up(n, OS_HIST_THREADS), OS_HIST_BLOCKS), OS_HIST_THREADS, 0, s>>>(
-        key_a, n, status, (size_t)DEPTH_PASSES * nb * RADIX, ghist);
-    auto kern = os_tile(n) == OS_TILE ? onesweep_kernel<uint32_t, OS_TILE, true>
-                                      : onesweep_kernel<uint32_t, OS_TILE_SMALL, true>;
+    if (use_onesweep(n)) {
+        const uint32_t nb = div_up(n, os_tile(n));
+        uint32_t* status = hist;
+        uint32_t* ghist = hist + (size_t)DEPTH_PASSES * nb * RADIX;
+        uint32_t* tickets = ghist + (size_t)DEPTH_PASSES * RADIX;
+        depth_hist_kernel<<<std::min(div_up(n, OS_HIST_THREADS), OS_HIST_BLOCKS), OS_HIST_THREADS, 0, s>>>(
+            key_a, n, status, (size_t)DEPTH_PASSES * nb * RADIX, ghist);
+        for (int p = 0; p < DEPTH_PASSES; ++p) {
+            DepthPass dp;
+            dp.pass = p;
+            dp.vals_final = order;
+            auto kern = os_tile(n) == OS_TILE ? onesweep_kernel<uint32_t, OS_TILE, true>
+                                              : onesweep_kernel<uint32_t, OS_TILE_SMALL, true>;
+            kern<<<nb, OS_THREADS, 0, s>>>(ki, vi, ko, vo, n, nullptr, nullptr, 0,
+                                            status + (size_t)p * nb * RADIX, ghist + (size_t)p * RADIX, tickets + p,
+                                            err, dp);
+            std::swap(ki, ko);
+            std::swap(vi, vo);
+        }
+        return;
+    }
+    const uint32_t nb = div_up(n, SORT_TILE);
+    const uint32_t nbs = div_up((size_t)RADIX * nb, SCAN_TILE);
+    uint64_t* lb = reinterpret_cast<uint64_t*>(scan_partials);
+    uint32_t* lb_ticket = scan_partials + 2 * (size_t)nbs;
     for (int p = 0; p < DEPTH_PASSES; ++p) {
         DepthPass dp;
         dp.pass = p;
         dp.words = words;
         dp.vals_final = order;
-        if (p == 0 && !use_onesweep(n)) {
-            const uint32_t nb0 = div_up(n, SORT_TILE);
-            uint32_t* hist0 = words + 4;
-            const uint32_t nbs = div_up((size_t)RADIX * nb0, SCAN_TILE);
-            uint64_t* lb = reinterpret_cast<uint64_t*>(scan_partials);
-            uint32_t* lb_ticket = scan_partials + 2 * (size_t)nbs;
-            radix_upsweep_kernel<uint32_t, false, SORT_ITEMS_S, SORT_THREADS_S, true><<<nb0, SORT_THREADS_S, 0, s>>>(
-                ki, n, nullptr, 0, hist0, nb0, scan_partials, 2 * nbs + 2, dp);
-            scan_lookback_kernel<<<std::min(nbs, SCAN_GRID_MAX), SCAN_THREADS, 0, s>>>(
-                hist0, hist0, (size_t)RADIX * nb0, nullptr, lb, lb_ticket, err ? err : lb_ticket + 1);
-            radix_downsweep_kernel<uint32_t, false, SORT_ITEMS_S, SORT_THREADS_S, true><<<nb0, SORT_THREADS_S, 0, s>>>(
-                ki, vi, ko, vo, n, nullptr, nullptr, 0, hist0, nb0, dp);
-        } else {
-            kern<<<nb, OS_THREADS, 0, s>>>(ki, vi, ko, vo, n, nullptr, nullptr, 0, status + (size_t)p * nb * RADIX,
-                                            ghist + (size_t)p * RADIX, tickets + p, err, dp);
-        }
+        const uint32_t* count = p == 0 ? nullptr : words;
+        radix_upsweep_kernel<uint32_t, false, SORT_ITEMS_S, SORT_THREADS_S, true><<<nb, SORT_THREADS_S, 0, s>>>(
+            ki, n, count, 0, hist, nb, scan_partials, 2 * nbs + 2, dp);
+        scan_lookback_kernel<<<std::min(nbs, SCAN_GRID_MAX), SCAN_THREADS, 0, s>>>(
+            hist, hist, (size_t)RADIX * nb, nullptr, lb, lb_ticket, err ? err : lb_ticket + 1);
+        radix_downsweep_kernel<uint32_t, false, SORT_ITEMS_S, SORT_THREADS_S, true><<<nb, SORT_THREADS_S, 0, s>>>(
+            ki, vi, ko, vo, n, count, nullptr, 0, hist, nb, dp);
         std::swap(ki, ko);
         std::swap(vi, vo);
     }

@@ -73,8 +73,6 @@ def lib() -> C.CDLL:
         L.omr_debug_image_state.argtypes = [vp, i, i, vp, vp, vp]
         L.omr_debug_tile_cost.argtypes = [vp, i, i, vp, vp]
         L.omr_debug_counters.argtypes = [vp, i, vp, vp]
-        L.omr_debug_gbwd_compact.restype = i
-        L.omr_debug_gbwd_compact.argtypes = [i]
         L.omr_debug_depth_sort_mode.restype = i
         L.omr_debug_depth_sort_mode.argtypes = [i]
         L.omr_debug_set_sh_jac.restype = i
@@ -569,12 +567,6 @@ def debug_depth_sort_mode(mode: int) -> int:
     if rc < 0:
         raise RasterizerError(f"debug_depth_sort_mode({mode}): {lib().omr_last_error().decode()}")
     return rc
-
-
-def debug_gbwd_compact(on: bool) -> bool:
-    """Pinhole views' per-Gaussian backward: the compacted kernel (True, the default) or one wave per 64 Gaussians
-    (omr_debug_gbwd_compact). Process-wide; returns the previous setting."""
-    return bool(lib().omr_debug_gbwd_compact(1 if on else 0))
 
 
 def debug_set_sh_jac(P, geomBuffer, enabled: bool):

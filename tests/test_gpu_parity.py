@@ -278,49 +278,6 @@ def test_depth_sort_multi_launch_path_with_culled_gaussians(oracle_mt, depth_sor
     _compare(g, cam, None, nthreads=oracle_mt)
 
 
-@pytest.mark.parametrize("P,W,H,view,jac,skip_dsh", [(30000, 320, 180, 3, True, False),
-                                                    (30000, 320, 180, 5, False, False),
-                                                    (5000, 160, 90, 0, True, False), (30000, 320, 180, 3, True, True),
-                                                    (30000, 320, 180, 5, False, True)])
-def test_compacted_gaussian_backward_matches_the_wave_kernel(P, W, H, view, jac, skip_dsh):
-    """Pinhole views run the per-Gaussian backward compacted (gaussian_bwd.hip: gaussian_bwd_compact_kernel; a
-    workgroup lists its span's visible Gaussians and runs them densely, zeros the culled ones' outputs). Same
-    arithmetic per Gaussian as the wave-per-64 kernel: every gradient bitwise equal, with the stored dRGB/ddir and
-    with the SH rows read (jac False), with dL_dsh not written (skip_dsh: the compact exchange's backward), and
-    against the oracle (test_parity's pinhole cases, E_pinhole at full size)."""
-    g, cam, dL = make_case(P, W, H, PIN, 71, view_index=view, spread=2.0)
-    R = omr.rasterizer
-
-    def run():
-        h = hip_run(g, cam, None)
-        if not jac:
-            R.debug_set_sh_jac(g.P, h["geom"], False)
-        import torch
-
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).cuda()  # noqa: E731
-        e = torch.empty(0, device="cuda")
-        gr = R.RasterizeGaussiansBackwardCUDA(torch.zeros(3, device="cuda"), t(g.means3D), h["radii"], e,
-                                              t(g.scales), t(g.rotations), 1.0, e, t(cam.viewmatrix),
-                                              t(cam.projmatrix), cam.tanfovx, cam.tanfovy, t(dL), t(g.shs),
-                                              g.sh_degree, t(cam.campos), h["geom"], h["L"], h["binning"], h["img"],
-                                              cam.camera_type, skip_dsh=skip_dsh)
-        torch.cuda.synchronize()
-        if skip_dsh:
-            assert gr[5] is None
-        return [to_np(x) for x in gr if x is not None], to_np(h["radii"])
-
-    old = R.debug_gbwd_compact(True)
-    try:
-        compact, radii = run()
-        R.debug_gbwd_compact(False)
-        wave, _ = run()
-    finally:
-        R.debug_gbwd_compact(old)
-    assert 0 < (radii > 0).sum() < g.P  # some culled, some visible
-    for a, b in zip(compact, wave):
-        np.testing.assert_array_equal(a, b)
-
-
 def test_row_binning_reports_its_row_slots():
     """bin.hip's rows pass: M = the sum of the visible Gaussians' rect heights (counters[4])."""
     g, cam, _ = make_case(3000, 512, 256, LON, 53, view_index=1, spread=1.5)
