@@ -279,6 +279,10 @@ int omr_debug_set_sh_jac(char* geom_buffer, int P, int enabled, void* stream);
  * process-wide, for tests and A/B runs (the environment's OMR_DEPTH_SORT=bytes / visible sets the start value).
  * Returns the previous mode, or -1 for a mode outside 0..2 (omr_last_error says why) */
 int omr_debug_depth_sort_mode(int mode);
+/* omr_l1_ssim_loss's kernel: 0 = by image size (the streaming kernel once its strips fill the chip, else the tiled
+ * one), 1 = always tiled, 2 = always streaming (both give bitwise the same dL_dimg); process-wide, for tests and A/B
+ * runs. Returns the previous mode, or -1 for a mode outside 0..2 */
+int omr_debug_ssim_mode(int mode);
 /* per-Gaussian pixel centre [P,2], conic+opacity [P,4], rgb [P,3], depth [P], tiles_touched [P] */
 /* one wave64 through the render backward's gradient reduction: in [64][9] -> out [9] (column sums) */
 int omr_debug_wave_sum9(const float* in, float* out, void* stream); /* wave_sum9_rows */

@@ -1334,6 +1334,15 @@ int omr_debug_depth_sort_mode(int mode)
     return old;
 }
 
+int omr_debug_ssim_mode(int mode)
+{
+    if (mode < 0 || mode > 2) {
+        fail(OMR_ERR_INVALID_ARGUMENT, "ssim mode: 0 (by image size), 1 (tiled), 2 (streaming)");
+        return -1;
+    }
+    return ssim_debug_mode(mode);
+}
+
 int omr_debug_set_sh_jac(char* geom_buffer, int P, int enabled, void* stream)
 {
     g_last_error.clear();

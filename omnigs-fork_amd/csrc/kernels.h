@@ -284,6 +284,8 @@ SsimWindow ssim_window();
 size_t l1_ssim_scratch_floats(int C, int H, int W);
 void launch_l1_ssim(const float* img, const float* gt, int C, int H, int W, float lambda, float* dimg, float* out3,
                     float* scratch, hipStream_t s);
+// 0: kernel by image size, 1: tiled, 2: streaming; returns the previous mode (omr_debug_ssim_mode)
+int ssim_debug_mode(int mode);
 
 // optim.hip: Adam over the GaussianModel groups, densification stats, densifyAndPrune, resetOpacity
 constexpr int ADAM_MAX_GROUPS = 6;

@@ -16,7 +16,12 @@
 //     dL/dx = dL/dS (G * A + 2 x G * B + y G * C) + (1 - lambda) sign(x - y) / (C H W).
 // Per-block partial sums of S and |x - y| go to scratch; loss_finish_kernel adds them in a fixed order, so the loss
 // is deterministic. HBM: reads img and gt once (plus halo), writes dL/dimg once: 12 B per pixel-channel.
+//
+// Both kernels (tiled, streaming) sum every filter's taps in the same order with fused multiply-adds and form SSIM
+// and its partials with the same helper (ssim_partials), so their dL/dimg is bitwise identical
+// (tests/test_gpu_losses.py). The streaming kernel runs the x | y and x^2 | y^2 taps as packed FMAs.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 
 #include "kernels.h"
@@ -33,6 +38,38 @@ constexpr int SS_R1 = SS_TILE + 2 * SS_HALO;  // 26: SSIM values feeding the til
 constexpr int SS_R2 = SS_R1 + 2 * SS_HALO;    // 36: input region
 constexpr float SS_C1 = 0.01f * 0.01f;
 constexpr float SS_C2 = 0.03f * 0.03f;
+
+// 0: by image size, 1: tiled, 2: streaming (omr_debug_ssim_mode: tests run both kernels on the same images)
+std::atomic<int> g_ssim_mode{0};
+
+// SSIM at one position from its five local moments E[x], E[y], E[x^2], E[y^2], E[xy], and its partials times dL/dS
+//   A = dS/dmu1, B = dS/dE[x^2], C = dS/dE[xy] (zero outside the image: the zero padding's positions have no SSIM)
+// One reciprocal (v_rcp_f32, 1 ulp) for the three quotients: den = a2 b2 >= C1 C2 > 0; 1 / b2 = a2 / den.
+struct SsimPart {
+    float S, A, B, C;
+};
+__device__ __forceinline__ SsimPart ssim_partials(float mu1, float mu2, float exx, float eyy, float exy, float dS,
+                                                  bool in)
+{
+    const float mu1_sq = mu1 * mu1, mu2_sq = mu2 * mu2, mu1_mu2 = mu1 * mu2;
+    const float s11 = exx - mu1_sq, s22 = eyy - mu2_sq, s12 = exy - mu1_mu2;
+    const float a1 = 2.f * mu1_mu2 + SS_C1, b1 = 2.f * s12 + SS_C2;
+    const float a2 = mu1_sq + mu2_sq + SS_C1, b2 = s11 + s22 + SS_C2;
+    const float inv = __builtin_amdgcn_rcpf(a2 * b2);
+    SsimPart p;
+    p.S = (a1 * b1) * inv;
+    p.A = in ? dS * ((2.f * mu2 * (b1 - a1)) * inv - p.S * (2.f * mu1 * (b2 - a2)) * inv) : 0.f;
+    p.B = in ? dS * (-p.S * (a2 * inv)) : 0.f;
+    p.C = in ? dS * (2.f * a1 * inv) : 0.f;
+    return p;
+}
+// dL/dimg at one pixel from its back-filtered partials: dL/dS (G*A + 2 x G*B + y G*C) + (1 - lambda) sign(x - y) / n
+__device__ __forceinline__ float ssim_pixel_grad(float fa, float fb, float fc, float x, float y, float l1_scale)
+{
+    const float d = x - y;
+    const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);  // torch.abs backward: sign(0) = 0
+    return fa + 2.f * x * fb + y * fc + l1_scale * sgn;
+}
 
 __global__ __launch_bounds__(256) void l1_ssim_kernel(const float* img, const float* gt, int H, int W, SsimWindow win,
                                                       float l1_scale, float dS_scale, float* dimg, float* partials)
@@ -68,11 +105,11 @@ __global__ __launch_bounds__(256) void l1_ssim_kernel(const float* img, const fl
 #pragma unroll
         for (int k = 0; k < SS_WIN; ++k) {
             const float x = s_x[r][c + k], y = s_y[r][c + k];
-            hx += w[k] * x;
-            hy += w[k] * y;
-            hxx += w[k] * (x * x);
-            hyy += w[k] * (y * y);
-            hxy += w[k] * (x * y);
+            hx = __builtin_fmaf(w[k], x, hx);
+            hy = __builtin_fmaf(w[k], y, hy);
+            hxx = __builtin_fmaf(w[k], x * x, hxx);
+            hyy = __builtin_fmaf(w[k], y * y, hyy);
+            hxy = __builtin_fmaf(w[k], x * y, hxy);
         }
         s_h[0][r][c] = hx;
         s_h[1][r][c] = hy;
@@ -88,7 +125,7 @@ __global__ __launch_bounds__(256) void l1_ssim_kernel(const float* img, const fl
         for (int q = 0; q < 5; ++q) {
             float m = 0.f;
 #pragma unroll
-            for (int k = 0; k < SS_WIN; ++k) m += w[k] * s_h[q][r + k][c];
+            for (int k = 0; k < SS_WIN; ++k) m = __builtin_fmaf(w[k], s_h[q][r + k][c], m);
             s_m[q][r][c] = m;
         }
     }
@@ -98,26 +135,14 @@ __global__ __launch_bounds__(256) void l1_ssim_kernel(const float* img, const fl
     for (int i = t; i < SS_R1 * SS_R1; i += 256) {
         const int r = i / SS_R1, c = i - r * SS_R1;
         const int gy = oy - SS_HALO + r, gx = ox - SS_HALO + c;
-        const float mu1 = s_m[0][r][c], mu2 = s_m[1][r][c];
-        const float mu1_sq = mu1 * mu1, mu2_sq = mu2 * mu2, mu1_mu2 = mu1 * mu2;
-        const float s11 = s_m[2][r][c] - mu1_sq, s22 = s_m[3][r][c] - mu2_sq, s12 = s_m[4][r][c] - mu1_mu2;
-        const float a1 = 2.f * mu1_mu2 + SS_C1, b1 = 2.f * s12 + SS_C2;
-        const float a2 = mu1_sq + mu2_sq + SS_C1, b2 = s11 + s22 + SS_C2;
-        const float den = a2 * b2;
-        const float S = (a1 * b1) / den;
         const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
-        float A = 0.f, B = 0.f, C = 0.f;
-        if (in) {
-            const float inv = 1.f / den;
-            A = dS_scale * ((2.f * mu2 * (b1 - a1)) * inv - S * (2.f * mu1 * (b2 - a2)) * inv);
-            B = dS_scale * (-S / b2);
-            C = dS_scale * (2.f * a1 * inv);
-            if (r >= SS_HALO && r < SS_HALO + SS_TILE && c >= SS_HALO && c < SS_HALO + SS_TILE) ssim_sum += S;
-        }
+        const SsimPart p = ssim_partials(s_m[0][r][c], s_m[1][r][c], s_m[2][r][c], s_m[3][r][c], s_m[4][r][c],
+                                         dS_scale, in);
+        if (in && r >= SS_HALO && r < SS_HALO + SS_TILE && c >= SS_HALO && c < SS_HALO + SS_TILE) ssim_sum += p.S;
         // s_m[0..2] are read only by this thread at this position: overwrite in place
-        s_m[0][r][c] = A;
-        s_m[1][r][c] = B;
-        s_m[2][r][c] = C;
+        s_m[0][r][c] = p.A;
+        s_m[1][r][c] = p.B;
+        s_m[2][r][c] = p.C;
     }
     __syncthreads();
     // 5. horizontal pass of A, B, C: rows 0..25, columns 0..15
@@ -127,7 +152,7 @@ __global__ __launch_bounds__(256) void l1_ssim_kernel(const float* img, const fl
         for (int q = 0; q < 3; ++q) {
             float h = 0.f;
 #pragma unroll
-            for (int k = 0; k < SS_WIN; ++k) h += w[k] * s_m[q][r][c + k];
+            for (int k = 0; k < SS_WIN; ++k) h = __builtin_fmaf(w[k], s_m[q][r][c + k], h);
             s_h[q][r][c] = h;
         }
     }
@@ -138,17 +163,15 @@ __global__ __launch_bounds__(256) void l1_ssim_kernel(const float* img, const fl
     float fa = 0.f, fb = 0.f, fc = 0.f;
 #pragma unroll
     for (int k = 0; k < SS_WIN; ++k) {
-        fa += w[k] * s_h[0][r + k][c];
-        fb += w[k] * s_h[1][r + k][c];
-        fc += w[k] * s_h[2][r + k][c];
+        fa = __builtin_fmaf(w[k], s_h[0][r + k][c], fa);
+        fb = __builtin_fmaf(w[k], s_h[1][r + k][c], fb);
+        fc = __builtin_fmaf(w[k], s_h[2][r + k][c], fc);
     }
     float l1_sum = 0.f;
     if (gy < H && gx < W) {
         const float x = s_x[r + 2 * SS_HALO][c + 2 * SS_HALO], y = s_y[r + 2 * SS_HALO][c + 2 * SS_HALO];
-        const float d = x - y;
-        const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);  // torch.abs backward: sign(0) = 0
-        dimg[ch * plane + (size_t)gy * W + gx] = fa + 2.f * x * fb + y * fc + l1_scale * sgn;
-        l1_sum = fabsf(d);
+        dimg[ch * plane + (size_t)gy * W + gx] = ssim_pixel_grad(fa, fb, fc, x, y, l1_scale);
+        l1_sum = fabsf(x - y);
     }
     // 7. block partial sums (fixed order: wave shuffle tree, then the 4 waves in order)
 #pragma unroll
@@ -173,16 +196,24 @@ __global__ __launch_bounds__(256) void l1_ssim_kernel(const float* img, const fl
 // bottom. Each lane owns one column of the 64 product / partial columns (x0-5 .. x0+58) and keeps, in registers,
 // rings of the last 11 rows of its column's horizontally filtered products (5 values) and of its output column's
 // horizontally back-filtered partials (3 values), so every vertical 11-tap pass is register-only and every value is
-// computed once per strip instead of once per 16x16 tile (36x26 / 26x26 halo regions there). LDS holds one input
-// row (x, y) and one row of partials. Per input row i: horizontal products of row i; moments, SSIM and partials
-// of row i - 5; the back-filtered gradient of output row i - 10. The taps are summed in the same order as the tiled
-// kernel above, so dL/dimg is bitwise the same; the loss sums differ only in their (fixed) blocking.
+// computed once per strip instead of once per 16x16 tile (36x26 / 26x26 halo regions there). Per input row i:
+// horizontal products of row i; moments, SSIM and partials of row i - 5; the back-filtered gradient of output row
+// i - 10.
+//  * Input rows are requested 11 rows ahead into registers (3 words per lane per row: x and y of the lane's column,
+//    and one of the 20 words of the strip's last 10 columns), one ring slot per unrolled row, so a row's loads have
+//    eleven rows of filtering to land in; the only other vector-memory operation is the gradient store.
+//  * LDS keeps the last 11 input rows (x, y): the output row's own x and y (row i - 10) come from there, not from a
+//    second global load whose wait would also wait for every prefetch issued before it.
+//  * x^2, y^2, xy are formed once per input column (not once per tap); the x | y and x^2 | y^2 taps, the vertical
+//    moment pairs and the A | B back-filter pairs are v_pk_fma_f32 — the kernel is VALU-bound once the loads are
+//    hidden (VALU per row: ~450 issue slots as separate multiply + add, ~190 fused and packed).
 #ifndef OMR_SSIM_ROWS
 #define OMR_SSIM_ROWS 48
 #endif
 constexpr int ST_OUT = 54;  // output columns per strip: lanes 0..53
 constexpr int ST_IN = 74;   // input columns x0-10 .. x0+63
 constexpr int ST_ROWS = OMR_SSIM_ROWS;
+constexpr int ST_EXTRA = ST_IN - 64;  // input columns past the wave's 64 lanes
 
 struct StreamCtx {
     const float* X;
@@ -192,103 +223,116 @@ struct StreamCtx {
     float* dimg;
 };
 
-// this lane's input columns (lane and 64 + lane) of row i, zero outside the image
-__device__ __forceinline__ void ssim_load_row(const StreamCtx& c, int i, float2 (&pre)[2])
+// this lane's three words of input row i: x and y of input column `lane`, and x (lanes 0..9) or y (lanes 10..19) of
+// input column 64 + lane % 10; zero outside the image and past the strip's last input row (never requested)
+struct RowWords {
+    float x, y, e;
+};
+__device__ __forceinline__ RowWords ssim_fetch_row(const StreamCtx& c, int i)
 {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int k = c.lane + 64 * h;
-        const int gx = c.x0 - 2 * SS_HALO + k;
-        const bool in = k < ST_IN && i >= 0 && i < c.H && gx >= 0 && gx < c.W;
-        pre[h] = in ? make_float2(c.X[(size_t)i * c.W + gx], c.Y[(size_t)i * c.W + gx]) : make_float2(0.f, 0.f);
+    RowWords r{0.f, 0.f, 0.f};
+    if (i > c.i1 || i < 0 || i >= c.H) return r;  // wave-uniform
+    const size_t row = (size_t)i * c.W;
+    const int gx = c.x0 - 2 * SS_HALO + c.lane;
+    if (gx >= 0 && gx < c.W) {
+        r.x = c.X[row + gx];
+        r.y = c.Y[row + gx];
     }
+    const bool ex = c.lane < ST_EXTRA;
+    const int ge = c.x0 - 2 * SS_HALO + 64 + (ex ? c.lane : c.lane - ST_EXTRA);  // >= 54 > 0
+    if (c.lane < 2 * ST_EXTRA && ge < c.W) r.e = (ex ? c.X : c.Y)[row + ge];
+    return r;
 }
 
 template <int S>
-__device__ __forceinline__ void ssim_stream_row(const StreamCtx& c, const float* w, int i, float2 (*s_in)[ST_IN],
-                                                float4* s_p, float (&hb)[SS_WIN][5], float (&hd)[SS_WIN][3],
-                                                float2 (&pre)[2], float& ssim_sum, float& l1_sum)
+__device__ __forceinline__ void ssim_stream_row(const StreamCtx& c, const float* w, int i, float2 (*s_xy)[ST_IN],
+                                                float4* s_sq, float4* s_p, f2v (&hm)[SS_WIN], f2v (&hs)[SS_WIN],
+                                                float (&hc)[SS_WIN], f2v (&dab)[SS_WIN], float (&dc)[SS_WIN],
+                                                RowWords (&pre)[SS_WIN], float& ssim_sum, float& l1_sum)
 {
     if (i > c.i1) return;  // wave-uniform
     const int lane = c.lane;
-    // A. input row i to LDS (a one-row register prefetch measured no faster); horizontal products at product
-    //    column x0 - 5 + lane
-    float2* buf = s_in[i & 1];
-    ssim_load_row(c, i, pre);
-    buf[lane] = pre[0];
-    if (lane < ST_IN - 64) buf[64 + lane] = pre[1];
-    wave_sync();
+    float2* row = s_xy[S];  // ring slot of input row i (rows base .. base + 10 of this 11-row step)
+    wave_sync();  // the previous row's LDS reads before this row's writes (other lanes read what a lane overwrites)
+    // A. input row i to LDS; row i + 11 requested into the registers it came from
     {
-        float hx = 0.f, hy = 0.f, hxx = 0.f, hyy = 0.f, hxy = 0.f;
+        const RowWords r = pre[S];
+        row[lane] = make_float2(r.x, r.y);
+        if (lane < ST_EXTRA) row[64 + lane].x = r.e;
+        else if (lane < 2 * ST_EXTRA) row[64 + lane - ST_EXTRA].y = r.e;
+        s_sq[lane] = make_float4(r.x * r.x, r.y * r.y, r.x * r.y, 0.f);
+        pre[S] = ssim_fetch_row(c, i + SS_WIN);
+    }
+    wave_sync();
+    if (lane < ST_EXTRA) {  // the last 10 columns' products: their x and y came from two lanes
+        const float2 v = row[64 + lane];
+        s_sq[64 + lane] = make_float4(v.x * v.x, v.y * v.y, v.x * v.y, 0.f);
+    }
+    wave_sync();
+    // B. horizontal 11-tap pass of x | y, x^2 | y^2, xy at product column x0 - 5 + lane
+    {
+        f2v m = {0.f, 0.f}, q = {0.f, 0.f};
+        float xy = 0.f;
 #pragma unroll
         for (int k = 0; k < SS_WIN; ++k) {
-            const float2 v = buf[lane + k];
-            hx += w[k] * v.x;
-            hy += w[k] * v.y;
-            hxx += w[k] * (v.x * v.x);
-            hyy += w[k] * (v.y * v.y);
-            hxy += w[k] * (v.x * v.y);
+            const f2v wk = {w[k], w[k]};
+            const float2 v = row[lane + k];
+            const float4 p = s_sq[lane + k];
+            m = __builtin_elementwise_fma(wk, f2v{v.x, v.y}, m);
+            q = __builtin_elementwise_fma(wk, f2v{p.x, p.y}, q);
+            xy = __builtin_fmaf(w[k], p.z, xy);
         }
-        hb[S][0] = hx, hb[S][1] = hy, hb[S][2] = hxx, hb[S][3] = hyy, hb[S][4] = hxy;
+        hm[S] = m;
+        hs[S] = q;
+        hc[S] = xy;
     }
-    // B. moments, SSIM and partials of row m = i - 5 (the ring holds input rows i-10 .. i)
+    // C. moments, SSIM and partials of row m = i - 5 (the ring holds input rows i-10 .. i)
     if (i >= c.y0) {
-        const int m = i - SS_HALO, pc = c.x0 - SS_HALO + lane;
-        float mo[5];
+        const int mr = i - SS_HALO, pc = c.x0 - SS_HALO + lane;
+        f2v mu = {0.f, 0.f}, ex2 = {0.f, 0.f};
+        float exy = 0.f;
 #pragma unroll
-        for (int q = 0; q < 5; ++q) {
-            float acc = 0.f;
-#pragma unroll
-            for (int k = 0; k < SS_WIN; ++k) acc += w[k] * hb[(S + 1 + k) % SS_WIN][q];
-            mo[q] = acc;
+        for (int k = 0; k < SS_WIN; ++k) {
+            const int j = (S + 1 + k) % SS_WIN;
+            const f2v wk = {w[k], w[k]};
+            mu = __builtin_elementwise_fma(wk, hm[j], mu);
+            ex2 = __builtin_elementwise_fma(wk, hs[j], ex2);
+            exy = __builtin_fmaf(w[k], hc[j], exy);
         }
-        const float mu1 = mo[0], mu2 = mo[1];
-        const float mu1_sq = mu1 * mu1, mu2_sq = mu2 * mu2, mu1_mu2 = mu1 * mu2;
-        const float s11 = mo[2] - mu1_sq, s22 = mo[3] - mu2_sq, s12 = mo[4] - mu1_mu2;
-        const float a1 = 2.f * mu1_mu2 + SS_C1, b1 = 2.f * s12 + SS_C2;
-        const float a2 = mu1_sq + mu2_sq + SS_C1, b2 = s11 + s22 + SS_C2;
-        const float den = a2 * b2;
-        const float Sv = (a1 * b1) / den;
-        const bool in = m >= 0 && m < c.H && pc >= 0 && pc < c.W;
-        float A = 0.f, B = 0.f, C = 0.f;
-        if (in) {
-            const float inv = 1.f / den;
-            A = c.dS_scale * ((2.f * mu2 * (b1 - a1)) * inv - Sv * (2.f * mu1 * (b2 - a2)) * inv);
-            B = c.dS_scale * (-Sv / b2);
-            C = c.dS_scale * (2.f * a1 * inv);
-            if (m >= c.y0 && m < c.y0 + ST_ROWS && lane >= SS_HALO && lane < SS_HALO + ST_OUT) ssim_sum += Sv;
-        }
-        s_p[lane] = make_float4(A, B, C, 0.f);
-        wave_sync();  // the next row's input sync separates these reads from the next write
+        const bool in = mr >= 0 && mr < c.H && pc >= 0 && pc < c.W;
+        const SsimPart p = ssim_partials(mu.x, mu.y, ex2.x, ex2.y, exy, c.dS_scale, in);
+        if (in && mr >= c.y0 && mr < c.y0 + ST_ROWS && lane >= SS_HALO && lane < SS_HALO + ST_OUT)
+            ssim_sum += p.S;  // the strip's own output rows and columns
+        s_p[lane] = make_float4(p.A, p.B, p.C, 0.f);
+        wave_sync();  // the next row's syncs separate these reads from the next write
         if (lane < ST_OUT) {
-            float fa = 0.f, fb = 0.f, fc = 0.f;
+            f2v ab = {0.f, 0.f};
+            float cc = 0.f;
 #pragma unroll
             for (int k = 0; k < SS_WIN; ++k) {
                 const float4 v = s_p[lane + k];
-                fa += w[k] * v.x;
-                fb += w[k] * v.y;
-                fc += w[k] * v.z;
+                ab = __builtin_elementwise_fma(f2v{w[k], w[k]}, f2v{v.x, v.y}, ab);
+                cc = __builtin_fmaf(w[k], v.z, cc);
             }
-            hd[S][0] = fa, hd[S][1] = fb, hd[S][2] = fc;
+            dab[S] = ab;
+            dc[S] = cc;
         }
     }
-    // D. output row o = i - 10 (the partial ring holds moment rows o-5 .. o+5)
+    // D. output row o = i - 10 (the partial ring holds moment rows o-5 .. o+5; the input ring holds row o)
     if (i >= c.y0 + 2 * SS_HALO && lane < ST_OUT) {
         const int o = i - 2 * SS_HALO, col = c.x0 + lane;
-        float fa = 0.f, fb = 0.f, fc = 0.f;
+        f2v ab = {0.f, 0.f};
+        float cc = 0.f;
 #pragma unroll
         for (int k = 0; k < SS_WIN; ++k) {
-            fa += w[k] * hd[(S + 1 + k) % SS_WIN][0];
-            fb += w[k] * hd[(S + 1 + k) % SS_WIN][1];
-            fc += w[k] * hd[(S + 1 + k) % SS_WIN][2];
+            const int j = (S + 1 + k) % SS_WIN;
+            ab = __builtin_elementwise_fma(f2v{w[k], w[k]}, dab[j], ab);
+            cc = __builtin_fmaf(w[k], dc[j], cc);
         }
         if (o < c.H && col < c.W) {
-            const size_t at = (size_t)o * c.W + col;
-            const float x = c.X[at], y = c.Y[at];
-            const float d = x - y;
-            const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-            c.dimg[at] = fa + 2.f * x * fb + y * fc + c.l1_scale * sgn;
-            l1_sum += fabsf(d);
+            const float2 v = s_xy[(S + 1) % SS_WIN][lane + 2 * SS_HALO];
+            c.dimg[(size_t)o * c.W + col] = ssim_pixel_grad(ab.x, ab.y, cc, v.x, v.y, c.l1_scale);
+            l1_sum += fabsf(v.x - v.y);
         }
     }
 }
@@ -297,8 +341,9 @@ __global__ __launch_bounds__(64) void l1_ssim_stream_kernel(const float* img, co
                                                             SsimWindow win, float l1_scale, float dS_scale,
                                                             float* dimg, float* partials)
 {
-    __shared__ float2 s_in[2][ST_IN];
-    __shared__ float4 s_p[64 + SS_WIN];
+    __shared__ float2 s_xy[SS_WIN][ST_IN];
+    __shared__ float4 s_sq[ST_IN];
+    __shared__ float4 s_p[64];
     const int ch = blockIdx.z;
     const size_t plane = (size_t)H * W;
     StreamCtx c;
@@ -313,29 +358,29 @@ __global__ __launch_bounds__(64) void l1_ssim_stream_kernel(const float* img, co
     float w[SS_WIN];
 #pragma unroll
     for (int k = 0; k < SS_WIN; ++k) w[k] = win.w[k];
-    if (threadIdx.x < SS_WIN) s_p[64 + threadIdx.x] = make_float4(0.f, 0.f, 0.f, 0.f);  // lanes 54..63 read up to 63
-    float hb[SS_WIN][5], hd[SS_WIN][3];
+    f2v hm[SS_WIN], hs[SS_WIN], dab[SS_WIN];
+    float hc[SS_WIN], dc[SS_WIN];
+    RowWords pre[SS_WIN];
+    const int first = c.y0 - 2 * SS_HALO;
 #pragma unroll
     for (int k = 0; k < SS_WIN; ++k) {
-#pragma unroll
-        for (int q = 0; q < 5; ++q) hb[k][q] = 0.f;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) hd[k][q] = 0.f;
+        hm[k] = hs[k] = dab[k] = f2v{0.f, 0.f};
+        hc[k] = dc[k] = 0.f;
+        pre[k] = ssim_fetch_row(c, first + k);
     }
     float ssim_sum = 0.f, l1_sum = 0.f;
-    float2 pre[2];
-    for (int base = c.y0 - 2 * SS_HALO; base <= c.i1; base += SS_WIN) {
-        ssim_stream_row<0>(c, w, base + 0, s_in, s_p, hb, hd, pre, ssim_sum, l1_sum);
-        ssim_stream_row<1>(c, w, base + 1, s_in, s_p, hb, hd, pre, ssim_sum, l1_sum);
-        ssim_stream_row<2>(c, w, base + 2, s_in, s_p, hb, hd, pre, ssim_sum, l1_sum);
-        ssim_stream_row<3>(c, w, base + 3, s_in, s_p, hb, hd, pre, ssim_sum, l1_sum);
-        ssim_stream_row<4>(c, w, base + 4, s_in, s_p, hb, hd, pre, ssim_sum, l1_sum);
-        ssim_stream_row<5>(c, w, base + 5, s_in, s_p, hb, hd, pre, ssim_sum, l1_sum);
-        ssim_stream_row<6>(c, w, base + 6, s_in, s_p, hb, hd, pre, ssim_sum, l1_sum);
-        ssim_stream_row<7>(c, w, base + 7, s_in, s_p, hb, hd, pre, ssim_sum, l1_sum);
-        ssim_stream_row<8>(c, w, base + 8, s_in, s_p, hb, hd, pre, ssim_sum, l1_sum);
-        ssim_stream_row<9>(c, w, base + 9, s_in, s_p, hb, hd, pre, ssim_sum, l1_sum);
-        ssim_stream_row<10>(c, w, base + 10, s_in, s_p, hb, hd, pre, ssim_sum, l1_sum);
+    for (int base = first; base <= c.i1; base += SS_WIN) {
+        ssim_stream_row<0>(c, w, base + 0, s_xy, s_sq, s_p, hm, hs, hc, dab, dc, pre, ssim_sum, l1_sum);
+        ssim_stream_row<1>(c, w, base + 1, s_xy, s_sq, s_p, hm, hs, hc, dab, dc, pre, ssim_sum, l1_sum);
+        ssim_stream_row<2>(c, w, base + 2, s_xy, s_sq, s_p, hm, hs, hc, dab, dc, pre, ssim_sum, l1_sum);
+        ssim_stream_row<3>(c, w, base + 3, s_xy, s_sq, s_p, hm, hs, hc, dab, dc, pre, ssim_sum, l1_sum);
+        ssim_stream_row<4>(c, w, base + 4, s_xy, s_sq, s_p, hm, hs, hc, dab, dc, pre, ssim_sum, l1_sum);
+        ssim_stream_row<5>(c, w, base + 5, s_xy, s_sq, s_p, hm, hs, hc, dab, dc, pre, ssim_sum, l1_sum);
+        ssim_stream_row<6>(c, w, base + 6, s_xy, s_sq, s_p, hm, hs, hc, dab, dc, pre, ssim_sum, l1_sum);
+        ssim_stream_row<7>(c, w, base + 7, s_xy, s_sq, s_p, hm, hs, hc, dab, dc, pre, ssim_sum, l1_sum);
+        ssim_stream_row<8>(c, w, base + 8, s_xy, s_sq, s_p, hm, hs, hc, dab, dc, pre, ssim_sum, l1_sum);
+        ssim_stream_row<9>(c, w, base + 9, s_xy, s_sq, s_p, hm, hs, hc, dab, dc, pre, ssim_sum, l1_sum);
+        ssim_stream_row<10>(c, w, base + 10, s_xy, s_sq, s_p, hm, hs, hc, dab, dc, pre, ssim_sum, l1_sum);
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -411,7 +456,8 @@ void launch_l1_ssim(const float* img, const float* gt, int C, int H, int W, floa
     const double n = (double)C * H * W;
     // the streaming kernel walks its strip's rows in sequence: it needs enough strips to fill the chip
     // (>= ~2 waves per SIMD); smaller images take the tiled kernel (same dL/dimg bits)
-    const bool stream = (size_t)div_up(W, ST_OUT) * div_up(H, ST_ROWS) * C >= 2048;
+    const int mode = g_ssim_mode.load(std::memory_order_relaxed);
+    const bool stream = mode ? mode == 2 : (size_t)div_up(W, ST_OUT) * div_up(H, ST_ROWS) * C >= 2048;
     dim3 grid;
     if (stream) {
         grid = dim3(div_up(W, ST_OUT), div_up(H, ST_ROWS), C);
@@ -424,5 +470,7 @@ void launch_l1_ssim(const float* img, const float* gt, int C, int H, int W, floa
     }
     loss_finish_kernel<<<1, 1024, 0, s>>>(scratch, grid.x * grid.y * grid.z, (float)(1.0 / n), lambda, out3);
 }
+
+int ssim_debug_mode(int mode) { return g_ssim_mode.exchange(mode); }
 
 }  // namespace omr

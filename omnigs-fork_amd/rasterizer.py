@@ -75,6 +75,8 @@ def lib() -> C.CDLL:
         L.omr_debug_counters.argtypes = [vp, i, vp, vp]
         L.omr_debug_depth_sort_mode.restype = i
         L.omr_debug_depth_sort_mode.argtypes = [i]
+        L.omr_debug_ssim_mode.restype = i
+        L.omr_debug_ssim_mode.argtypes = [i]
         L.omr_debug_set_sh_jac.restype = i
         L.omr_debug_set_sh_jac.argtypes = [vp, i, i, vp]
         L.omr_debug_geometry.argtypes = [vp, i, vp, vp, vp, vp, vp, vp]
@@ -566,6 +568,15 @@ def debug_depth_sort_mode(mode: int) -> int:
     rc = int(lib().omr_debug_depth_sort_mode(int(mode)))
     if rc < 0:
         raise RasterizerError(f"debug_depth_sort_mode({mode}): {lib().omr_last_error().decode()}")
+    return rc
+
+
+def debug_ssim_mode(mode: int) -> int:
+    """The fused loss's kernel, process-wide (omr_debug_ssim_mode): 0 by image size, 1 tiled, 2 streaming. Returns the
+    previous mode."""
+    rc = int(lib().omr_debug_ssim_mode(int(mode)))
+    if rc < 0:
+        raise RasterizerError(f"debug_ssim_mode({mode}): {lib().omr_last_error().decode()}")
     return rc
 
 
