@@ -951,41 +951,96 @@ int omr_l1_ssim_loss(const float* img, const float* gt, int C, int H, int W, flo
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-int omr_adam_step(int P, int Mr, float* const params[6], float* const exp_avg[6], float* const exp_avg_sq[6],
-                  const float* const grads[6], int grad_kind, const float lr[6], const int64_t step[6], float beta1,
-                  float beta2, float eps, void* stream)
+// act (4 pointers or NULL): shs, opacity, scales, rotations written from the updated parameters (AdamGroup::act)
+static int adam_impl(int P, int Mr, float* const params[6], float* const exp_avg[6], float* const exp_avg_sq[6],
+                     const float* const grads[6], int grad_kind, const float lr[6], const int64_t step[6], float beta1,
+                     float beta2, float eps, float* const act[4], hipStream_t stream)
 {
     g_last_error.clear();
     if (P < 0 || Mr < 0 || Mr > 15) return fail(OMR_ERR_INVALID_ARGUMENT, "bad P / Mr");
     if (grad_kind != OMR_ADAM_RAW_GRADS && grad_kind != OMR_ADAM_RASTER_GRADS)
         return fail(OMR_ERR_INVALID_ARGUMENT, "bad grad_kind");
     if (!params || !exp_avg || !exp_avg_sq || !grads || !lr || !step) return fail(OMR_ERR_INVALID_ARGUMENT, "missing array");
-    if ((size_t)P * 3 * (size_t)Mr > 0xFFFFFFF0u) return fail(OMR_ERR_INVALID_ARGUMENT, "P too large");
+    if ((size_t)P * 3 * (size_t)(Mr + 1) > 0xFFFFFFF0u) return fail(OMR_ERR_INVALID_ARGUMENT, "P too large");
     const uint32_t width[6] = {3u, 3u, 3u * (uint32_t)Mr, 1u, 3u, 4u};
     static const int raster_kind[6] = {ADAM_PLAIN, ADAM_SH_DC, ADAM_SH_REST, ADAM_OPACITY, ADAM_SCALING, ADAM_ROTATION};
-    AdamArgs a{};
-    a.M = Mr + 1;
-    a.beta1 = beta1, a.beta2 = beta2, a.omb1 = (float)(1.0 - (double)beta1), a.omb2 = (float)(1.0 - (double)beta2);
-    a.eps = eps;
+    bool active[6];
     for (int k = 0; k < 6; ++k) {
-        const uint32_t n = (uint32_t)P * width[k];
-        if (n == 0 || !params[k] || !grads[k]) continue;  // adam.cpp skips parameters without a gradient
+        active[k] = (uint32_t)P * width[k] != 0 && params[k] && grads[k];  // adam.cpp skips parameters without a gradient
+        if (!active[k]) continue;
         if (!exp_avg[k] || !exp_avg_sq[k]) return fail(OMR_ERR_INVALID_ARGUMENT, "missing optimizer state");
         const bool gplain = grad_kind == OMR_ADAM_RAW_GRADS || (k != 1 && k != 2);
         if (!aligned16(params[k]) || !aligned16(exp_avg[k]) || !aligned16(exp_avg_sq[k]) || (gplain && !aligned16(grads[k])))
             return fail(OMR_ERR_INVALID_ARGUMENT, "parameter / state / gradient not 16-byte aligned");
         if (step[k] < 1) return fail(OMR_ERR_INVALID_ARGUMENT, "step must be >= 1");
-        // adam.cpp: bias corrections in double, step_size = lr / bias_correction1
+    }
+    // the activated outputs: only from the rasterizer's gradients, and only for groups that step (a skipped group's
+    // output would be stale); SH needs both f_dc and f_rest (Mr = 0: f_dc alone)
+    static const int act_group[4] = {1, 3, 4, 5};
+    if (act)
+        for (int j = 0; j < 4; ++j) {
+            if (!act[j] || P == 0) continue;
+            if (grad_kind != OMR_ADAM_RASTER_GRADS)
+                return fail(OMR_ERR_INVALID_ARGUMENT, "activated outputs need the rasterizer's gradients (grad_kind 1)");
+            if (!active[act_group[j]] || (j == 0 && Mr > 0 && !active[2]))
+                return fail(OMR_ERR_INVALID_ARGUMENT, "an activated output of a group that does not step");
+            if (!aligned16(act[j])) return fail(OMR_ERR_INVALID_ARGUMENT, "activated output not 16-byte aligned");
+        }
+    AdamArgs a{};
+    a.M = Mr + 1;
+    a.beta1 = beta1, a.beta2 = beta2, a.omb1 = (float)(1.0 - (double)beta1), a.omb2 = (float)(1.0 - (double)beta2);
+    a.eps = eps;
+    // adam.cpp: bias corrections in double, step_size = lr / bias_correction1
+    auto consts = [&](int k, float& nss, float& bc2s) {
         const double bc1 = 1.0 - std::pow((double)beta1, (double)step[k]);
         const double bc2 = 1.0 - std::pow((double)beta2, (double)step[k]);
+        nss = (float)(-((double)lr[k] / bc1));
+        bc2s = (float)std::sqrt(bc2);
+    };
+    // f_dc + f_rest as one walk over dL_dsh's rows (ADAM_SH_ROWS) whenever both step from the rasterizer's dL_dsh
+    // (OMR_ADAM_SH_ROWS=0 in the environment: the two gathering groups instead, for A/B runs)
+    static const bool sh_rows_enabled = [] {
+        const char* v = std::getenv("OMR_ADAM_SH_ROWS");
+        return !(v && std::strcmp(v, "0") == 0);
+    }();
+    const bool rows = sh_rows_enabled && grad_kind == OMR_ADAM_RASTER_GRADS && Mr > 0 && active[1] && active[2];
+    if (act && act[0] && P > 0 && Mr > 0 && !rows)
+        return fail(OMR_ERR_INVALID_ARGUMENT, "the activated SH output needs the f_dc + f_rest row walk");
+    for (int k = 0; k < 6; ++k) {
+        if (!active[k] || (rows && k == 1)) continue;  // rows: f_dc steps with f_rest's group
         AdamGroup& G = a.group[a.ngroups++];
-        G.p = params[k], G.m = exp_avg[k], G.v = exp_avg_sq[k], G.g = grads[k], G.n = n;
+        G.p = params[k], G.m = exp_avg[k], G.v = exp_avg_sq[k], G.g = grads[k], G.n = (uint32_t)P * width[k];
         G.kind = grad_kind == OMR_ADAM_RAW_GRADS ? ADAM_PLAIN : raster_kind[k];
-        G.neg_step_size = (float)(-((double)lr[k] / bc1));
-        G.bc2_sqrt = (float)std::sqrt(bc2);
+        consts(k, G.neg_step_size, G.bc2_sqrt);
+        for (int j = 0; j < 4; ++j)
+            if (act && act_group[j] == k) G.act = act[j];  // SH (j = 0) on f_dc's group only when Mr = 0: a copy
+        if (rows && k == 2) {
+            G.kind = ADAM_SH_ROWS;
+            G.act = act ? act[0] : nullptr;
+            G.p2 = params[1], G.m2 = exp_avg[1], G.v2 = exp_avg_sq[1];
+            consts(1, G.neg_step_size2, G.bc2_sqrt2);
+        }
     }
-    launch_adam(a, (hipStream_t)stream);
+    launch_adam(a, stream);
     return hip_check("adam_step");
+}
+
+int omr_adam_step(int P, int Mr, float* const params[6], float* const exp_avg[6], float* const exp_avg_sq[6],
+                  const float* const grads[6], int grad_kind, const float lr[6], const int64_t step[6], float beta1,
+                  float beta2, float eps, void* stream)
+{
+    return adam_impl(P, Mr, params, exp_avg, exp_avg_sq, grads, grad_kind, lr, step, beta1, beta2, eps, nullptr,
+                     (hipStream_t)stream);
+}
+
+int omr_adam_step_activate(int P, int Mr, float* const params[6], float* const exp_avg[6],
+                           float* const exp_avg_sq[6], const float* const grads[6], const float lr[6],
+                           const int64_t step[6], float beta1, float beta2, float eps, float* shs, float* opacity,
+                           float* scales, float* rotations, void* stream)
+{
+    float* const act[4] = {shs, opacity, scales, rotations};
+    return adam_impl(P, Mr, params, exp_avg, exp_avg_sq, grads, OMR_ADAM_RASTER_GRADS, lr, step, beta1, beta2, eps,
+                     act, (hipStream_t)stream);
 }
 
 int omr_activate(int P, int Mr, const float* const params[6], float* shs, float* opacity, float* scales,

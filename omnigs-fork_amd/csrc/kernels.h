@@ -290,7 +290,11 @@ int ssim_debug_mode(int mode);
 // optim.hip: Adam over the GaussianModel groups, densification stats, densifyAndPrune, resetOpacity
 constexpr int ADAM_MAX_GROUPS = 6;
 enum AdamKind : int { ADAM_PLAIN = 0, ADAM_SH_DC = 1, ADAM_SH_REST = 2, ADAM_OPACITY = 3, ADAM_SCALING = 4,
-                      ADAM_ROTATION = 5 };
+                      ADAM_ROTATION = 5, ADAM_SH_ROWS = 6 };
+// ADAM_SH_ROWS: f_rest (p / m / v, 16-B chunks) and f_dc (p2 / m2 / v2) as ONE group, each block stepping a range of
+// f_rest plus the f_dc of the Gaussians whose rows start there, so the block's dL_dsh positions are one contiguous
+// span, read once (and the activated SH copy, act, written as that span); f_rest's constants are neg_step_size /
+// bc2_sqrt, f_dc's the *2 ones. n = f_rest floats (3 Mr P, Mr > 0).
 struct AdamGroup {
     float* p;               // raw parameter (16-B aligned)
     float* m;               // exp_avg
@@ -300,6 +304,10 @@ struct AdamGroup {
     int kind;               // AdamKind
     float neg_step_size;    // -(lr / (1 - beta1^step))
     float bc2_sqrt;         // sqrt(1 - beta2^step)
+    float* act;             // NULL, or the activation of the updated parameter (the next forward's input): sigmoid
+                            // (OPACITY), exp (SCALING), normalize (ROTATION), cat(f_dc, f_rest) (SH_ROWS)
+    float *p2, *m2, *v2;    // ADAM_SH_ROWS: f_dc and its state
+    float neg_step_size2, bc2_sqrt2;
 };
 struct AdamArgs {
     AdamGroup group[ADAM_MAX_GROUPS];

@@ -30,16 +30,24 @@ constexpr int DENSIFY_THREADS = 256;
 constexpr int DENSIFY_ITEMS = 4;
 constexpr int DENSIFY_TILE = DENSIFY_THREADS * DENSIFY_ITEMS;
 
-__device__ __forceinline__ void adam_update(float& p, float& m, float& v, float g, const AdamGroup& a, float b1,
-                                            float b2, float omb1, float omb2, float eps)
+__device__ __forceinline__ void adam_update(float& p, float& m, float& v, float g, float neg_step_size, float bc2_sqrt,
+                                            float b1, float b2, float omb1, float omb2, float eps)
 {
     m = fmaf(omb1, g, m * b1);
     v = fmaf(omb2 * g, g, v * b2);
-    const float denom = sqrtf(v) / a.bc2_sqrt + eps;
-    p = fmaf(a.neg_step_size, m / denom, p);
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    p = fmaf(neg_step_size, m / denom, p);
 }
 
+// the renderer's activations (gaussian_model.cpp:54-77) in torch's expressions: 1 / (1 + exp(-x)), exp(x),
+// x / max(||x||_2, 1e-12) (F.normalize; the norm summed left to right, no contraction: -ffp-contract=off).
+// activate_kernel and adam_kernel's fused outputs share them, so both give the same bits.
 __device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + expf(-x)); }
+__device__ __forceinline__ float4 normalize4(float4 q)
+{
+    const float d = fmaxf(sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w), 1e-12f);
+    return make_float4(q.x / d, q.y / d, q.z / d, q.w / d);
+}
 
 // raster-gradient index of f_rest element e ([P, Mr, 3] flat) inside dL_dsh [P, M, 3], M = Mr + 1
 struct RestIndex {
@@ -53,6 +61,79 @@ struct RestIndex {
     }
 };
 
+
+// ADAM_SH_ROWS, one block: f_rest elements [E0, E1) (E0 = 1024 x block) as 16-B chunks (one per thread, float4 p / m /
+// v like every other group), the f_dc elements of the Gaussians whose f_rest row starts in that range, and their
+// dL_dsh / activated-SH positions, which form ONE contiguous span of the [P, M, 3] rows: the span's gradients are
+// read into LDS and the updated values written back from there with lane-contiguous dword accesses (a thread reading
+// its own 4 positions instead strides each wave instruction 16 B apart: 4x the transactions, and measured 44 us
+// slower at 1 M Gaussians, profiles/r05l_adam_ab.txt).
+constexpr int SH_SPAN_MAX = 4 * ADAM_THREADS + 3 * (4 * ADAM_THREADS / 3 + 1);  // f_rest row of 3 floats: Mr = 1
+__device__ __forceinline__ void adam_sh_rows(const AdamArgs& a, const AdamGroup& G, uint32_t blk)
+{
+    __shared__ float s_span[SH_SPAN_MAX];
+    const uint32_t R = 3u * (uint32_t)(a.M - 1), W = R + 3u;  // f_rest floats per Gaussian, dL_dsh floats per Gaussian
+    const uint32_t E0 = blk * ADAM_THREADS * 4u, E1 = min(E0 + ADAM_THREADS * 4u, G.n);
+    const uint32_t q0 = E0 / R, k0 = E0 - q0 * R;
+    const uint32_t s0 = q0 * W + (k0 == 0u ? 0u : 3u + k0);  // the span: [s0, s1) of dL_dsh / act
+    const uint32_t ql = (E1 - 1u) / R;
+    const uint32_t s1 = ql * W + 3u + (E1 - 1u - ql * R) + 1u;
+    const uint32_t qa = (E0 + R - 1u) / R, qb = (E1 + R - 1u) / R;  // Gaussians whose f_dc this block steps
+    const uint32_t t = threadIdx.x;
+    for (uint32_t i = t; i < s1 - s0; i += ADAM_THREADS) s_span[i] = G.g[s0 + i];
+    __syncthreads();
+    // f_rest: elements E0 + 4t .. +3
+    const uint32_t e = E0 + 4u * t;
+    if (e < E1) {
+        const uint32_t cnt = min(4u, E1 - e);
+        float p[4], m[4], v[4];
+        if (cnt == 4) {
+            const float4 p4 = *reinterpret_cast<const float4*>(G.p + e);
+            const float4 m4 = *reinterpret_cast<const float4*>(G.m + e);
+            const float4 v4 = *reinterpret_cast<const float4*>(G.v + e);
+            p[0] = p4.x, p[1] = p4.y, p[2] = p4.z, p[3] = p4.w;
+            m[0] = m4.x, m[1] = m4.y, m[2] = m4.z, m[3] = m4.w;
+            v[0] = v4.x, v[1] = v4.y, v[2] = v4.z, v[3] = v4.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                p[j] = j < (int)cnt ? G.p[e + j] : 0.f;
+                m[j] = j < (int)cnt ? G.m[e + j] : 0.f;
+                v[j] = j < (int)cnt ? G.v[e + j] : 0.f;
+            }
+        }
+        uint32_t q = e / R, k = e - q * R;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t at = q * W + 3u + k - s0;
+            if (j < (int)cnt) {
+                adam_update(p[j], m[j], v[j], s_span[at], G.neg_step_size, G.bc2_sqrt, a.beta1, a.beta2, a.omb1,
+                            a.omb2, a.eps);
+                s_span[at] = p[j];  // the activated SH value (cat is the identity on each element)
+            }
+            if (++k == R) k = 0, ++q;
+        }
+        if (cnt == 4) {
+            *reinterpret_cast<float4*>(G.p + e) = make_float4(p[0], p[1], p[2], p[3]);
+            *reinterpret_cast<float4*>(G.m + e) = make_float4(m[0], m[1], m[2], m[3]);
+            *reinterpret_cast<float4*>(G.v + e) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+            for (uint32_t j = 0; j < cnt; ++j) G.p[e + j] = p[j], G.m[e + j] = m[j], G.v[e + j] = v[j];
+        }
+    }
+    // f_dc of Gaussians qa .. qb-1: 3 consecutive elements each, consecutive threads
+    for (uint32_t i = t; i < 3u * (qb - qa); i += ADAM_THREADS) {
+        const uint32_t q = qa + i / 3u, k = i - (i / 3u) * 3u, idx = 3u * q + k;
+        const uint32_t at = q * W + k - s0;
+        float p = G.p2[idx], m = G.m2[idx], v = G.v2[idx];
+        adam_update(p, m, v, s_span[at], G.neg_step_size2, G.bc2_sqrt2, a.beta1, a.beta2, a.omb1, a.omb2, a.eps);
+        G.p2[idx] = p, G.m2[idx] = m, G.v2[idx] = v;
+        s_span[at] = p;
+    }
+    if (!G.act) return;
+    __syncthreads();
+    for (uint32_t i = t; i < s1 - s0; i += ADAM_THREADS) G.act[s0 + i] = s_span[i];
+}
 }  // namespace
 
 // one launch over every group: blocks [a.block0[s], a.block0[s+1]) handle group s
@@ -63,6 +144,10 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(AdamArgs a)
     for (int k = 1; k < ADAM_MAX_GROUPS; ++k)
         if (k < a.ngroups && blockIdx.x >= a.block0[k]) s = k;
     const AdamGroup& G = a.group[s];
+    if (G.kind == ADAM_SH_ROWS) {
+        adam_sh_rows(a, G, blockIdx.x - a.block0[s]);
+        return;
+    }
     const uint32_t c = (blockIdx.x - a.block0[s]) * ADAM_THREADS + threadIdx.x;
     const uint32_t e = c * 4;  // first float of the chunk
     if (e >= G.n) return;
@@ -132,7 +217,8 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(AdamArgs a)
     } break;
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) adam_update(p[j], m[j], v[j], g[j], G, a.beta1, a.beta2, a.omb1, a.omb2, a.eps);
+    for (int j = 0; j < 4; ++j)
+        adam_update(p[j], m[j], v[j], g[j], G.neg_step_size, G.bc2_sqrt, a.beta1, a.beta2, a.omb1, a.omb2, a.eps);
     if (cnt == 4) {
         *reinterpret_cast<float4*>(G.p + e) = make_float4(p[0], p[1], p[2], p[3]);
         *reinterpret_cast<float4*>(G.m + e) = make_float4(m[0], m[1], m[2], m[3]);
@@ -140,6 +226,20 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(AdamArgs a)
     } else {
         for (uint32_t j = 0; j < cnt; ++j) G.p[e + j] = p[j], G.m[e + j] = m[j], G.v[e + j] = v[j];
     }
+    if (!G.act) return;
+    // the next forward's input from the updated parameter (activate_kernel's expressions)
+    float o[4];
+    if (G.kind == ADAM_ROTATION) {  // cnt == 4: one quaternion
+        const float4 r = normalize4(make_float4(p[0], p[1], p[2], p[3]));
+        o[0] = r.x, o[1] = r.y, o[2] = r.z, o[3] = r.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)  // SH_DC only for Mr = 0, where the SH array is f_dc itself
+            o[j] = G.kind == ADAM_OPACITY ? sigmoidf(p[j]) : (G.kind == ADAM_SH_DC ? p[j] : expf(p[j]));  // SCALING
+    }
+    if (cnt == 4) *reinterpret_cast<float4*>(G.act + e) = make_float4(o[0], o[1], o[2], o[3]);
+    else
+        for (uint32_t j = 0; j < cnt; ++j) G.act[e + j] = o[j];
 }
 
 // addDensificationStats (gaussian_model.cpp:839-853) and the max_radii2D update (gaussian_mapper.cpp:427-432)
@@ -373,8 +473,8 @@ __global__ __launch_bounds__(256) void reset_opacity_kernel(int P, float* opacit
 // One launch instead of torch's cat + sigmoid + exp + normalize (six launches, 0.20 ms at config C in
 // profiles/r05e_train_kernel_stats.csv): blocks [0, sh_blocks) copy cat(f_dc, f_rest) into the [P, Mr + 1, 3] SH
 // array the rasterizer reads (16 B of output per thread, gathered from the two inputs), the rest apply sigmoid /
-// exp / normalize per Gaussian. The expressions are torch's: 1 / (1 + exp(-x)), exp(x), x / max(||x||_2, 1e-12)
-// (F.normalize), the norm summed left to right without contraction (optim.hip builds with -ffp-contract=off).
+// exp / normalize per Gaussian (sigmoidf, expf, normalize4 above). In the training loop Adam writes these outputs
+// itself (AdamGroup::act) and this launch runs only when the parameters changed outside Adam.
 constexpr int ACT_THREADS = 256;
 __global__ __launch_bounds__(ACT_THREADS) void activate_kernel(ActivateArgs a, uint32_t sh_blocks)
 {
@@ -400,9 +500,8 @@ __global__ __launch_bounds__(ACT_THREADS) void activate_kernel(ActivateArgs a, u
     a.opacity_out[i] = sigmoidf(a.opacity[i]);
 #pragma unroll
     for (int c = 0; c < 3; ++c) a.scales_out[3 * i + c] = expf(a.scaling[3 * i + c]);
-    const float4 q = *reinterpret_cast<const float4*>(a.rotation + 4 * (size_t)i);
-    const float d = fmaxf(sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w), 1e-12f);
-    *reinterpret_cast<float4*>(a.rotations_out + 4 * (size_t)i) = make_float4(q.x / d, q.y / d, q.z / d, q.w / d);
+    *reinterpret_cast<float4*>(a.rotations_out + 4 * (size_t)i) =
+        normalize4(*reinterpret_cast<const float4*>(a.rotation + 4 * (size_t)i));
 }
 
 // ---- launchers -------------------------------------------------------------------------------------------------

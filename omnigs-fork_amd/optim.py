@@ -115,6 +115,7 @@ class GaussianOptimizer:
         self.max_radii2D = torch.zeros((P,), device=dev)
         self.exist_since_iter = torch.zeros((P,), dtype=torch.int32, device=dev)
         self._plan = None
+        self._act_key = None  # what the last activated outputs were computed from (activate_cached)
 
     # ---- parameters ------------------------------------------------------------------------------------------
     def params(self):
@@ -155,10 +156,7 @@ class GaussianOptimizer:
         self.lr[5] = lr
 
     # ---- the renderer's activations (gaussian_model.cpp:54-77) ----------------------------------------------------
-    def activate(self, out: Optional[dict] = None) -> dict:
-        """cat(features_dc, features_rest), sigmoid(opacity), exp(scaling), normalize(rotation) in one launch
-        (omr_activate), into the tensors of `out` (keys shs, opacity, scales, rotations; reused when their shapes
-        match, else allocated). xyz is passed through. Returns the dict."""
+    def _act_buffers(self, out: Optional[dict]) -> dict:
         ps = self.params()
         P, Mr, dev = self.P, self.Mr, ps[0].device
         shapes = dict(shs=(P, Mr + 1, 3), opacity=(P, 1), scales=(P, 3), rotations=(P, 4))
@@ -167,18 +165,46 @@ class GaussianOptimizer:
             t = out.get(k)
             if t is None or tuple(t.shape) != shp or t.device != dev:
                 out[k] = torch.empty(shp, dtype=torch.float32, device=dev)
-        rc = R.lib().omr_activate(P, Mr, _p6(ps), out["shs"].data_ptr(), out["opacity"].data_ptr(),
-                                  out["scales"].data_ptr(), out["rotations"].data_ptr(), R._stream(dev))
-        R._check(rc, "omr_activate")
         out["xyz"] = ps[0]
         return out
 
+    def _key(self, out: dict):
+        """The activated outputs in `out` are current while the parameters are the same tensors, untouched by torch
+        in-place ops (their _version), and no raw-pointer write other than Adam's (reset_opacity, densify) happened."""
+        return (id(out), tuple((p.data_ptr(), p._version, tuple(p.shape)) for p in self.params()),
+                tuple(out[k].data_ptr() for k in ("shs", "opacity", "scales", "rotations")))
+
+    def activate(self, out: Optional[dict] = None) -> dict:
+        """cat(features_dc, features_rest), sigmoid(opacity), exp(scaling), normalize(rotation) in one launch
+        (omr_activate), into the tensors of `out` (keys shs, opacity, scales, rotations; reused when their shapes
+        match, else allocated). xyz is passed through. Returns the dict."""
+        out = self._act_buffers(out)
+        ps = self.params()
+        rc = R.lib().omr_activate(self.P, self.Mr, _p6(ps), out["shs"].data_ptr(), out["opacity"].data_ptr(),
+                                  out["scales"].data_ptr(), out["rotations"].data_ptr(), R._stream(ps[0].device))
+        R._check(rc, "omr_activate")
+        self._act_key = self._key(out)
+        return out
+
+    def activate_cached(self, out: dict) -> dict:
+        """`out` as activate() would fill it, launching omr_activate only when the last step(act_out=out) (or
+        activate(out)) did not already leave the activations of the current parameters there."""
+        if self._act_key is not None and all(k in out for k in ("shs", "opacity", "scales", "rotations")):
+            out["xyz"] = self.params()[0]
+            if self._key(out) == self._act_key:
+                return out
+        return self.activate(out)
+
     # ---- Adam ------------------------------------------------------------------------------------------------
-    def step(self, raster_grads: Optional[dict] = None):
+    def step(self, raster_grads: Optional[dict] = None, act_out: Optional[dict] = None):
         """optimizer_->step(). Without arguments: Adam on each parameter's .grad (groups whose .grad is None are
         skipped, as adam.cpp does). With raster_grads = the rasterizer backward's outputs (dL_dmeans3D, dL_dsh,
         dL_dopacity, dL_dscales, dL_drotations — e.g. parallel.GradBuffer.views), the activation backward is fused
-        into the same launch and no .grad is needed."""
+        into the same launch and no .grad is needed. With act_out (a dict as activate() fills; raster_grads
+        required) the same launch also writes the activations of the updated parameters there
+        (omr_adam_step_activate), and activate_cached(act_out) then has nothing to do."""
+        if act_out is not None and raster_grads is None:
+            raise R.RasterizerError("step(act_out=...) needs raster_grads")
         ps = self.params()
         P, Mr = self.P, self.Mr
         if raster_grads is not None:
@@ -205,9 +231,20 @@ class GaussianOptimizer:
         use = lambda ts: [t if active[k] else None for k, t in enumerate(ts)]  # noqa: E731
         lr = (C.c_float * 6)(*self.lr)
         st = (C.c_int64 * 6)(*[max(s, 1) for s in self.steps])
+        stream = R._stream(ps[0].device)
+        if act_out is not None:
+            act_out = self._act_buffers(act_out)
+            rc = R.lib().omr_adam_step_activate(P, Mr, _p6(ps), _p6(self.exp_avg), _p6(self.exp_avg_sq), _p6(grads), lr,
+                                                st, self.betas[0], self.betas[1], self.eps, act_out["shs"].data_ptr(),
+                                                act_out["opacity"].data_ptr(), act_out["scales"].data_ptr(),
+                                                act_out["rotations"].data_ptr(), stream)
+            R._check(rc, "omr_adam_step_activate")
+            self._act_key = self._key(act_out)
+            return
         rc = R.lib().omr_adam_step(P, Mr, _p6(use(ps)), _p6(self.exp_avg), _p6(self.exp_avg_sq), _p6(use(grads)), kind,
-                                   lr, st, self.betas[0], self.betas[1], self.eps, R._stream(ps[0].device))
+                                   lr, st, self.betas[0], self.betas[1], self.eps, stream)
         R._check(rc, "omr_adam_step")
+        self._act_key = None  # the parameters moved
 
     def zero_grad(self):
         """zero_grad(true): gradients are set to None."""
@@ -279,6 +316,7 @@ class GaussianOptimizer:
         for old, new in zip(ps, new_p):
             new.requires_grad_(old.requires_grad)
         self._set_params(new_p)
+        self._act_key = None
         self.exp_avg, self.exp_avg_sq, self.exist_since_iter = new_m, new_v, new_exist
         # densificationPostfix resets the statistics (:728-730)
         self.xyz_gradient_accum = torch.zeros((P_new, 1), device=dev)
@@ -294,3 +332,4 @@ class GaussianOptimizer:
         rc = R.lib().omr_reset_opacity(self.P, op.data_ptr(), self.exp_avg[3].data_ptr(), self.exp_avg_sq[3].data_ptr(),
                                        float(ceiling), R._stream(op.device))
         R._check(rc, "omr_reset_opacity")
+        self._act_key = None

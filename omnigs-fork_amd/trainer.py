@@ -3,7 +3,8 @@
 GaussianMapper::trainForOneIteration (gaussian_mapper.cpp:338-488), minus the SLAM bookkeeping:
   activations (gaussian_model.cpp:54-77) -> RasterizeGaussiansCUDA -> fused L1 + SSIM loss and dloss/dimage
   (loss_utils.h, csrc/ssim.hip) -> RasterizeGaussiansBackwardCUDA -> max_radii2D + addDensificationStats
-  -> Adam on the rasterizer's activated-space gradients with the activation backward fused (csrc/optim.hip).
+  -> Adam on the rasterizer's activated-space gradients with the activation backward fused (csrc/optim.hip), which
+  also writes the next forward's activated tensors.
 The reference reaches the same state through torch autograd (loss.backward()) and torch::optim::Adam;
 tests/test_gpu_optim.py checks the two agree. Densification / opacity reset stay with the caller, as in the
 reference's loop (:436-452), through GaussianOptimizer.densify_and_prune / reset_opacity.
@@ -59,8 +60,9 @@ def train_step(opt: O.GaussianOptimizer, viewpoint, image_height: int, image_wid
     state = state or TrainStep()
     P, Mr = opt.P, opt.Mr
     dev = pc.xyz.device
-    # the activations (cat / sigmoid / exp / normalize) in one launch (omr_activate; six torch launches before)
-    act = opt.activate(state.act)
+    # the activations (cat / sigmoid / exp / normalize): written by the previous step's Adam launch
+    # (omr_adam_step_activate), else one omr_activate launch (first step, after densification / opacity reset)
+    act = opt.activate_cached(state.act)
     means3D, shs, opacity, scales, rotations = act["xyz"], act["shs"], act["opacity"], act["scales"], act["rotations"]
     if camera_type == R.CAMERA_PINHOLE:  # std::tan(FoV * 0.5f) in float (gaussian_renderer.cpp:58-59)
         tanfovx = float(np.tan(np.float32(viewpoint.FoVx) * np.float32(0.5)))
@@ -102,5 +104,5 @@ def train_step(opt: O.GaussianOptimizer, viewpoint, image_height: int, image_wid
                            lambda c, d, out: R.sh_grad_from_colors(means3D, shs, pc.active_sh_degree, c, d, out=out),
                            rebuild_packed=lambda pk, out: R.sh_grad_from_colors_packed(means3D, shs,
                                                                                       pc.active_sh_degree, pk, out=out))
-    opt.step(raster_grads=out)
+    opt.step(raster_grads=out, act_out=state.act)
     return terms, image, radii

@@ -122,6 +122,16 @@ def main():
     out["adam_fused_ms"] = round(t_fused, 4)
     out["adam_fused_alg_GBps"] = round(nbytes / (t_fused * 1e-3) / 1e9, 1)
     out["adam_alg_bytes"] = nbytes
+    act = {}
+    try:  # + the activated tensors' writes
+        out["adam_fused_activate_ms"] = round(event_ms(lambda: opt.step(raster_grads=g, act_out=act)), 4)
+    except Exception as e:  # noqa: BLE001  (OMR_ADAM_SH_ROWS=0 has no activated SH output)
+        out["adam_fused_activate_ms"] = f"unavailable: {e}"
+    out["activate_ms"] = round(event_ms(lambda: opt.activate(act)), 4)
+    out["adam_sh_rows"] = os.environ.get("OMR_ADAM_SH_ROWS", "1")
+    if os.environ.get("BENCH_OPTIM_HIP_ONLY"):
+        print(json.dumps(out))
+        return
 
     ref = make_model(P, Mr, RD, requires_grad=True)
     ps = ref.parameters()

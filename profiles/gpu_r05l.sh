@@ -1,0 +1,19 @@
+set -uo pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R
+mkdir -p gpurun_out
+TAG=${1:-r05l}
+# Adam A/B: f_dc + f_rest as one row walk (OMR_ADAM_SH_ROWS=1) vs two gathering groups (0); with / without act writes
+for r in 0 1 2; do
+  for v in 1 0; do
+    echo "$(OMR_ADAM_SH_ROWS=$v BENCH_OPTIM_HIP_ONLY=1 timeout -k 10 120 python3 profiles/bench_optim.py 2>/dev/null | tail -1)" >> gpurun_out/${TAG}_adam_ab.txt
+  done
+done
+cat gpurun_out/${TAG}_adam_ab.txt
+timeout -k 10 600 python -u -m pytest tests/test_gpu_optim.py tests/test_gpu_train_dist.py -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_gputest.txt 2>&1
+rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/${TAG}_gputest.txt; [ $rc -eq 0 ] || exit 1
+cd /tmp
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_${TAG}_train" -o run -- \
+    python3 "$R/profiles/train_prof.py" --config C --steps 10 > "$R/gpurun_out/${TAG}_train.json" 2> "$R/gpurun_out/${TAG}_train.err"
+echo "train prof rc=$?"; cat "$R/gpurun_out/${TAG}_train.json"

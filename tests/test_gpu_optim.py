@@ -312,3 +312,67 @@ def test_activate_matches_the_torch_activations():
     ref = torch.nn.functional.normalize(m.rotation)
     torch.testing.assert_close(act["rotations"], ref, rtol=2.4e-7, atol=0)
 
+
+
+@pytest.mark.parametrize("P,Mr", [(100003, 15), (4097, 3), (777, 0), (1, 8)])
+def test_adam_step_activate_equals_step_then_activate(P, Mr):
+    """omr_adam_step_activate (trainer.train_step's Adam launch) writes exactly omr_activate's outputs of the updated
+    parameters, and updates parameters and moments exactly as omr_adam_step does; activate_cached then reuses them
+    and recomputes after the parameters change outside Adam (a torch in-place op, resetOpacity, densification)."""
+    rng = np.random.default_rng(P + 7 * Mr)
+    params = _random_params(P, Mr, P + 1)
+    opt1 = OPT.GaussianOptimizer(_model(params), OPT.OptimizationParams())
+    opt2 = OPT.GaussianOptimizer(_model(params), OPT.OptimizationParams())
+    act1 = {}
+    for s in range(2):
+        g = {"dL_dmeans3D": rng.normal(0, 1e-4, (P, 3)), "dL_dsh": rng.normal(0, 1e-4, (P, Mr + 1, 3)),
+             "dL_dopacity": rng.normal(0, 1e-3, (P, 1)), "dL_dscales": rng.normal(0, 1e-3, (P, 3)),
+             "dL_drotations": rng.normal(0, 1e-4, (P, 4))}
+        g = {k: _cuda(v) for k, v in g.items()}
+        opt1.step(raster_grads=g, act_out=act1)
+        opt2.step(raster_grads=g)
+    act2 = opt2.activate()
+    torch.cuda.synchronize()
+    for k in range(6):
+        for a, b in ((opt1.params()[k], opt2.params()[k]), (opt1.exp_avg[k], opt2.exp_avg[k]),
+                     (opt1.exp_avg_sq[k], opt2.exp_avg_sq[k])):
+            assert torch.equal(a, b), k
+    for k in ("shs", "opacity", "scales", "rotations"):
+        assert torch.equal(act1[k], act2[k]), k
+    assert act1["xyz"] is opt1.model.xyz
+
+    # cached: the same tensors, untouched (a launch would rewrite the same bits: poison them to see it does not run)
+    act1["opacity"].fill_(-1.0)
+    again = opt1.activate_cached(act1)
+    torch.cuda.synchronize()
+    assert again is act1 and bool((act1["opacity"] == -1.0).all())
+    # a torch in-place op on a parameter: recomputed
+    opt1.model.opacity.add_(0.5)
+    opt1.activate_cached(act1)
+    torch.cuda.synchronize()
+    assert torch.equal(act1["opacity"], torch.sigmoid(opt1.model.opacity))
+    # resetOpacity (a raw-pointer write): recomputed
+    opt1.reset_opacity(0.01)
+    act1["opacity"].fill_(-1.0)
+    opt1.activate_cached(act1)
+    torch.cuda.synchronize()
+    assert torch.equal(act1["opacity"], torch.sigmoid(opt1.model.opacity))
+
+
+def test_adam_step_activate_rejects_outputs_of_groups_that_do_not_step():
+    params = _random_params(64, 15, 5)
+    opt = OPT.GaussianOptimizer(_model(params), OPT.OptimizationParams())
+    L = omr.rasterizer.lib()
+    import ctypes as C
+    out = opt._act_buffers({})
+    g = [torch.zeros_like(p) for p in opt.params()]
+    g[1] = g[2] = torch.zeros((64, 16, 3), device="cuda")
+    g[3] = None  # opacity does not step: its activated output would be stale
+    lr = (C.c_float * 6)(*opt.lr)
+    st = (C.c_int64 * 6)(*[1] * 6)
+    rc = L.omr_adam_step_activate(64, 15, OPT._p6(opt.params()), OPT._p6(opt.exp_avg), OPT._p6(opt.exp_avg_sq),
+                                  OPT._p6(g), lr, st, 0.9, 0.999, 1e-15, out["shs"].data_ptr(),
+                                  out["opacity"].data_ptr(), out["scales"].data_ptr(), out["rotations"].data_ptr(),
+                                  omr.rasterizer._stream(torch.device("cuda")))
+    assert rc != 0
+    assert "does not step" in L.omr_last_error().decode()
