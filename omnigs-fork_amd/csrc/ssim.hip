@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256) void l1_ssim_kernel(const float* img, const fl
 }
 
 // ---- streaming variant (default) ------------------------------------------------------------------------------
-// One wave per strip of 54 output columns x OMR_SSIM_ROWS output rows and channel, walking the input rows top to
+// One wave per strip of 54 output columns x `rows` output rows and channel, walking the input rows top to
 // bottom. Each lane owns one column of the 64 product / partial columns (x0-5 .. x0+58) and keeps, in registers,
 // rings of the last 11 rows of its column's horizontally filtered products (5 values) and of its output column's
 // horizontally back-filtered partials (3 values), so every vertical 11-tap pass is register-only and every value is
@@ -207,18 +207,20 @@ __global__ __launch_bounds__(256) void l1_ssim_kernel(const float* img, const fl
 //  * x^2, y^2, xy are formed once per input column (not once per tap); the x | y and x^2 | y^2 taps, the vertical
 //    moment pairs and the A | B back-filter pairs are v_pk_fma_f32 — the kernel is VALU-bound once the loads are
 //    hidden (VALU per row: ~450 issue slots as separate multiply + add, ~190 fused and packed).
-#ifndef OMR_SSIM_ROWS
-#define OMR_SSIM_ROWS 48
-#endif
 constexpr int ST_OUT = 54;  // output columns per strip: lanes 0..53
 constexpr int ST_IN = 74;   // input columns x0-10 .. x0+63
-constexpr int ST_ROWS = OMR_SSIM_ROWS;
+// Strip height: the tallest that still gives every resident wave slot of the device one strip (stream_rows below):
+// each strip re-walks 2 x 10 halo rows, so fewer, taller strips do less work, while a second round of strips would
+// leave most of the chip idle behind the first. 3x1024x2048 on MI355X: 40 rows, 2964 strips for 3072 slots
+// (48 rows: 0.136 ms, 40: 0.127, 32: 0.146; profiles/r05m_ssim_ab.txt).
+constexpr int ST_ROWS_MIN = 16;   // the strip height used to size the partial sums (the shortest stream_rows gives)
+constexpr int ST_ROWS_AUTO = 48;  // the tiled / streaming decision counts strips of this height
 constexpr int ST_EXTRA = ST_IN - 64;  // input columns past the wave's 64 lanes
 
 struct StreamCtx {
     const float* X;
     const float* Y;
-    int H, W, x0, y0, i1, lane;
+    int H, W, x0, y0, i1, lane, rows;
     float l1_scale, dS_scale;
     float* dimg;
 };
@@ -301,7 +303,7 @@ __device__ __forceinline__ void ssim_stream_row(const StreamCtx& c, const float*
         }
         const bool in = mr >= 0 && mr < c.H && pc >= 0 && pc < c.W;
         const SsimPart p = ssim_partials(mu.x, mu.y, ex2.x, ex2.y, exy, c.dS_scale, in);
-        if (in && mr >= c.y0 && mr < c.y0 + ST_ROWS && lane >= SS_HALO && lane < SS_HALO + ST_OUT)
+        if (in && mr >= c.y0 && mr < c.y0 + c.rows && lane >= SS_HALO && lane < SS_HALO + ST_OUT)
             ssim_sum += p.S;  // the strip's own output rows and columns
         s_p[lane] = make_float4(p.A, p.B, p.C, 0.f);
         wave_sync();  // the next row's syncs separate these reads from the next write
@@ -339,7 +341,7 @@ __device__ __forceinline__ void ssim_stream_row(const StreamCtx& c, const float*
 
 __global__ __launch_bounds__(64) void l1_ssim_stream_kernel(const float* img, const float* gt, int H, int W,
                                                             SsimWindow win, float l1_scale, float dS_scale,
-                                                            float* dimg, float* partials)
+                                                            float* dimg, float* partials, int rows)
 {
     __shared__ float2 s_xy[SS_WIN][ST_IN];
     __shared__ float4 s_sq[ST_IN];
@@ -350,8 +352,9 @@ __global__ __launch_bounds__(64) void l1_ssim_stream_kernel(const float* img, co
     c.X = img + ch * plane;
     c.Y = gt + ch * plane;
     c.H = H, c.W = W;
-    c.x0 = blockIdx.x * ST_OUT, c.y0 = blockIdx.y * ST_ROWS;
-    c.i1 = min(c.y0 + ST_ROWS, H) - 1 + 2 * SS_HALO;  // input row of the chunk's last output row
+    c.rows = rows;
+    c.x0 = blockIdx.x * ST_OUT, c.y0 = blockIdx.y * rows;
+    c.i1 = min(c.y0 + rows, H) - 1 + 2 * SS_HALO;  // input row of the chunk's last output row
     c.lane = threadIdx.x;
     c.l1_scale = l1_scale, c.dS_scale = dS_scale;
     c.dimg = dimg + ch * plane;
@@ -444,9 +447,30 @@ SsimWindow ssim_window()
     return w;
 }
 
+// the streaming kernel's strip height for a [C,H,W] image (see ST_ROWS_MIN): one strip per resident wave slot
+static int stream_rows(int C, int H, int W)
+{
+    static thread_local int cached_dev = -1;
+    static thread_local long slots = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (dev != cached_dev) {
+        int cus = 0, per_cu = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, l1_ssim_stream_kernel, 64, 0) != hipSuccess ||
+            per_cu <= 0)
+            per_cu = 12;
+        slots = (long)cus * per_cu;
+        cached_dev = dev;
+    }
+    const long per_column = slots / ((long)div_up(W, ST_OUT) * C);  // strips each strip column may have
+    if (per_column <= 1) return std::max(H, 1);
+    return std::max(ST_ROWS_MIN, (int)div_up((uint32_t)H, (uint32_t)per_column));
+}
+
 size_t l1_ssim_scratch_floats(int C, int H, int W)
 {
-    return 2 * std::max((size_t)div_up(W, SS_TILE) * div_up(H, SS_TILE), (size_t)div_up(W, ST_OUT) * div_up(H, ST_ROWS)) *
+    return 2 * std::max((size_t)div_up(W, SS_TILE) * div_up(H, SS_TILE), (size_t)div_up(W, ST_OUT) * div_up(H, ST_ROWS_MIN)) *
            (size_t)C;
 }
 
@@ -457,12 +481,13 @@ void launch_l1_ssim(const float* img, const float* gt, int C, int H, int W, floa
     // the streaming kernel walks its strip's rows in sequence: it needs enough strips to fill the chip
     // (>= ~2 waves per SIMD); smaller images take the tiled kernel (same dL/dimg bits)
     const int mode = g_ssim_mode.load(std::memory_order_relaxed);
-    const bool stream = mode ? mode == 2 : (size_t)div_up(W, ST_OUT) * div_up(H, ST_ROWS) * C >= 2048;
+    const bool stream = mode ? mode == 2 : (size_t)div_up(W, ST_OUT) * div_up(H, ST_ROWS_AUTO) * C >= 2048;
     dim3 grid;
     if (stream) {
-        grid = dim3(div_up(W, ST_OUT), div_up(H, ST_ROWS), C);
+        const int rows = stream_rows(C, H, W);
+        grid = dim3(div_up(W, ST_OUT), div_up(H, rows), C);
         l1_ssim_stream_kernel<<<grid, 64, 0, s>>>(img, gt, H, W, ssim_window(), (float)((1.0 - lambda) / n),
-                                                  (float)(-(double)lambda / n), dimg, scratch);
+                                                  (float)(-(double)lambda / n), dimg, scratch, rows);
     } else {
         grid = dim3(div_up(W, SS_TILE), div_up(H, SS_TILE), C);
         l1_ssim_kernel<<<grid, 256, 0, s>>>(img, gt, H, W, ssim_window(), (float)((1.0 - lambda) / n),
