@@ -179,11 +179,15 @@ int omr_activate(int P, int Mr, const float* const params[6], float* shs, float*
 /* omr_adam_step with OMR_ADAM_RASTER_GRADS that also writes omr_activate's four outputs from the UPDATED parameters
  * (bitwise what omr_activate would give after the step), so a training loop needs no separate activation launch
  * before its next forward. Any output may be NULL (not written); the others must be 16-byte aligned and their
- * groups must step (an output of a skipped group would be stale: OMR_ERR_INVALID_ARGUMENT). */
+ * groups must step (an output of a skipped group would be stale: OMR_ERR_INVALID_ARGUMENT). With radii != NULL the
+ * same launch also does omr_densification_stats(P, radii, viewspace_grad, viewspace_stride, xyz_gradient_accum,
+ * denom, max_radii2D) (the same arithmetic; the statistics and Adam touch disjoint arrays). */
 int omr_adam_step_activate(int P, int Mr, float* const params[6], float* const exp_avg[6],
                            float* const exp_avg_sq[6], const float* const grads[6], const float lr[6],
                            const int64_t step[6], float beta1, float beta2, float eps, float* shs, float* opacity,
-                           float* scales, float* rotations, void* stream);
+                           float* scales, float* rotations, const int* radii, const float* viewspace_grad,
+                           int viewspace_stride, float* xyz_gradient_accum, float* denom, float* max_radii2D,
+                           void* stream);
 /* addDensificationStats (gaussian_model.cpp:839-853) + the max_radii2D update (gaussian_mapper.cpp:427-432) for
  * visibility_filter = radii > 0: accum[i] += |viewspace_grad[i][0:2]|, denom[i] += 1, max_radii2D[i] =
  * max(max_radii2D[i], radii[i]). viewspace_grad is dL_dmeans2D with row stride viewspace_stride (3). */

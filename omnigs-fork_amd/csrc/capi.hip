@@ -954,7 +954,8 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 // act (4 pointers or NULL): shs, opacity, scales, rotations written from the updated parameters (AdamGroup::act)
 static int adam_impl(int P, int Mr, float* const params[6], float* const exp_avg[6], float* const exp_avg_sq[6],
                      const float* const grads[6], int grad_kind, const float lr[6], const int64_t step[6], float beta1,
-                     float beta2, float eps, float* const act[4], hipStream_t stream)
+                     float beta2, float eps, float* const act[4], const DensifyStatsArgs* stats,
+                     hipStream_t stream)
 {
     g_last_error.clear();
     if (P < 0 || Mr < 0 || Mr > 15) return fail(OMR_ERR_INVALID_ARGUMENT, "bad P / Mr");
@@ -1021,6 +1022,12 @@ static int adam_impl(int P, int Mr, float* const params[6], float* const exp_avg
             consts(1, G.neg_step_size2, G.bc2_sqrt2);
         }
     }
+    if (stats && stats->P > 0) {
+        if (stats->P != P) return fail(OMR_ERR_INVALID_ARGUMENT, "densification statistics for another P");
+        if (!stats->radii || !stats->vgrad || !stats->accum || !stats->denom || !stats->max_radii || stats->vstride < 2)
+            return fail(OMR_ERR_INVALID_ARGUMENT, "densification statistics: missing pointer / bad stride");
+        a.stats = *stats;
+    }
     launch_adam(a, stream);
     return hip_check("adam_step");
 }
@@ -1030,17 +1037,24 @@ int omr_adam_step(int P, int Mr, float* const params[6], float* const exp_avg[6]
                   float beta2, float eps, void* stream)
 {
     return adam_impl(P, Mr, params, exp_avg, exp_avg_sq, grads, grad_kind, lr, step, beta1, beta2, eps, nullptr,
-                     (hipStream_t)stream);
+                     nullptr, (hipStream_t)stream);
 }
 
 int omr_adam_step_activate(int P, int Mr, float* const params[6], float* const exp_avg[6],
                            float* const exp_avg_sq[6], const float* const grads[6], const float lr[6],
                            const int64_t step[6], float beta1, float beta2, float eps, float* shs, float* opacity,
-                           float* scales, float* rotations, void* stream)
+                           float* scales, float* rotations, const int* radii, const float* viewspace_grad,
+                           int viewspace_stride, float* xyz_gradient_accum, float* denom, float* max_radii2D,
+                           void* stream)
 {
     float* const act[4] = {shs, opacity, scales, rotations};
+    DensifyStatsArgs st;
+    if (radii) {  // the statistics ride along (omr_densification_stats' arithmetic)
+        st.P = P, st.radii = radii, st.vgrad = viewspace_grad, st.vstride = viewspace_stride;
+        st.accum = xyz_gradient_accum, st.denom = denom, st.max_radii = max_radii2D;
+    }
     return adam_impl(P, Mr, params, exp_avg, exp_avg_sq, grads, OMR_ADAM_RASTER_GRADS, lr, step, beta1, beta2, eps,
-                     act, (hipStream_t)stream);
+                     act, radii ? &st : nullptr, (hipStream_t)stream);
 }
 
 int omr_activate(int P, int Mr, const float* const params[6], float* shs, float* opacity, float* scales,

@@ -309,9 +309,19 @@ struct AdamGroup {
     float *p2, *m2, *v2;    // ADAM_SH_ROWS: f_dc and its state
     float neg_step_size2, bc2_sqrt2;
 };
+// addDensificationStats + the max_radii2D update as extra blocks of the Adam launch (omr_adam_step_activate)
+struct DensifyStatsArgs {
+    int P = 0;                        // 0: none
+    const int* radii = nullptr;
+    const float* vgrad = nullptr;     // dL_dmeans2D, row stride vstride
+    int vstride = 0;
+    float *accum = nullptr, *denom = nullptr, *max_radii = nullptr;
+};
 struct AdamArgs {
     AdamGroup group[ADAM_MAX_GROUPS];
     uint32_t block0[ADAM_MAX_GROUPS];  // first block of each group (filled by launch_adam)
+    uint32_t stats_block0;             // blocks from here on: the densification statistics (filled by launch_adam)
+    DensifyStatsArgs stats;
     int ngroups;
     int M;                             // SH coefficients per Gaussian in dL_dsh (f_dc + f_rest)
     float beta1, beta2, omb1, omb2, eps;

@@ -136,9 +136,31 @@ __device__ __forceinline__ void adam_sh_rows(const AdamArgs& a, const AdamGroup&
 }
 }  // namespace
 
-// one launch over every group: blocks [a.block0[s], a.block0[s+1]) handle group s
+// addDensificationStats (gaussian_model.cpp:839-853) and the max_radii2D update (gaussian_mapper.cpp:427-432) for
+// visibility_filter = radii > 0 (gaussian_renderer.cpp:288): one Gaussian per element
+__device__ __forceinline__ void densify_stats_one(const DensifyStatsArgs& d, int i)
+{
+    const int r = d.radii[i];
+    if (r <= 0) return;
+    d.max_radii[i] = fmaxf(d.max_radii[i], (float)r);
+    const float gx = d.vgrad[(size_t)i * d.vstride], gy = d.vgrad[(size_t)i * d.vstride + 1];
+    d.accum[i] += sqrtf(gx * gx + gy * gy);
+    d.denom[i] += 1.f;
+}
+
+// one launch over every group: blocks [a.block0[s], a.block0[s+1]) handle group s, blocks from a.stats_block0 on the
+// densification statistics (4 x 256 Gaussians each, lane-contiguous)
 __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(AdamArgs a)
 {
+    if (blockIdx.x >= a.stats_block0) {
+        const int i0 = (int)((blockIdx.x - a.stats_block0) * ADAM_THREADS * 4u + threadIdx.x);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = i0 + j * ADAM_THREADS;
+            if (i < a.stats.P) densify_stats_one(a.stats, i);
+        }
+        return;
+    }
     int s = 0;
 #pragma unroll
     for (int k = 1; k < ADAM_MAX_GROUPS; ++k)
@@ -250,12 +272,10 @@ __global__ __launch_bounds__(256) void densification_stats_kernel(int P, const i
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
-    const int r = radii[i];
-    if (r <= 0) return;
-    max_radii[i] = fmaxf(max_radii[i], (float)r);
-    const float gx = vgrad[(size_t)i * vstride], gy = vgrad[(size_t)i * vstride + 1];
-    accum[i] += sqrtf(gx * gx + gy * gy);
-    denom[i] += 1.f;
+    DensifyStatsArgs d;
+    d.P = P, d.radii = radii, d.vgrad = vgrad, d.vstride = vstride, d.accum = accum, d.denom = denom;
+    d.max_radii = max_radii;
+    densify_stats_one(d, i);
 }
 
 // ---- densifyAndPrune -----------------------------------------------------------------------------------------
@@ -522,6 +542,8 @@ void launch_adam(AdamArgs a, hipStream_t s)
         blocks += div_up(div_up(a.group[k].n, 4u), (uint32_t)ADAM_THREADS);
     }
     for (int k = a.ngroups; k < ADAM_MAX_GROUPS; ++k) a.block0[k] = blocks;
+    a.stats_block0 = blocks;
+    if (a.stats.P > 0) blocks += div_up((uint32_t)a.stats.P, 4u * ADAM_THREADS);
     if (blocks) adam_kernel<<<blocks, ADAM_THREADS, 0, s>>>(a);
 }
 

@@ -196,15 +196,18 @@ class GaussianOptimizer:
         return self.activate(out)
 
     # ---- Adam ------------------------------------------------------------------------------------------------
-    def step(self, raster_grads: Optional[dict] = None, act_out: Optional[dict] = None):
+    def step(self, raster_grads: Optional[dict] = None, act_out: Optional[dict] = None, densify_stats=None):
         """optimizer_->step(). Without arguments: Adam on each parameter's .grad (groups whose .grad is None are
         skipped, as adam.cpp does). With raster_grads = the rasterizer backward's outputs (dL_dmeans3D, dL_dsh,
         dL_dopacity, dL_dscales, dL_drotations — e.g. parallel.GradBuffer.views), the activation backward is fused
         into the same launch and no .grad is needed. With act_out (a dict as activate() fills; raster_grads
         required) the same launch also writes the activations of the updated parameters there
-        (omr_adam_step_activate), and activate_cached(act_out) then has nothing to do."""
+        (omr_adam_step_activate), and activate_cached(act_out) then has nothing to do; densify_stats =
+        (viewspace_grad, radii) (act_out required) folds add_densification_stats into that launch too."""
         if act_out is not None and raster_grads is None:
             raise R.RasterizerError("step(act_out=...) needs raster_grads")
+        if densify_stats is not None and act_out is None:
+            raise R.RasterizerError("step(densify_stats=...) needs act_out (omr_adam_step_activate)")
         ps = self.params()
         P, Mr = self.P, self.Mr
         if raster_grads is not None:
@@ -234,10 +237,15 @@ class GaussianOptimizer:
         stream = R._stream(ps[0].device)
         if act_out is not None:
             act_out = self._act_buffers(act_out)
+            stats = [None, None, 0, None, None, None]
+            if densify_stats is not None:
+                vgrad, radii = self._stats_inputs(*densify_stats)
+                stats = [radii.data_ptr(), vgrad.data_ptr(), vgrad.shape[1], self.xyz_gradient_accum.data_ptr(),
+                         self.denom.data_ptr(), self.max_radii2D.data_ptr()]
             rc = R.lib().omr_adam_step_activate(P, Mr, _p6(ps), _p6(self.exp_avg), _p6(self.exp_avg_sq), _p6(grads), lr,
                                                 st, self.betas[0], self.betas[1], self.eps, act_out["shs"].data_ptr(),
                                                 act_out["opacity"].data_ptr(), act_out["scales"].data_ptr(),
-                                                act_out["rotations"].data_ptr(), stream)
+                                                act_out["rotations"].data_ptr(), *stats, stream)
             R._check(rc, "omr_adam_step_activate")
             self._act_key = self._key(act_out)
             return
@@ -252,6 +260,14 @@ class GaussianOptimizer:
             p.grad = None
 
     # ---- densification (gaussian_model.cpp:564-853) -----------------------------------------------------------
+    def _stats_inputs(self, viewspace_grad: torch.Tensor, radii: torch.Tensor):
+        _check_dev(viewspace_grad, "viewspace_grad")
+        _check_dev(radii, "radii", torch.int32)
+        if viewspace_grad.shape[0] != self.P or radii.numel() != self.P or viewspace_grad.dim() != 2 \
+                or viewspace_grad.shape[1] < 2:
+            raise R.RasterizerError("viewspace_grad [P, >=2] / radii [P] do not match the model's P")
+        return viewspace_grad, radii
+
     def add_densification_stats(self, viewspace_grad: torch.Tensor, radii: torch.Tensor):
         """max_radii2D[vis] = max(max_radii2D[vis], radii[vis]) (gaussian_mapper.cpp:429-432) and
         addDensificationStats (gaussian_model.cpp:839-853) for vis = radii > 0. viewspace_grad is the means2D

@@ -94,7 +94,7 @@ def lib() -> C.CDLL:
         P6 = C.c_void_p * 6
         L.omr_adam_step.argtypes = [i, i, P6, P6, P6, P6, i, C.c_float * 6, C.c_int64 * 6, f, f, f, vp]
         L.omr_adam_step_activate.argtypes = [i, i, P6, P6, P6, P6, C.c_float * 6, C.c_int64 * 6, f, f, f, vp, vp, vp,
-                                             vp, vp]
+                                             vp, vp, vp, i, vp, vp, vp, vp]
         L.omr_densification_stats.argtypes = [i, vp, vp, i, vp, vp, vp, vp]
         L.omr_activate.argtypes = [i, i, P6, vp, vp, vp, vp, vp]
         L.omr_densify_plan_bytes.restype = sz

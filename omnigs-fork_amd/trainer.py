@@ -2,9 +2,9 @@
 
 GaussianMapper::trainForOneIteration (gaussian_mapper.cpp:338-488), minus the SLAM bookkeeping:
   activations (gaussian_model.cpp:54-77) -> RasterizeGaussiansCUDA -> fused L1 + SSIM loss and dloss/dimage
-  (loss_utils.h, csrc/ssim.hip) -> RasterizeGaussiansBackwardCUDA -> max_radii2D + addDensificationStats
-  -> Adam on the rasterizer's activated-space gradients with the activation backward fused (csrc/optim.hip), which
-  also writes the next forward's activated tensors.
+  (loss_utils.h, csrc/ssim.hip) -> RasterizeGaussiansBackwardCUDA -> Adam on the rasterizer's activated-space
+  gradients with the activation backward fused (csrc/optim.hip), which also writes the next forward's activated
+  tensors and does max_radii2D + addDensificationStats in the same launch.
 The reference reaches the same state through torch autograd (loss.backward()) and torch::optim::Adam;
 tests/test_gpu_optim.py checks the two agree. Densification / opacity reset stay with the caller, as in the
 reference's loop (:436-452), through GaussianOptimizer.densify_and_prune / reset_opacity.
@@ -97,12 +97,13 @@ def train_step(opt: O.GaussianOptimizer, viewpoint, image_height: int, image_wid
     R.RasterizeGaussiansBackwardCUDA(bg_color, means3D, radii, None, scales, rotations, 1.0, None, vm, pm, tanfovx,
                                      tanfovy, dimg, shs, pc.active_sh_degree, cp, geom, nr, binning, img, camera_type,
                                      out=out)
-    if densification_stats:
-        opt.add_densification_stats(out["dL_dmeans2D"], radii)
     if dist_info is not None and dist_info.enabled:
         allreduce_compact_(state.buf, dist_info, out["dL_dcolors"], cp,
                            lambda c, d, out: R.sh_grad_from_colors(means3D, shs, pc.active_sh_degree, c, d, out=out),
                            rebuild_packed=lambda pk, out: R.sh_grad_from_colors_packed(means3D, shs,
                                                                                       pc.active_sh_degree, pk, out=out))
-    opt.step(raster_grads=out, act_out=state.act)
+    # Adam + the next step's activations + max_radii2D / addDensificationStats (this rank's own dL_dmeans2D, which the
+    # exchange leaves alone) in one launch
+    opt.step(raster_grads=out, act_out=state.act,
+             densify_stats=(out["dL_dmeans2D"], radii) if densification_stats else None)
     return terms, image, radii

@@ -373,6 +373,35 @@ def test_adam_step_activate_rejects_outputs_of_groups_that_do_not_step():
     rc = L.omr_adam_step_activate(64, 15, OPT._p6(opt.params()), OPT._p6(opt.exp_avg), OPT._p6(opt.exp_avg_sq),
                                   OPT._p6(g), lr, st, 0.9, 0.999, 1e-15, out["shs"].data_ptr(),
                                   out["opacity"].data_ptr(), out["scales"].data_ptr(), out["rotations"].data_ptr(),
-                                  omr.rasterizer._stream(torch.device("cuda")))
+                                  None, None, 0, None, None, None, omr.rasterizer._stream(torch.device("cuda")))
     assert rc != 0
     assert "does not step" in L.omr_last_error().decode()
+
+
+def test_adam_step_with_densification_stats_equals_the_separate_call():
+    """step(..., densify_stats=(dL_dmeans2D, radii)) (the statistics as extra blocks of the Adam launch) updates
+    xyz_gradient_accum / denom / max_radii2D bit for bit as add_densification_stats, and Adam as without them."""
+    P, Mr = 70001, 15
+    rng = np.random.default_rng(9)
+    params = _random_params(P, Mr, 12)
+    opt1 = OPT.GaussianOptimizer(_model(params), OPT.OptimizationParams())
+    opt2 = OPT.GaussianOptimizer(_model(params), OPT.OptimizationParams())
+    act1, act2 = {}, {}
+    for s in range(2):
+        g = {"dL_dmeans3D": rng.normal(0, 1e-4, (P, 3)), "dL_dsh": rng.normal(0, 1e-4, (P, Mr + 1, 3)),
+             "dL_dopacity": rng.normal(0, 1e-3, (P, 1)), "dL_dscales": rng.normal(0, 1e-3, (P, 3)),
+             "dL_drotations": rng.normal(0, 1e-4, (P, 4))}
+        g = {k: _cuda(v) for k, v in g.items()}
+        vgrad = _cuda(rng.normal(0, 1e-3, (P, 3)))
+        radii = torch.tensor(rng.integers(-1, 40, P), dtype=torch.int32, device="cuda")
+        opt1.step(raster_grads=g, act_out=act1, densify_stats=(vgrad, radii))
+        opt2.add_densification_stats(vgrad, radii)
+        opt2.step(raster_grads=g, act_out=act2)
+    torch.cuda.synchronize()
+    for a, b in ((opt1.xyz_gradient_accum, opt2.xyz_gradient_accum), (opt1.denom, opt2.denom),
+                 (opt1.max_radii2D, opt2.max_radii2D)):
+        assert torch.equal(a, b)
+    for k in range(6):
+        assert torch.equal(opt1.params()[k], opt2.params()[k]), k
+    with pytest.raises(omr.rasterizer.RasterizerError, match="act_out"):
+        opt1.step(raster_grads=g, densify_stats=(vgrad, radii))
