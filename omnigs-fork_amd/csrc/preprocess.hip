@@ -315,31 +315,31 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     // 1295 -> 1317 MP/s, against requesting the rows of every point in front of the camera before the geometry.
     // Equirect views see every point, so their rows are requested first and their latency overlaps the projection.
     constexpr bool LATE = CAM != CAM_LONLAT;
+    // equirect: every row is requested now, into registers, and parked in LDS only after the projection, so the
+    // loads' latency overlaps it (the 48 VGPRs are free: the LDS image caps the kernel at 3 waves per SIMD). Waiting
+    // for them before the projection (wave_rows_load) cost C 0.024 ms of the kernel's 0.092: without the rows it took
+    // 0.068 ms (profiles/r05v_ab.txt).
+    rowv4 early[SH_F4];
+    // every load issued so far lands before the rows are requested, on both sides of the branch below: loads retire
+    // in order on vmcnt, and a later wait for one of them would otherwise have to count the rows in (the wait
+    // counter merges the branch's sides conservatively), i.e. wait for the rows too
+    if (!LATE)
+        asm volatile("" ::"v"(in.opacity), "v"(in.sx), "v"(in.sy), "v"(in.sz), "v"(in.q.x), "v"(in.q.y), "v"(in.q.z),
+                     "v"(in.q.w), "v"(p_orig.x), "v"(p_orig.y), "v"(p_orig.z));
     if (sh16 && !LATE) {
-        const uint64_t rows = __ballot(valid);
-        const float4* src = reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4;
-        float4 shq[SH_F4];
-        wave_rows_load<SH_F4>(src, rows, nf4, stage, lane);
-        wave_sync();
-#pragma unroll
-        for (int q = 0; q < SH_F4; ++q)
-            shq[q] = q < nf4 ? stage[lane * stage_stride<SH_F4>() + q] : make_float4(0.f, 0.f, 0.f, 0.f);
-        wave_sync();  // the image is reused for the records below
-#pragma unroll
-        for (int q = 0; q < SH_F4; ++q) {
-            shv[4 * q] = shq[q].x;
-            shv[4 * q + 1] = shq[q].y;
-            shv[4 * q + 2] = shq[q].z;
-            shv[4 * q + 3] = shq[q].w;
-        }
+        wave_rows_fetch<SH_F4>(reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4, __ballot(valid), nf4,
+                               lane, early);
     }
     PreOut o;
-    const bool vis = valid && preprocess_point<CAM>(a, in, idx, p_orig, sh16, shv, o, LATE);
-    if (LATE && sh16) {
+    const bool vis = valid && preprocess_point<CAM>(a, in, idx, p_orig, sh16, shv, o, sh16);
+    if (sh16) {
         const uint64_t rows = __ballot(vis);
         if (rows) {  // wave-uniform
-            wave_rows_load<SH_F4>(reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4, rows, nf4, stage,
-                                  lane);
+            if (LATE)
+                wave_rows_load<SH_F4>(reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4, rows, nf4,
+                                      stage, lane);
+            else
+                wave_rows_park<SH_F4>(early, stage, lane);
             wave_sync();
 #pragma unroll
             for (int q = 0; q < SH_F4; ++q) {

@@ -54,6 +54,37 @@ __device__ __forceinline__ void wave_rows_load(const float4* __restrict__ src, u
     }
 }
 
+// wave_rows_load in two halves: wave_rows_fetch issues the NF4 loads into registers (the same lane-contiguous spans
+// and the same src[0] stand-in outside the selection) without waiting for them; wave_rows_park later moves them into
+// the LDS image. Between the two the wave does other work while the loads are in flight.
+// the registers of an in-flight row span: native vectors (an array of float4 — HIP's struct vector type — held
+// across other code is kept in scratch memory by the compiler)
+typedef float rowv4 __attribute__((ext_vector_type(4)));
+template <int NF4>
+__device__ __forceinline__ void wave_rows_fetch(const float4* __restrict__ src, uint64_t rows, int ncols, uint32_t lane,
+                                                rowv4 (&v)[NF4])
+{
+    const rowv4* s = reinterpret_cast<const rowv4*>(src);
+#pragma unroll
+    for (int q = 0; q < NF4; ++q) {
+        const uint32_t k = (uint32_t)q * 64u + lane;
+        const uint32_t r = k / NF4, c = k - r * NF4;
+        const bool ok = ((rows >> r) & 1u) && (int)c < ncols;
+        v[q] = s[ok ? k : 0u];
+    }
+}
+template <int NF4>
+__device__ __forceinline__ void wave_rows_park(const rowv4 (&v)[NF4], float4* lds, uint32_t lane)
+{
+    constexpr int S = stage_stride<NF4>();
+#pragma unroll
+    for (int q = 0; q < NF4; ++q) {
+        const uint32_t k = (uint32_t)q * 64u + lane;
+        const uint32_t r = k / NF4, c = k - r * NF4;
+        reinterpret_cast<rowv4*>(lds)[r * S + c] = v[q];
+    }
+}
+
 // Rows r with bit r of `rows` set: lds[r*S + c] -> global dst[r*NF4 + c], all NF4 columns.
 template <int NF4>
 __device__ __forceinline__ void wave_rows_store(float4* __restrict__ dst, uint64_t rows, const float4* lds,
