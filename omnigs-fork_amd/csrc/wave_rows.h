@@ -91,11 +91,20 @@ __device__ __forceinline__ void wave_rows_store(float4* __restrict__ dst, uint64
                                                 uint32_t lane)
 {
     constexpr int S = stage_stride<NF4>();
+    // every LDS read first, into registers of their own, then the stores: a store reads its data registers after it
+    // issues, so refilling one register quad per store made each store wait (vmcnt) for the one before it
+    rowv4 v[NF4];
 #pragma unroll
     for (int q = 0; q < NF4; ++q) {
         const uint32_t k = (uint32_t)q * 64u + lane;
         const uint32_t r = k / NF4, c = k - r * NF4;
-        if ((rows >> r) & 1u) dst[k] = lds[r * S + c];
+        v[q] = reinterpret_cast<const rowv4*>(lds)[r * S + c];
+    }
+#pragma unroll
+    for (int q = 0; q < NF4; ++q) {
+        const uint32_t k = (uint32_t)q * 64u + lane;
+        const uint32_t r = k / NF4;
+        if ((rows >> r) & 1u) reinterpret_cast<rowv4*>(dst)[k] = v[q];
     }
 }
 
