@@ -1,0 +1,18 @@
+set -uo pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R
+mkdir -p gpurun_out
+TAG=${1:-r05ad}
+# columns scatter: in-tree (the next chunk's registers and descriptor consumed before the write-out) vs HEAD (cols_old)
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > gpurun_out/${TAG}_gputest.txt 2>&1
+rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/${TAG}_gputest.txt; [ $rc -eq 0 ] || exit 1
+for r in 0 1; do
+  echo "== E round $r" >> gpurun_out/${TAG}_ab.txt
+  timeout -k 10 400 bash profiles/ab.sh --config E --steps 20 --warmup 5 --no-train-step >> gpurun_out/${TAG}_ab.txt 2>&1 || exit 1
+  echo "== C round $r" >> gpurun_out/${TAG}_ab.txt
+  timeout -k 10 400 bash profiles/ab.sh --steps 20 --warmup 5 --no-train-step >> gpurun_out/${TAG}_ab.txt 2>&1 || exit 1
+done
+for v in v1; do
+  OMR_LIB_PATH=omnigs-fork_amd/lib/stamps/${v}_stamps.so timeout -k 10 200 python3 profiles/bin_stamps.py E > gpurun_out/${TAG}_stamps_$v.json 2>gpurun_out/${TAG}_stamps_$v.err || exit 1
+done
+cat gpurun_out/${TAG}_ab.txt gpurun_out/${TAG}_stamps_*.json
