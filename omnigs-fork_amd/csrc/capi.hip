@@ -565,8 +565,7 @@ int forward_impl(const ForwardIn& in)
                                                nullptr, 0, DEPTH_SORT_PASSES, s, true, err_dev);
             g.order = which ? g.val_b : g.val_a;
         } else {
-            depth_sort(g.key_a, g.key_b, g.val_a, g.val_b, g.order, g.hist, g.scan_partials, P, s, err_dev,
-                       g.counters + 7);
+            depth_sort(g.key_a, g.key_b, g.val_a, g.val_b, g.order, g.hist, g.scan_partials, P, s, err_dev);
         }
     }
     { StageScope st_(ST_SCAN, s); launch_forward_scans(g.tiles_touched, rows_path ? g.rect : nullptr, g.order, g.offsets, g.row_first, g.row_offsets, g.drect, g.desc_r, g.huge_list, g.counters + 2, g.scan2_status, g.counters, err_dev, P, s); }
@@ -776,10 +775,6 @@ int backward_impl(const BackwardIn& in)
     ga.jac_flag = g.counters + 5;
     ga.row_sums = g.row_sums;
     ga.conic_op = g.conic_op;
-    // the visible list of a view whose depth sort set the culled Gaussians aside (the device word is 0 if that forward
-    // sorted otherwise, and the list kernel then does nothing)
-    ga.vis_count = depth_sort_plain(in.camera_type) ? nullptr : g.counters + 7;
-    ga.order = g.order;
     ga.dL_dmean2D = in.dL_dmean2D; ga.dL_dconic = in.dL_dconic; ga.dL_dopacity = in.dL_dopacity; ga.dL_dcolor = in.dL_dcolor;
     ga.dL_dmean3D = in.dL_dmean3D; ga.dL_dcov3D = in.dL_dcov3D; ga.dL_dsh = in.M > 0 ? in.dL_dsh : nullptr;
     ga.dL_dscale = in.dL_dscale; ga.dL_drot = in.dL_drot; ga.dpx_dt = in.dpx_dt; ga.dpy_dt = in.dpy_dt;

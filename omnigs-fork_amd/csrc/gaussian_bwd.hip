@@ -719,10 +719,7 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
     float g[GRAD_ROW];
     float4 co = make_float4(0.f, 0.f, 0.f, 0.f);  // conic + opacity of the render record (raw-moment rows)
     const bool valid = idx < a.g_end;
-    // with a visible list (launch_gaussian_backward) this launch writes every Gaussian's outputs as a culled one's and
-    // gaussian_bwd_list_kernel, launched after it, overwrites the visible ones: no wave runs the visible chain here
-    const bool listed = a.vis_count && *a.vis_count != 0u;  // uniform
-    const bool vis = valid && !listed && a.radii[idx] > 0;
+    const bool vis = valid && a.radii[idx] > 0;
     // sums and conic are read for visible Gaussians only (radii > 0 implies instances, preprocess.hip, so
     // row_sum_kernel wrote the row): at config E pinhole 88 % of the Gaussians are culled
     if (vis) {
@@ -758,33 +755,6 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
             wave_rows_store<SH_F4>(reinterpret_cast<float4*>(a.dL_dsh) + (size_t)wave_first * SH_F4, __ballot(valid),
                                    stage, lane);
         }
-    }
-}
-
-// The visible Gaussians of a view whose depth sort set the culled ones aside (order[0, nvis), depth order), densely:
-// at config E pinhole 12 % of the Gaussians are visible, and in index order every wave of 64 holds a few of them, so
-// every wave of gaussian_bwd_kernel paid the visible chain (≈ 18 us at 3 waves per SIMD) for ~8 lanes. Here every lane
-// of a wave is visible; grid-striding waves over the list. The rows are this lane's own (random Gaussians: the SH rows
-// are read and dL_dsh written per lane, not through the wave's LDS image). Same arithmetic as the wave kernel.
-template <int CAM, int MC>
-__global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_list_kernel(GaussBwdArgs a)
-{
-    const uint32_t cnt = *a.vis_count;
-    if (cnt == 0u) return;  // no visible list: gaussian_bwd_kernel did everything
-    const uint32_t nvis = cnt - 1u;
-    const bool jac = MC == 16 && a.shs && a.sh_jac && a.campos &&
-                     *a.jac_flag == sh_jac_key(a.shs, a.means3D, __float_as_uint(a.campos[0]),
-                                               __float_as_uint(a.campos[1]), __float_as_uint(a.campos[2]));  // uniform
-    for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < nvis; t += gridDim.x * 256u) {
-        const int idx = (int)a.order[t];
-        float g[GRAD_ROW];
-#pragma unroll
-        for (int c = 0; c < GRAD_ROW; ++c) g[c] = a.row_sums[(size_t)idx * GRAD_ROW + c];
-        const float4 co = a.conic_op[idx];
-        const float4* sh4 = MC == 16 && a.shs ? reinterpret_cast<const float4*>(a.shs) + (size_t)idx * 12 : nullptr;
-        float4* dsh4 = MC == 16 ? reinterpret_cast<float4*>(a.dL_dsh) + (size_t)idx * 12 : nullptr;
-        raw_row_to_grads(g, co, a.W, a.H);
-        gaussian_bwd_point<CAM, MC>(a, idx, g, sh4, dsh4, jac ? a.sh_jac + (size_t)idx * 9 : nullptr);
     }
 }
 
@@ -909,39 +879,8 @@ void launch_gaussian_backward(int camera_type, const GaussBwdArgs& a, hipStream_
                      (reinterpret_cast<uintptr_t>(a.shs) % 16) == 0;
     auto k = camera_type == CAM_LONLAT ? (m16 ? gaussian_bwd_kernel<CAM_LONLAT, 16> : gaussian_bwd_kernel<CAM_LONLAT, 0>)
                                        : (m16 ? gaussian_bwd_kernel<CAM_PINHOLE, 16> : gaussian_bwd_kernel<CAM_PINHOLE, 0>);
-    // the visible list (device word; 0 = none) serves a launch over all P Gaussians that writes dL_dsh rows or has no
-    // 16-float rows (the list kernel writes an MC == 16 row straight to dL_dsh)
-    GaussBwdArgs b = a;
-    const bool list = a.vis_count && a.order && a.g_begin == 0 && a.g_end == a.P && (a.dL_dsh || !m16);
-    if (!list) b.vis_count = nullptr;
-    if (list) {
-        auto kl = camera_type == CAM_LONLAT
-                      ? (m16 ? gaussian_bwd_list_kernel<CAM_LONLAT, 16> : gaussian_bwd_list_kernel<CAM_LONLAT, 0>)
-                      : (m16 ? gaussian_bwd_list_kernel<CAM_PINHOLE, 16> : gaussian_bwd_list_kernel<CAM_PINHOLE, 0>);
-        // grid-striding over the list with the blocks the device holds at once (asked once per device)
-        static thread_local int cached_dev = -1;
-        static thread_local uint32_t resident = 0;
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-        if (dev != cached_dev) {
-            int cus = 0, per_cu = 0;
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gaussian_bwd_list_kernel<CAM_PINHOLE, 16>, 256, 0) !=
-                    hipSuccess ||
-                per_cu <= 0)
-                per_cu = 3;
-            resident = (uint32_t)(cus * per_cu);
-            cached_dev = dev;
-        }
-        const dim3 gl(std::min<uint32_t>(grid.x, resident));
-        if (ev_start) hipExtLaunchKernelGGL(k, grid, dim3(256), 0, s, ev_start, nullptr, 0, b);
-        else k<<<grid, 256, 0, s>>>(b);
-        if (ev_stop) hipExtLaunchKernelGGL(kl, gl, dim3(256), 0, s, nullptr, ev_stop, 0, b);
-        else kl<<<gl, 256, 0, s>>>(b);
-        return;
-    }
-    if (ev_start || ev_stop) hipExtLaunchKernelGGL(k, grid, dim3(256), 0, s, ev_start, ev_stop, 0, b);
-    else k<<<grid, 256, 0, s>>>(b);
+    if (ev_start || ev_stop) hipExtLaunchKernelGGL(k, grid, dim3(256), 0, s, ev_start, ev_stop, 0, a);
+    else k<<<grid, 256, 0, s>>>(a);
 }
 
 }  // namespace omr

@@ -84,9 +84,8 @@ ZeroSpan radix_zero_span(uint32_t* hist, size_t n, int passes);
 size_t depth_sort_scratch_words(size_t n);
 size_t depth_sort_partials_words(size_t n);
 ZeroSpan depth_sort_zero_span(uint32_t* hist, size_t n);
-// vis_out (device word, may be NULL): nvis + 1 after the sort, nvis = the visible Gaussians, order[0, nvis)
 void depth_sort(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* order, uint32_t* hist,
-                uint32_t* scan_partials, size_t n, hipStream_t s, uint32_t* err, uint32_t* vis_out = nullptr);
+                uint32_t* scan_partials, size_t n, hipStream_t s, uint32_t* err);
 // one-launch exclusive scan of n u32 (in may equal out) of in[i] & mask; n_dev (device word, may be NULL) = live
 // length <= n; status: scan_status_words(n) words zeroed before the launch; err: the look-back error word (NULL: a
 // private one)
@@ -249,10 +248,6 @@ struct GaussBwdArgs {
     const uint32_t* jac_flag;  // GeomState::counters + 5 (sh_jac_key of the forward's inputs, 0: none)
     const float* row_sums;  // [P][GRAD_ROW] each Gaussian's instance rows summed (launch_row_sums)
     const float4* conic_op;  // [P] conic + opacity (GeomState) for the raw-moment rows
-    // the visible list (NULL: none): *vis_count = nvis + 1 when the forward's depth sort put the visible Gaussians
-    // first in order[0, nvis) (GeomState::counters[7]; 0 = it did not). Only a launch over all P Gaussians uses it
-    const uint32_t* vis_count;
-    const uint32_t* order;
     float* dL_dmean2D;   // [P,3]
     float* dL_dconic;    // [P,4] optional (may be null)
     float* dL_dopacity;  // [P]

@@ -297,7 +297,6 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     float4* stage = s_stage[wv];
     GeomState& g = a.g;
     // sh_jac stored (preprocess_point's sh16 rows; the host carved it on the same condition): the key of the inputs
-    if (idx == 0) g.counters[7] = 0u;  // the depth sort's visible count, if it is the culled-aside sort (sort.hip)
     if (idx == 0)
         g.counters[5] = sh_jac_stored(a.colors_precomp, a.M, a.shs)
                             ? sh_jac_key(a.shs, a.means3D, __float_as_uint(a.campos[0]), __float_as_uint(a.campos[1]),

@@ -383,7 +383,6 @@ struct DepthPass {
     int pass = -1;  // < 0: a plain LSD pass (digit = bits [shift, shift + 8) of the key)
     uint32_t* words = nullptr;
     uint32_t* vals_final = nullptr;
-    uint32_t* vis_out = nullptr;  // pass 0 stores nvis + 1 here (depth_sort's caller: the backward's visible list)
 };
 
 // BLOCK_MAJOR: hist[block][digit] (read back by the self-scanning downsweep of small sorts); else hist[digit][block].
@@ -516,10 +515,7 @@ __global__ __launch_bounds__(THREADS) void radix_downsweep_kernel(const K* keys_
     } else if (dig) {
         s_gbase[tid] = hist_scanned[(size_t)tid * nblocks + blockIdx.x];
         // depth pass 0: block 0's start of the culled bucket = the number of visible keys, for passes 1..3
-        if (depth && dp.pass == 0 && blockIdx.x == 0 && tid == DEPTH_CULLED_BUCKET) {
-            dp.words[0] = s_gbase[tid];
-            if (dp.vis_out) *dp.vis_out = s_gbase[tid] + 1u;
-        }
+        if (depth && dp.pass == 0 && blockIdx.x == 0 && tid == DEPTH_CULLED_BUCKET) dp.words[0] = s_gbase[tid];
     }
     const size_t base = tile0 + (size_t)w * PER_WAVE + lane;
     uint32_t k[ROUNDS], v[ROUNDS], lr[ROUNDS];
@@ -711,8 +707,6 @@ __global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, 
     const uint32_t vb = s_vb;
     uint32_t total;
     const uint32_t gstart = block_exclusive_scan<OS_THREADS>(dig ? ghist[tid] : 0u, s_wave, &total);
-    // depth pass 0: the start of the culled bucket = the number of visible keys
-    if (depth && dp.pass == 0 && vb == 0 && tid == DEPTH_CULLED_BUCKET && dp.vis_out) *dp.vis_out = gstart + 1u;
     // depth passes 1..3 sort the visible keys alone, which their digit totals count: no count word to wait for
     const size_t n = depth && dp.pass > 0 ? (size_t)total : n_live;
     const size_t tile0 = (size_t)vb * TILE_N;
@@ -1390,7 +1384,7 @@ ZeroSpan depth_sort_zero_span(uint32_t* hist, size_t n)
 }
 
 void depth_sort(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* order, uint32_t* hist,
-                uint32_t* scan_partials, size_t n, hipStream_t s, uint32_t* err, uint32_t* vis_out)
+                uint32_t* scan_partials, size_t n, hipStream_t s, uint32_t* err)
 {
     if (n == 0) return;
     uint32_t* words = hist + depth_words_at(n);
@@ -1406,7 +1400,6 @@ void depth_sort(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val
             DepthPass dp;
             dp.pass = p;
             dp.vals_final = order;
-            dp.vis_out = vis_out;
             auto kern = os_tile(n) == OS_TILE ? onesweep_kernel<uint32_t, OS_TILE, true>
                                               : onesweep_kernel<uint32_t, OS_TILE_SMALL, true>;
             kern<<<nb, OS_THREADS, 0, s>>>(ki, vi, ko, vo, n, nullptr, nullptr, 0,
@@ -1426,7 +1419,6 @@ void depth_sort(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val
         dp.pass = p;
         dp.words = words;
         dp.vals_final = order;
-        dp.vis_out = vis_out;
         const uint32_t* count = p == 0 ? nullptr : words;
         radix_upsweep_kernel<uint32_t, false, SORT_ITEMS_S, SORT_THREADS_S, true><<<nb, SORT_THREADS_S, 0, s>>>(
             ki, n, count, 0, hist, nb, scan_partials, 2 * nbs + 2, dp);

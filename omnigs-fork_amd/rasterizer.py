@@ -561,9 +561,7 @@ def debug_counters(P, geomBuffer) -> dict:
            "debug_counters")
     c = [int(v) & 0xFFFFFFFF for v in out.cpu().tolist()]
     return {"num_rendered": c[0], "prefiltered_flag": c[1], "huge": c[2], "error": c[3], "row_slots": c[4],
-            "sh_jac": c[5] != 0, "sh_jac_key": c[5],
-            # the culled-aside depth sort's visible count (the backward's visible list), None after another sort
-            "visible": c[7] - 1 if c[7] else None}
+            "sh_jac": c[5] != 0, "sh_jac_key": c[5]}
 
 
 def debug_depth_sort_mode(mode: int) -> int:
