@@ -500,22 +500,39 @@ __global__ __launch_bounds__(256, OMR_RS_MINW) void row_sum_kernel(RowSumArgs a)
 #endif
 
 
+// A Gaussian's small outputs (every [P][k] gradient but dL_dsh and dL_dcolor), held in registers until its wave
+// stores them as contiguous spans through LDS (wave_small_store; the MC == 16 kernel), or written lane by lane (so ==
+// nullptr).
+struct SmallOut {
+    float m2[2], op, con[3], cov[6], px[3], py[3], m3[3], sc[3], rot[4];
+};
+
 // Everything after the row sums for one visible Gaussian idx (radii > 0). dsh4: where the MC == 16 dL_dsh row goes.
 template <int CAM, int MC>
 __device__ __forceinline__ void gaussian_bwd_point(const GaussBwdArgs& a, int idx, float (&g)[GRAD_ROW],
-                                                   const float4* sh4, float4* dsh4, const float* jac = nullptr)
+                                                   const float4* sh4, float4* dsh4, const float* jac = nullptr,
+                                                   SmallOut* so = nullptr)
 {
     const int Mr = MC > 0 ? MC : a.M;
     // 1. this Gaussian's summed instance rows
-    a.dL_dmean2D[3 * idx + 0] = g[0];
-    a.dL_dmean2D[3 * idx + 1] = g[1];
-    a.dL_dmean2D[3 * idx + 2] = 0.f;
-    a.dL_dopacity[idx] = g[5];  // dL_dcolor = g[6..8] was written by row_sum_kernel
-    if (a.dL_dconic) {
-        a.dL_dconic[4 * idx + 0] = g[2];
-        a.dL_dconic[4 * idx + 1] = g[3];
-        a.dL_dconic[4 * idx + 2] = 0.f;
-        a.dL_dconic[4 * idx + 3] = g[4];
+    if (so) {
+        so->m2[0] = g[0];
+        so->m2[1] = g[1];
+        so->op = g[5];
+        so->con[0] = g[2];
+        so->con[1] = g[3];
+        so->con[2] = g[4];
+    } else {
+        a.dL_dmean2D[3 * idx + 0] = g[0];
+        a.dL_dmean2D[3 * idx + 1] = g[1];
+        a.dL_dmean2D[3 * idx + 2] = 0.f;
+        a.dL_dopacity[idx] = g[5];  // dL_dcolor = g[6..8] was written by row_sum_kernel
+        if (a.dL_dconic) {
+            a.dL_dconic[4 * idx + 0] = g[2];
+            a.dL_dconic[4 * idx + 1] = g[3];
+            a.dL_dconic[4 * idx + 2] = 0.f;
+            a.dL_dconic[4 * idx + 3] = g[4];
+        }
     }
 
     // 2. covariance backward
@@ -633,11 +650,18 @@ __device__ __forceinline__ void gaussian_bwd_point(const GaussBwdArgs& a, int id
         dmean.y += (proj[4] * m_w - proj[7] * mul1) * g[0] + (proj[5] * m_w - proj[7] * mul2) * g[1];
         dmean.z += (proj[8] * m_w - proj[11] * mul1) * g[0] + (proj[9] * m_w - proj[11] * mul2) * g[1];
     }
+    if (so) {
 #pragma unroll
-    for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * idx + k] = dcov[k];
-    if (a.dpx_dt) {
-        a.dpx_dt[3 * idx + 0] = dpx.x; a.dpx_dt[3 * idx + 1] = dpx.y; a.dpx_dt[3 * idx + 2] = dpx.z;
-        a.dpy_dt[3 * idx + 0] = dpy.x; a.dpy_dt[3 * idx + 1] = dpy.y; a.dpy_dt[3 * idx + 2] = dpy.z;
+        for (int k = 0; k < 6; ++k) so->cov[k] = dcov[k];
+        so->px[0] = dpx.x; so->px[1] = dpx.y; so->px[2] = dpx.z;
+        so->py[0] = dpy.x; so->py[1] = dpy.y; so->py[2] = dpy.z;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * idx + k] = dcov[k];
+        if (a.dpx_dt) {
+            a.dpx_dt[3 * idx + 0] = dpx.x; a.dpx_dt[3 * idx + 1] = dpx.y; a.dpx_dt[3 * idx + 2] = dpx.z;
+            a.dpy_dt[3 * idx + 0] = dpy.x; a.dpy_dt[3 * idx + 1] = dpy.y; a.dpy_dt[3 * idx + 2] = dpy.z;
+        }
     }
 
     // 3. SH backward
@@ -655,25 +679,39 @@ __device__ __forceinline__ void gaussian_bwd_point(const GaussBwdArgs& a, int id
             for (int c = 0; c < Mr * 3; ++c) a.dL_dsh[(size_t)idx * Mr * 3 + c] = 0.f;
         }
     }
-    a.dL_dmean3D[3 * idx + 0] = dmean.x;
-    a.dL_dmean3D[3 * idx + 1] = dmean.y;
-    a.dL_dmean3D[3 * idx + 2] = dmean.z;
-
     // 4. scale / rotation backward
     float ds[3] = {0.f, 0.f, 0.f}, dr[4] = {0.f, 0.f, 0.f, 0.f};
     if (a.scales) cov3d_backward(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2], a.scale_modifier, q, dcov, ds, dr);
+    if (so) {
+        so->m3[0] = dmean.x; so->m3[1] = dmean.y; so->m3[2] = dmean.z;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) a.dL_dscale[3 * idx + k] = ds[k];
+        for (int k = 0; k < 3; ++k) so->sc[k] = ds[k];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) a.dL_drot[4 * idx + k] = dr[k];
+        for (int k = 0; k < 4; ++k) so->rot[k] = dr[k];
+    } else {
+        a.dL_dmean3D[3 * idx + 0] = dmean.x;
+        a.dL_dmean3D[3 * idx + 1] = dmean.y;
+        a.dL_dmean3D[3 * idx + 2] = dmean.z;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) a.dL_dscale[3 * idx + k] = ds[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a.dL_drot[4 * idx + k] = dr[k];
+    }
 }
 
 // backward.cu:805-840 targets etc. of a culled Gaussian (radii == 0): every output zero (the caller allocates the
 // gradient tensors without zero-filling them)
 template <int MC>
-__device__ __forceinline__ void gaussian_bwd_culled(const GaussBwdArgs& a, int idx, float4* dsh4)
+__device__ __forceinline__ void gaussian_bwd_culled(const GaussBwdArgs& a, int idx, float4* dsh4, SmallOut* so = nullptr)
 {
     const int Mr = MC > 0 ? MC : a.M;
+    if (so) {
+        *so = SmallOut{};
+        if (a.dL_dsh && MC == 16)
+#pragma unroll
+            for (int q = 0; q < 12; ++q) dsh4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         a.dL_dmean2D[3 * idx + c] = 0.f;  // dL_dcolor: zeros from row_sum_kernel
@@ -699,6 +737,55 @@ __device__ __forceinline__ void gaussian_bwd_culled(const GaussBwdArgs& a, int i
     if (a.dpx_dt)
 #pragma unroll
         for (int c = 0; c < 3; ++c) a.dpx_dt[3 * idx + c] = a.dpy_dt[3 * idx + c] = 0.f;
+}
+
+// The wave's small outputs as contiguous spans: each lane parks its values in the LDS image ([array][lane][k]), then
+// every [P][k] array gets its 64 k floats from wave_first on as 16-B stores (1 KiB per instruction) where the span is
+// 16-B aligned, else as dword stores (256 B per instruction), instead of k dword stores per lane 4k bytes apart.
+// n: the wave's valid Gaussians (a tail wave stores only theirs).
+__device__ __forceinline__ void wave_small_store(const GaussBwdArgs& a, const SmallOut& so, int wave_first, int n,
+                                                 float* img, uint32_t lane)
+{
+    constexpr int O_M2 = 0, O_OP = O_M2 + 64 * 3, O_CON = O_OP + 64, O_COV = O_CON + 64 * 4, O_PX = O_COV + 64 * 6,
+                  O_PY = O_PX + 64 * 3, O_M3 = O_PY + 64 * 3, O_SC = O_M3 + 64 * 3, O_ROT = O_SC + 64 * 3;
+    float* m2 = img + O_M2 + lane * 3;
+    m2[0] = so.m2[0]; m2[1] = so.m2[1]; m2[2] = 0.f;
+    img[O_OP + lane] = so.op;
+    float* con = img + O_CON + lane * 4;
+    con[0] = so.con[0]; con[1] = so.con[1]; con[2] = 0.f; con[3] = so.con[2];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) img[O_COV + lane * 6 + k] = so.cov[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        img[O_PX + lane * 3 + k] = so.px[k];
+        img[O_PY + lane * 3 + k] = so.py[k];
+        img[O_M3 + lane * 3 + k] = so.m3[k];
+        img[O_SC + lane * 3 + k] = so.sc[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) img[O_ROT + lane * 4 + k] = so.rot[k];
+    wave_sync();
+    auto span = [&](float* dst, int off, int K) {
+        if (!dst) return;
+        dst += (size_t)wave_first * K;
+        const int nf = n * K;
+        if (((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) && (nf & 3) == 0) {  // wave-uniform
+            float4* d4 = reinterpret_cast<float4*>(dst);
+            const float4* s4 = reinterpret_cast<const float4*>(img + off);
+            for (int j = (int)lane; j < nf / 4; j += 64) d4[j] = s4[j];
+        } else {
+            for (int j = (int)lane; j < nf; j += 64) dst[j] = img[off + j];
+        }
+    };
+    span(a.dL_dmean2D, O_M2, 3);
+    span(a.dL_dopacity, O_OP, 1);
+    span(a.dL_dconic, O_CON, 4);
+    span(a.dL_dcov3D, O_COV, 6);
+    span(a.dpx_dt, O_PX, 3);
+    span(a.dpy_dt, O_PY, 3);
+    span(a.dL_dmean3D, O_M3, 3);
+    span(a.dL_dscale, O_SC, 3);
+    span(a.dL_drot, O_ROT, 4);
 }
 
 // One wave per 64 consecutive Gaussians. For MC == 16 (launch_gaussian_backward checks the 16-B alignment) the
@@ -744,16 +831,27 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
             wave_sync();
         }
     }
+    // pinhole views store the small outputs as spans (wave_small_store): their waves are mostly culled Gaussians, whose
+    // zeros are most of the bytes (E pinhole gaussian_bwd 0.445 -> 0.396 ms); at lonlat views, whose Gaussians are
+    // nearly all visible, the LDS round trip at the end of the chain costs more than the coalescing gains (C 0.081 ->
+    // 0.089, E 0.376 -> 0.386 ms), so they keep the lane stores (profiles/r05ai_ab.txt)
+    constexpr bool SPANS = STAGED && CAM == CAM_PINHOLE;
+    SmallOut so;
+    SmallOut* sop = SPANS ? &so : nullptr;
     if (vis) {
         raw_row_to_grads(g, co, a.W, a.H);
-        gaussian_bwd_point<CAM, MC>(a, idx, g, sh4, dsh4, jac ? a.sh_jac + (size_t)idx * 9 : nullptr);
+        gaussian_bwd_point<CAM, MC>(a, idx, g, sh4, dsh4, jac ? a.sh_jac + (size_t)idx * 9 : nullptr, sop);
     }
-    else if (valid) gaussian_bwd_culled<MC>(a, idx, dsh4);
+    else if (valid) gaussian_bwd_culled<MC>(a, idx, dsh4, sop);
     if constexpr (STAGED) {
         if (a.dL_dsh) {
             wave_sync();
             wave_rows_store<SH_F4>(reinterpret_cast<float4*>(a.dL_dsh) + (size_t)wave_first * SH_F4, __ballot(valid),
                                    stage, lane);
+        }
+        if constexpr (SPANS) {
+            wave_sync();  // the image's dL_dsh rows are read: it now stages the small outputs
+            wave_small_store(a, so, wave_first, min(64, a.g_end - wave_first), reinterpret_cast<float*>(stage), lane);
         }
     }
 }
