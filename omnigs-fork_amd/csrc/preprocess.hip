@@ -310,24 +310,30 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     float shv[48];
     PreIn in;
     load_pre_in<CAM>(a, idx, valid, in);
-    // Pinhole views request the rows after the geometry, for the visible lanes only: a frustum culls most of a scene
-    // (88 % at E pinhole), and the rows of the visible ones are all the colour needs. Interleaved A/B at E pinhole (profiles/r04p3_ab_Ep.txt): preprocess 0.314 -> 0.300 ms,
-    // 1295 -> 1317 MP/s, against requesting the rows of every point in front of the camera before the geometry.
-    // Equirect views see every point, so their rows are requested first and their latency overlaps the projection.
-    constexpr bool LATE = CAM != CAM_LONLAT;
-    // equirect: every row is requested now, into registers, and parked in LDS only after the projection, so the
-    // loads' latency overlaps it (the 48 VGPRs are free: the LDS image caps the kernel at 3 waves per SIMD). Waiting
-    // for them before the projection (wave_rows_load) cost C 0.024 ms of the kernel's 0.092: without the rows it took
-    // 0.068 ms (profiles/r05v_ab.txt).
+    // Every view requests the SH rows before the projection, into registers, and parks them in LDS after it, so the
+    // loads' latency overlaps the projection (the 48 VGPRs are free: the LDS image caps the kernel at 3 waves per
+    // SIMD). Waiting for them before the projection (wave_rows_load) cost C 0.024 ms of the kernel's 0.092: without
+    // the rows it took 0.068 ms (profiles/r05v_ab.txt). Equirect views see every point: every valid lane's row. A
+    // frustum culls most of a pinhole view's scene (88 % at E pinhole), so there only the rows of the lanes whose mean
+    // lies in front of the near plane and inside the 1.3x widened view cone (the cov2D clamp's, forward.cu:92-106) are
+    // requested: a prediction from the mean alone. A visible lane outside it (a large Gaussian whose mean is off-view)
+    // reads its row itself after the projection.
+    uint64_t fetch_rows = __ballot(valid);
+    if constexpr (CAM != CAM_LONLAT) {
+        const float tz = in.v[2] * p_orig.x + in.v[6] * p_orig.y + in.v[10] * p_orig.z + in.v[14];
+        const float tx = in.v[0] * p_orig.x + in.v[4] * p_orig.y + in.v[8] * p_orig.z + in.v[12];
+        const float ty = in.v[1] * p_orig.x + in.v[5] * p_orig.y + in.v[9] * p_orig.z + in.v[13];
+        const bool near = valid && tz > 0.2f && fabsf(tx) <= 1.3f * a.tan_fovx * tz && fabsf(ty) <= 1.3f * a.tan_fovy * tz;
+        fetch_rows = __ballot(near);
+    }
     rowv4 early[SH_F4];
     // every load issued so far lands before the rows are requested, on both sides of the branch below: loads retire
     // in order on vmcnt, and a later wait for one of them would otherwise have to count the rows in (the wait
     // counter merges the branch's sides conservatively), i.e. wait for the rows too
-    if (!LATE)
-        asm volatile("" ::"v"(in.opacity), "v"(in.sx), "v"(in.sy), "v"(in.sz), "v"(in.q.x), "v"(in.q.y), "v"(in.q.z),
-                     "v"(in.q.w), "v"(p_orig.x), "v"(p_orig.y), "v"(p_orig.z));
-    if (sh16 && !LATE) {
-        wave_rows_fetch<SH_F4>(reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4, __ballot(valid), nf4,
+    asm volatile("" ::"v"(in.opacity), "v"(in.sx), "v"(in.sy), "v"(in.sz), "v"(in.q.x), "v"(in.q.y), "v"(in.q.z),
+                 "v"(in.q.w), "v"(p_orig.x), "v"(p_orig.y), "v"(p_orig.z));
+    if (sh16 && fetch_rows) {
+        wave_rows_fetch<SH_F4>(reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4, fetch_rows, nf4,
                                lane, early);
     }
     PreOut o;
@@ -335,16 +341,22 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     if (sh16) {
         const uint64_t rows = __ballot(vis);
         if (rows) {  // wave-uniform
-            if (LATE)
-                wave_rows_load<SH_F4>(reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4, rows, nf4,
-                                      stage, lane);
-            else
-                wave_rows_park<SH_F4>(early, stage, lane);
+            wave_rows_park<SH_F4>(early, stage, lane);
             wave_sync();
 #pragma unroll
             for (int q = 0; q < SH_F4; ++q) {
                 const float4 v = q < nf4 ? stage[lane * stage_stride<SH_F4>() + q] : make_float4(0.f, 0.f, 0.f, 0.f);
                 shv[4 * q] = v.x, shv[4 * q + 1] = v.y, shv[4 * q + 2] = v.z, shv[4 * q + 3] = v.w;
+            }
+            if constexpr (CAM != CAM_LONLAT) {
+                if (vis && !((fetch_rows >> lane) & 1u)) {  // a visible lane outside the prediction: its own row
+                    const float4* row = reinterpret_cast<const float4*>(a.shs) + (size_t)idx * SH_F4;
+#pragma unroll
+                    for (int q = 0; q < SH_F4; ++q) {
+                        const float4 v = q < nf4 ? row[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+                        shv[4 * q] = v.x, shv[4 * q + 1] = v.y, shv[4 * q + 2] = v.z, shv[4 * q + 3] = v.w;
+                    }
+                }
             }
             wave_sync();  // the image is reused for the records below
             if (vis) {
