@@ -127,12 +127,24 @@ __device__ __forceinline__ void cov3d_forward(float sx, float sy, float sz, floa
 // MC == 16: the SH row is read as 12 float4 from row4 and the dL_dsh row written as 12 float4 to out4 (both the
 // lane's row of the wave's LDS staging image, or both global rows; the row is read before it is overwritten);
 // otherwise both are read/written in global memory at idx.
+// A visible Gaussian's per-Gaussian inputs, loaded together with its row sums (the MC == 16 kernel): read where
+// gaussian_bwd_point uses them, the loads issued only after its first stores (which may alias them, as far as the
+// compiler knows), a second memory round trip on every wave's chain
+struct GIn {
+    F3 mean;
+    float s[3];
+    float4 q;
+    float jac[9];
+    uint8_t clamp;
+};
+
 // jac != NULL: the forward's dRGB/ddir of this Gaussian (GeomState::sh_jac: gx, gy, gz per channel), and the SH row is
 // not read at all.
 template <int MC>
 __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const float* campos, const float* shs,
                                           const float4* row4, uint8_t clamp_bits, F3 dRGB, float* dL_dsh,
-                                          float4* out4, const float* jac = nullptr)
+                                          float4* out4, const float* jac = nullptr, const GIn* gin = nullptr,
+                                          bool gin_jac = false)
 {
     const int Mr = MC > 0 ? MC : M;
     const float dox = pos.x - campos[0], doy = pos.y - campos[1], doz = pos.z - campos[2];
@@ -144,7 +156,10 @@ __device__ __forceinline__ F3 sh_backward(int idx, int deg, int M, F3 pos, const
     float coef[16];
     sh_basis(deg, x, y, z, coef);
     float gx[3], gy[3], gz[3];  // dRGB/dx etc per channel
-    if (jac) {
+    if (gin_jac) {  // the same nine values, already in registers (GIn)
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) gx[ch] = gin->jac[ch], gy[ch] = gin->jac[3 + ch], gz[ch] = gin->jac[6 + ch];
+    } else if (jac) {
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) gx[ch] = jac[ch], gy[ch] = jac[3 + ch], gz[ch] = jac[6 + ch];
     } else if constexpr (MC == 16) {
@@ -511,7 +526,7 @@ struct SmallOut {
 template <int CAM, int MC>
 __device__ __forceinline__ void gaussian_bwd_point(const GaussBwdArgs& a, int idx, float (&g)[GRAD_ROW],
                                                    const float4* sh4, float4* dsh4, const float* jac = nullptr,
-                                                   SmallOut* so = nullptr)
+                                                   SmallOut* so = nullptr, const GIn* gin = nullptr)
 {
     const int Mr = MC > 0 ? MC : a.M;
     // 1. this Gaussian's summed instance rows
@@ -536,19 +551,28 @@ __device__ __forceinline__ void gaussian_bwd_point(const GaussBwdArgs& a, int id
     }
 
     // 2. covariance backward
-    const F3 mean = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
+    const F3 mean = gin ? gin->mean : F3{a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
     const float* v = a.viewmatrix;
     float c3[6];
     float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    float sc[3] = {0.f, 0.f, 0.f};
     if (a.scales) {
-        if ((reinterpret_cast<uintptr_t>(a.rotations) & 15u) == 0) q = reinterpret_cast<const float4*>(a.rotations)[idx];
-        else q = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
+        if (gin) {
+            q = gin->q;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) sc[k] = gin->s[k];
+        } else {
+            if ((reinterpret_cast<uintptr_t>(a.rotations) & 15u) == 0) q = reinterpret_cast<const float4*>(a.rotations)[idx];
+            else q = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) sc[k] = a.scales[3 * idx + k];
+        }
     }
     if (a.cov3D_precomp) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) c3[k] = a.cov3D_precomp[6 * idx + k];
     } else {
-        cov3d_forward(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2], a.scale_modifier, q, c3);
+        cov3d_forward(sc[0], sc[1], sc[2], a.scale_modifier, q, c3);
     }
     const float tx = v[0] * mean.x + v[4] * mean.y + v[8] * mean.z + v[12];
     const float ty = v[1] * mean.x + v[5] * mean.y + v[9] * mean.z + v[13];
@@ -666,8 +690,8 @@ __device__ __forceinline__ void gaussian_bwd_point(const GaussBwdArgs& a, int id
 
     // 3. SH backward
     if (a.shs) {
-        const F3 dm = sh_backward<MC>(idx, a.D, a.M, mean, a.campos, a.shs, sh4, a.clamped[idx], F3{g[6], g[7], g[8]},
-                                      a.dL_dsh, dsh4, jac);
+        const F3 dm = sh_backward<MC>(idx, a.D, a.M, mean, a.campos, a.shs, sh4, gin ? gin->clamp : a.clamped[idx],
+                                      F3{g[6], g[7], g[8]}, a.dL_dsh, dsh4, gin ? nullptr : jac, gin, gin && jac);
         dmean.x += dm.x;
         dmean.y += dm.y;
         dmean.z += dm.z;
@@ -681,7 +705,7 @@ __device__ __forceinline__ void gaussian_bwd_point(const GaussBwdArgs& a, int id
     }
     // 4. scale / rotation backward
     float ds[3] = {0.f, 0.f, 0.f}, dr[4] = {0.f, 0.f, 0.f, 0.f};
-    if (a.scales) cov3d_backward(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2], a.scale_modifier, q, dcov, ds, dr);
+    if (a.scales) cov3d_backward(sc[0], sc[1], sc[2], a.scale_modifier, q, dcov, ds, dr);
     if (so) {
         so->m3[0] = dmean.x; so->m3[1] = dmean.y; so->m3[2] = dmean.z;
 #pragma unroll
@@ -706,7 +730,7 @@ __device__ __forceinline__ void gaussian_bwd_culled(const GaussBwdArgs& a, int i
 {
     const int Mr = MC > 0 ? MC : a.M;
     if (so) {
-        *so = SmallOut{};
+        // the caller zeroed *so
         if (a.dL_dsh && MC == 16)
 #pragma unroll
             for (int q = 0; q < 12; ++q) dsh4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -807,22 +831,37 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
     float4 co = make_float4(0.f, 0.f, 0.f, 0.f);  // conic + opacity of the render record (raw-moment rows)
     const bool valid = idx < a.g_end;
     const bool vis = valid && a.radii[idx] > 0;
-    // sums and conic are read for visible Gaussians only (radii > 0 implies instances, preprocess.hip, so
-    // row_sum_kernel wrote the row): at config E pinhole 88 % of the Gaussians are culled
-    if (vis) {
-#pragma unroll
-        for (int c = 0; c < GRAD_ROW; ++c) g[c] = a.row_sums[(size_t)idx * GRAD_ROW + c];
-        co = a.conic_op[idx];
-    }
-    float4* stage = s_stage[wv];
-    // MC == 16 only (the MC == 0 path reads and writes the rows itself, and skips the write for dL_dsh == NULL)
-    float4* dsh4 = STAGED ? stage + lane * stage_stride<SH_F4>() : nullptr;
-    const float4* sh4 = dsh4;
     // the forward stored dRGB/ddir (sh_jac) when it staged these rows: the SH rows are then not needed here, unless
     // this backward was handed other SH, means or campos than that forward (raster_common.h: sh_jac_key)
     const bool jac = STAGED && a.shs && a.sh_jac && a.campos &&
                      *a.jac_flag == sh_jac_key(a.shs, a.means3D, __float_as_uint(a.campos[0]),
                                                __float_as_uint(a.campos[1]), __float_as_uint(a.campos[2]));  // uniform
+    // sums and conic are read for visible Gaussians only (radii > 0 implies instances, preprocess.hip, so
+    // row_sum_kernel wrote the row): at config E pinhole 88 % of the Gaussians are culled. The MC == 16 kernel reads
+    // every other per-Gaussian input with them (GIn)
+    GIn gin;
+    if (vis) {
+#pragma unroll
+        for (int c = 0; c < GRAD_ROW; ++c) g[c] = a.row_sums[(size_t)idx * GRAD_ROW + c];
+        co = a.conic_op[idx];
+        if constexpr (STAGED) {
+            gin.mean = F3{a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
+            if (a.scales) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) gin.s[k] = a.scales[3 * idx + k];
+                if ((reinterpret_cast<uintptr_t>(a.rotations) & 15u) == 0) gin.q = reinterpret_cast<const float4*>(a.rotations)[idx];
+                else gin.q = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
+            }
+            if (a.shs) gin.clamp = a.clamped[idx];
+            if (jac)
+#pragma unroll
+                for (int k = 0; k < 9; ++k) gin.jac[k] = a.sh_jac[(size_t)idx * 9 + k];
+        }
+    }
+    float4* stage = s_stage[wv];
+    // MC == 16 only (the MC == 0 path reads and writes the rows itself, and skips the write for dL_dsh == NULL)
+    float4* dsh4 = STAGED ? stage + lane * stage_stride<SH_F4>() : nullptr;
+    const float4* sh4 = dsh4;
     if constexpr (STAGED) {
         if (a.shs && !jac) {
             const int nf4 = (3 * (a.D + 1) * (a.D + 1) + 3) >> 2;
@@ -837,10 +876,20 @@ __global__ __launch_bounds__(256, OMR_GBWD_MINW) void gaussian_bwd_kernel(GaussB
     // 0.089, E 0.376 -> 0.386 ms), so they keep the lane stores (profiles/r05ai_ab.txt)
     constexpr bool SPANS = STAGED && CAM == CAM_PINHOLE;
     SmallOut so;
+    if constexpr (SPANS) {  // a culled Gaussian's values; a visible one overwrites them all
+        so.m2[0] = so.m2[1] = so.op = 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) so.con[k] = so.px[k] = so.py[k] = so.m3[k] = so.sc[k] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) so.cov[k] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) so.rot[k] = 0.f;
+    }
     SmallOut* sop = SPANS ? &so : nullptr;
     if (vis) {
         raw_row_to_grads(g, co, a.W, a.H);
-        gaussian_bwd_point<CAM, MC>(a, idx, g, sh4, dsh4, jac ? a.sh_jac + (size_t)idx * 9 : nullptr, sop);
+        gaussian_bwd_point<CAM, MC>(a, idx, g, sh4, dsh4, jac ? a.sh_jac + (size_t)idx * 9 : nullptr, sop,
+                                    STAGED ? &gin : nullptr);
     }
     else if (valid) gaussian_bwd_culled<MC>(a, idx, dsh4, sop);
     if constexpr (STAGED) {
