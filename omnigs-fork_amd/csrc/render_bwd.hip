@@ -125,20 +125,10 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
     uint32_t max_c = 0;
 #pragma unroll
     for (int b = 0; b < TW_BANDS; ++b) last[b] = a.n_contrib[pix[b]];
-#pragma unroll
-    for (int b = 0; b < TW_BANDS; ++b) {
-        last[b] = inside[b] ? last[b] : 0u;
-        band_end[b] = uniform(wave_max_u32(last[b]));
-        min_last = min(min_last, ~uniform(wave_max_u32(~(inside[b] ? (last[b] ? last[b] : ~0u) : 0u))));
-        max_c = max(max_c, band_end[b]);
-    }
+    // the range and the per-pixel state depend on none of the last contributors: requested with them, one memory
+    // round trip for the prologue's independent loads instead of three (n_contrib, then ranges, then the pixels)
     const uint2 range = a.ranges[tile];
-    const uint32_t n = range.y - range.x;
-    max_c = min(max_c, n);
-    // this unit's depth segment of the list, local positions [seg_lo, seg_hi) (raster_common.h: CKPT)
-    const uint32_t seg_lo = max(range.x, chunk * CKPT) - range.x;
-    const uint32_t seg_hi = min(range.x + max_c, (chunk + 1) * CKPT) - range.x;
-    const bool resume = seg_hi < max_c;  // a boundary inside the list: some pixels blend behind it
+    const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
     float Tf[TW_BANDS], d0[TW_BANDS], d1[TW_BANDS], d2[TW_BANDS];
 #pragma unroll
     for (int b = 0; b < TW_BANDS; ++b) {
@@ -147,6 +137,19 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
         d1[b] = a.dL_dpix[plane + pix[b]];
         d2[b] = a.dL_dpix[2 * plane + pix[b]];
     }
+#pragma unroll
+    for (int b = 0; b < TW_BANDS; ++b) {
+        last[b] = inside[b] ? last[b] : 0u;
+        band_end[b] = uniform(wave_max_u32(last[b]));
+        min_last = min(min_last, ~uniform(wave_max_u32(~(inside[b] ? (last[b] ? last[b] : ~0u) : 0u))));
+        max_c = max(max_c, band_end[b]);
+    }
+    const uint32_t n = range.y - range.x;
+    max_c = min(max_c, n);
+    // this unit's depth segment of the list, local positions [seg_lo, seg_hi) (raster_common.h: CKPT)
+    const uint32_t seg_lo = max(range.x, chunk * CKPT) - range.x;
+    const uint32_t seg_hi = min(range.x + max_c, (chunk + 1) * CKPT) - range.x;
+    const bool resume = seg_hi < max_c;  // a boundary inside the list: some pixels blend behind it
     float4 ck[TW_BANDS];
     float fc0[TW_BANDS], fc1[TW_BANDS], fc2[TW_BANDS];
     if (resume) {  // wave-uniform; the checkpoint row (chunk + 1) exists: its boundary lies inside this tile's list
@@ -164,7 +167,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
         dp01[b] = f2v{e0, e1};
         dp2[b] = e2;
         T[b] = inside[b] ? Tf[b] : 0.f;
-        s[b] = T[b] * (a.bg[0] * e0 + a.bg[1] * e1 + a.bg[2] * e2);
+        s[b] = T[b] * (bg0 * e0 + bg1 * e1 + bg2 * e2);
         if (resume && last[b] > seg_hi) {
             // the pixel still blends behind the boundary: start from the forward's state there, T in front of the
             // boundary and s = bg . dL/dpix T_final + dL/dpix . (C_final - C in front of the boundary)
