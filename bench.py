@@ -31,6 +31,10 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, Chip-level parameters)
 VALU_PEAK_TFLOPS = 157.3  # MI355X f32 vector peak with v_pk_fma_f32 (MI355X_MICROARCH.md, MFMA/VALU peak table)
+# VALU issue roofline: 256 CUs x 4 SIMDs, each issuing one wave64 VALU instruction per 2 cycles at 2.4 GHz
+# (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles")
+VALU_SIMDS = 1024
+VALU_ISSUE_PER_SIMD = 1.2e9
 
 
 def parse():
@@ -455,13 +459,14 @@ def main():
 
     # dominant kernel: the largest stage of the per-stage pass; its launch duration from the timed pass (HIP events
     # on the launch stream around that kernel alone)
-    pmc, pmc_file = {}, None
+    pmc, pmc_file, pmc_sq_file = {}, None, None
     try:
         with open(args.traffic_json) as f:
             pj = json.load(f)
         if pj.get("config") == cfg_name and pj.get("P") == P:
             pmc = pj.get("kernels", {})
             pmc_file = pj.get("kernel_stats_file")
+            pmc_sq_file = pj.get("sq_file")
     except (OSError, ValueError):
         pass
 
@@ -481,6 +486,11 @@ def main():
         # `frac` from it as algorithmic bytes / avg / peak
         rp = pmc.get(k, {}).get("rocprof_avg_ms")
         ach_rp = b / (rp * 1e-3) / 1e9 if rp else None
+        # VALU roofline beside the HBM one: the kernel's VALU wave-instructions per launch (committed SQ pass of the
+        # same tree, profiles/<tag>_sq.csv via pmc_latest.json) over what the chip issues in its launch time
+        sq = pmc.get(k, {}).get("sq") or {}
+        vi = sq.get("valu_insts_per_launch")
+        vfrac = vi / (VALU_SIMDS * VALU_ISSUE_PER_SIMD * ms_k * 1e-3) if (vi and ms_k > 0) else None
         # traffic = (2 FETCH + WRITE): exact for 16-B/lane streams, an upper bound for gathers, which
         # profiles/calib_fetch.hip shows FETCH counting 1:1 (traffic_lower = FETCH + WRITE)
         return {"stage": k, "avg_launch_ms": round(ms_k, 4), "timed_launches": int(cnt_l) if live_ok else 0,
@@ -489,7 +499,9 @@ def main():
                 "traffic_lower": lo, "traffic_over_algorithmic": round(tr / b, 3) if (tr and b) else None,
                 "traffic_lower_over_algorithmic": round(lo / b, 3) if (lo and b) else None,
                 "avg_launch_ms_rocprof": rp, "frac_rocprof": round(ach_rp / HBM_PEAK_GBS, 5) if ach_rp else None,
-                "rocprof_file": pmc_file if rp else None}
+                "rocprof_file": pmc_file if rp else None,
+                "valu_issue_frac": round(vfrac, 4) if vfrac else None,
+                "valu_insts_per_launch": vi, "sq_file": pmc_sq_file if vi else None}
 
     d = stage_entry(dom)
     survey_b = survey_step_bytes(P, V, L, N, T, cam.camera_type)
@@ -546,6 +558,11 @@ def main():
                      "avg_launch_ms": d["avg_launch_ms"], "timed_launches": d["timed_launches"],
                      "avg_launch_ms_rocprof": d["avg_launch_ms_rocprof"], "frac_rocprof": d["frac_rocprof"],
                      "rocprof_file": d["rocprof_file"],
+                     # the VALU issue roofline of the same kernel (SQ_INSTS_VALU over 1024 SIMDs x 1.2 G/s x launch
+                     # time): what the render kernels can actually be driven towards
+                     "valu_issue_frac": d["valu_issue_frac"], "valu_insts_per_launch": d["valu_insts_per_launch"],
+                     "valu_issue_peak": f"{VALU_SIMDS} SIMDs x {VALU_ISSUE_PER_SIMD / 1e9:.1f} G wave-instructions/s",
+                     "sq_file": d["sq_file"],
                      "step_algorithmic_GBps": round(algo_total / (ms_per_step * 1e-3) / 1e9, 2),
                      "step_algorithmic_bytes": int(algo_total),
                      # SURVEY.md §8(d)'s whole-step formula (the reference's own kernels' compulsory bytes, its 324 B/G

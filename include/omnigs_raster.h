@@ -38,7 +38,11 @@
  *   - the forward keeps, in the geometry buffer, what the backward would otherwise recompute from the inputs it
  *     is passed again: with 16-coefficient SH rows, each visible Gaussian's dRGB/ddir (from the forward's SH
  *     rows and camera position). The backward must therefore be given the forward's inputs, as the reference's
- *     autograd callers do (its gradients are those of that forward);
+ *     autograd callers do (its gradients are those of that forward). CONTRACT: the SH array, means3D and campos
+ *     must not be modified in place between a forward and its backward. The backward recognises other arrays or
+ *     another campos by a key of their addresses and the campos bits, and then recomputes dRGB/ddir from the SH
+ *     it is given as the reference does (backward.cu:56-112). The key does not cover the contents: an in-place
+ *     edit at the same addresses yields the gradients of the forward's SH/means;
  *   - errors: calls return OMR_OK (0) or an OMR_ERR_* code; omr_last_error() gives the message of the last
  *     failing call on this thread. The reference throws std::runtime_error / traps instead.
  */
@@ -280,8 +284,8 @@ int omr_debug_image_state(char* image_buffer, int width, int height, float* fina
 int omr_debug_tile_cost(char* image_buffer, int width, int height, uint32_t* dst, void* stream);
 /* the forward's count words: [0] num_rendered, [1] prefiltered flag, [2] huge-Gaussian count, [3] look-back error,
  * [4] row slots M of the row binning (bin.hip; 0 on sort.hip's path), [5] the stored-dRGB/ddir key (sh_jac: a key of
- * the forward's SH array, means and campos, 0 if not stored), [6] omr_debug_set_sh_jac's copy of [5]; dst: 8 device
- * words */
+ * the forward's SH array, means and campos, 0 if not stored), [6] the same key (omr_debug_set_sh_jac restores [5]
+ * from it); dst: 8 device words */
 int omr_debug_counters(char* geom_buffer, int P, uint32_t* dst, void* stream);
 /* clears (0) or restores (1) the key by which the backward uses the forward's stored dRGB/ddir (GeomState::sh_jac)
  * instead of reading the SH rows: lets a test run both backward paths on one forward */
@@ -295,6 +299,15 @@ int omr_debug_depth_sort_mode(int mode);
  * one), 1 = always tiled, 2 = always streaming (both give bitwise the same dL_dimg); process-wide, for tests and A/B
  * runs. Returns the previous mode, or -1 for a mode outside 0..2 */
 int omr_debug_ssim_mode(int mode);
+/* pinhole preprocess with 16-coefficient SH rows: 1 = a geometry pass over every Gaussian, then the colour pass over
+ * the visible ones (the default), 0 = one fused kernel (same results; A/B runs). Process-wide; the environment's
+ * OMR_PRE_SPLIT=0 sets the start value. Returns the previous value, or -1 for a value outside 0..1 */
+int omr_debug_preprocess_split(int mode);
+/* omr_adam_step / omr_adam_step_activate: 1 = f_dc and f_rest stepped as one walk over dL_dsh's rows (the default),
+ * 0 = two gathering groups, the activated SH array then written by a separate copy launch (same results; A/B runs).
+ * Process-wide; the environment's OMR_ADAM_SH_ROWS=0 sets the start value. Returns the previous value, or -1 for a
+ * value outside 0..1 */
+int omr_debug_adam_sh_rows(int enabled);
 /* per-Gaussian pixel centre [P,2], conic+opacity [P,4], rgb [P,3], depth [P], tiles_touched [P] */
 /* one wave64 through the render backward's gradient reduction: in [64][9] -> out [9] (column sums) */
 int omr_debug_wave_sum9(const float* in, float* out, void* stream); /* wave_sum9_rows */

@@ -419,6 +419,16 @@ static std::atomic<int>& depth_sort_mode()  // 0: by camera type, 1: plain, 2: d
     return mode;
 }
 static int depth_sort_forced() { return depth_sort_mode().load(std::memory_order_relaxed); }
+// Adam's f_dc + f_rest row walk (adam_impl): 1 on by default, 0 the gathering groups (omr_debug_adam_sh_rows;
+// OMR_ADAM_SH_ROWS=0 sets the start value)
+static std::atomic<int>& adam_sh_rows_mode()
+{
+    static std::atomic<int> mode{[] {
+        const char* v = std::getenv("OMR_ADAM_SH_ROWS");
+        return (v && std::strcmp(v, "0") == 0) ? 0 : 1;
+    }()};
+    return mode;
+}
 static bool depth_sort_plain(int camera_type)
 {
     const int f = depth_sort_forced();
@@ -554,6 +564,10 @@ int forward_impl(const ForwardIn& in)
     pa.radii = radii;
     pa.g = g;
     pa.error_flag = reinterpret_cast<int*>(g.counters + 1);
+    // the pinhole geometry pass's visibility words live in `offsets` until the forward scans write it (ceil(P / 64)
+    // u64 fit in its P u32: the carve aligns every array to ALIGN bytes)
+    static_assert(ALIGN >= 8, "vis_mask words");
+    pa.vis_mask = reinterpret_cast<uint64_t*>(g.offsets);
     { StageScope st_(ST_PREPROCESS, s); launch_preprocess(in.camera_type, pa, s); }
 
     // depth order of the Gaussians (stable: ties keep index order)
@@ -999,22 +1013,19 @@ static int adam_impl(int P, int Mr, float* const params[6], float* const exp_avg
         bc2s = (float)std::sqrt(bc2);
     };
     // f_dc + f_rest as one walk over dL_dsh's rows (ADAM_SH_ROWS) whenever both step from the rasterizer's dL_dsh
-    // (OMR_ADAM_SH_ROWS=0 in the environment: the two gathering groups instead, for A/B runs)
-    static const bool sh_rows_enabled = [] {
-        const char* v = std::getenv("OMR_ADAM_SH_ROWS");
-        return !(v && std::strcmp(v, "0") == 0);
-    }();
-    const bool rows = sh_rows_enabled && grad_kind == OMR_ADAM_RASTER_GRADS && Mr > 0 && active[1] && active[2];
-    if (act && act[0] && P > 0 && Mr > 0 && !rows)
-        return fail(OMR_ERR_INVALID_ARGUMENT, "the activated SH output needs the f_dc + f_rest row walk");
+    // (omr_debug_adam_sh_rows(0) / OMR_ADAM_SH_ROWS=0: the two gathering groups instead, for A/B runs)
+    const bool rows = adam_sh_rows_mode().load() != 0 && grad_kind == OMR_ADAM_RASTER_GRADS && Mr > 0 && active[1] &&
+                      active[2];
+    // without the row walk (A/B switch) the activated SH array is copied from the updated f_dc / f_rest afterwards
+    const bool sh_copy_after = act && act[0] && P > 0 && Mr > 0 && !rows;
     for (int k = 0; k < 6; ++k) {
         if (!active[k] || (rows && k == 1)) continue;  // rows: f_dc steps with f_rest's group
         AdamGroup& G = a.group[a.ngroups++];
         G.p = params[k], G.m = exp_avg[k], G.v = exp_avg_sq[k], G.g = grads[k], G.n = (uint32_t)P * width[k];
         G.kind = grad_kind == OMR_ADAM_RAW_GRADS ? ADAM_PLAIN : raster_kind[k];
         consts(k, G.neg_step_size, G.bc2_sqrt);
-        for (int j = 0; j < 4; ++j)
-            if (act && act_group[j] == k) G.act = act[j];  // SH (j = 0) on f_dc's group only when Mr = 0: a copy
+        for (int j = 0; j < 4; ++j)  // SH (j = 0) on f_dc's group only when Mr = 0: a copy
+            if (act && act_group[j] == k && !(j == 0 && sh_copy_after)) G.act = act[j];
         if (rows && k == 2) {
             G.kind = ADAM_SH_ROWS;
             G.act = act ? act[0] : nullptr;
@@ -1029,6 +1040,11 @@ static int adam_impl(int P, int Mr, float* const params[6], float* const exp_avg
         a.stats = *stats;
     }
     launch_adam(a, stream);
+    if (sh_copy_after) {  // activate_kernel's SH blocks alone (opacity_out NULL), on the parameters Adam just wrote
+        ActivateArgs c{};
+        c.P = P, c.Mr = Mr, c.f_dc = params[1], c.f_rest = params[2], c.shs = act[0];
+        launch_activate(c, stream);
+    }
     return hip_check("adam_step");
 }
 
@@ -1412,18 +1428,35 @@ int omr_debug_ssim_mode(int mode)
     return ssim_debug_mode(mode);
 }
 
+int omr_debug_preprocess_split(int mode)
+{
+    if (mode < 0 || mode > 1) {
+        fail(OMR_ERR_INVALID_ARGUMENT, "preprocess split: 0 (one fused kernel) or 1 (geometry + colour passes)");
+        return -1;
+    }
+    return preprocess_split_mode(mode);
+}
+
+int omr_debug_adam_sh_rows(int enabled)
+{
+    if (enabled < 0 || enabled > 1) {
+        fail(OMR_ERR_INVALID_ARGUMENT, "adam SH rows: 0 (gathering groups) or 1 (row walk)");
+        return -1;
+    }
+    return adam_sh_rows_mode().exchange(enabled);
+}
+
 int omr_debug_set_sh_jac(char* geom_buffer, int P, int enabled, void* stream)
 {
     g_last_error.clear();
     GeomState g;
     GeomState::carve(geom_buffer, (size_t)std::max(P, 0), &g);
-    // clearing keeps the forward's key in counters[6]; setting restores it
+    // preprocess writes the forward's key to counters[5] and [6]; clearing zeroes [5] only, setting copies [6] back,
+    // so any sequence of clears and sets restores the forward's own key
     if (enabled) {
         OMR_HIP(hipMemcpyAsync(g.counters + 5, g.counters + 6, sizeof(uint32_t), hipMemcpyDeviceToDevice,
                                (hipStream_t)stream));
     } else {
-        OMR_HIP(hipMemcpyAsync(g.counters + 6, g.counters + 5, sizeof(uint32_t), hipMemcpyDeviceToDevice,
-                               (hipStream_t)stream));
         OMR_HIP(hipMemsetAsync(g.counters + 5, 0, sizeof(uint32_t), (hipStream_t)stream));
     }
     OMR_HIP(hipStreamSynchronize((hipStream_t)stream));

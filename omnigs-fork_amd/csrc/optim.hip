@@ -530,7 +530,9 @@ void launch_activate(const ActivateArgs& a, hipStream_t s)
     if (a.P <= 0) return;
     const uint32_t sh_blocks =
         a.shs ? (uint32_t)div_up(div_up((size_t)a.P * 3 * (a.Mr + 1), (size_t)4), (size_t)ACT_THREADS) : 0u;
-    const uint32_t blocks = sh_blocks + div_up((uint32_t)a.P, (uint32_t)ACT_THREADS);
+    // opacity_out NULL: the SH copy alone (omr_adam_step_activate without the SH row walk)
+    const uint32_t blocks = sh_blocks + (a.opacity_out ? div_up((uint32_t)a.P, (uint32_t)ACT_THREADS) : 0u);
+    if (blocks == 0) return;
     activate_kernel<<<blocks, ACT_THREADS, 0, s>>>(a, sh_blocks);
 }
 

@@ -107,7 +107,8 @@ struct GeomState {
     uint32_t* offsets;        // inclusive scan of tiles_touched in depth order
     uint32_t* counters;       // [0] num_rendered, [1] prefiltered-cull flag, [2] huge_list count, [3] look-back error,
                               // [4] M = row slots of the row binning (sum of rect heights), [5] sh_jac_key of the
-                              // inputs when preprocess stored sh_jac (else 0), [6] omr_debug_set_sh_jac's copy of [5]
+                              // inputs when preprocess stored sh_jac (else 0), [6] the same key, kept for
+                              // omr_debug_set_sh_jac (which clears and restores [5])
     uint32_t* order;          // [P] depth order: the visible Gaussians by depth key (ties by index), then the culled (depth_sort)
     uint32_t* row_first;      // first gradient row of each Gaussian (index-order exclusive scan, launch_forward_scans)
     float* row_sums;          // backward: [P][GRAD_ROW] each Gaussian's instance rows summed (launch_row_sums)

@@ -169,10 +169,23 @@ class GaussianOptimizer:
         return out
 
     def _key(self, out: dict):
-        """The activated outputs in `out` are current while the parameters are the same tensors, untouched by torch
-        in-place ops (their _version), and no raw-pointer write other than Adam's (reset_opacity, densify) happened."""
-        return (id(out), tuple((p.data_ptr(), p._version, tuple(p.shape)) for p in self.params()),
+        """The activated outputs in `out` are current while the parameters are the same tensor OBJECTS (the key holds
+        them, so a new tensor at a reused address never matches), untouched by torch in-place ops (their _version),
+        and no raw-pointer write other than Adam's (reset_opacity, densify) happened. Writes torch does not version
+        (through `p.data`, e.g. p.data.copy_ when loading a checkpoint) are invisible here: call invalidate()."""
+        ps = self.params()
+        return (id(out), tuple(ps), tuple((p.data_ptr(), p._version, tuple(p.shape)) for p in ps),
                 tuple(out[k].data_ptr() for k in ("shs", "opacity", "scales", "rotations")))
+
+    @staticmethod
+    def _same_key(a, b) -> bool:
+        return (a is not None and b is not None and a[0] == b[0] and len(a[1]) == len(b[1])
+                and all(x is y for x, y in zip(a[1], b[1])) and a[2:] == b[2:])
+
+    def invalidate(self):
+        """Forget that the activated outputs are current: the next activate_cached() recomputes them. Needed after
+        any write to the parameters that torch does not version (p.data.copy_, raw-pointer writes by other code)."""
+        self._act_key = None
 
     def activate(self, out: Optional[dict] = None) -> dict:
         """cat(features_dc, features_rest), sigmoid(opacity), exp(scaling), normalize(rotation) in one launch
@@ -191,7 +204,7 @@ class GaussianOptimizer:
         activate(out)) did not already leave the activations of the current parameters there."""
         if self._act_key is not None and all(k in out for k in ("shs", "opacity", "scales", "rotations")):
             out["xyz"] = self.params()[0]
-            if self._key(out) == self._act_key:
+            if self._same_key(self._key(out), self._act_key):
                 return out
         return self.activate(out)
 

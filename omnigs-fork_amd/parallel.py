@@ -46,10 +46,13 @@ class DistInfo:
     rank: int = 0
     world_size: int = 1
     local_rank: int = 0
+    # test-only: run the exchange's collectives even at world size 1 (tests/test_gpu_rccl_one_rank.py executes the
+    # RCCL calls on a one-GPU box, where a 1-rank communicator makes every collective an identity)
+    force_exchange: bool = False
 
     @property
     def enabled(self) -> bool:
-        return self.world_size > 1
+        return self.world_size > 1 or self.force_exchange
 
 
 class GradBuffer:

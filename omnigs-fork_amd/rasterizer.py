@@ -77,6 +77,10 @@ def lib() -> C.CDLL:
         L.omr_debug_depth_sort_mode.argtypes = [i]
         L.omr_debug_ssim_mode.restype = i
         L.omr_debug_ssim_mode.argtypes = [i]
+        L.omr_debug_preprocess_split.restype = i
+        L.omr_debug_preprocess_split.argtypes = [i]
+        L.omr_debug_adam_sh_rows.restype = i
+        L.omr_debug_adam_sh_rows.argtypes = [i]
         L.omr_debug_set_sh_jac.restype = i
         L.omr_debug_set_sh_jac.argtypes = [vp, i, i, vp]
         L.omr_debug_geometry.argtypes = [vp, i, vp, vp, vp, vp, vp, vp]
@@ -579,6 +583,24 @@ def debug_ssim_mode(mode: int) -> int:
     rc = int(lib().omr_debug_ssim_mode(int(mode)))
     if rc < 0:
         raise RasterizerError(f"debug_ssim_mode({mode}): {lib().omr_last_error().decode()}")
+    return rc
+
+
+def debug_preprocess_split(mode: int) -> int:
+    """Pinhole preprocess, process-wide (omr_debug_preprocess_split): 1 geometry pass + colour pass over the visible
+    Gaussians (default), 0 one fused kernel. Returns the previous value."""
+    rc = int(lib().omr_debug_preprocess_split(int(mode)))
+    if rc < 0:
+        raise RasterizerError(f"debug_preprocess_split({mode}): {lib().omr_last_error().decode()}")
+    return rc
+
+
+def debug_adam_sh_rows(enabled: int) -> int:
+    """Adam's f_dc + f_rest row walk, process-wide (omr_debug_adam_sh_rows): 1 on (default), 0 the two gathering
+    groups (the activated SH output then comes from a separate copy launch). Returns the previous value."""
+    rc = int(lib().omr_debug_adam_sh_rows(int(enabled)))
+    if rc < 0:
+        raise RasterizerError(f"debug_adam_sh_rows({enabled}): {lib().omr_last_error().decode()}")
     return rc
 
 

@@ -23,18 +23,22 @@
 //    (:434-435), T (1 - alpha) at 1e-4 (:440-444). The window of power is the rounding bound of its evaluation from
 //    rounded conic and centre: (kappa_g + k_eval eps) S + u G, S = a dx^2 / 2 + c dy^2 / 2 + |b dx dy|,
 //    G = |a dx + b dy| + |b dx + c dy|, u = k_pos ulp of the centre, kappa_g = k_eval eps (|ac| + b^2) / |ac - b^2|
-//    (the conic's condition); plus eps_exp for the exp implementations. T's window accumulates alpha x the power
-//    window of every blended Gaussian in front;
+//    (the conic's condition); plus eps_exp for the exp implementations. T's window accumulates, over every blended
+//    Gaussian in front, the relative change of its factor (1 - alpha): alpha (power window + eps_exp) / (1 - alpha);
 //  * per flagged pixel, a bound on the colour change the flagged decisions can make (Allowance::bound, any channel):
 //    each flipped term moves the pixel by at most its blend weight alpha T times the colour span 2 cmax (cmax = the
 //    largest |colour| of the scene and background): alpha ~1/255 for an alpha flip, the opacity for a power-0 flip,
 //    alpha_a alpha_b for an order swap, the transmittance ~1e-4 at saturation, the Gaussian's reach for a rect;
 //  * flip Gaussians: the Gaussians owning any such decision. When one flips, that Gaussian gains or loses a whole
 //    pixel term (or swaps its order with its pair) and its gradient may leave the bar;
-//  * exposed Gaussians (G_EXPOSED): the ones blending behind such a decision (alpha, power 0, order, rect). Their
-//    pixel term there scales by the flipped alpha (~1/255 for a threshold flip) — small against the Gaussian's total,
-//    unless its pixel terms cancel; the parity tests give them a wider bar (tests/helpers.py). A saturation flip only
-//    moves terms of transmittance ~1e-4 and exposes no one.
+//  * exposed Gaussians (G_EXPOSED): the ones blending behind such a decision (alpha, power 0, order, rect) and the
+//    ones blending IN FRONT of it. Behind, their pixel term scales by the flipped alpha (~1/255 for a threshold
+//    flip); in front, the colour accumulated behind them (accum_rec, backward.cu:745-760) gains or loses the flipped
+//    term, which moves their dL/dalpha at that pixel by the same order. Small against the Gaussian's total, unless
+//    its pixel terms cancel; the parity tests give them a wider bar (tests/helpers.py). The front half was found by
+//    oracle/contraction.py's libm variant (glibc atan2f / asinf, round 6): a Gaussian in front of a neighbour's
+//    alpha flip left the strict bar by 1.1x at A and B. A saturation flip only moves terms of transmittance ~1e-4
+//    and exposes no one.
 #pragma once
 
 #include <cmath>
@@ -257,6 +261,7 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
     for (int t = 0; t < (int)T; ++t) {
         const uint32_t tx = t % s.gx, ty = t / s.gx;
         const uint32_t rx = s.ranges[2 * t], ry = s.ranges[2 * t + 1];
+        std::vector<uint32_t> front_buf;
         const uint32_t n = ry - rx;
         std::vector<uint32_t> run(n);  // run id of each position: consecutive positions in one run may swap
         uint32_t rid = 0;
@@ -283,6 +288,14 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
                 uint32_t last_run = ~0u, last_run_id = 0;
                 bool behind = false;  // a decision in front of this position is ambiguous (alpha, power 0, order, rect)
                 double last_G = 0.0;
+                // the Gaussians blended so far at this pixel: a flagged decision behind them exposes them too
+                std::vector<uint32_t>& front = front_buf;
+                front.clear();
+                size_t front_marked = 0;
+                auto expose_front = [&](uint32_t except) {
+                    for (; front_marked < front.size(); ++front_marked)
+                        if (front[front_marked] != except) marked[t].push_back({front[front_marked], G_EXPOSED});
+                };
                 double dLp[3] = {0, 0, 0}, bg_dot = 0.0, T_fin = 0.0;
                 if (dL_dpix) {
                     const size_t pid = (size_t)py * W + px;
@@ -310,6 +323,17 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
                     const double G = std::fabs(co.x * dx + co.y * dy) + std::fabs(co.y * dx + co.z * dy);
                     dp = (kappa[id] + prm.k_eval * EPS32) * S + upos[id] * G;
                 };
+                // a rect-ambiguous Gaussian that may join the tile (below) may blend at any depth: T's window starts
+                // with the factor it can bring
+                for (int id : gx_extra[t]) {
+                    double power, dp;
+                    eval((uint32_t)id, power, dp);
+                    const float o = s.conic_opacity[id].w;
+                    if (power - dp <= 0.0 && power + dp >= -std::log(255.0 * o) - prm.eps_exp) {
+                        const double ax = std::fmin(0.99, o * std::exp(std::fmin(0.0, power + dp)));
+                        errT += ax / std::fmax(1.0 - ax, 1e-2);
+                    }
+                }
                 for (uint32_t k = 0; k < n; ++k) {
                     const uint32_t id = s.point_list[rx + k];
                     double power, dp;
@@ -318,16 +342,25 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
                     if (std::fabs(power) <= dp && power + dp > 0.0) {  // power > 0 skip (forward.cu:434-435)
                         pf |= PX_ZERO;
                         marked[t].push_back({id, G_THRESHOLD});
+                        expose_front(id);
                         bnd += span * Tr * std::fmin(0.99, (double)co.w);
                         const double Gz = std::exp(std::fmin(power, 0.0));
-                        add_term(id, std::fmin(0.99, co.w * Gz), Gz, Tr, 1.0);
+                        const double az = std::fmin(0.99, co.w * Gz);
+                        add_term(id, az, Gz, Tr, 1.0);
+                        errT += az / std::fmax(1.0 - az, 1e-2);  // T behind it moves by that factor either way
                     }
                     if (power > 0) continue;
                     const double thr = -std::log(255.0 * co.w);  // alpha = o exp(power) = 1/255
                     if (std::fabs(power - thr) <= dp + prm.eps_exp) {
                         pf |= PX_ALPHA;
                         marked[t].push_back({id, G_THRESHOLD});
+                        expose_front(id);
                         bnd += span * Tr * (1.0 / 255.0) * std::exp(dp + prm.eps_exp);
+                        // blended or not, T behind it moves by the flipped factor (1 - alpha): a later saturation test
+                        // (T (1 - alpha) at 1e-4) within that much of its threshold may flip too (found by
+                        // oracle/contraction.py's libm variant at E: an alpha flip 170 positions in front of one)
+                        const double af = (1.0 / 255.0) * std::exp(dp + prm.eps_exp);
+                        errT += af / (1.0 - af);
                         const double Ga = std::exp(std::fmin(power + dp + prm.eps_exp, 0.0));
                         add_term(id, std::fmin(0.99, co.w * Ga), Ga, Tr, 1.0);
                     }
@@ -343,6 +376,8 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
                             pf |= PX_RECT;
                             bnd += span * Tr * alpha;
                             add_term(id, alpha, std::exp(power), Tr, 1.0);
+                            expose_front(id);
+                            errT += alpha / std::fmax(1.0 - alpha, 1e-2);
                         }
                     }
                     behind = behind || (pf & (PX_ALPHA | PX_ZERO | PX_ORDER | PX_RECT));
@@ -352,6 +387,7 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
                         pf |= PX_ORDER;
                         marked[t].push_back({id, G_ORDER});
                         marked[t].push_back({last_run_id, G_ORDER});
+                        expose_front(last_run_id);
                         // swapping a, b moves (alpha_a alpha_b T_a)(c_a - c_b); T after both is unchanged
                         bnd += span * (Tr / std::fmax(1.0 - last_alpha, 1e-2)) * last_alpha * alpha;
                         // swapped, b's transmittance grows by 1 / (1 - alpha_a), a's shrinks by (1 - alpha_b), and
@@ -359,12 +395,17 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
                         add_term(id, alpha, std::exp(power), Tr, 1.0 + last_alpha / std::fmax(1.0 - last_alpha, 1e-2));
                         add_term(last_run_id, last_alpha, last_G, T_before_last, 1.0 + alpha);
                     }
+                    front.push_back(id);
                     last_run = run[k];
                     last_run_id = id;
                     last_alpha = alpha;
                     last_G = std::exp(power);
                     const double test_T = Tr * (1.0 - alpha);
-                    const double errk = errT + alpha * dp;
+                    // relative error of T (1 - alpha): each blended factor (1 - alpha_j) moves by alpha_j dalpha_j /
+                    // (1 - alpha_j) relative (dalpha = alpha dp, plus the exp implementations' eps_exp); the 1 / (1 -
+                    // alpha) factor matters for opaque Gaussians (found by oracle/contraction.py's libm variant at E:
+                    // a pixel 303 Gaussians deep whose saturation test flipped outside the window without it)
+                    const double errk = errT + alpha * (dp + prm.eps_exp) / std::fmax(1.0 - alpha, 1e-2);
                     if (std::fabs(test_T - 1e-4) <= (prm.eps_exp + errk) * 1e-4) {
                         pf |= PX_SAT;
                         marked[t].push_back({id, G_THRESHOLD});
@@ -391,6 +432,7 @@ inline Allowance allowance_scan(const State<float>& s, const AllowanceParams& pr
                     const float o = s.conic_opacity[id].w;
                     if (power - dp <= 0.0 && power + dp >= -std::log(255.0 * o) - prm.eps_exp) {
                         pf |= PX_RECT;
+                        expose_front(~0u);  // it may blend at any depth: every blended Gaussian may lie in front
                         bnd += span * std::fmin(0.99, o * std::exp(std::fmin(0.0, power + dp)));
                         // it may blend at any depth position: transmittance <= 1
                         const double Gr = std::exp(std::fmin(0.0, power + dp));

@@ -5,7 +5,9 @@ nvcc compiles the reference with its default --fmad=true (no -fmad flag in /root
 so every mul+add pair of the preprocess, the falloff and the backward may be fused into one FMA; the oracle
 (liboracle.so) is built with -ffp-contract=off and evaluates the reference expressions as written. No nvcc exists
 here, so two contracted builds of the same oracle sources stand in for the reference binary: GCC and LLVM fuse
-different multiplies of a sum of products (oracle/Makefile: liboracle_fma_gcc.so, liboracle_fma_clang.so).
+different multiplies of a sum of products (oracle/Makefile: liboracle_fma_gcc.so, liboracle_fma_clang.so). The
+reference also takes atan2f / asinf from libdevice, the oracle and the HIP kernels from the shared omni_math.h; a
+third build with glibc's atan2f / asinf (liboracle_libm.so) measures what a second implementation changes.
 
 For each BASELINE config this measures what changes between the oracle and each contracted build — depth /
 centre / conic / radius / rect bits, num_rendered, sorted point-list positions, pixels over 1e-4, gradient entries
@@ -114,7 +116,25 @@ def unexplained(cmp: dict) -> int:
     return sum(v for k, v in cmp.items() if k.endswith("_unexplained"))
 
 
-def run_config(name, threads, variants=("fma_gcc", "fma_clang"), backward=True):
+VARIANTS = ("fma_gcc", "fma_clang", "libm")
+
+
+def modelled_vs_measured(counts: dict, variants: dict) -> dict:
+    """The allowance's modelled counts next to what each variant actually changed (every measured change must lie
+    inside the modelled set: the *_unexplained counts of compare_variant are 0)."""
+    out = {"modelled": {k: counts.get(k) for k in ("rect_gaussians", "radius_gaussians", "order_pairs",
+                                                     "flip_gaussians", "exposed_gaussians", "allowed_pixels")}}
+    for v, c in variants.items():
+        out[v] = {"rects_changed": c.get("tiles_touched_changed"), "radii_changed": c.get("radii_changed"),
+                  "centres_changed": c.get("means2D_changed"), "depth_keys_changed": c.get("depths_changed"),
+                  "point_list_positions_changed": c.get("point_list_positions_changed"),
+                  "num_rendered_delta": c.get("num_rendered_delta"), "pixels_over_1e-4": c.get("pixels_over_1e-4"),
+                  "grad_gaussians_outside_bar": c.get("grad_gaussians_outside_bar"),
+                  "unexplained": unexplained(c)}
+    return out
+
+
+def run_config(name, threads, variants=VARIANTS, backward=True):
     import _omnigs
     import oracle as O
     from helpers import reference_allowance
@@ -133,6 +153,7 @@ def run_config(name, threads, variants=("fma_gcc", "fma_clang"), backward=True):
         ov, _, gv = O.run_scene(g, cam, dL if backward else None, nthreads=threads, variant=v)
         res["variants"][v] = compare_variant(ob, gb, ov, gv, allow, cam.height, cam.width)
         del ov, gv
+    res["measured_vs_modelled"] = modelled_vs_measured(counts, res["variants"])
     res["seconds"] = round(time.time() - t0, 1)
     return res
 
@@ -157,14 +178,16 @@ def main():
     doc["method"] = (
         "oracle/ambiguity.hpp (allowance_scan) on the oracle forward of each config's bench view, and "
         "oracle/contraction.py: the oracle vs two FMA-contracted builds of it (GCC, LLVM; the proxy of nvcc's "
-        "--fmad=true reference binary). allowance: rect_gaussians = tile rect moves within the centre / "
+        "--fmad=true reference binary) and a build with glibc's atan2f / asinf instead of omni_math.h's (libm: an "
+        "independent implementation of the transcendentals, as libdevice's is for the reference). allowance: rect_gaussians = tile rect moves within the centre / "
         "atan2 / radius rounding windows; order_pairs = same-tile neighbours whose depths differ by less than their "
         "rounding windows; alpha / saturation / zero_power pixels = a blend decision inside its rounding window; "
         "order_pixels = two members of an order-ambiguous run blend; flip_gaussians own such a decision (gradients "
-        "within the owner bound of ambiguity.hpp: owner_grad_bound), exposed_gaussians blend behind one (wide bar 1e-2 / 1e-3). variants: what actually changes, and "
-        "what the allowance leaves unexplained (*_unexplained, all 0 expected)")
+        "within the owner bound of ambiguity.hpp: owner_grad_bound), exposed_gaussians blend behind or in front of "
+        "one (wide bar 1e-2 / 1e-3). variants: what actually changes, and what the allowance leaves unexplained "
+        "(*_unexplained, all 0 expected); measured_vs_modelled puts the counts side by side")
     for name in args.configs:
-        res = run_config(name, args.threads, variants=() if args.no_variants else ("fma_gcc", "fma_clang"))
+        res = run_config(name, args.threads, variants=() if args.no_variants else VARIANTS)
         doc["configs"][name] = res
         print(name, json.dumps(res), flush=True)
         with open(args.out, "w") as f:

@@ -44,8 +44,16 @@ constexpr int NUM_CHANNELS = 3;  // config.h:25
 // ---------------------------------------------------------------------------------------------------------
 template <typename R> struct Math;
 template <> struct Math<float> {
+#ifdef OMR_ORACLE_LIBM_TRIG
+    // liboracle_libm.so (oracle/Makefile): glibc's atan2f / asinf, an implementation independent of omni_math.h (as
+    // libdevice's is for the reference, auxiliary.h:240-241), so oracle/contraction.py can measure what the choice
+    // of transcendental implementation changes in the tile rects, keys and point list
+    static float atan2(float y, float x) { return ::atan2f(y, x); }
+    static float asin(float x) { return ::asinf(x); }
+#else
     static float atan2(float y, float x) { return omni::atan2f_(y, x); }
     static float asin(float x) { return omni::asinf_(x); }
+#endif
     static float sqrt(float x) { return std::sqrt(x); }
     static float exp(float x) { return std::exp(x); }
     static float ceil(float x) { return std::ceil(x); }

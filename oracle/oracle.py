@@ -15,9 +15,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
 # builds of the same sources (oracle/Makefile): "base" is the parity checker (no FMA contraction); "fma_gcc" /
 # "fma_clang" contract mul+add into FMA as nvcc compiles the reference (oracle/contraction.py); "fast" is the
-# -O3 timing build of bench.py's cpu_baseline
+# -O3 timing build of bench.py's cpu_baseline; "libm" is "base" with glibc's atan2f / asinf instead of omni_math.h's
+# (an independent implementation of the transcendentals the tile rects depend on, oracle/contraction.py)
 VARIANTS = {"base": "liboracle.so", "fma_gcc": "liboracle_fma_gcc.so", "fma_clang": "liboracle_fma_clang.so",
-            "fast": "liboracle_fast.so"}
+            "fast": "liboracle_fast.so", "libm": "liboracle_libm.so"}
 _libs = {}
 
 _F32 = {"out_color", "depths", "cov3D", "rgb", "final_T", "means2D", "conic_opacity", "dmean2D", "dconic",

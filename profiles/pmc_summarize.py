@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise the rocprofv3 runs of profiles/collect.sh (CPU side, after gpurun merged gpurun_out/).
 
-    python profiles/pmc_summarize.py r01e
+    python profiles/pmc_summarize.py r01e [sq_tag]
 
 Writes profiles/<tag>_kernel_stats.csv (copy of the --stats summary), profiles/<tag>_pmc.csv (per-kernel FETCH_SIZE /
 WRITE_SIZE averages) and profiles/pmc_latest.json, which bench.py reads for roofline.traffic.
@@ -148,7 +148,24 @@ def main():
         w = csv.writer(f)
         w.writerow(["kernel", "dispatches", "FETCH_SIZE_KiB_avg", "WRITE_SIZE_KiB_avg", "hbm_bytes_per_launch"])
         w.writerows(rows)
-    latest = {"tag": tag, "config": cfg, "P": bench["config"]["P"], "L": bench["config"]["L"],
+    # the SQ passes of the same tree (profiles/sq.sh + sq_summarize.py -> profiles/<sq_tag>_sq.csv): each stage kernel's
+    # VALU wave-instructions per launch, for bench.py's roofline.valu_issue_frac (VALU issue time against the chip's
+    # 1024 SIMDs x 1.2 G wave-instructions/s)
+    sq_tag = sys.argv[2] if len(sys.argv) > 2 else tag
+    sq_path = os.path.join(HERE, f"{sq_tag}_sq.csv")
+    sq_file = None
+    if os.path.exists(sq_path):
+        sq_file = os.path.relpath(sq_path, ROOT)
+        with open(sq_path) as f:
+            for r in csv.DictReader(f):
+                for frag, stage in STAGES.items():
+                    if frag in r["kernel"] and stage in kernels:
+                        waves, vpw = float(r["waves"]), float(r["valu_per_wave"])
+                        kernels[stage]["sq"] = {"waves": waves, "valu_per_wave": vpw,
+                                                "valu_insts_per_launch": int(round(waves * vpw)),
+                                                "valu_issue_share": float(r["valu_issue_share"]),
+                                                "wait_inst_share": float(r["wait_inst_share"])}
+    latest = {"tag": tag, "config": cfg, "P": bench["config"]["P"], "L": bench["config"]["L"], "sq_file": sq_file,
               "method": "(2*FETCH_SIZE + WRITE_SIZE) KiB * 1024, separate --pmc passes, gfx950 FETCH x2 correction",
               "kernel_stats_file": timed_file,
               "kernel_stats_all_launches_file": f"profiles/{tag}_kernel_stats.csv" if stats else None,

@@ -288,16 +288,20 @@ def test_fused_train_step_matches_autograd_reference_composition(masked, skip_bo
     np.testing.assert_array_equal(to_np(opt1.denom), to_np(opt2.denom))
 
 
-def test_activate_matches_the_torch_activations():
+@pytest.mark.parametrize("P,cam,deg", [(5000, "lonlat", 3), (4999, "pinhole", 3), (1023, "pinhole", 1),
+                                       (6, "lonlat", 0)])
+def test_activate_matches_the_torch_activations(P, cam, deg):
     """omr_activate (optim.hip: activate_kernel) against gaussian_model.cpp:54-77's torch expressions: the SH
     concatenation, sigmoid and exp bit for bit; normalize within an ulp of torch's (its norm reduction may sum the
-    four squares in another order)."""
+    four squares in another order). Lonlat and pinhole scenes, P not a multiple of 4 (ragged 16-B SH chunks), SH
+    degrees 3 / 1 / 0."""
     from helpers import make_case, scene
 
-    g, _, _ = make_case(5000, 64, 32, scene.CAMERA_LONLAT, 31)
+    g, _, _ = make_case(P, 64, 32, scene.CAMERA_LONLAT if cam == "lonlat" else scene.CAMERA_PINHOLE, 31 + P)
     rng = np.random.default_rng(2)
     o = np.clip(g.opacity.astype(np.float64), 1e-4, 1 - 1e-4)
-    params = [g.means3D, g.shs[:, :1], g.shs[:, 1:], np.log(o / (1 - o)), np.log(g.scales),
+    nsh = (deg + 1) ** 2
+    params = [g.means3D, g.shs[:, :1], g.shs[:, 1:nsh], np.log(o / (1 - o)), np.log(g.scales),
               g.rotations * rng.uniform(0.5, 2.0, (g.P, 1))]
     m = _model([np.ascontiguousarray(p, dtype=np.float32) for p in params])
     opt = OPT.GaussianOptimizer(m, OPT.OptimizationParams())
@@ -357,6 +361,54 @@ def test_adam_step_activate_equals_step_then_activate(P, Mr):
     opt1.activate_cached(act1)
     torch.cuda.synchronize()
     assert torch.equal(act1["opacity"], torch.sigmoid(opt1.model.opacity))
+    # a parameter replaced by a NEW tensor (same shape, version 0, possibly the freed block's address): recomputed
+    opt1.model.opacity = opt1.model.opacity.detach().clone() + 0.25
+    act1["opacity"].fill_(-1.0)
+    opt1.activate_cached(act1)
+    torch.cuda.synchronize()
+    assert torch.equal(act1["opacity"], torch.sigmoid(opt1.model.opacity))
+    # a write torch does not version (through .data): invisible to the key, so invalidate() is the contract
+    v0 = opt1.model.scaling._version
+    opt1.model.scaling.data.copy_(opt1.model.scaling.data * 0.5)
+    assert opt1.model.scaling._version == v0
+    opt1.invalidate()
+    act1["scales"].fill_(-1.0)
+    opt1.activate_cached(act1)
+    torch.cuda.synchronize()
+    assert torch.equal(act1["scales"], torch.exp(opt1.model.scaling))
+
+
+@pytest.mark.parametrize("P,Mr", [(4099, 15), (513, 3)])
+def test_adam_step_activate_without_the_sh_row_walk(P, Mr):
+    """omr_debug_adam_sh_rows(0) (OMR_ADAM_SH_ROWS=0, the A/B switch): f_dc and f_rest step as two gathering groups and
+    the activated SH array is copied after the launch. Same bits as the row walk, and train steps still run (ADVICE
+    r05: the switch used to make every omr_adam_step_activate with SH outputs fail)."""
+    rng = np.random.default_rng(P)
+    params = _random_params(P, Mr, P + 3)
+    opts = [OPT.GaussianOptimizer(_model(params), OPT.OptimizationParams()) for _ in range(2)]
+    acts = [{}, {}]
+    old = omr.rasterizer.debug_adam_sh_rows(1)
+    try:
+        for s in range(2):
+            g = {"dL_dmeans3D": rng.normal(0, 1e-4, (P, 3)), "dL_dsh": rng.normal(0, 1e-4, (P, Mr + 1, 3)),
+                 "dL_dopacity": rng.normal(0, 1e-3, (P, 1)), "dL_dscales": rng.normal(0, 1e-3, (P, 3)),
+                 "dL_drotations": rng.normal(0, 1e-4, (P, 4))}
+            g = {k: _cuda(v) for k, v in g.items()}
+            for k, (opt, act) in enumerate(zip(opts, acts)):
+                omr.rasterizer.debug_adam_sh_rows(1 - k)
+                opt.step(raster_grads=g, act_out=act)
+        torch.cuda.synchronize()
+    finally:
+        omr.rasterizer.debug_adam_sh_rows(old)
+    for k in range(6):
+        assert torch.equal(opts[0].params()[k], opts[1].params()[k]), k
+        assert torch.equal(opts[0].exp_avg_sq[k], opts[1].exp_avg_sq[k]), k
+    for k in ("shs", "opacity", "scales", "rotations"):
+        assert torch.equal(acts[0][k], acts[1][k]), k
+    m = opts[1].model
+    assert torch.equal(acts[1]["shs"], torch.cat([m.features_dc, m.features_rest], dim=1))
+    with pytest.raises(omr.rasterizer.RasterizerError):
+        omr.rasterizer.debug_adam_sh_rows(2)
 
 
 def test_adam_step_activate_rejects_outputs_of_groups_that_do_not_step():

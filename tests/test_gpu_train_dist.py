@@ -86,8 +86,14 @@ def test_view_parallel_train_step_replicas_agree_with_summed_views():
     bg = torch.zeros(3, device=dev)
     for it in range(2):
         total = None
-        # the trainer's activations (omr_activate; against torch's in tests/test_gpu_optim.py)
+        # the trainer's activations (omr_activate), checked here against torch's independent expressions
+        # (gaussian_model.cpp:54-77) so this test does not rest on the kernel it is comparing the trainer with
         a = opt.activate()
+        m = opt.model
+        assert torch.equal(a["shs"], torch.cat([m.features_dc, m.features_rest], dim=1))
+        assert torch.equal(a["opacity"], torch.sigmoid(m.opacity))
+        assert torch.equal(a["scales"], torch.exp(m.scaling))
+        torch.testing.assert_close(a["rotations"], torch.nn.functional.normalize(m.rotation), rtol=2.4e-7, atol=0)
         shs = a["shs"]
         act = (a["xyz"], a["opacity"], a["scales"], a["rotations"])
         for vp, gt in ((vp0, gt0), (vp1, gt1)):
