@@ -299,10 +299,6 @@ int omr_debug_depth_sort_mode(int mode);
  * one), 1 = always tiled, 2 = always streaming (both give bitwise the same dL_dimg); process-wide, for tests and A/B
  * runs. Returns the previous mode, or -1 for a mode outside 0..2 */
 int omr_debug_ssim_mode(int mode);
-/* pinhole preprocess with 16-coefficient SH rows: 1 = a geometry pass over every Gaussian, then the colour pass over
- * the visible ones (the default), 0 = one fused kernel (same results; A/B runs). Process-wide; the environment's
- * OMR_PRE_SPLIT=0 sets the start value. Returns the previous value, or -1 for a value outside 0..1 */
-int omr_debug_preprocess_split(int mode);
 /* omr_adam_step / omr_adam_step_activate: 1 = f_dc and f_rest stepped as one walk over dL_dsh's rows (the default),
  * 0 = two gathering groups, the activated SH array then written by a separate copy launch (same results; A/B runs).
  * Process-wide; the environment's OMR_ADAM_SH_ROWS=0 sets the start value. Returns the previous value, or -1 for a

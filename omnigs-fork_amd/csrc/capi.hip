@@ -564,10 +564,6 @@ int forward_impl(const ForwardIn& in)
     pa.radii = radii;
     pa.g = g;
     pa.error_flag = reinterpret_cast<int*>(g.counters + 1);
-    // the pinhole geometry pass's visibility words live in `offsets` until the forward scans write it (ceil(P / 64)
-    // u64 fit in its P u32: the carve aligns every array to ALIGN bytes)
-    static_assert(ALIGN >= 8, "vis_mask words");
-    pa.vis_mask = reinterpret_cast<uint64_t*>(g.offsets);
     { StageScope st_(ST_PREPROCESS, s); launch_preprocess(in.camera_type, pa, s); }
 
     // depth order of the Gaussians (stable: ties keep index order)
@@ -1426,15 +1422,6 @@ int omr_debug_ssim_mode(int mode)
         return -1;
     }
     return ssim_debug_mode(mode);
-}
-
-int omr_debug_preprocess_split(int mode)
-{
-    if (mode < 0 || mode > 1) {
-        fail(OMR_ERR_INVALID_ARGUMENT, "preprocess split: 0 (one fused kernel) or 1 (geometry + colour passes)");
-        return -1;
-    }
-    return preprocess_split_mode(mode);
 }
 
 int omr_debug_adam_sh_rows(int enabled)

@@ -37,16 +37,9 @@ struct PreprocessArgs {
     int* radii;
     GeomState g;
     int* error_flag;  // set to 1 if prefiltered and a point is culled (auxiliary.h:183-187 traps instead)
-    // pinhole views (preprocess.hip: preprocess_geom_kernel / preprocess_colour_kernel): per 64 consecutive
-    // Gaussians, the ballot of the visible ones ([ceil(P / 64)] words; carved over GeomState::offsets, which the
-    // forward scans write only after the depth sort)
-    uint64_t* vis_mask;
 };
 
 void launch_preprocess(int camera_type, const PreprocessArgs& a, hipStream_t s);
-// pinhole preprocess as one fused kernel (0) or as the geometry pass over every Gaussian followed by the colour pass
-// over the visible ones (1, default); process-wide (omr_debug_preprocess_split, OMR_PRE_SPLIT=0), returns the previous
-int preprocess_split_mode(int mode);
 void launch_mark_visible(int camera_type, int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                          bool* present, hipStream_t s);
 

@@ -11,10 +11,6 @@
 // contiguous lanes; the depth sort's first-pass keys/values are written here directly (no extra pass).
 // HBM per Gaussian (D=3): reads 12 (xyz) + 12 (scale) + 16 (rot) + 4 (opacity) + 192 (SH) = 236 B,
 // writes 8 + 16 + 16 + 4 + 1 + 4 + 4 (radius) + 8 (sort key/value) = 61 B.
-#include <atomic>
-#include <cstdlib>
-#include <cstring>
-
 #include "kernels.h"
 #include "sh_eval.h"
 #include "wave_rows.h"
@@ -420,85 +416,6 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     wave_rows_store<SPLAT_F4>(g.splat + (size_t)wave_first * SPLAT_F4, rec_rows, stage, lane);
 }
 
-// ---- pinhole views: the geometry over every Gaussian, then the colour over the visible ones ---------------------
-// A frustum culls most of a pinhole view's Gaussians (88 % at config E's 1920x1080 ranks), but the fused kernel above
-// runs the whole per-wave chain — the 13-KiB SH row image that caps it at 3 waves per SIMD included — for every wave
-// of 64, and every wave holds a few visible lanes (0.88^64 ~ 0). The pinhole path is therefore two kernels
-// (VERDICT r05 item 3):
-//   preprocess_geom_kernel    every Gaussian: cull, projection, cov3D / cov2D, conic, radius, rect, the depth key,
-//                             everything but the colour (preprocess_point with the colour left to the caller), with no
-//                             LDS image (VGPR-bound occupancy); the render record's colour slot is written as
-//                             {0, 0, 0, rect width}; per wave, the ballot of its visible lanes into vis_mask;
-//   preprocess_colour_kernel  the visible Gaussians only: each wave compacts the visible lanes of a run of
-//                             vis_mask words into an LDS list and evaluates, densely, SH -> RGB and dRGB/ddir for
-//                             them (sh16_colour: the same expressions, so the same bits as the fused kernel).
-// Equirect views see every point (lonlat culls only |t| <= 0.2) and keep the fused kernel.
-template <int CAM>
-__global__ __launch_bounds__(256) void preprocess_geom_kernel(PreprocessArgs a)
-{
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    preprocess_prologue(a);
-    const int wave_first = (int)(blockIdx.x * 256u + wv * 64u);
-    if (wave_first >= a.P) return;  // wave-uniform
-    const int idx = wave_first + (int)lane;
-    const bool valid = idx < a.P;
-    const float3 p_orig = valid ? make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2])
-                                : make_float3(0.f, 0.f, 0.f);
-    PreIn in;
-    load_pre_in<CAM>(a, idx, valid, in);
-    PreOut o;
-    float shv[48];  // not read: the colour is the colour kernel's (sh16_late)
-    const bool vis = valid && preprocess_point<CAM>(a, in, idx, p_orig, true, shv, o, true);
-    const uint64_t vm = __ballot(vis);
-    if (lane == 0) a.vis_mask[wave_first >> 6] = vm;
-    if (valid) store_geometry(a, idx, vis, o);
-    if (vis) {  // 64 B per visible lane; the colour kernel fills rec[2].xyz
-        float4* rec = a.g.splat + (size_t)idx * SPLAT_F4;
-#pragma unroll
-        for (int j = 0; j < SPLAT_F4; ++j) rec[j] = o.rec[j];
-    }
-}
-
-constexpr uint32_t COLOUR_MAX_WORDS = 16;  // vis_mask words (64 Gaussians each) per colour-kernel wave
-__global__ __launch_bounds__(256) void preprocess_colour_kernel(PreprocessArgs a, uint32_t words_per_wave)
-{
-    __shared__ uint32_t s_list[4][COLOUR_MAX_WORDS * 64];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint32_t nwords = ((uint32_t)a.P + 63u) >> 6;
-    const uint32_t w0 = (blockIdx.x * 4u + wv) * words_per_wave;
-    if (w0 >= nwords) return;  // wave-uniform
-    const uint32_t w1 = min(w0 + words_per_wave, nwords);
-    uint32_t* list = s_list[wv];
-    uint32_t n = 0;  // wave-uniform
-    const uint64_t below = (1ull << lane) - 1ull;
-    for (uint32_t w = w0; w < w1; ++w) {
-        const uint64_t m = a.vis_mask[w];
-        if ((m >> lane) & 1u) list[n + (uint32_t)__popcll(m & below)] = w * 64u + lane;
-        n += (uint32_t)__popcll(m);
-    }
-    wave_sync();
-    const int nf4 = (3 * (a.D + 1) * (a.D + 1) + 3) >> 2;
-    for (uint32_t base = 0; base < n; base += 64) {
-        const uint32_t i = base + lane;
-        if (i >= n) continue;
-        const int idx = (int)list[i];
-        const float3 p_orig = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
-        const float4* row = reinterpret_cast<const float4*>(a.shs) + (size_t)idx * 12;
-        float shv[48];
-#pragma unroll
-        for (int q = 0; q < 12; ++q) {
-            const float4 v = q < nf4 ? row[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-            shv[4 * q] = v.x, shv[4 * q + 1] = v.y, shv[4 * q + 2] = v.z, shv[4 * q + 3] = v.w;
-        }
-        float rgb[3];
-        uint8_t clamp_bits = 0;
-        sh16_colour(a, idx, p_orig, shv, rgb, clamp_bits);
-        float* c = reinterpret_cast<float*>(a.g.splat + (size_t)idx * SPLAT_F4 + 2);
-        c[0] = rgb[0], c[1] = rgb[1], c[2] = rgb[2];
-        a.g.clamped[idx] = clamp_bits;
-    }
-}
-
 __global__ void mark_frustum_kernel(int P, const float* means3D, const float* viewmatrix, bool* present)
 {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -515,34 +432,12 @@ __global__ void mark_all_kernel(int P, bool* present)  // markAllVisible, raster
 
 }  // namespace
 
-int preprocess_split_mode(int mode)
-{
-    static std::atomic<int> m{[] {
-        const char* v = std::getenv("OMR_PRE_SPLIT");
-        return (v && std::strcmp(v, "0") == 0) ? 0 : 1;
-    }()};
-    return mode < 0 ? m.load() : m.exchange(mode);
-}
-
 void launch_preprocess(int camera_type, const PreprocessArgs& a, hipStream_t s)
 {
     if (a.P <= 0) return;
     const dim3 grid(div_up(a.P, 256));
-    const bool sh16 = a.colors_precomp == nullptr && a.M == 16 && (reinterpret_cast<uintptr_t>(a.shs) & 15u) == 0;
-    if (camera_type == CAM_LONLAT) {
-        preprocess_kernel<CAM_LONLAT><<<grid, 256, 0, s>>>(a);
-    } else if (sh16 && a.vis_mask && preprocess_split_mode(-1) == 1) {
-        preprocess_geom_kernel<CAM_PINHOLE><<<grid, 256, 0, s>>>(a);
-        // the colour kernel's waves each take `per` mask words: one word (64 Gaussians) per wave while that gives up
-        // to 8192 waves (a full chip at 8 waves per SIMD), more per wave past that (at most COLOUR_MAX_WORDS), so a
-        // sparse view's visible Gaussians are packed densely into few waves
-        const uint32_t words = (uint32_t)div_up(a.P, 64);
-        const uint32_t per = min(COLOUR_MAX_WORDS, max(1u, div_up(words, 8192u)));
-        const uint32_t waves = div_up(words, per);
-        preprocess_colour_kernel<<<div_up(waves, 4u), 256, 0, s>>>(a, per);
-    } else {
-        preprocess_kernel<CAM_PINHOLE><<<grid, 256, 0, s>>>(a);
-    }
+    if (camera_type == CAM_LONLAT) preprocess_kernel<CAM_LONLAT><<<grid, 256, 0, s>>>(a);
+    else preprocess_kernel<CAM_PINHOLE><<<grid, 256, 0, s>>>(a);
 }
 
 void launch_mark_visible(int camera_type, int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

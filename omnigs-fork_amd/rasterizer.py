@@ -77,8 +77,6 @@ def lib() -> C.CDLL:
         L.omr_debug_depth_sort_mode.argtypes = [i]
         L.omr_debug_ssim_mode.restype = i
         L.omr_debug_ssim_mode.argtypes = [i]
-        L.omr_debug_preprocess_split.restype = i
-        L.omr_debug_preprocess_split.argtypes = [i]
         L.omr_debug_adam_sh_rows.restype = i
         L.omr_debug_adam_sh_rows.argtypes = [i]
         L.omr_debug_set_sh_jac.restype = i
@@ -583,15 +581,6 @@ def debug_ssim_mode(mode: int) -> int:
     rc = int(lib().omr_debug_ssim_mode(int(mode)))
     if rc < 0:
         raise RasterizerError(f"debug_ssim_mode({mode}): {lib().omr_last_error().decode()}")
-    return rc
-
-
-def debug_preprocess_split(mode: int) -> int:
-    """Pinhole preprocess, process-wide (omr_debug_preprocess_split): 1 geometry pass + colour pass over the visible
-    Gaussians (default), 0 one fused kernel. Returns the previous value."""
-    rc = int(lib().omr_debug_preprocess_split(int(mode)))
-    if rc < 0:
-        raise RasterizerError(f"debug_preprocess_split({mode}): {lib().omr_last_error().decode()}")
     return rc
 
 

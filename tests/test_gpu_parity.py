@@ -347,46 +347,6 @@ def test_pinhole_render_depth():
     _compare(g, cam, None, render_depth=True)
 
 
-@pytest.mark.parametrize("case", ["sparse", "dense", "off_cone"])
-def test_pinhole_split_preprocess_equals_the_fused_kernel(case):
-    """Pinhole views with 16-coefficient SH rows run preprocess as a geometry pass over every Gaussian plus a colour
-    pass over the visible ones (preprocess.hip: preprocess_geom_kernel / preprocess_colour_kernel, VERDICT r05 item 3);
-    omr_debug_preprocess_split(0) selects the fused kernel. Every output of the forward and the backward must be
-    bitwise the same: a sparse view (most Gaussians culled, several mask words per colour wave at 600 k Gaussians),
-    a dense one, and large off-view Gaussians."""
-    import torch
-
-    if case == "sparse":
-        g, cam, dL = make_case(600000, 480, 270, PIN, 98, view_index=4, spread=1.0)
-    elif case == "dense":
-        g, cam, dL = make_case(20000, 320, 180, PIN, 99, view_index=1, spread=2.0)
-        g.means3D = (g.means3D * np.float32(0.3) + np.array([0, 0, 4], np.float32)).astype(np.float32)  # in front
-    else:
-        g, cam, dL = make_case(6000, 320, 180, PIN, 97, view_index=2, spread=2.0)
-        g.scales = (g.scales * np.float32(6.0)).astype(np.float32)
-    R = omr.rasterizer
-    old = R.debug_preprocess_split(1)
-    try:
-        split = hip_run(g, cam, dL)
-        R.debug_preprocess_split(0)
-        fused = hip_run(g, cam, dL)
-    finally:
-        R.debug_preprocess_split(old)
-    assert split["L"] == fused["L"] and split["L"] > 0
-    torch.testing.assert_close(split["color"], fused["color"], rtol=0, atol=0)
-    torch.testing.assert_close(split["radii"], fused["radii"], rtol=0, atol=0)
-    vis = to_np(split["radii"]) > 0
-    for k, v in split["state"].items():
-        a, b = to_np(v), to_np(fused["state"][k])
-        if a.shape and a.shape[0] == g.P and k != "point_list":
-            a, b = a[vis], b[vis]  # culled Gaussians' geometry is never written nor read
-        np.testing.assert_array_equal(a, b, err_msg=k)
-    for k, v in split["grads"].items():
-        torch.testing.assert_close(v, fused["grads"][k], rtol=0, atol=0, msg=k)
-    if case == "sparse":
-        assert vis.mean() < 0.5
-
-
 def test_pinhole_visible_gaussians_outside_the_predicted_cone():
     """Pinhole preprocess requests, before the projection, the SH rows of the lanes whose mean lies in front of the
     near plane and inside the 1.3x widened view cone (preprocess.hip: `near`, a prediction from the mean alone). A
