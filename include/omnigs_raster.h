@@ -299,6 +299,11 @@ int omr_debug_depth_sort_mode(int mode);
  * one), 1 = always tiled, 2 = always streaming (both give bitwise the same dL_dimg); process-wide, for tests and A/B
  * runs. Returns the previous mode, or -1 for a mode outside 0..2 */
 int omr_debug_ssim_mode(int mode);
+/* the render backward's mapping: 0 = by view (two waves per (tile, segment) unit, two 16x4 bands each, when every
+ * unit is resident at once — small views; else one wave of four bands), 2 / 4 = always that one (rows equal up to the
+ * order of the float additions; A/B runs and tests). Process-wide; the environment's OMR_BWD_BANDS=2|4 sets the start
+ * value. Returns the previous mode, or -1 for another value */
+int omr_debug_bwd_bands(int mode);
 /* omr_adam_step / omr_adam_step_activate: 1 = f_dc and f_rest stepped as one walk over dL_dsh's rows (the default),
  * 0 = two gathering groups, the activated SH array then written by a separate copy launch (same results; A/B runs).
  * Process-wide; the environment's OMR_ADAM_SH_ROWS=0 sets the start value. Returns the previous value, or -1 for a

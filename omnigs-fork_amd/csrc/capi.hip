@@ -1424,6 +1424,15 @@ int omr_debug_ssim_mode(int mode)
     return ssim_debug_mode(mode);
 }
 
+int omr_debug_bwd_bands(int mode)
+{
+    if (mode != 0 && mode != 2 && mode != 4) {
+        fail(OMR_ERR_INVALID_ARGUMENT, "render backward bands per wave: 0 (by view), 2 or 4");
+        return -1;
+    }
+    return bwd_bands_mode(mode);
+}
+
 int omr_debug_adam_sh_rows(int enabled)
 {
     if (enabled < 0 || enabled > 1) {

@@ -219,6 +219,9 @@ struct RenderBwdArgs {
 // profiling the stage inserts no marker packets around it (each costs a system-scope release: GPU idle, capi.hip)
 void launch_render_backward(const RenderBwdArgs& a, size_t max_units, hipStream_t s, hipEvent_t ev_start = nullptr,
                             hipEvent_t ev_stop = nullptr);
+// the render backward's mapping: 0 by view (two waves per unit when every unit is resident at once, else one), 2 or 4
+// forces two / one wave(s) per unit; process-wide (omr_debug_bwd_bands, OMR_BWD_BANDS), returns the previous mode
+int bwd_bands_mode(int mode);
 // the backward's work list: every (tile, depth segment) below the tile's last contributor (max over the forward's
 // max_contrib words), costed by its positions, sorted longest first within each of the 8 XCD shares of the unit list
 // (the shares xcd_remap gives each XCD); writes units, *unit_count

@@ -35,6 +35,9 @@
 // T_i is recovered with v_rcp_f32 (T_{i+1} / (1 - alpha_i)), as the reference divides (backward.cu:782).
 // Instances at or behind every band's last contributor are skipped; batches in front of every pixel's last
 // contributor run an instance loop without the per-lane position test (min_last below).
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "kernels.h"
@@ -336,6 +339,258 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_BWD_MINW) void render_bwd_kernel
 #endif
 }
 
+// ---- small views: two waves per unit, two bands per wave ----------------------------
+// Each (tile, segment) unit is one 128-thread workgroup: wave h owns bands 2h and 2h + 1 (rows 8h .. 8h + 7), so a
+// lane carries two pixels' state instead of four. Wave 0 stages each batch for both; each wave walks the staged
+// instances its bands reach and reduces its own nine moments per contributing instance (paired as in
+// render_bwd_kernel when PAIR, else one wave_sum9_lds each) into an LDS row per (half, staged instance); after the
+// batch the two half-tile rows are added (a half that took no contribution adds nothing) and stored as the
+// instance's 36-B row. The same rows as render_bwd_kernel up to the order of the float additions (both fixed:
+// deterministic).
+// It issues 27 % more VALU than one wave per unit (instances reaching both halves are set up and reduced twice) and
+// its two waves meet at three barriers per batch: at config C it is 45 % slower. But on
+// views whose units all fit on the chip at once as one-wave workgroups (A, B) the kernel's time is the chains of its
+// few waves per SIMD, and twice the waves cover them: A render_bwd 25.6 -> 21.6 us, B 75.8 -> 71.6 us
+// (profiles/r06h_ab_{A,B}.txt). launch_render_backward takes it there.
+template <int BWD_BATCH, bool PAIR>
+__global__ __launch_bounds__(128) void render_bwd2_kernel(RenderBwdArgs a)
+{
+    constexpr int NB = 2;  // bands per wave
+    __shared__ float4 s_geo[BWD_BATCH];   // x, y, position in range (u32 bits), band mask (u32 bits)
+    __shared__ float4 s_quad[BWD_BATCH];  // qa, qb, qc, log2(opacity)
+    __shared__ float4 s_rgb[BWD_BATCH];   // colour, gradient row slot (u32 bits)
+    __shared__ __attribute__((aligned(16))) float s_red_all[2][(PAIR ? 16 : 8) * WS_LDS_STRIDE];
+    __shared__ float s_R[2][BWD_BATCH][GRAD_ROW];  // each half's reduced nine values per staged instance
+    __shared__ uint32_t s_F[2][BWD_BATCH];         // 1: that half reduced the instance
+    __shared__ uint32_t s_bend[4], s_maxc[2], s_nuse;
+
+    const uint32_t nunits = *a.unit_count;
+    if (blockIdx.x >= nunits) return;  // block-uniform
+    const uint2 unit = a.units[xcd_remap(blockIdx.x, nunits)];
+    const uint32_t tile = unit.x, chunk = unit.y;
+    const uint32_t h = uniform(threadIdx.x >> 6);
+    float* s_red = s_red_all[h];
+    const TileLane tl(tile, a.gx);
+    const uint32_t lane = tl.lane;
+    const float pxf = (float)tl.px;
+    const size_t plane = (size_t)a.H * a.W;
+
+    float T[NB], s[NB];
+    f2v dp01[NB];
+    float dp2[NB];
+    uint32_t last[NB], band_end[NB];
+    uint32_t min_last = ~0u;
+    bool inside[NB];
+    uint32_t pix[NB];
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+        const uint32_t py = tl.py(2 * (int)h + bb);
+        inside[bb] = tl.px < (uint32_t)a.W && py < (uint32_t)a.H;
+        pix[bb] = inside[bb] ? a.W * py + tl.px : 0u;
+    }
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) last[bb] = a.n_contrib[pix[bb]];
+    const uint2 range = a.ranges[tile];
+    const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
+    float Tf[NB], d0[NB], d1[NB], d2[NB];
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+        Tf[bb] = a.final_T[pix[bb]];
+        d0[bb] = a.dL_dpix[pix[bb]];
+        d1[bb] = a.dL_dpix[plane + pix[bb]];
+        d2[bb] = a.dL_dpix[2 * plane + pix[bb]];
+    }
+    uint32_t max_c = 0;
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+        last[bb] = inside[bb] ? last[bb] : 0u;
+        band_end[bb] = uniform(wave_max_u32(last[bb]));
+        min_last = min(min_last, ~uniform(wave_max_u32(~(inside[bb] ? (last[bb] ? last[bb] : ~0u) : 0u))));
+        max_c = max(max_c, band_end[bb]);
+    }
+    if (lane == 0) {
+        s_bend[2 * h] = band_end[0];
+        s_bend[2 * h + 1] = band_end[1];
+        s_maxc[h] = max_c;
+    }
+    for (uint32_t j = threadIdx.x; j < 2u * BWD_BATCH; j += 128u) (&s_F[0][0])[j] = 0u;
+    __syncthreads();
+    const uint32_t bend_all[4] = {s_bend[0], s_bend[1], s_bend[2], s_bend[3]};
+    const uint32_t n = range.y - range.x;
+    max_c = min(max(s_maxc[0], s_maxc[1]), n);
+    const uint32_t seg_lo = max(range.x, chunk * CKPT) - range.x;
+    const uint32_t seg_hi = min(range.x + max_c, (chunk + 1) * CKPT) - range.x;
+    const bool resume = seg_hi < max_c;
+    float4 ck[NB];
+    float fc0[NB], fc1[NB], fc2[NB];
+    if (resume) {
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) {
+            ck[bb] = a.ckpt[(size_t)(chunk + 1) * BLOCK_SIZE + (2 * h + bb) * 64 + lane];
+            fc0[bb] = a.final_C[pix[bb]];
+            fc1[bb] = a.final_C[plane + pix[bb]];
+            fc2[bb] = a.final_C[2 * plane + pix[bb]];
+        }
+    }
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+        const float e0 = inside[bb] ? d0[bb] : 0.f, e1 = inside[bb] ? d1[bb] : 0.f, e2 = inside[bb] ? d2[bb] : 0.f;
+        dp01[bb] = f2v{e0, e1};
+        dp2[bb] = e2;
+        T[bb] = inside[bb] ? Tf[bb] : 0.f;
+        s[bb] = T[bb] * (bg0 * e0 + bg1 * e1 + bg2 * e2);
+        if (resume && last[bb] > seg_hi) {
+            T[bb] = ck[bb].x;
+            s[bb] += e0 * (fc0[bb] - ck[bb].y) + e1 * (fc1[bb] - ck[bb].z) + e2 * (fc2[bb] - ck[bb].w);
+        }
+    }
+
+    float pv8 = 0.f;       // PAIR: the held instance's 9th value
+    uint32_t pj = ~0u;     // PAIR: its staged index (an SGPR); ~0: nothing held
+    for (int hi = (int)seg_hi; hi > (int)seg_lo; hi -= BWD_BATCH) {
+        const int cnt = min(hi - (int)seg_lo, BWD_BATCH);
+        if (h == 0) {  // wave 0 stages the batch for both halves
+            uint32_t m = 0;
+            float4 p, co, c;
+            uint32_t pos = 0, slot = 0;
+            if ((int)lane < cnt) {
+                pos = (uint32_t)(hi - 1 - (int)lane);
+                const uint32_t v = a.point_list[range.x + pos];
+                m = v >> PL_GID_BITS;
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (pos >= bend_all[b]) m &= ~(1u << b);
+                if (m) {
+                    const uint32_t gid = v & PL_GID_MASK;
+                    const float4* rec = a.splat + (size_t)gid * SPLAT_F4;
+                    const uint32_t first = a.row_first[gid];
+                    p = rec[0];
+                    co = rec[1];
+                    c = rec[2];
+                    const float4 rect = rec[3];
+                    slot = first + (tl.ty - __builtin_bit_cast(uint32_t, rect.y)) * __builtin_bit_cast(uint32_t, c.w) +
+                           (tl.tx - __builtin_bit_cast(uint32_t, rect.x));
+                }
+            }
+            const uint64_t useful = __ballot(m != 0);
+            if (m != 0) {
+                const uint32_t r = mask_rank(useful);
+                const Quad q = quad_of_conic(co);
+                s_geo[r] = make_float4(p.x, p.y, __builtin_bit_cast(float, pos), __builtin_bit_cast(float, m));
+                s_quad[r] = make_float4(q.qa, q.qb, q.qc, p2_log2o(co.w));
+                s_rgb[r] = make_float4(c.x, c.y, c.z, __builtin_bit_cast(float, slot));
+            }
+            if (lane == 0) s_nuse = (uint32_t)__popcll(useful);
+        }
+        __syncthreads();
+        const uint32_t nuse = uniform(s_nuse);
+        auto reduce_store = [&](const float (&v)[8], float v8, uint32_t j) {  // one instance, unpaired
+            float t8;
+            const float tv = wave_sum9_lds(v, v8, lane, s_red, &t8);
+            if ((lane & 7) == 0) s_R[h][j][lane >> 3] = tv;
+            if (lane == 1) s_R[h][j][8] = t8;
+            if (lane == 0) s_F[h][j] = 1u;
+            wave_sync();  // the image is rewritten by the next instance
+        };
+        auto instances = [&](auto pos_test) {
+            for (uint32_t j = 0; j < nuse; ++j) {
+                const float4 g = s_geo[j];
+                const uint32_t mb = (uniform(__builtin_bit_cast(uint32_t, g.w)) >> (2 * h)) & 3u;
+                if (!mb) continue;  // scalar: this half's bands are not reached
+                const float4 qo = s_quad[j];
+                const float4 f = s_rgb[j];
+                const uint32_t ipos = __builtin_bit_cast(uint32_t, g.z);
+                const Quad q = {qo.x, qo.y, qo.z};
+                const float dx = g.x - pxf;
+                const float lo = qo.w;
+                const ColQuad kq = column_quad(q, dx, lo);
+                const float dy0 = g.y - (float)tl.py0;
+                f2v s_uy = {0.f, 0.f};
+                f2v sc01 = {0.f, 0.f};
+                float suyy = 0.f, sc2 = 0.f;
+                uint32_t any = 0;
+#pragma unroll
+                for (int bb = 0; bb < NB; ++bb) {
+                    if (!(mb & (1u << bb))) continue;
+                    const float dp0b = dp01[bb].x, dp1b = dp01[bb].y, dp2b = dp2[bb];
+                    const uint32_t lastb = last[bb];
+                    const float dy = dy0 - (float)(4 * (2 * (int)h + bb));
+                    const float p2 = falloff_p2(kq, dy);
+                    const bool contrib = (decltype(pos_test)::value ? ipos < lastb : true) && p2_in_band(p2, lo);
+                    if (!__ballot(contrib)) continue;
+                    any |= 1u << bb;
+                    const float oG = __builtin_amdgcn_exp2f(contrib ? p2 : -__builtin_inff());
+                    const float alpha = fminf(0.99f, oG);
+                    const float inv = __builtin_amdgcn_rcpf(1.0f - alpha);
+                    T[bb] *= inv;
+                    const float Ti = T[bb];
+                    const float cdot = __builtin_fmaf(f.x, dp0b, __builtin_fmaf(f.y, dp1b, f.z * dp2b));
+                    const float dL_dalpha = __builtin_fmaf(Ti, cdot, -s[bb] * inv);
+                    const float wc = alpha * Ti;
+                    s[bb] = __builtin_fmaf(cdot, wc, s[bb]);
+                    const float u = oG * dL_dalpha;
+                    const float uy = u * dy;
+                    s_uy += f2v{u, uy};
+                    suyy = __builtin_fmaf(uy, dy, suyy);
+                    sc01 = __builtin_elementwise_fma(f2v{wc, wc}, dp01[bb], sc01);
+                    sc2 = __builtin_fmaf(wc, dp2b, sc2);
+                }
+                if (!any) continue;
+                const float su = s_uy.x, suy = s_uy.y;
+                const float sux = su * dx, suxx = sux * dx, suxy = suy * dx;
+                float v[8] = {sux, suy, suxx, suxy, suyy, su, sc01.x, sc01.y};
+                if constexpr (PAIR) {
+                    const bool held = pj != ~0u;  // scalar
+                    const uint32_t base = held ? 8u * WS_LDS_STRIDE : 0u;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) s_red[base + k * WS_LDS_STRIDE + lane] = v[k];
+                    if (!held) {
+                        pv8 = sc2;
+                        pj = j;
+                        continue;
+                    }
+                    float t8;
+                    const float tv = wave_sum9x2_stored(pv8, sc2, lane, s_red, &t8);
+                    const bool lead = (lane & 3) == 0;
+                    const uint32_t dj = (lane < 32) ? pj : j;
+                    if (lead) s_R[h][dj][(lane >> 2) & 7u] = tv;
+                    if ((lane & 31) == 1) s_R[h][dj][8] = t8;
+                    if ((lane & 31) == 0) s_F[h][dj] = 1u;
+                    pj = ~0u;
+                    wave_sync();  // the image is rewritten by the next pair
+                } else {
+                    reduce_store(v, sc2, j);
+                }
+            }
+        };
+        if ((uint32_t)(hi - 1) < min_last) instances(std::false_type{});
+        else instances(std::true_type{});
+        if constexpr (PAIR) {
+            if (pj != ~0u) {  // the batch's last contributing instance of this half had no partner
+                float v[8];
+                wave_sync();
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = s_red[k * WS_LDS_STRIDE + lane];
+                reduce_store(v, pv8, pj);
+                pj = ~0u;
+            }
+        }
+        __syncthreads();  // both halves' rows of the batch are in s_R
+        for (uint32_t e = threadIdx.x; e < nuse * (uint32_t)GRAD_ROW; e += 128u) {
+            const uint32_t j = e / GRAD_ROW, k = e - j * GRAD_ROW;
+            const uint32_t f0 = s_F[0][j], f1 = s_F[1][j];
+            if (f0 | f1) {
+                const float v = (f0 ? s_R[0][j][k] : 0.f) + (f1 ? s_R[1][j][k] : 0.f);
+                const uint32_t slot = __builtin_bit_cast(uint32_t, s_rgb[j].w);
+                a.inst_grad[(size_t)slot * GRAD_ROW + k] = v;
+                if (k == 0) a.row_valid[slot] = 1;
+            }
+        }
+        __syncthreads();  // the combine's reads are done before the flags are cleared and the next batch is staged
+        for (uint32_t j = threadIdx.x; j < nuse; j += 128u) s_F[0][j] = s_F[1][j] = 0u;
+    }
+}
+
 }  // namespace
 
 #ifdef OMR_STAMPS
@@ -356,6 +611,16 @@ extern "C" int omr_debug_bwd_counts(uint64_t* dst, int reset)
     return rc;
 }
 #endif
+
+int bwd_bands_mode(int mode)
+{
+    static std::atomic<int> m{[] {
+        const char* v = std::getenv("OMR_BWD_BANDS");
+        const int b = v ? std::atoi(v) : 0;
+        return (b == 2 || b == 4) ? b : 0;
+    }()};
+    return mode < 0 ? m.load() : m.exchange(mode);
+}
 
 void launch_render_backward(const RenderBwdArgs& a, size_t max_units, hipStream_t s, hipEvent_t ev_start,
                             hipEvent_t ev_stop)
@@ -385,6 +650,18 @@ void launch_render_backward(const RenderBwdArgs& a, size_t max_units, hipStream_
         else
             kernel<<<(uint32_t)max_units, 64 * TW_WAVES, 0, s>>>(a);
     };
+    // views whose units all fit at once as one-wave workgroups (A, B): two waves per unit, 64-position batches;
+    // larger views (C, D, E): one wave per unit and 40-position batches. OMR_BWD_BANDS=4 / 2 (omr_debug_bwd_bands)
+    // forces one kernel for A/B runs and tests: 4 = the one-wave kernel with its own batch rule (64 below RESIDENT)
+    const int bands = bwd_bands_mode(-1);
+    if (bands == 2 || (bands == 0 && max_units <= RESIDENT)) {
+        if (ev_start || ev_stop)
+            hipExtLaunchKernelGGL(render_bwd2_kernel<TW_BATCH, true>, dim3((uint32_t)max_units), dim3(128), 0, s, ev_start,
+                                  ev_stop, 0, a);
+        else
+            render_bwd2_kernel<TW_BATCH, true><<<(uint32_t)max_units, 128, 0, s>>>(a);
+        return;
+    }
     if (max_units > RESIDENT) launch(render_bwd_kernel<OMR_BWD_BATCH>);
     else launch(render_bwd_kernel<TW_BATCH>);
 }

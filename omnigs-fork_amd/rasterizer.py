@@ -77,6 +77,8 @@ def lib() -> C.CDLL:
         L.omr_debug_depth_sort_mode.argtypes = [i]
         L.omr_debug_ssim_mode.restype = i
         L.omr_debug_ssim_mode.argtypes = [i]
+        L.omr_debug_bwd_bands.restype = i
+        L.omr_debug_bwd_bands.argtypes = [i]
         L.omr_debug_adam_sh_rows.restype = i
         L.omr_debug_adam_sh_rows.argtypes = [i]
         L.omr_debug_set_sh_jac.restype = i
@@ -581,6 +583,15 @@ def debug_ssim_mode(mode: int) -> int:
     rc = int(lib().omr_debug_ssim_mode(int(mode)))
     if rc < 0:
         raise RasterizerError(f"debug_ssim_mode({mode}): {lib().omr_last_error().decode()}")
+    return rc
+
+
+def debug_bwd_bands(mode: int) -> int:
+    """The render backward's mapping, process-wide (omr_debug_bwd_bands): 0 by view (two waves of two bands per unit
+    when every unit is resident at once), 2 or 4 forced. Returns the previous mode."""
+    rc = int(lib().omr_debug_bwd_bands(int(mode)))
+    if rc < 0:
+        raise RasterizerError(f"debug_bwd_bands({mode}): {lib().omr_last_error().decode()}")
     return rc
 
 

@@ -102,6 +102,37 @@ def test_parity(case):
     _compare(g, cam, dL)
 
 
+@pytest.mark.parametrize("bands", [2, 4])
+@pytest.mark.parametrize("case", ["lonlat_1k_128x64", "pinhole_ragged_5k_301x157", "lonlat_ragged_10k_333x171"])
+def test_render_backward_mappings(case, bands):
+    """render_bwd.hip has two mappings of a (tile, segment) unit: one wave of four 16x4 bands (render_bwd_kernel, the
+    views whose units outnumber the resident one-wave workgroups: C, D, E) and two waves of two bands each
+    (render_bwd2_kernel, smaller views: A, B and every small case here). omr_debug_bwd_bands forces each on the same
+    small scenes; both must meet the oracle bars (their rows differ only in the order of the float additions)."""
+    c = next(x for x in CASES if x[0] == case)
+    _, P, W, H, cam_t, seed, view, deg, mult = c
+    g, cam, dL = make_case(P, W, H, cam_t, seed, view_index=view, sh_degree=deg, spread=mult)
+    old = omr.rasterizer.debug_bwd_bands(bands)
+    try:
+        _compare(g, cam, dL)
+    finally:
+        omr.rasterizer.debug_bwd_bands(old)
+    with pytest.raises(omr.rasterizer.RasterizerError):
+        omr.rasterizer.debug_bwd_bands(3)
+
+
+def test_two_band_backward_on_a_multi_segment_view(oracle_mt):
+    """The two-waves-per-unit backward (the default at B) forced on config B's full scene: 336 of its 2048 tiles'
+    lists cross a global multiple of CKPT = 1024, so their back units resume from the forward's checkpoints; the two
+    halves' rows are added per batch."""
+    g, cam, dL = scene.config_scene("B")
+    old = omr.rasterizer.debug_bwd_bands(2)
+    try:
+        _compare(g, cam, dL, nthreads=oracle_mt, budget=CONFIG_BUDGETS["B"])
+    finally:
+        omr.rasterizer.debug_bwd_bands(old)
+
+
 @pytest.mark.parametrize("M,deg,cam_t", [(4, 1, LON), (9, 2, LON), (9, 1, PIN), (1, 0, LON), (25, 3, LON)],
                          ids=["M4_deg1", "M9_deg2", "M9_deg1_pinhole", "M1_deg0", "M25_deg3"])
 def test_generic_sh_layout(M, deg, cam_t):
