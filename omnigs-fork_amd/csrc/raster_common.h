@@ -170,13 +170,15 @@ __host__ __device__ inline size_t row_valid_offset(size_t L)
 #define OMR_BWD_CK 1024
 #endif
 constexpr uint32_t CKPT = OMR_BWD_CK;
-// forward waves per tile (render_fwd.hip: launch_render_forward picks 2 bands per wave, i.e. two waves per tile, or
-// 4 bands, one wave per tile, by the view's tile count); max_contrib keeps FWD_GROUPS slots per tile either way
-constexpr int FWD_GROUPS = 2;
+// forward waves per tile (render_fwd.hip: launch_render_forward picks 1, 2 or 4 bands per wave, i.e. four, two or
+// one wave(s) per tile, by the view's tile count); max_contrib keeps FWD_GROUPS slots per tile either way
+constexpr int FWD_GROUPS = 4;
 // views with at least this many tiles render one wave per tile: enough waves to fill the chip without splitting, and
 // each tile's instances staged once (config E, 32 k tiles: render_fwd 0.476 -> 0.449 ms; config C, 8 k tiles: 0.272
 // with two waves per tile vs 0.295 with one, profiles/r03z_ab_fwd_bands.txt)
 constexpr uint32_t FWD_ONE_WAVE_TILES = 16384;
+// views of at most this many tiles render four waves per tile (one band each): config A, 512 tiles (round 6)
+constexpr uint32_t FWD_FOUR_WAVE_TILES = 1024;
 // OMR_SH_JAC (default 1): preprocess stores each visible Gaussian's dRGB/ddir (GeomState::sh_jac) for gaussian_bwd
 // when it stages 16-coefficient SH rows (0: never; gaussian_bwd then reads the SH rows)
 #ifndef OMR_SH_JAC

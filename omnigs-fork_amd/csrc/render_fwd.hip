@@ -17,6 +17,7 @@
 // HBM per tile instance: 4 (point_list) + 48 of the Gaussian's 64-B record (one random line);
 // per pixel: 12 (colour) + 4 (final_T) + 4 (n_contrib) = 20 B written.
 #include <algorithm>
+#include <cstdlib>
 
 #include "kernels.h"
 #include "tile_wave.h"
@@ -236,7 +237,8 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
     }
     maxc = wave_max_u32(maxc);
     if (lane == 0) a.max_contrib[(size_t)tile * FWD_GROUPS + grp] = maxc;
-    if (NG == 1 && lane == 1) a.max_contrib[(size_t)tile * FWD_GROUPS + 1] = 0u;  // one wave: the second slot empty
+    // the slots no wave of this tile writes (NG < FWD_GROUPS) are cleared by its first wave
+    if (grp == 0 && lane >= NG && lane < (uint32_t)FWD_GROUPS) a.max_contrib[(size_t)tile * FWD_GROUPS + lane] = 0u;
     if (lane == 0 && work) atomicAdd(&a.tile_cost[tile], work);
     // The backward's row_valid map is zeroed here, one slice per wave with 16-B stores after the wave's image stores, in
     // the shadow of the VALU-bound blend, rather than by the binning's latency-bound scatter loop (one byte store per
@@ -257,7 +259,17 @@ void launch_render_forward(const RenderFwdArgs& a, bool depth_mode, hipStream_t 
 {
     const uint32_t T = a.gx * a.gy;
     if (T == 0) return;
-    if (T >= FWD_ONE_WAVE_TILES) {
+    // bands per wave by view: one (four waves per tile) up to FWD_FOUR_WAVE_TILES tiles, where two bands would give at
+    // most two waves per SIMD (config A: render_fwd 12.4 -> 10.9 us; at B, 2048 tiles, one band is slower: 40.4 vs
+    // 38.5 us; profiles/r06j_ab_{A,B}.txt), two below FWD_ONE_WAVE_TILES, four from there; OMR_FWD_BANDS=1|2|4 forces
+    static const int forced = [] { const char* v = std::getenv("OMR_FWD_BANDS"); return v ? std::atoi(v) : 0; }();
+    if (forced == 1 || (forced == 0 && T <= FWD_FOUR_WAVE_TILES)) {
+        const uint32_t blocks = div_up(T * 4, TW_WAVES);
+        if (depth_mode) render_fwd_kernel<true, 1><<<blocks, 64 * TW_WAVES, 0, s>>>(a);
+        else render_fwd_kernel<false, 1><<<blocks, 64 * TW_WAVES, 0, s>>>(a);
+        return;
+    }
+    if (forced == 4 || (forced != 2 && T >= FWD_ONE_WAVE_TILES)) {
         const uint32_t blocks = div_up(T, TW_WAVES);
         if (depth_mode) render_fwd_kernel<true, 4><<<blocks, 64 * TW_WAVES, 0, s>>>(a);
         else render_fwd_kernel<false, 4><<<blocks, 64 * TW_WAVES, 0, s>>>(a);
