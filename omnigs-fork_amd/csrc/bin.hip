@@ -33,6 +33,8 @@
 // scanned count at its first chunk and at the next tile's.
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace omr {
@@ -48,11 +50,16 @@ struct Geo {
     static constexpr int PER_WAVE = (int)N / WAVES, ROUNDS = PER_WAVE / 64;
 };
 using RowGeo = Geo<256, 8>;  // rows pass: 2048-slot chunks
-// columns pass: 2048-slot chunks, or 4096 for large views (BinArgs::cb_shift; half the chunks: fewer counts to scan
-// and fewer descriptors and barriers per instance, at the same 16 waves per CU — config E tile sort 1.27 -> 1.17 ms,
-// while config C, whose 2048-slot chunks are only ~7 per block, lost 7 us to the coarser tail)
+// columns pass: 2048-slot chunks, 1024 for small views, 4096 for large views (BinArgs::cb_shift; 4096: half the
+// chunks, fewer counts to scan and fewer descriptors and barriers per instance, at the same 16 waves per CU — config E
+// tile sort 1.27 -> 1.17 ms, while config C, whose 2048-slot chunks are only ~7 per block, lost 7 us to the coarser
+// tail)
 using ColGeoS = Geo<256, 8>;
 using ColGeoL = Geo<512, 8>;
+// small views: 512- or 1024-slot chunks on one- or two-wave blocks, so a few thousand instances still spread over
+// many CUs (config A: 22 k instances were 11 chunks of 2048, 11 blocks on 256 CUs)
+using ColGeoT = Geo<64, 8>;
+using ColGeoM = Geo<128, 8>;
 constexpr int RB_THREADS = RowGeo::THREADS;
 constexpr int RB_ITEMS = RowGeo::ITEMS;
 constexpr uint32_t RB_N = RowGeo::N;  // slots per rows-pass chunk
@@ -60,7 +67,8 @@ static_assert(RB_N == BIN_CHUNK, "launch_forward_scans cuts the rows pass's chun
 constexpr int RB_WAVES = RowGeo::WAVES;
 constexpr int RB_PER_WAVE = RowGeo::PER_WAVE;
 constexpr int RB_ROUNDS = RowGeo::ROUNDS;
-static_assert(ColGeoS::N == 1u << 11 && ColGeoL::N == 1u << 12, "cb_shift 11 / 12");
+static_assert(ColGeoT::N == 1u << 9 && ColGeoM::N == 1u << 10 && ColGeoS::N == 1u << 11 && ColGeoL::N == 1u << 12,
+              "cb_shift 9 .. 12");
 // grid caps of the grid-stride chunk kernels (256 CUs: 8 resident hist blocks of 256 threads, 4 scatter blocks of
 // 256 threads and <= 40 KiB LDS, or 2 of 512 threads and <= 80 KiB)
 constexpr uint32_t BIN_GRID_HIST = 2048, BIN_GRID_SCATTER = 1024;
@@ -804,7 +812,18 @@ extern "C" int omr_debug_bin_stamps(uint64_t* dst, size_t bytes)
 
 // scratch of the row binning for a binning capacity of `cap` instances (BinningState::carve)
 size_t bin_chunks_r(size_t cap) { return div_up(cap, RB_N) + 1; }
-uint32_t bin_cols_shift(size_t cap) { return cap >= ((size_t)1 << 25) ? 12u : 11u; }
+uint32_t bin_cols_shift(size_t cap)
+{
+    static const uint32_t forced = [] {  // OMR_BIN_COLS_SHIFT=9..12 (A/B runs): the columns-pass chunk for every view
+        const char* v = std::getenv("OMR_BIN_COLS_SHIFT");
+        const int k = v ? std::atoi(v) : 0;
+        return (k >= 9 && k <= 12) ? (uint32_t)k : 0u;
+    }();
+    if (forced) return forced;
+    // 1024-slot chunks below 2 M instances (configs A, B: +0.5-0.8 %, profiles/r06k_ab_{A,B}.txt); C's 2048 (1024:
+    // -1 %, 512: -2.6 %, r06k_ab_C.txt), E's 4096
+    return cap >= ((size_t)1 << 25) ? 12u : cap >= ((size_t)1 << 21) ? 11u : 10u;
+}
 size_t bin_chunks_b(size_t cap, uint32_t gy) { return (div_up(cap, (size_t)1 << bin_cols_shift(cap))) + gy + 1; }
 
 void launch_row_binning(const BinArgs& a_in, hipStream_t s)
@@ -827,15 +846,16 @@ void launch_row_binning(const BinArgs& a_in, hipStream_t s)
     else rows_scatter_kernel<10><<<gs_r, RB_THREADS, 0, s>>>(a);
     cols_hist_kernel<<<gh_b, RB_THREADS, 0, s>>>(a);
     launch_exclusive_scan(a.hist_b, a.hist_b, nb_hist, a.words + 3, st_b, a.err, s);
-    if (a.cb_shift == 12) {
-        const uint32_t g = std::min(cbk, BIN_GRID_SCATTER / 2);
-        if (a.gx <= 256) cols_scatter_kernel<8, ColGeoL><<<g, ColGeoL::THREADS, 0, s>>>(a);
-        else cols_scatter_kernel<10, ColGeoL><<<g, ColGeoL::THREADS, 0, s>>>(a);
-    } else {
-        const uint32_t g = std::min(cbk, BIN_GRID_SCATTER);
-        if (a.gx <= 256) cols_scatter_kernel<8, ColGeoS><<<g, ColGeoS::THREADS, 0, s>>>(a);
-        else cols_scatter_kernel<10, ColGeoS><<<g, ColGeoS::THREADS, 0, s>>>(a);
-    }
+    auto scatter = [&](auto geo) {
+        using G = decltype(geo);
+        const uint32_t g = std::min(cbk, BIN_GRID_SCATTER * (uint32_t)(ColGeoS::THREADS / G::THREADS));
+        if (a.gx <= 256) cols_scatter_kernel<8, G><<<g, G::THREADS, 0, s>>>(a);
+        else cols_scatter_kernel<10, G><<<g, G::THREADS, 0, s>>>(a);
+    };
+    if (a.cb_shift == 12) scatter(ColGeoL{});
+    else if (a.cb_shift == 11) scatter(ColGeoS{});
+    else if (a.cb_shift == 10) scatter(ColGeoM{});
+    else scatter(ColGeoT{});
 }
 
 }  // namespace omr
