@@ -79,7 +79,7 @@ constexpr uint32_t BIN_GRID_HIST = 2048, BIN_GRID_SCATTER = 1024;
 
 #ifdef OMR_BIN_STAMPS  // diagnostic: per-phase s_memrealtime stamps of cols_scatter_kernel (profiles/bin_stamps.py)
 constexpr int BSTAMP_ITERS = 16, BSTAMP_PH = 8;
-__device__ uint64_t g_bin_stamps[BIN_GRID_SCATTER][BSTAMP_ITERS][BSTAMP_PH];
+__device__ uint64_t g_bin_stamps[BIN_GRID_SCATTER * 4][BSTAMP_ITERS][BSTAMP_PH];  // the one-wave chunks' grid
 #define BSTAMP(it, ph)                                                                             \
     do {                                                                                           \
         const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                                      \
@@ -848,7 +848,7 @@ void launch_row_binning(const BinArgs& a_in, hipStream_t s)
     launch_exclusive_scan(a.hist_b, a.hist_b, nb_hist, a.words + 3, st_b, a.err, s);
     auto scatter = [&](auto geo) {
         using G = decltype(geo);
-        const uint32_t g = std::min(cbk, BIN_GRID_SCATTER * (uint32_t)(ColGeoS::THREADS / G::THREADS));
+        const uint32_t g = std::min(cbk, BIN_GRID_SCATTER * (uint32_t)ColGeoS::THREADS / (uint32_t)G::THREADS);
         if (a.gx <= 256) cols_scatter_kernel<8, G><<<g, G::THREADS, 0, s>>>(a);
         else cols_scatter_kernel<10, G><<<g, G::THREADS, 0, s>>>(a);
     };
