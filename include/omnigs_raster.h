@@ -290,10 +290,11 @@ int omr_debug_counters(char* geom_buffer, int P, uint32_t* dst, void* stream);
 /* clears (0) or restores (1) the key by which the backward uses the forward's stored dRGB/ddir (GeomState::sh_jac)
  * instead of reading the SH rows: lets a test run both backward paths on one forward */
 int omr_debug_set_sh_jac(char* geom_buffer, int P, int enabled, void* stream);
-/* the forward's depth sort: 0 = by camera type (pinhole: the sort that sets culled Gaussians aside first; lonlat: the
- * plain 4 x 8-bit radix sort), 1 = always the plain sort, 2 = always the culled-aside sort (the same permutation);
- * process-wide, for tests and A/B runs (the environment's OMR_DEPTH_SORT=bytes / visible sets the start value).
- * Returns the previous mode, or -1 for a mode outside 0..2 (omr_last_error says why) */
+/* the forward's depth sort: 0 = by size and camera type (views of at most 12288 Gaussians: the sort by counting;
+ * else pinhole: the sort that sets culled Gaussians aside first; lonlat: the plain 4 x 8-bit radix sort), 1 = always
+ * the plain sort, 2 = always the culled-aside sort, 3 = the sort by counting up to 2^18 Gaussians (the same
+ * permutation every way); process-wide, for tests and A/B runs (the environment's OMR_DEPTH_SORT=bytes / visible /
+ * count sets the start value). Returns the previous mode, or -1 for a mode outside 0..3 (omr_last_error says why) */
 int omr_debug_depth_sort_mode(int mode);
 /* omr_l1_ssim_loss's kernel: 0 = by image size (the streaming kernel once its strips fill the chip, else the tiled
  * one), 1 = always tiled, 2 = always streaming (both give bitwise the same dL_dimg); process-wide, for tests and A/B

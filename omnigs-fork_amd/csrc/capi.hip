@@ -407,13 +407,15 @@ static bool sort_binning_forced()
 // other three sort the visible keys alone (config E pinhole culls 88 %: 0.206 -> 0.137 ms); lonlat views cull only
 // what is too close to the camera, and there the plain 4 x 8-bit radix sort of every key is 2-4 us faster (C 0.0795
 // vs 0.0812 ms, A 0.029 vs 0.033: profiles/r05e_ab_*.txt). The same permutation either way. OMR_DEPTH_SORT (read once)
-// forces one for A/B runs and tests: "bytes" the plain sort, "visible" depth_sort.
-static std::atomic<int>& depth_sort_mode()  // 0: by camera type, 1: plain, 2: depth_sort (omr_debug_depth_sort_mode)
-{
+// forces one for A/B runs and tests: "bytes" the plain sort, "visible" depth_sort, "count" depth_count_sort.
+// Views of at most DEPTH_COUNT_SORT_MAX Gaussians take depth_count_sort (one launch instead of five chained ones).
+static std::atomic<int>& depth_sort_mode()  // 0: by size and camera type, 1: plain, 2: depth_sort, 3: count
+{                                           // (omr_debug_depth_sort_mode)
     static std::atomic<int> mode{[] {
         const char* v = std::getenv("OMR_DEPTH_SORT");
         if (v && std::strcmp(v, "bytes") == 0) return 1;
         if (v && std::strcmp(v, "visible") == 0) return 2;
+        if (v && std::strcmp(v, "count") == 0) return 3;
         return 0;
     }()};
     return mode;
@@ -429,10 +431,14 @@ static std::atomic<int>& adam_sh_rows_mode()
     }()};
     return mode;
 }
-static bool depth_sort_plain(int camera_type)
+enum DepthSortKind { DS_PLAIN, DS_VISIBLE, DS_COUNT };
+static DepthSortKind depth_sort_kind(int camera_type, size_t P)
 {
     const int f = depth_sort_forced();
-    return f ? f == 1 : camera_type != CAM_PINHOLE;
+    if (f == 3 && P <= DEPTH_COUNT_SORT_FORCED_MAX) return DS_COUNT;  // forced: any size a test can afford
+    if (f == 1 || f == 2) return f == 1 ? DS_PLAIN : DS_VISIBLE;
+    if (f == 0 && P <= DEPTH_COUNT_SORT_MAX) return DS_COUNT;
+    return camera_type != CAM_PINHOLE ? DS_PLAIN : DS_VISIBLE;
 }
 static bool row_binning(uint32_t gx, uint32_t gy)
 {
@@ -549,9 +555,10 @@ int forward_impl(const ForwardIn& in)
     pa.zero[0] = {g.counters + 2, 2};                                  // huge-list count (scan), look-back error word
     pa.zero[1] = {reinterpret_cast<uint32_t*>(im.ranges), 2 * (size_t)d.T};  // tile_ranges writes boundaries only
     pa.zero[2] = {im.tile_cost, (size_t)d.T};                          // render_forward adds into it
-    const bool plain_sort = depth_sort_plain(in.camera_type);
-    pa.zero[3] = plain_sort ? radix_zero_span(g.hist, P, DEPTH_SORT_PASSES)
-                            : depth_sort_zero_span(g.hist, P);  // the depth sort's digit totals / tickets / words
+    const DepthSortKind dsk = depth_sort_kind(in.camera_type, P);
+    pa.zero[3] = dsk == DS_PLAIN     ? radix_zero_span(g.hist, P, DEPTH_SORT_PASSES)
+                 : dsk == DS_VISIBLE ? depth_sort_zero_span(g.hist, P)  // the depth sort's digit totals / tickets / words
+                                     : ZeroSpan{};
     pa.zero[4] = {g.scan2_status, scan2_status_words(P)};             // the forward scans' look-back words
     pa.P = in.P; pa.D = in.D; pa.M = in.M; pa.W = in.width; pa.H = in.height; pa.gx = d.gx; pa.gy = d.gy;
     pa.means3D = in.means3D; pa.scales = in.scales; pa.scale_modifier = in.scale_modifier; pa.rotations = in.rotations;
@@ -570,10 +577,13 @@ int forward_impl(const ForwardIn& in)
     uint32_t* const err_dev = g.counters + 3;  // every decoupled look-back of the forward reports a give-up here
     {
         StageScope st_(ST_DEPTH_SORT, s);
-        if (plain_sort) {  // the plain 4 x 8-bit radix sort over all P keys
+        if (dsk == DS_PLAIN) {  // the plain 4 x 8-bit radix sort over all P keys
             const int which = radix_sort_pairs(g.key_a, g.key_b, g.val_a, g.val_b, g.hist, g.scan_partials, P, nullptr,
                                                nullptr, 0, DEPTH_SORT_PASSES, s, true, err_dev);
             g.order = which ? g.val_b : g.val_a;
+        } else if (dsk == DS_COUNT) {  // small views: by counting, one launch
+            g.order = g.val_b;
+            depth_count_sort(g.key_a, g.order, P, s);
         } else {
             depth_sort(g.key_a, g.key_b, g.val_a, g.val_b, g.order, g.hist, g.scan_partials, P, s, err_dev);
         }
@@ -1407,8 +1417,8 @@ int omr_debug_counters(char* geom_buffer, int P, uint32_t* dst, void* stream)
 
 int omr_debug_depth_sort_mode(int mode)
 {
-    if (mode < 0 || mode > 2) {
-        fail(OMR_ERR_INVALID_ARGUMENT, "depth sort mode: 0 (by camera type), 1, 2");
+    if (mode < 0 || mode > 3) {
+        fail(OMR_ERR_INVALID_ARGUMENT, "depth sort mode: 0 (by size and camera type), 1, 2, 3");
         return -1;
     }
     const int old = depth_sort_mode().exchange(mode);

@@ -86,6 +86,13 @@ size_t depth_sort_partials_words(size_t n);
 ZeroSpan depth_sort_zero_span(uint32_t* hist, size_t n);
 void depth_sort(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* order, uint32_t* hist,
                 uint32_t* scan_partials, size_t n, hipStream_t s, uint32_t* err);
+// The depth sort of small views (sort.hip): the same permutation as depth_sort / the plain radix sort (visible keys in
+// order, ties by index, then the culled ones by index) by counting, O(n^2) compares in one launch; keys: the n keys.
+// the default up to this many keys (capi.hip: depth_sort_kind): 18.8 us at 10 k keys on 157 CUs against the radix
+// sort's 29 us; past ~15 k keys every CU is busy and the time grows with n^2 (profiles/r06m_ab_A.txt)
+constexpr size_t DEPTH_COUNT_SORT_MAX = 12288;
+constexpr size_t DEPTH_COUNT_SORT_FORCED_MAX = 1u << 18;  // forced (tests, A/Bs) up to this many
+void depth_count_sort(const uint32_t* keys, uint32_t* order, size_t n, hipStream_t s);
 // one-launch exclusive scan of n u32 (in may equal out) of in[i] & mask; n_dev (device word, may be NULL) = live
 // length <= n; status: scan_status_words(n) words zeroed before the launch; err: the look-back error word (NULL: a
 // private one)

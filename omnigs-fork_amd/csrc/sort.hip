@@ -1431,6 +1431,93 @@ void depth_sort(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val
     }
 }
 
+// ---- the depth sort of small views by counting (depth_count_sort) -------------------------------------------------
+// Key i lands at #{j : k_j < k_i} + #{j < i : k_j == k_i}: the stable sort's position, so the permutation is the
+// radix sorts' bit for bit (ties in index order, the culled keys 0xFFFFFFFF last in index order). One launch of
+// O(n^2) compares instead of a histogram and four look-back passes (config A, 10 k keys: ~30 us of chained launches).
+// Workgroup = 64 keys, one per lane, x CS_WAVES waves; wave w compares them with the w-th slice of all n keys and the
+// slices' counts are summed through LDS. A wave stages its slice in CS_PIECE-key pieces in its own LDS region (vector
+// loads, the next piece's in flight while the current one is compared) and reads each group of 4 keys back with one
+// wave-uniform ds_read_b128 (a broadcast). Each slice splits at the workgroup's own 64 keys: before them a key counts
+// when <= k_i, after them when < k_i, and only the 64 in between compare indices too. At A (10 k keys, 157
+// workgroups) it takes 18.8 us, bound by the compares (2 VALU each) of the 16 waves on each busy CU; reading the keys
+// with wave-uniform scalar loads instead took 19.2 us (profiles/r06l_A_kernel_stats.csv, r06m_A_kernel_stats.csv).
+constexpr int CS_WAVES = 16;
+constexpr int CS_PIECE = 512;  // keys per wave and staged piece: 2 uint4 per lane
+// keys [s, e) of a staged piece (p: its LDS words, from key index p0) that order before k_i; s, e wave-uniform
+template <bool OR_EQUAL>
+__device__ __forceinline__ uint32_t count_staged(const uint32_t* p, uint32_t p0, uint32_t s, uint32_t e, uint32_t ki)
+{
+    uint32_t c = 0, j = s;
+    for (; j + 4 <= e; j += 4) {  // s - p0 is a multiple of 4 (slices, pieces and workgroups start at multiples of 4)
+        const uint4 q = *reinterpret_cast<const uint4*>(p + (j - p0));
+        c += OR_EQUAL ? (q.x <= ki) + (q.y <= ki) + (q.z <= ki) + (q.w <= ki)
+                      : (q.x < ki) + (q.y < ki) + (q.z < ki) + (q.w < ki);
+    }
+    for (; j < e; ++j) c += OR_EQUAL ? (p[j - p0] <= ki) : (p[j - p0] < ki);
+    return c;
+}
+__global__ __launch_bounds__(64 * CS_WAVES) void depth_count_sort_kernel(const uint32_t* __restrict__ keys,
+                                                                         uint32_t* __restrict__ order, uint32_t n)
+{
+    __shared__ uint4 s_piece[CS_WAVES][CS_PIECE / 4];
+    __shared__ uint32_t s_cnt[CS_WAVES][64];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t b0 = blockIdx.x * 64u, i = b0 + lane, b1 = min(n, b0 + 64u);
+    const uint32_t ki = i < n ? keys[i] : 0u;
+    const uint32_t per = ((n + CS_WAVES - 1) / CS_WAVES + 15u) / 16u * 16u;
+    const uint32_t j0 = min(n, w * per), j1 = min(n, j0 + per);
+    const uint32_t* sp = reinterpret_cast<const uint32_t*>(s_piece[w]);
+    static_assert(CS_PIECE == 512, "two uint4 per lane and piece");
+    // lanes past the slice reload the piece's first group; a group that starts below n lies inside the keys'
+    // allocation, whose end Carver rounds up to 16 B (keys past the slice are never read back)
+    auto group = [&](uint32_t p0, uint32_t q) {
+        const uint32_t k = p0 + 4u * (lane + 64u * q);
+        return *reinterpret_cast<const uint4*>(keys + (k < j1 ? k : p0));
+    };
+    uint4 nx0 = make_uint4(0u, 0u, 0u, 0u), nx1 = nx0;
+    if (j0 < j1) {
+        nx0 = group(j0, 0);
+        nx1 = group(j0, 1);
+    }
+    uint32_t c = 0;
+    for (uint32_t p0 = j0; p0 < j1; p0 += CS_PIECE) {
+        const uint32_t p1 = min(j1, p0 + CS_PIECE);
+        s_piece[w][lane] = nx0;
+        s_piece[w][lane + 64u] = nx1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // a wave's LDS ops complete in issue order
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (p1 < j1) {  // the next piece in flight while this one is compared
+            nx0 = group(p1, 0);
+            nx1 = group(p1, 1);
+        }
+        c += count_staged<true>(sp, p0, p0, min(p1, b0), ki);         // before the workgroup's keys: ties count
+        c += count_staged<false>(sp, p0, max(p0, b1), p1, ki);        // after them: ties do not
+        for (uint32_t j = max(p0, b0); j < min(p1, b1); ++j) {        // among them: by index
+            const uint32_t kj = sp[j - p0];
+            c += (kj < ki) | ((kj == ki) & (j < i));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // every read of this piece before the next store
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    s_cnt[w][lane] = c;
+    __syncthreads();
+    if (w == 0 && i < n) {
+        uint32_t pos = 0;
+#pragma unroll
+        for (int q = 0; q < CS_WAVES; ++q) pos += s_cnt[q][lane];
+        order[pos] = i;
+    }
+}
+void depth_count_sort(const uint32_t* keys, uint32_t* order, size_t n, hipStream_t s)
+{
+    if (n == 0) return;
+    depth_count_sort_kernel<<<div_up((uint32_t)n, 64u), 64 * CS_WAVES, 0, s>>>(keys, order, (uint32_t)n);
+}
+
 template int radix_sort_pairs<uint32_t>(uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, size_t,
                                         const uint32_t*, char*, int, int, hipStream_t, bool, uint32_t*);
 template int radix_sort_pairs<uint16_t>(uint16_t*, uint16_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, size_t,

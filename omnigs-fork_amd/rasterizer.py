@@ -569,8 +569,9 @@ def debug_counters(P, geomBuffer) -> dict:
 
 
 def debug_depth_sort_mode(mode: int) -> int:
-    """The forward's depth sort, process-wide (omr_debug_depth_sort_mode): 0 by camera type, 1 the plain 4 x 8-bit
-    radix sort, 2 the sort that sets culled Gaussians aside first. Returns the previous mode."""
+    """The forward's depth sort, process-wide (omr_debug_depth_sort_mode): 0 by size and camera type, 1 the plain
+    4 x 8-bit radix sort, 2 the sort that sets culled Gaussians aside first, 3 the sort by counting (views of at most
+    2^18 Gaussians; the default up to 12288). Returns the previous mode."""
     rc = int(lib().omr_debug_depth_sort_mode(int(mode)))
     if rc < 0:
         raise RasterizerError(f"debug_depth_sort_mode({mode}): {lib().omr_last_error().decode()}")

@@ -94,9 +94,18 @@ def _worker(rank, world, port, q, tmpdir, config):
 
 
 @pytest.mark.parametrize("config", ["D", "E"])
-def test_config_eight_ranks_compact_exchange(config, tmp_path):
+def test_config_eight_ranks_compact_exchange(config, tmp_path, capsys):
     """allreduce_compact_ after the backward and the overlapped CompactExchange (ar_chunks 1, 3) at eight ranks."""
+    import queue
+    import time
+
     import torch
+
+    t0 = time.monotonic()
+
+    def progress(what):  # a line past pytest's capture every half minute: config E runs for minutes without output
+        with capsys.disabled():
+            print(f"\n  [{config}, {time.monotonic() - t0:.0f} s] {what}", flush=True)
 
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -106,7 +115,16 @@ def test_config_eight_ranks_compact_exchange(config, tmp_path):
     procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q, str(tmp_path), config)) for r in range(WORLD)]
     for p in procs:
         p.start()
-    digests = dict(q.get(timeout=600) for _ in procs)
+    digests, last = {}, time.monotonic()
+    while len(digests) < WORLD:
+        try:
+            r, d = q.get(timeout=30)
+            digests[r] = d
+        except queue.Empty:
+            assert time.monotonic() - t0 < 600, f"{WORLD - len(digests)} ranks silent after 600 s"
+        if time.monotonic() - last >= 30:
+            progress(f"{len(digests)} of {WORLD} ranks done")
+            last = time.monotonic()
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -120,6 +138,7 @@ def test_config_eight_ranks_compact_exchange(config, tmp_path):
     R, par = omr.rasterizer, omr.parallel
     sums, mags, dsh_seq, dcolors, campos = None, None, None, [], []
     for v in range(WORLD):
+        progress(f"sequential reference, view {v}")
         g, cam, dL = omr.scene.config_scene(_scene_name(config, v), view_index=v)
         h = hip_run(g, cam, dL)
         gr = h["grads"]

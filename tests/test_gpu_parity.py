@@ -272,9 +272,10 @@ def _depths_between(g, lo, hi, seed, levels=None):
     g.means3D = (d * r[:, None]).astype(np.float32)
 
 
-@pytest.fixture(params=[1, 2], ids=["plain_sort", "culled_aside_sort"])
+@pytest.fixture(params=[1, 2, 3], ids=["plain_sort", "culled_aside_sort", "count_sort"])
 def depth_sort_mode(request):
-    """Both depth sorts (capi.hip: depth_sort_plain; omr_debug_depth_sort_mode) on every camera type."""
+    """Every depth sort (capi.hip: depth_sort_kind; omr_debug_depth_sort_mode) on every camera type; the sort by
+    counting only up to its forced limit of 2^18 Gaussians (beyond it the mode falls back to the radix sorts)."""
     old = omr.rasterizer.debug_depth_sort_mode(request.param)
     yield request.param
     omr.rasterizer.debug_depth_sort_mode(old)
@@ -304,9 +305,25 @@ def test_depth_sort_multi_launch_path_with_culled_gaussians(oracle_mt, depth_sor
     here 2.2 M Gaussians between 0.1 and 3000 m, some culled (too close): pass 0's downsweep publishes the visible
     count and passes 1..3 run over the visible keys only. Forward integers bit-exact and the image against the
     oracle."""
+    if depth_sort_mode == 3:
+        pytest.skip("past the sort by counting's forced limit (2^18): the mode falls back to the radix sorts")
     g, cam, _ = make_case(2_200_000, 256, 128, LON, 65, view_index=2, spread=0.3)
     _depths_between(g, 0.1, 3000.0, 66)
     _compare(g, cam, None, nthreads=oracle_mt)
+
+
+@pytest.mark.parametrize("P", [17, 1001, 4097])
+def test_count_sort_ragged_sizes_with_ties(P):
+    """depth_count_sort (sort.hip) at sizes that are not multiples of its 16-key scalar groups or 64-key workgroups,
+    depths tied in runs and some culled: the permutation equals the stable sort's, forward and backward against the
+    oracle."""
+    old = omr.rasterizer.debug_depth_sort_mode(3)
+    try:
+        g, cam, dL = make_case(P, 128, 64, LON, 67, view_index=0, spread=1.5)
+        _depths_between(g, 0, 0, 68, levels=np.array([2.0, 3.0, 0.1], dtype=np.float32))  # 0.1: too close, culled
+        _compare(g, cam, dL)
+    finally:
+        omr.rasterizer.debug_depth_sort_mode(old)
 
 
 def test_row_binning_reports_its_row_slots():
