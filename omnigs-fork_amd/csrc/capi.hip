@@ -671,17 +671,19 @@ int forward_impl(const ForwardIn& in)
             StageScope st_(ST_RANGES, s);
             launch_tile_ranges(capacity, count_dev, b.point_keys, keys16, im.ranges, s);
         }
-        { StageScope st_(ST_RANGES, s); launch_tile_order(im.ranges, nullptr, d.T, im.tile_order, s); }
+        const bool fwd_depth = in.render_depth && in.camera_type == CAM_PINHOLE;
+        const bool fwd_order = render_forward_needs_order(d.T);
+        if (fwd_order) { StageScope st_(ST_RANGES, s); launch_tile_order(im.ranges, nullptr, d.T, im.tile_order, s); }
         if (rerun) OMR_HIP(hipMemsetAsync(im.tile_cost, 0, d.T * sizeof(uint32_t), s));
         RenderFwdArgs ra;
         ra.W = in.width; ra.H = in.height; ra.gx = d.gx; ra.gy = d.gy;
-        ra.ranges = im.ranges; ra.tile_order = im.tile_order; ra.binning = bin_base; ra.count = count_dev; ra.capacity = capacity;
+        ra.ranges = im.ranges; ra.tile_order = fwd_order ? im.tile_order : nullptr; ra.binning = bin_base; ra.count = count_dev; ra.capacity = capacity;
         ra.splat = g.splat;
         ra.bg = in.background; ra.tile_cost = im.tile_cost; ra.final_T = im.final_T; ra.n_contrib = im.n_contrib;
         ra.max_contrib = im.max_contrib; ra.final_C = im.final_C;
         ra.out_color = in.out_color;
         // lonlat never renders depth (rasterize_points.cu:133-156 passes render_depth to the pinhole path only)
-        { StageScope st_(ST_RENDER_FWD, s); launch_render_forward(ra, in.render_depth && in.camera_type == CAM_PINHOLE, s); }
+        { StageScope st_(ST_RENDER_FWD, s); launch_render_forward(ra, fwd_depth, s); }
         return OMR_OK;
     };
     if (int e = back_half(cap)) return e;
@@ -777,7 +779,7 @@ int backward_impl(const BackwardIn& in)
     if (R > 0)
         launch_backward_schedule(err_words, im.ranges, im.max_contrib, d.T, reinterpret_cast<uint2*>(lb + units_tmp_offset(R, d.T)),
                                  reinterpret_cast<uint32_t*>(lb + units_tmp_offset(R, d.T) + seg_count(R, d.T) * 8),
-                                 units, unit_count, s);
+                                 units, unit_count, render_backward_needs_order(seg_count(R, d.T)), s);
     {
         StageScope st_(ST_RENDER_BWD, s, true);
         if (R > 0) launch_render_backward(rb, seg_count(R, d.T), s, st_.start(), st_.stop());

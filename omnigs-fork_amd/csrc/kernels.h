@@ -187,7 +187,7 @@ struct RenderFwdArgs {
     int W, H;
     uint32_t gx, gy;
     const uint2* ranges;
-    const uint32_t* tile_order;  // [T] schedule (launch_tile_order)
+    const uint32_t* tile_order;  // [T] schedule (launch_tile_order), or NULL: tiles in index order
     char* binning;               // binning buffer: point list at binning + canonical_list_offset(L); checkpoints, segment work
     const uint32_t* count;       // device count words (GeomState::counters; raster_common.h binning_count)
     size_t capacity;             // instances the binning buffer was sized for (count > capacity: render nothing)
@@ -201,6 +201,9 @@ struct RenderFwdArgs {
     float* out_color;
 };
 void launch_render_forward(const RenderFwdArgs& a, bool depth_mode, hipStream_t s);
+// whether the forward of a T-tile view wants the longest-first tile order: not at two or fewer waves per SIMD (config
+// A), where every wave starts at once and dispatch order does not change the makespan
+bool render_forward_needs_order(uint32_t T);
 
 // render_bwd.hip
 struct RenderBwdArgs {
@@ -231,9 +234,12 @@ void launch_render_backward(const RenderBwdArgs& a, size_t max_units, hipStream_
 int bwd_bands_mode(int mode);
 // the backward's work list: every (tile, depth segment) below the tile's last contributor (max over the forward's
 // max_contrib words), costed by its positions, sorted longest first within each of the 8 XCD shares of the unit list
-// (the shares xcd_remap gives each XCD); writes units, *unit_count
+// (the shares xcd_remap gives each XCD), or, sorted = false, in tile order; writes units, *unit_count
 void launch_backward_schedule(const HostWords& hw, const uint2* ranges, const uint32_t* max_contrib, uint32_t T, uint2* units_tmp,
-                              uint32_t* cost_tmp, uint2* units, uint32_t* unit_count, hipStream_t s);
+                              uint32_t* cost_tmp, uint2* units, uint32_t* unit_count, bool sorted, hipStream_t s);
+// whether the backward of a view with at most max_units units wants them longest first: not when the kernel that
+// launch_render_backward picks holds every unit's workgroup at once (configs A, B)
+bool render_backward_needs_order(size_t max_units);
 #ifdef OMR_STAMPS
 int omr_debug_stamps_bwd(uint64_t* dst, size_t bytes);  // diagnostic builds only (tile_wave.h)
 #endif

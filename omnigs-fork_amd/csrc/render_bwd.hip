@@ -622,6 +622,49 @@ int bwd_bands_mode(int mode)
     return mode < 0 ? m.load() : m.exchange(mode);
 }
 
+// workgroups of `kernel` (block size `threads`) the device holds at once, asked of the runtime; `fallback` per CU
+// when it cannot say
+template <class K>
+static size_t device_resident(K kernel, int threads, int fallback)
+{
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu <= 0)
+        per_cu = fallback;
+    return (size_t)cus * (size_t)per_cu;
+}
+struct BwdResident {
+    size_t one_wave = 0, two_band = 0;  // render_bwd_kernel<OMR_BWD_BATCH> (one wave), render_bwd2_kernel (128 threads)
+};
+static const BwdResident& bwd_resident()  // once per device and host thread
+{
+    static thread_local int cached_dev = -1;
+    static thread_local BwdResident r;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (dev != cached_dev) {
+        r.one_wave = device_resident(render_bwd_kernel<OMR_BWD_BATCH>, 64 * TW_WAVES, 24);
+        r.two_band = device_resident(render_bwd2_kernel<TW_BATCH, true>, 128, 0);  // 0 (unknown): units stay sorted
+        cached_dev = dev;
+    }
+    return r;
+}
+// the two-band kernel runs when every unit fits the resident one-wave workgroups (or OMR_BWD_BANDS=2 forces it)
+static bool bwd_two_band(size_t max_units)
+{
+    const int bands = bwd_bands_mode(-1);
+    return bands == 2 || (bands == 0 && max_units <= bwd_resident().one_wave);
+}
+
+bool render_backward_needs_order(size_t max_units)
+{
+    // OMR_BWD_SCHED_SORT=1 / 0 (A/B runs): units longest first always / never
+    static const int forced = [] { const char* v = std::getenv("OMR_BWD_SCHED_SORT"); return v ? std::atoi(v) : -1; }();
+    if (forced == 0 || forced == 1) return forced == 1;
+    return !(bwd_two_band(max_units) && max_units <= bwd_resident().two_band);
+}
+
 void launch_render_backward(const RenderBwdArgs& a, size_t max_units, hipStream_t s, hipEvent_t ev_start,
                             hipEvent_t ev_stop)
 {
@@ -629,21 +672,7 @@ void launch_render_backward(const RenderBwdArgs& a, size_t max_units, hipStream_
     // max_units (tiles + L / CKPT + 1) bounds the unit count; it is compared with the one-wave workgroups of the
     // batch-BWD_BATCH kernel the device holds at once (24 per CU on MI355X's 256 CUs: 6144), asked of the runtime once
     // per device
-    static thread_local int cached_dev = -1;
-    static thread_local size_t resident = 0;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    if (dev != cached_dev) {
-        int cus = 0, per_cu = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_bwd_kernel<OMR_BWD_BATCH>, 64 * TW_WAVES, 0) !=
-                hipSuccess ||
-            per_cu <= 0)
-            per_cu = 24;
-        resident = (size_t)cus * (size_t)per_cu;
-        cached_dev = dev;
-    }
-    const size_t RESIDENT = resident;
+    const size_t RESIDENT = bwd_resident().one_wave;
     auto launch = [&](auto kernel) {
         if (ev_start || ev_stop)
             hipExtLaunchKernelGGL(kernel, dim3((uint32_t)max_units), dim3(64 * TW_WAVES), 0, s, ev_start, ev_stop, 0, a);
@@ -653,8 +682,7 @@ void launch_render_backward(const RenderBwdArgs& a, size_t max_units, hipStream_
     // views whose units all fit at once as one-wave workgroups (A, B): two waves per unit, 64-position batches;
     // larger views (C, D, E): one wave per unit and 40-position batches. OMR_BWD_BANDS=4 / 2 (omr_debug_bwd_bands)
     // forces one kernel for A/B runs and tests: 4 = the one-wave kernel with its own batch rule (64 below RESIDENT)
-    const int bands = bwd_bands_mode(-1);
-    if (bands == 2 || (bands == 0 && max_units <= RESIDENT)) {
+    if (bwd_two_band(max_units)) {
         if (ev_start || ev_stop)
             hipExtLaunchKernelGGL(render_bwd2_kernel<TW_BATCH, true>, dim3((uint32_t)max_units), dim3(128), 0, s, ev_start,
                                   ev_stop, 0, a);

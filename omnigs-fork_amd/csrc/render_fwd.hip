@@ -60,7 +60,7 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
     float4* s_geo = s_geo_all[wv];
     float4* s_quad = s_quad_all[wv];
     float4* s_rgb = s_rgb_all[wv];
-    const uint32_t tile = a.tile_order[unit / NG];
+    const uint32_t tile = a.tile_order ? a.tile_order[unit / NG] : unit / NG;  // NULL: every workgroup resident at once
     const uint32_t grp = unit % NG;
     const uint32_t band0 = grp * FWD_BANDS;  // this wave's bands: band0 .. band0 + FWD_BANDS - 1
     const TileLane tl(tile, a.gx);
@@ -255,21 +255,51 @@ __global__ __launch_bounds__(64 * TW_WAVES, OMR_FWD_MINW) void render_fwd_kernel
 
 }  // namespace
 
+// bands per wave by view: one (four waves per tile) up to FWD_FOUR_WAVE_TILES tiles, where two bands would give at
+// most two waves per SIMD (config A: render_fwd 12.4 -> 10.9 us; at B, 2048 tiles, one band is slower: 40.4 vs
+// 38.5 us; profiles/r06j_ab_{A,B}.txt), two below FWD_ONE_WAVE_TILES, four from there; OMR_FWD_BANDS=1|2|4 forces
+static int forward_bands(uint32_t T)
+{
+    static const int forced = [] { const char* v = std::getenv("OMR_FWD_BANDS"); return v ? std::atoi(v) : 0; }();
+    if (forced == 1 || (forced == 0 && T <= FWD_FOUR_WAVE_TILES)) return 1;
+    if (forced == 4 || (forced != 2 && T >= FWD_ONE_WAVE_TILES)) return 4;
+    return 2;
+}
+
+bool render_forward_needs_order(uint32_t T)
+{
+    // OMR_FWD_TILE_ORDER=1 / 0 (A/B runs): the longest-first order always / never
+    static const int forced = [] { const char* v = std::getenv("OMR_FWD_TILE_ORDER"); return v ? std::atoi(v) : -1; }();
+    if (forced == 0 || forced == 1) return forced == 1;
+    // at most two waves per SIMD (config A, 512 tiles x 4 waves): all start at once and none shares its SIMD with
+    // more than one other, so the order changes nothing and its launch is saved (A 896 -> 962 MP/s with the backward
+    // schedule's sort also skipped). At B (4 waves per SIMD) the order still spreads the heavy tiles over the SIMDs:
+    // render_fwd 36.9 vs 42.8 us without it (profiles/r06p_ab_{A,B}.txt)
+    static thread_local int cached_dev = -1;
+    static thread_local size_t simds = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (dev != cached_dev) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
+        simds = 4 * (size_t)std::max(cus, 0);  // 0 (unknown): the order is kept
+        cached_dev = dev;
+    }
+    return (size_t)T * (size_t)(4 / forward_bands(T)) > 2 * simds;
+}
+
 void launch_render_forward(const RenderFwdArgs& a, bool depth_mode, hipStream_t s)
 {
     const uint32_t T = a.gx * a.gy;
     if (T == 0) return;
-    // bands per wave by view: one (four waves per tile) up to FWD_FOUR_WAVE_TILES tiles, where two bands would give at
-    // most two waves per SIMD (config A: render_fwd 12.4 -> 10.9 us; at B, 2048 tiles, one band is slower: 40.4 vs
-    // 38.5 us; profiles/r06j_ab_{A,B}.txt), two below FWD_ONE_WAVE_TILES, four from there; OMR_FWD_BANDS=1|2|4 forces
-    static const int forced = [] { const char* v = std::getenv("OMR_FWD_BANDS"); return v ? std::atoi(v) : 0; }();
-    if (forced == 1 || (forced == 0 && T <= FWD_FOUR_WAVE_TILES)) {
+    const int bands = forward_bands(T);
+    if (bands == 1) {
         const uint32_t blocks = div_up(T * 4, TW_WAVES);
         if (depth_mode) render_fwd_kernel<true, 1><<<blocks, 64 * TW_WAVES, 0, s>>>(a);
         else render_fwd_kernel<false, 1><<<blocks, 64 * TW_WAVES, 0, s>>>(a);
         return;
     }
-    if (forced == 4 || (forced != 2 && T >= FWD_ONE_WAVE_TILES)) {
+    if (bands == 4) {
         const uint32_t blocks = div_up(T, TW_WAVES);
         if (depth_mode) render_fwd_kernel<true, 4><<<blocks, 64 * TW_WAVES, 0, s>>>(a);
         else render_fwd_kernel<false, 4><<<blocks, 64 * TW_WAVES, 0, s>>>(a);

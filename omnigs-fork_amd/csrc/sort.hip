@@ -1123,6 +1123,9 @@ __device__ __forceinline__ uint32_t tile_units(const uint2* ranges, const uint32
     *mc_out = mc;
     return mc ? (r.x + mc - 1) / CKPT - r.x / CKPT + 1 : 0u;
 }
+// SORTED = false (views whose units are all resident at once, render_backward_needs_order): the units go straight to
+// `units` in tile order, without the costs and the counting sort.
+template <bool SORTED>
 __global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(HostWords hw, const uint2* ranges,
                                                                           const uint32_t* max_contrib, uint32_t T,
                                                                           uint2* units_tmp, uint32_t* cost_tmp,
@@ -1153,8 +1156,8 @@ __global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(HostWo
     const uint32_t lo = x * q + min(x, rem), hi = lo + q + (x < rem ? 1u : 0u);
     // the share's unsorted units and costs: in LDS when they fit (config C: ~3 k units per share), which saves the
     // global round trips of the three passes below; else in the global scratch
-    const bool in_lds = hi - lo <= (uint32_t)SCHED_LDS_UNITS;  // block-uniform
-    uint2* uu = in_lds ? s_units : units_tmp;
+    const bool in_lds = SORTED && hi - lo <= (uint32_t)SCHED_LDS_UNITS;  // block-uniform
+    uint2* uu = !SORTED ? units : in_lds ? s_units : units_tmp;
     uint32_t* cc = in_lds ? s_cost : cost_tmp;
     const uint32_t ub = in_lds ? lo : 0u;  // index of unit u = u - ub
     if (first0 < hi && first0 + mine > lo) {
@@ -1175,11 +1178,15 @@ __global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(HostWo
                     const uint32_t chunk = rx / CKPT + k;
                     uu[u - ub] = make_uint2(t, chunk);
                     // cost: the segment's positions below the tile's last contributor
-                    cc[u - ub] = min(rx + mc, (chunk + 1) * CKPT) - max(rx, chunk * CKPT);
+                    if (SORTED) cc[u - ub] = min(rx + mc, (chunk + 1) * CKPT) - max(rx, chunk * CKPT);
                 }
                 first += c;
             }
         }
+    }
+    if (!SORTED) {
+        if (x == 0 && tid == 0) *unit_count = total;
+        return;
     }
     if (tid < RADIX) s_hist[tid] = 0;
     if (tid == 0) s_max = 0;
@@ -1222,14 +1229,15 @@ __global__ __launch_bounds__(SCHED_THREADS) void backward_schedule_kernel(HostWo
 }  // namespace
 
 void launch_backward_schedule(const HostWords& hw, const uint2* ranges, const uint32_t* max_contrib, uint32_t T,
-                              uint2* units_tmp, uint32_t* cost_tmp, uint2* units, uint32_t* unit_count, hipStream_t s)
+                              uint2* units_tmp, uint32_t* cost_tmp, uint2* units, uint32_t* unit_count, bool sorted,
+                              hipStream_t s)
 {
     if (T == 0) {
         if (hw.dst) launch_host_words(hw, s);
         return;
     }
-    backward_schedule_kernel<<<8, SCHED_THREADS, 0, s>>>(hw, ranges, max_contrib, T, units_tmp, cost_tmp, units,
-                                                         unit_count);
+    (sorted ? backward_schedule_kernel<true> : backward_schedule_kernel<false>)<<<8, SCHED_THREADS, 0, s>>>(
+        hw, ranges, max_contrib, T, units_tmp, cost_tmp, units, unit_count);
 }
 
 __global__ void host_words_kernel(HostWords hw) { write_host_words(hw, threadIdx.x); }
