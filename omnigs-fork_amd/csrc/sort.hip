@@ -185,6 +185,11 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint
         }
         s_i[pad(li)] = i < n ? in[i] : 0u;
     }
+    // the rows of the next tile's first rank, which the tile's last rank needs for its chunk owner word: gathered now,
+    // behind the loads above, instead of as two dependent round trips at the end of the kernel's chain
+    uint32_t next_tile_rows = 0;
+    if (rows && tid == SCAN_THREADS - 1 && base + SCAN_TILE < n && order_ok)
+        next_tile_rows = rects[order[base + SCAN_TILE]].x & ROWS_MASK;
     __syncthreads();
     uint32_t va[SCAN_ITEMS], vi[SCAN_ITEMS];
     uint32_t sum_a = 0, sum_i = 0;
@@ -229,7 +234,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint
         if (i >= n) continue;
         const uint32_t ex_i = s_i[pad(li)];
         row_first[i] = ex_i;
-        if (i == n - 1) count_out[0] = ex_i + in[i];  // num_rendered next to the flag words the host reads
+        if (i == n - 1) count_out[0] = s_excl[1] + total_i;  // num_rendered next to the flag words the host reads
         if (hrank[k] != 0xFFFFFFFFu) huge_list[s_huge_base + hrank[k]] = (uint32_t)i;
         const uint32_t incl = s_a[pad(li)];
         if (!rows) {
@@ -239,8 +244,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint
         }
         row_offsets[i] = incl;
         if (i == n - 1) count_out[4] = incl;  // M, the row binning's slot count
-        const uint32_t start = li == 0 ? incl - (order_ok ? rects[order[i]].x & ROWS_MASK : 0u)
-                                       : s_a[pad(li - 1)];
+        // li == 0 is thread 0's first item in both layouts: its own rows are va[0]
+        const uint32_t start = li == 0 ? incl - va[0] : s_a[pad(li - 1)];
         if (incl == start) continue;  // no rows (culled: ranked last)
         const uint32_t r = (uint32_t)i;
         const uint32_t kk = (start + BIN_CHUNK - 1) / BIN_CHUNK;  // the first chunk start at or after `start`
@@ -252,7 +257,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint
         uint32_t next_rows;
         if (i + 1 >= n) next_rows = 0;
         else if (li + 1 < SCAN_TILE) next_rows = s_a[pad(li + 1)] - incl;
-        else next_rows = order_ok ? rects[order[i + 1]].x & ROWS_MASK : 0u;
+        else next_rows = next_tile_rows;  // tid == SCAN_THREADS - 1, k == SCAN_ITEMS - 1
         if (next_rows == 0) desc_r[2 * ((incl - 1) / BIN_CHUNK) + 1] = r;
     }
 }
