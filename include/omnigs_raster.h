@@ -296,6 +296,11 @@ int omr_debug_set_sh_jac(char* geom_buffer, int P, int enabled, void* stream);
  * permutation every way); process-wide, for tests and A/B runs (the environment's OMR_DEPTH_SORT=bytes / visible /
  * count sets the start value). Returns the previous mode, or -1 for a mode outside 0..3 (omr_last_error says why) */
 int omr_debug_depth_sort_mode(int mode);
+/* the forward's binning: 0 = by view (the emit + radix tile sort up to 1024 tiles and past 1024 tiles a side, the row
+ * binning between), 1 = the row binning wherever the grid allows it, 2 = always the emit + tile sort (the same point
+ * list and ranges); process-wide, for tests and A/B runs (OMR_BINNING=rows / sort sets the start value). A forward and
+ * its backward must run under the same mode. Returns the previous mode, or -1 outside 0..2 */
+int omr_debug_binning_mode(int mode);
 /* omr_l1_ssim_loss's kernel: 0 = by image size (the streaming kernel once its strips fill the chip, else the tiled
  * one), 1 = always tiled, 2 = always streaming (both give bitwise the same dL_dimg); process-wide, for tests and A/B
  * runs. Returns the previous mode, or -1 for a mode outside 0..2 */

@@ -394,14 +394,20 @@ size_t ImageState::carve(char* base, size_t N, size_t T, ImageState* s)
     return c.size();
 }
 
-// OMR_BINNING=sort (read once) forces the emit + radix sort binning on every view: an A/B switch for measurements
-static bool sort_binning_forced()
+// The binning: the row binning (bin.hip) on views of more than BIN_SORT_MAX_TILES tiles and at most BIN_MAX_GRID
+// tiles a side; the emit + radix tile sort (sort.hip) otherwise. On the smallest views the sort path's four launches
+// beat the row binning's seven (config A: 967 -> 1003 MP/s; B, 2048 tiles: 2010 vs 1978, profiles/r06r_ab_{A,B}.txt).
+// omr_debug_binning_mode / OMR_BINNING=rows|sort (the start value) force either for tests and A/B runs; a forward and
+// its backward must see the same mode (the binning buffer's layout follows it).
+static std::atomic<int>& binning_mode()  // 0: by view, 1: rows (where the grid allows), 2: sort
 {
-    static const bool forced = [] {
+    static std::atomic<int> mode{[] {
         const char* v = std::getenv("OMR_BINNING");
-        return v && std::strcmp(v, "sort") == 0;
-    }();
-    return forced;
+        if (v && std::strcmp(v, "rows") == 0) return 1;
+        if (v && std::strcmp(v, "sort") == 0) return 2;
+        return 0;
+    }()};
+    return mode;
 }
 // The depth sort: pinhole views take depth_sort (sort.hip), whose first pass sets the culled Gaussians aside so the
 // other three sort the visible keys alone (config E pinhole culls 88 %: 0.206 -> 0.137 ms); lonlat views cull only
@@ -442,7 +448,9 @@ static DepthSortKind depth_sort_kind(int camera_type, size_t P)
 }
 static bool row_binning(uint32_t gx, uint32_t gy)
 {
-    return gx <= BIN_MAX_GRID && gy <= BIN_MAX_GRID && !sort_binning_forced();
+    const int m = binning_mode().load(std::memory_order_relaxed);
+    if (m == 2 || gx > BIN_MAX_GRID || gy > BIN_MAX_GRID) return false;
+    return m == 1 || (size_t)gx * gy > BIN_SORT_MAX_TILES;
 }
 
 size_t BinningState::carve(char* base, size_t cap, uint32_t gx, uint32_t gy, BinningState* s)
@@ -1425,6 +1433,15 @@ int omr_debug_depth_sort_mode(int mode)
     }
     const int old = depth_sort_mode().exchange(mode);
     return old;
+}
+
+int omr_debug_binning_mode(int mode)
+{
+    if (mode < 0 || mode > 2) {
+        fail(OMR_ERR_INVALID_ARGUMENT, "binning mode: 0 (by view), 1 (rows), 2 (sort)");
+        return -1;
+    }
+    return binning_mode().exchange(mode);
 }
 
 int omr_debug_ssim_mode(int mode)

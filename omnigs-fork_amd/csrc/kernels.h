@@ -135,6 +135,7 @@ void launch_host_words(const HostWords& h, hipStream_t s);
 // bin.hip: tile binning by rows, then columns (the point list, its band masks and the tile ranges) for views of at most
 // BIN_MAX_GRID tiles a side; sort.hip's emit + tile sort + ranges otherwise
 constexpr uint32_t BIN_MAX_GRID = 1024;
+constexpr size_t BIN_SORT_MAX_TILES = 1024;  // views of at most this many tiles take the emit + tile sort (capi.hip)
 struct BinArgs {
     HostWords hw;               // the forward's count words, written by the first kernel
     int P;

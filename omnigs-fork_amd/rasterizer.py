@@ -75,6 +75,8 @@ def lib() -> C.CDLL:
         L.omr_debug_counters.argtypes = [vp, i, vp, vp]
         L.omr_debug_depth_sort_mode.restype = i
         L.omr_debug_depth_sort_mode.argtypes = [i]
+        L.omr_debug_binning_mode.restype = i
+        L.omr_debug_binning_mode.argtypes = [i]
         L.omr_debug_ssim_mode.restype = i
         L.omr_debug_ssim_mode.argtypes = [i]
         L.omr_debug_bwd_bands.restype = i
@@ -575,6 +577,16 @@ def debug_depth_sort_mode(mode: int) -> int:
     rc = int(lib().omr_debug_depth_sort_mode(int(mode)))
     if rc < 0:
         raise RasterizerError(f"debug_depth_sort_mode({mode}): {lib().omr_last_error().decode()}")
+    return rc
+
+
+def debug_binning_mode(mode: int) -> int:
+    """The forward's binning, process-wide (omr_debug_binning_mode): 0 by view, 1 the row binning wherever the grid
+    allows it, 2 the emit + radix tile sort. A forward and its backward must run under the same mode. Returns the
+    previous mode."""
+    rc = int(lib().omr_debug_binning_mode(int(mode)))
+    if rc < 0:
+        raise RasterizerError(f"debug_binning_mode({mode}): {lib().omr_last_error().decode()}")
     return rc
 
 

@@ -149,11 +149,11 @@ def test_scratch_buffers_free_without_cyclic_gc(omr):
 
 
 def test_kernel_switches_without_gpu(omr):
-    """omr_debug_depth_sort_mode / omr_debug_ssim_mode (process-wide switches between kernels that give the same
-    results): each returns the previous mode, rejects a mode outside its range (0..3, 0..2) with -1 and a message,
-    and is restored."""
+    """omr_debug_depth_sort_mode / omr_debug_ssim_mode / omr_debug_binning_mode (process-wide switches between
+    kernels that give the same results): each returns the previous mode, rejects a mode outside its range (0..3,
+    0..2, 0..2) with -1 and a message, and is restored."""
     R = omr.rasterizer
-    for setter, top in ((R.debug_depth_sort_mode, 3), (R.debug_ssim_mode, 2)):
+    for setter, top in ((R.debug_depth_sort_mode, 3), (R.debug_ssim_mode, 2), (R.debug_binning_mode, 2)):
         old = setter(2)
         try:
             assert setter(1) == 2

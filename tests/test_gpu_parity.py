@@ -95,8 +95,17 @@ def _compare(g, cam, dL, nthreads=1, budget=None, **kw):
     record_residuals(rec, budget)
 
 
+@pytest.fixture(params=[0, 1], ids=["binning_by_view", "row_binning"])
+def binning_mode(request):
+    """Both binnings (capi.hip: row_binning; omr_debug_binning_mode) on the small views, which take the emit + tile
+    sort by default (at most BIN_SORT_MAX_TILES tiles) and the row binning when forced."""
+    old = omr.rasterizer.debug_binning_mode(request.param)
+    yield request.param
+    omr.rasterizer.debug_binning_mode(old)
+
+
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-def test_parity(case):
+def test_parity(case, binning_mode):
     _, P, W, H, cam_t, seed, view, deg, mult = case
     g, cam, dL = make_case(P, W, H, cam_t, seed, view_index=view, sh_degree=deg, spread=mult)
     _compare(g, cam, dL)
@@ -327,10 +336,15 @@ def test_count_sort_ragged_sizes_with_ties(P):
 
 
 def test_row_binning_reports_its_row_slots():
-    """bin.hip's rows pass: M = the sum of the visible Gaussians' rect heights (counters[4])."""
+    """bin.hip's rows pass: M = the sum of the visible Gaussians' rect heights (counters[4]); the 512-tile view takes
+    the row binning when forced (omr_debug_binning_mode(1))."""
     g, cam, _ = make_case(3000, 512, 256, LON, 53, view_index=1, spread=1.5)
     o, _, _ = oracle_run(g, cam)
-    h = hip_run(g, cam, None)
+    old = omr.rasterizer.debug_binning_mode(1)
+    try:
+        h = hip_run(g, cam, None)
+    finally:
+        omr.rasterizer.debug_binning_mode(old)
     P = g.P
     r = o.get("radii").astype(np.float64)
     m = o.get("means2D").reshape(P, 2).astype(np.float32)
@@ -585,10 +599,10 @@ def _band_mask_misses(h, g, cam):
 
 @pytest.mark.parametrize("cam_t,n,w,hgt,seed", [(LON, 20000, 512, 256, 61), (PIN, 20000, 480, 270, 62),
                                                 (LON, 3000, 256, 128, 63)], ids=["lonlat", "pinhole", "lonlat_small"])
-def test_band_masks_cover_every_contributing_pixel(cam_t, n, w, hgt, seed):
-    """The row binning's band masks (bin.hip: band_row_intervals, one x-interval per (Gaussian, row, band)) may only
-    drop a 16x4 band of a tile in which no pixel reaches alpha >= 1/255 — checked by brute force over every pixel of
-    every instance's tile (the render kernels skip masked-out bands, so a miss would change images)."""
+def test_band_masks_cover_every_contributing_pixel(cam_t, n, w, hgt, seed, binning_mode):
+    """The band masks of both binnings (bin.hip: band_row_intervals, one x-interval per (Gaussian, row, band); sort.hip's
+    emit) may only drop a 16x4 band of a tile in which no pixel reaches alpha >= 1/255 — checked by brute force over
+    every pixel of every instance's tile (the render kernels skip masked-out bands, so a miss would change images)."""
     g, cam, _ = make_case(n, w, hgt, cam_t, seed, view_index=1, spread=1.5)
     h = hip_run(g, cam, None)
     misses, frac = _band_mask_misses(h, g, cam)
