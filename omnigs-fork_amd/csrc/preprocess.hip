@@ -323,11 +323,24 @@ __device__ __forceinline__ void preprocess_prologue(const PreprocessArgs& a)
 // the geometry (below). (Staging the rows by LDS-DMA instead, with the geometry computed while
 // they land, measured no faster — the kernel streams at ~4.2 TB/s either way: profiles/r04c_ab_preprocess_dma.txt;
 // the code is kept in profiles/r04_pruned_experiments.patch.)
+//
+// Pinhole views (round 6) read the SH rows lane by lane into registers instead: a frustum leaves few lanes of a wave
+// with a row to read (12 % at E pinhole), so the per-lane loads touch few lines, and the wave's LDS image only
+// stages the render records (5 KiB instead of 13): the kernel is no longer held at 3 waves per SIMD by LDS.
+// OMR_PRE_PINHOLE_SPAN=1 (A/B builds) keeps the staged spans for pinhole views too.
+#ifndef OMR_PRE_PINHOLE_SPAN
+#define OMR_PRE_PINHOLE_SPAN 0
+#endif
+#ifndef OMR_PRE_PIN_MINW
+#define OMR_PRE_PIN_MINW 1
+#endif
 template <int CAM>
-__global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CAM == CAM_LONLAT ? 1 : OMR_PRE_PIN_MINW)))
+void preprocess_kernel(PreprocessArgs a)
 {
     constexpr int SH_F4 = 12;  // 16 coefficients x 3 channels
-    constexpr int IMG_F4 = stage_f4<SH_F4>();
+    constexpr bool span_rows = CAM == CAM_LONLAT || OMR_PRE_PINHOLE_SPAN;  // SH rows as staged spans
+    constexpr int IMG_F4 = span_rows ? stage_f4<SH_F4>() : stage_f4<SPLAT_F4>();
     static_assert(IMG_F4 >= stage_f4<SPLAT_F4>(), "the image also stages the render records");
     __shared__ float4 s_stage[4][IMG_F4];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -368,13 +381,39 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessArgs a)
     // counter merges the branch's sides conservatively), i.e. wait for the rows too
     asm volatile("" ::"v"(in.opacity), "v"(in.sx), "v"(in.sy), "v"(in.sz), "v"(in.q.x), "v"(in.q.y), "v"(in.q.z),
                  "v"(in.q.w), "v"(p_orig.x), "v"(p_orig.y), "v"(p_orig.z));
-    if (sh16 && fetch_rows) {
-        wave_rows_fetch<SH_F4>(reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4, fetch_rows, nf4,
-                               lane, early);
+    const bool fetched = (fetch_rows >> lane) & 1u;
+    if constexpr (span_rows) {
+        if (sh16 && fetch_rows) {
+            wave_rows_fetch<SH_F4>(reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4, fetch_rows,
+                                   nf4, lane, early);
+        }
+    } else {
+        if (sh16 && fetched) {  // the lane's own row (columns past nf4 are never read)
+            const rowv4* row = reinterpret_cast<const rowv4*>(a.shs) + (size_t)idx * SH_F4;
+#pragma unroll
+            for (int q = 0; q < SH_F4; ++q) early[q] = q < nf4 ? row[q] : rowv4{0.f, 0.f, 0.f, 0.f};
+        }
     }
     PreOut o;
     const bool vis = valid && preprocess_point<CAM>(a, in, idx, p_orig, sh16, shv, o, sh16);
-    if (sh16) {
+    if constexpr (!span_rows) {
+        if (sh16 && vis) {
+            if (!fetched) {  // a visible lane outside the prediction: its row after the projection
+                const rowv4* row = reinterpret_cast<const rowv4*>(a.shs) + (size_t)idx * SH_F4;
+#pragma unroll
+                for (int q = 0; q < SH_F4; ++q) early[q] = q < nf4 ? row[q] : rowv4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int q = 0; q < SH_F4; ++q) {
+                shv[4 * q] = early[q].x, shv[4 * q + 1] = early[q].y, shv[4 * q + 2] = early[q].z;
+                shv[4 * q + 3] = early[q].w;
+            }
+            float rgb[3];
+            sh16_colour(a, idx, p_orig, shv, rgb, o.clamp_bits);
+            o.rec[2].x = rgb[0], o.rec[2].y = rgb[1], o.rec[2].z = rgb[2];
+        }
+    }
+    if (span_rows && sh16) {
         const uint64_t rows = __ballot(vis);
         if (rows) {  // wave-uniform
             wave_rows_park<SH_F4>(early, stage, lane);
