@@ -164,14 +164,16 @@ def test_unaligned_sh_rows(cam_t):
     _compare(g, cam, dL, sh_misalign=True)
 
 
-@pytest.mark.parametrize("M,misalign", [(1, False), (4, False), (9, False), (16, True), (16, False)],
-                         ids=["M1", "M4", "M9", "M16_unaligned", "M16"])
-def test_skip_dsh_any_layout(M, misalign):
+@pytest.mark.parametrize("M,misalign,cam_t", [(1, False, LON), (4, False, LON), (9, False, LON), (16, True, LON),
+                                               (16, False, LON), (16, False, PIN)],
+                         ids=["M1", "M4", "M9", "M16_unaligned", "M16", "M16_pinhole"])
+def test_skip_dsh_any_layout(M, misalign, cam_t):
     """skip_dsh (dL_dsh = NULL, the view-parallel exchange's per-view call) for every SH layout (the
-    generic-M path wrote through the null pointer): the other seven gradients equal the full call's bitwise."""
+    generic-M path wrote through the null pointer), and at a pinhole view (its 16-coefficient backward stores the
+    small outputs through the wave image too): the other seven gradients equal the full call's bitwise."""
     import torch
 
-    g, cam, dL = make_case(2000, 128, 64, LON, 80 + M, view_index=3, sh_degree={1: 0, 4: 1, 9: 2}.get(M, 3),
+    g, cam, dL = make_case(2000, 128, 64, cam_t, 80 + M, view_index=3, sh_degree={1: 0, 4: 1, 9: 2}.get(M, 3),
                            spread=3.0)
     g.shs = np.ascontiguousarray(g.shs[:, :M])
     full = hip_run(g, cam, dL, sh_misalign=misalign)
