@@ -122,7 +122,7 @@ struct PreOut {
 // The view direction (forward.cu:37-38) and, from the SH row in registers, the colour (sh_eval.h) and the backward's
 // dRGB/ddir: preprocess_point's sh16 colour, restated for rows staged after the geometry (the same expressions, so
 // the same bits).
-__device__ __forceinline__ void sh16_colour(const PreprocessArgs& a, int idx, float3 p_orig, const float (&shv)[48],
+__device__ __forceinline__ void sh16_colour(const PreprocessArgs& a, int idx, float3 p_orig, const float* shv,
                                             float rgb[3], uint8_t& clamp_bits)
 {
     const float3 cp = {a.campos[0], a.campos[1], a.campos[2]};
@@ -334,12 +334,27 @@ __device__ __forceinline__ void preprocess_prologue(const PreprocessArgs& a)
 #ifndef OMR_PRE_PIN_MINW
 #define OMR_PRE_PIN_MINW 1
 #endif
+// OMR_PRE_PIN_GLOBAL=1 (A/B builds): pinhole lanes evaluate the colour from the SH row in global memory (no 48
+// registers for it, no early request)
+#ifndef OMR_PRE_PIN_GLOBAL
+#define OMR_PRE_PIN_GLOBAL 0
+#endif
+// OMR_PRE_LON_LANE=1 / OMR_PRE_LON_GLOBAL=1 (A/B builds): the same two forms for equirect views
+#ifndef OMR_PRE_LON_LANE
+#define OMR_PRE_LON_LANE 0
+#endif
+#ifndef OMR_PRE_LON_GLOBAL
+#define OMR_PRE_LON_GLOBAL 0
+#endif
 template <int CAM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CAM == CAM_LONLAT ? 1 : OMR_PRE_PIN_MINW)))
 void preprocess_kernel(PreprocessArgs a)
 {
     constexpr int SH_F4 = 12;  // 16 coefficients x 3 channels
-    constexpr bool span_rows = CAM == CAM_LONLAT || OMR_PRE_PINHOLE_SPAN;  // SH rows as staged spans
+    // colour from the SH row in global memory / SH rows as staged spans (else: per-lane rows in registers)
+    constexpr bool global_colour = CAM == CAM_LONLAT ? OMR_PRE_LON_GLOBAL : OMR_PRE_PIN_GLOBAL;
+    constexpr bool span_rows =
+        !global_colour && (CAM == CAM_LONLAT ? !OMR_PRE_LON_LANE : (bool)OMR_PRE_PINHOLE_SPAN);
     constexpr int IMG_F4 = span_rows ? stage_f4<SH_F4>() : stage_f4<SPLAT_F4>();
     static_assert(IMG_F4 >= stage_f4<SPLAT_F4>(), "the image also stages the render records");
     __shared__ float4 s_stage[4][IMG_F4];
@@ -381,7 +396,7 @@ void preprocess_kernel(PreprocessArgs a)
     // counter merges the branch's sides conservatively), i.e. wait for the rows too
     asm volatile("" ::"v"(in.opacity), "v"(in.sx), "v"(in.sy), "v"(in.sz), "v"(in.q.x), "v"(in.q.y), "v"(in.q.z),
                  "v"(in.q.w), "v"(p_orig.x), "v"(p_orig.y), "v"(p_orig.z));
-    const bool fetched = (fetch_rows >> lane) & 1u;
+    const bool fetched = !global_colour && ((fetch_rows >> lane) & 1u);
     if constexpr (span_rows) {
         if (sh16 && fetch_rows) {
             wave_rows_fetch<SH_F4>(reinterpret_cast<const float4*>(a.shs) + (size_t)wave_first * SH_F4, fetch_rows,
@@ -396,7 +411,13 @@ void preprocess_kernel(PreprocessArgs a)
     }
     PreOut o;
     const bool vis = valid && preprocess_point<CAM>(a, in, idx, p_orig, sh16, shv, o, sh16);
-    if constexpr (!span_rows) {
+    if constexpr (global_colour) {
+        if (sh16 && vis) {
+            float rgb[3];
+            sh16_colour(a, idx, p_orig, a.shs + (size_t)idx * 48, rgb, o.clamp_bits);
+            o.rec[2].x = rgb[0], o.rec[2].y = rgb[1], o.rec[2].z = rgb[2];
+        }
+    } else if constexpr (!span_rows) {
         if (sh16 && vis) {
             if (!fetched) {  // a visible lane outside the prediction: its row after the projection
                 const rowv4* row = reinterpret_cast<const rowv4*>(a.shs) + (size_t)idx * SH_F4;
