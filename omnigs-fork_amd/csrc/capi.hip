@@ -596,7 +596,18 @@ int forward_impl(const ForwardIn& in)
             depth_sort(g.key_a, g.key_b, g.val_a, g.val_b, g.order, g.hist, g.scan_partials, P, s, err_dev);
         }
     }
-    { StageScope st_(ST_SCAN, s); launch_forward_scans(g.tiles_touched, rows_path ? g.rect : nullptr, g.order, g.offsets, g.row_first, g.row_offsets, g.drect, g.desc_r, g.huge_list, g.counters + 2, g.scan2_status, g.counters, err_dev, P, s); }
+    // after the culled-aside depth sort, depth ranks from nvis on are culled Gaussians: the scans skip their words
+    // (OMR_SCAN_NVIS=0 builds: every rank, for A/B runs)
+#ifndef OMR_SCAN_NVIS
+#define OMR_SCAN_NVIS 1
+#endif
+    {
+        StageScope st_(ST_SCAN, s);
+        const uint32_t* nvis = dsk == DS_VISIBLE && OMR_SCAN_NVIS ? depth_sort_nvis(g.hist, P) : nullptr;
+        launch_forward_scans(g.tiles_touched, rows_path ? g.rect : nullptr, g.order, g.offsets, g.row_first, g.row_offsets,
+                             g.drect, g.desc_r, g.huge_list, g.counters + 2, g.scan2_status, g.counters, err_dev, P, s,
+                             nvis);
+    }
 
     // num_rendered = offsets[P-1] (+ the prefiltered error flag) to pinned host memory, without waiting for it:
     // the binning buffer is sized from a capacity hint and everything after the scan reads the count on the device,

@@ -56,12 +56,14 @@ size_t radix_partials_words(size_t n);
 // kernel); err (device word, zeroed by the caller; NULL = a private word) is OR-ed with 1 if a look-back gave up
 // (sort.hip: LB_SPIN_MAX). rects == NULL (sort path): offsets = inclusive scan in depth order (gather by order).
 // rects != NULL (row path): drect = rects in depth order, row_offsets = inclusive scan of their rows in depth order,
-// count_out[4] = its total M, desc_r = each BIN_CHUNK-slot chunk's first and last owner rank.
+// count_out[4] = its total M, desc_r = each BIN_CHUNK-slot chunk's first and last owner rank. nvis (device word, may
+// be NULL): depth ranks from *nvis on are culled (depth_sort_nvis); their depth-order words are neither gathered nor,
+// on the row path, written.
 size_t scan2_status_words(size_t n);
 void launch_forward_scans(const uint32_t* tiles_touched, const uint2* rects, const uint32_t* order, uint32_t* offsets,
                           uint32_t* row_first, uint32_t* row_offsets, uint2* drect, uint2* desc_r, uint32_t* huge_list,
                           uint32_t* huge_count, uint32_t* status, uint32_t* count_out, uint32_t* err, size_t n,
-                          hipStream_t s);
+                          hipStream_t s, const uint32_t* nvis = nullptr);
 // stable LSD radix sort of (key, value) over bits [0, 8*passes); returns which buffer holds the result (0: a, 1: b).
 // n = capacity; count (device, may be NULL) = live element count <= n. canon != NULL: the last pass writes the
 // values to the canonical point list of the binning buffer at canon (raster_common.h) instead of val_a / val_b.
@@ -86,6 +88,8 @@ size_t depth_sort_partials_words(size_t n);
 ZeroSpan depth_sort_zero_span(uint32_t* hist, size_t n);
 void depth_sort(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* order, uint32_t* hist,
                 uint32_t* scan_partials, size_t n, hipStream_t s, uint32_t* err);
+// the device word holding the visible count once depth_sort has run (pass 0 sets it: the culled bucket's start)
+const uint32_t* depth_sort_nvis(const uint32_t* hist, size_t n);
 // The depth sort of small views (sort.hip): the same permutation as depth_sort / the plain radix sort (visible keys in
 // order, ties by index, then the culled ones by index) by counting, O(n^2) compares in one launch; keys: the n keys.
 // the default up to this many keys (capi.hip: depth_sort_kind): 18.8 us at 10 k keys on 157 CUs against the radix

@@ -150,7 +150,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint
                                                                       uint32_t* offsets, uint32_t* row_first,
                                                                       uint32_t* row_offsets, uint2* drect,
                                                                       uint32_t* desc_r, uint32_t* huge_list,
-                                                                      uint32_t* huge_count, uint32_t* count_out)
+                                                                      uint32_t* huge_count, uint32_t* count_out,
+                                                                      const uint32_t* nvis)
 {
     __shared__ uint32_t s_a[SCAN_TILE + SCAN_TILE / 32];  // depth order: tiles (sort path) or rows (row path)
     __shared__ uint32_t s_i[SCAN_TILE + SCAN_TILE / 32];  // +1 pad per 32 to break the 16-stride conflicts
@@ -170,25 +171,29 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint
     constexpr uint32_t ROWS_MASK = (1u << RECT_ROWS_BITS) - 1u;
     // a depth sort whose look-back gave up may leave `order` partly unwritten: never gather through it then
     const bool order_ok = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+    // depth ranks past n_a hold culled Gaussians (nvis: the culled-aside depth sort's visible count), which own no
+    // tiles and no rows: no order load or gather for them, and on the row path no drect / row_offsets word either (the
+    // row binning reads those only at owners of row slots, all visible)
+    const size_t n_a = nvis ? min((size_t)*nvis, n) : n;
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; ++k) {
         const uint32_t li = k * SCAN_THREADS + tid;
         const size_t i = base + li;
-        const uint32_t o = i < n && order_ok ? order[i] : 0u;
+        const uint32_t o = i < n_a && order_ok ? order[i] : 0u;
         if (rows) {
             // the one random gather of the forward scans: a second one measured +79 us at config E (139 -> 218 us)
-            const uint2 rw = i < n && order_ok ? rects[o] : make_uint2(0u, 0u);
-            if (i < n) drect[i] = rw;
+            const uint2 rw = i < n_a && order_ok ? rects[o] : make_uint2(0u, 0u);
+            if (i < n_a) drect[i] = rw;
             s_a[pad(li)] = rw.x & ROWS_MASK;
         } else {
-            s_a[pad(li)] = i < n && order_ok ? in[o] : 0u;
+            s_a[pad(li)] = i < n_a && order_ok ? in[o] : 0u;
         }
         s_i[pad(li)] = i < n ? in[i] : 0u;
     }
     // the rows of the next tile's first rank, which the tile's last rank needs for its chunk owner word: gathered now,
     // behind the loads above, instead of as two dependent round trips at the end of the kernel's chain
     uint32_t next_tile_rows = 0;
-    if (rows && tid == SCAN_THREADS - 1 && base + SCAN_TILE < n && order_ok)
+    if (rows && tid == SCAN_THREADS - 1 && base + SCAN_TILE < n_a && order_ok)
         next_tile_rows = rects[order[base + SCAN_TILE]].x & ROWS_MASK;
     __syncthreads();
     uint32_t va[SCAN_ITEMS], vi[SCAN_ITEMS];
@@ -242,8 +247,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan2_lookback_kernel(const uint
             if (i == n - 1) count_out[4] = 0u;  // no row slots on this path
             continue;
         }
-        row_offsets[i] = incl;
         if (i == n - 1) count_out[4] = incl;  // M, the row binning's slot count
+        if (i >= n_a) continue;  // culled: no rows
+        row_offsets[i] = incl;
         // li == 0 is thread 0's first item in both layouts: its own rows are va[0]
         const uint32_t start = li == 0 ? incl - va[0] : s_a[pad(li - 1)];
         if (incl == start) continue;  // no rows (culled: ranked last)
@@ -712,6 +718,8 @@ __global__ __launch_bounds__(OS_THREADS) void onesweep_kernel(const K* keys_in, 
     const uint32_t vb = s_vb;
     uint32_t total;
     const uint32_t gstart = block_exclusive_scan<OS_THREADS>(dig ? ghist[tid] : 0u, s_wave, &total);
+    // the depth sort's pass 0: the start of the culled bucket is the visible count (depth_sort_nvis)
+    if (depth && dp.pass == 0 && dp.words && vb == 0 && tid == DEPTH_CULLED_BUCKET) dp.words[0] = gstart;
     // depth passes 1..3 sort the visible keys alone, which their digit totals count: no count word to wait for
     const size_t n = depth && dp.pass > 0 ? (size_t)total : n_live;
     const size_t tile0 = (size_t)vb * TILE_N;
@@ -1264,7 +1272,7 @@ size_t scan2_status_words(size_t n) { return 4 * div_up(n, SCAN_TILE) + 2; }
 void launch_forward_scans(const uint32_t* tiles_touched, const uint2* rects, const uint32_t* order, uint32_t* offsets,
                           uint32_t* row_first, uint32_t* row_offsets, uint2* drect, uint2* desc_r, uint32_t* huge_list,
                           uint32_t* huge_count, uint32_t* status, uint32_t* count_out, uint32_t* err, size_t n,
-                          hipStream_t s)
+                          hipStream_t s, const uint32_t* nvis)
 {
     if (n == 0) return;
     const uint32_t nb = div_up(n, SCAN_TILE);
@@ -1273,7 +1281,7 @@ void launch_forward_scans(const uint32_t* tiles_touched, const uint2* rects, con
     scan2_lookback_kernel<<<nb, SCAN_THREADS, 0, s>>>(tiles_touched, rects, order, n, st, st + nb, ticket,
                                                       err ? err : ticket + 1, offsets, row_first, row_offsets, drect,
                                                       reinterpret_cast<uint32_t*>(desc_r), huge_list, huge_count,
-                                                      count_out);
+                                                      count_out, nvis);
 }
 
 size_t radix_hist_size(size_t n) { return (size_t)RADIX * div_up(n, SORT_TILE); }
@@ -1396,6 +1404,8 @@ ZeroSpan depth_sort_zero_span(uint32_t* hist, size_t n)
     return z;
 }
 
+const uint32_t* depth_sort_nvis(const uint32_t* hist, size_t n) { return hist + depth_words_at(n); }
+
 void depth_sort(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val_b, uint32_t* order, uint32_t* hist,
                 uint32_t* scan_partials, size_t n, hipStream_t s, uint32_t* err)
 {
@@ -1412,6 +1422,7 @@ void depth_sort(uint32_t* key_a, uint32_t* key_b, uint32_t* val_a, uint32_t* val
         for (int p = 0; p < DEPTH_PASSES; ++p) {
             DepthPass dp;
             dp.pass = p;
+            dp.words = words;
             dp.vals_final = order;
             auto kern = os_tile(n) == OS_TILE ? onesweep_kernel<uint32_t, OS_TILE, true>
                                               : onesweep_kernel<uint32_t, OS_TILE_SMALL, true>;

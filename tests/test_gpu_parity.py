@@ -293,11 +293,13 @@ def depth_sort_mode(request):
 
 
 @pytest.mark.parametrize("P,W,H,cam_t", [(20000, 256, 128, LON), (20000, 320, 180, PIN)])
-def test_depth_sort_wide_depth_span(P, W, H, cam_t, depth_sort_mode):
+def test_depth_sort_wide_depth_span(P, W, H, cam_t, depth_sort_mode, binning_mode):
     """depth_sort (sort.hip): pass 0 sorts bits 0..6 and sets the culled Gaussians aside (bucket 128, straight to
     their final places behind the visible ones), passes 1..3 sort bits 7..30 of the visible keys alone. Depths 0.1 ..
     3000 m make every one of those bits vary and cull the closest (lonlat: r <= 0.2; pinhole: z <= 0.2), forward and
-    backward against the oracle (the point list is the reference's (tile, depth, index) order bit for bit)."""
+    backward against the oracle (the point list is the reference's (tile, depth, index) order bit for bit). Under
+    both binnings: after the culled-aside sort the forward scans stop their depth-order words at its visible count
+    (sort.hip: scan2_lookback_kernel, nvis), which the row binning's rows pass then reads."""
     g, cam, dL = make_case(P, W, H, cam_t, 61, view_index=1, spread=2.0)
     _depths_between(g, 0.1, 3000.0, 62)
     _compare(g, cam, dL)
